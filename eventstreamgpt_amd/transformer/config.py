@@ -1,0 +1,389 @@
+"""Model / optimisation configuration — the contract of ``EventStream/transformer/config.py``.
+
+``StructuredTransformerConfig`` keeps the reference's constructor arguments, attribute names and derived fields
+(``config.py:355-899``) so that configs written by the reference (``config.json``) load unchanged. It is an HF
+``PretrainedConfig`` exactly like the reference's, so ``to_dict`` / ``to_json_file`` / ``from_dict`` round-trip.
+"""
+from __future__ import annotations
+
+import dataclasses
+import enum
+import math
+from typing import Any
+
+from transformers import PretrainedConfig
+
+from ..data.data_embedding_enums import MeasIndexGroupOptions, StaticEmbeddingMode
+from ..data.types import DataModality
+from ..utils import StrEnum
+
+
+class StructuredEventProcessingMode(StrEnum):
+    """CI: intra-event covariates independent given history. NA: predicted along a dependency chain."""
+
+    CONDITIONALLY_INDEPENDENT = enum.auto()
+    NESTED_ATTENTION = enum.auto()
+
+
+class TimeToEventGenerationHeadType(StrEnum):
+    EXPONENTIAL = enum.auto()
+    LOG_NORMAL_MIXTURE = enum.auto()
+
+
+class AttentionLayerType(StrEnum):
+    GLOBAL = enum.auto()
+    LOCAL = enum.auto()
+
+
+@dataclasses.dataclass
+class OptimizationConfig:
+    """AdamW + polynomial-decay-with-warmup settings (``config.py:209-311``)."""
+
+    init_lr: float = 1e-2
+    end_lr: float | None = None
+    end_lr_frac_of_init_lr: float | None = 1e-3
+    max_epochs: int = 100
+    batch_size: int = 32
+    validation_batch_size: int = 32
+    lr_frac_warmup_steps: float | None = 0.01
+    lr_num_warmup_steps: int | None = None
+    max_training_steps: int | None = None
+    lr_decay_power: float = 1.0
+    weight_decay: float = 0.01
+    patience: int | None = None
+    gradient_accumulation: int | None = None
+    num_dataloader_workers: int = 0
+
+    def __post_init__(self):
+        if self.end_lr_frac_of_init_lr is not None:
+            if not (0.0 < self.end_lr_frac_of_init_lr < 1.0):
+                raise ValueError("`end_lr_frac_of_init_lr` must be between 0.0 and 1.0!")
+            prod = self.end_lr_frac_of_init_lr * self.init_lr
+            if self.end_lr is not None and not math.isclose(self.end_lr, prod):
+                raise ValueError(
+                    "If both set, `end_lr` must be equal to `end_lr_frac_of_init_lr * init_lr`! Got "
+                    f"end_lr={self.end_lr}, end_lr_frac_of_init_lr * init_lr = {prod}!"
+                )
+            self.end_lr = prod
+        else:
+            if self.end_lr is None:
+                raise ValueError("Must set either end_lr or end_lr_frac_of_init_lr!")
+            self.end_lr_frac_of_init_lr = self.end_lr / self.init_lr
+
+    def set_to_dataset_size(self, n_subjects: int):
+        """``set_to_dataset`` (``config.py:265-311``) given only the number of training subjects."""
+        steps_per_epoch = int(math.ceil(n_subjects / self.batch_size))
+        if self.max_training_steps is None:
+            self.max_training_steps = steps_per_epoch * self.max_epochs
+        if self.lr_num_warmup_steps is None:
+            assert self.lr_frac_warmup_steps is not None
+            self.lr_num_warmup_steps = int(round(self.lr_frac_warmup_steps * self.max_training_steps))
+        elif self.lr_frac_warmup_steps is None:
+            self.lr_frac_warmup_steps = self.lr_num_warmup_steps / self.max_training_steps
+
+
+def _warn(msg: str):
+    print(f"WARNING: {msg}")
+
+
+class StructuredTransformerConfig(PretrainedConfig):
+    """Configuration of Event Stream GPT models (argument list of ``config.py:490-541``).
+
+    Derived fields reproduced: ``seq_attention_layers`` / ``dep_graph_attention_layers`` (via
+    ``expand_attention_types_params``), ``hidden_size``/``head_dim`` completion, ``vocab_size`` default
+    ``max(sum(vocab_sizes_by_measurement), 1)`` (overridable by kwarg, as the reference's tests do), and the
+    per-TTE-head parameter normalisation.
+    """
+
+    model_type = "esgpt_amd"
+
+    def __init__(
+        self,
+        vocab_sizes_by_measurement: dict[str, int] | None = None,
+        vocab_offsets_by_measurement: dict[str, int] | None = None,
+        measurement_configs: dict[str, Any] | None = None,
+        measurements_idxmap: dict[str, int] | None = None,
+        measurements_per_generative_mode: dict[str, list[str]] | None = None,
+        event_types_idxmap: dict[str, int] | None = None,
+        measurements_per_dep_graph_level: list[list[Any]] | None = None,
+        max_seq_len: int = 256,
+        do_split_embeddings: bool = False,
+        categorical_embedding_dim: int | None = None,
+        numerical_embedding_dim: int | None = None,
+        static_embedding_mode: StaticEmbeddingMode = StaticEmbeddingMode.SUM_ALL,
+        static_embedding_weight: float = 0.5,
+        dynamic_embedding_weight: float = 0.5,
+        categorical_embedding_weight: float = 0.5,
+        numerical_embedding_weight: float = 0.5,
+        do_normalize_by_measurement_index: bool = False,
+        structured_event_processing_mode: StructuredEventProcessingMode = (
+            StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT
+        ),
+        hidden_size: int | None = None,
+        head_dim: int | None = 64,
+        num_hidden_layers: int = 2,
+        num_attention_heads: int = 4,
+        seq_attention_types: Any = None,
+        seq_window_size: int = 32,
+        dep_graph_attention_types: Any = None,
+        dep_graph_window_size: int | None = 2,
+        intermediate_size: int = 32,
+        activation_function: str = "gelu",
+        attention_dropout: float = 0.1,
+        input_dropout: float = 0.1,
+        resid_dropout: float = 0.1,
+        init_std: float = 0.02,
+        layer_norm_epsilon: float = 1e-5,
+        do_full_block_in_dep_graph_attention: bool | None = True,
+        do_full_block_in_seq_attention: bool | None = False,
+        TTE_generation_layer_type: TimeToEventGenerationHeadType = "exponential",
+        TTE_lognormal_generation_num_components: int | None = None,
+        mean_log_inter_event_time_min: float | None = None,
+        std_log_inter_event_time_min: float | None = None,
+        use_cache: bool = True,
+        **kwargs,
+    ):
+        self.vocab_sizes_by_measurement = dict(vocab_sizes_by_measurement or {})
+        self.vocab_offsets_by_measurement = dict(vocab_offsets_by_measurement or {})
+        self.measurement_configs = dict(measurement_configs or {})
+        self.measurements_idxmap = dict(measurements_idxmap or {})
+        self.measurements_per_generative_mode = dict(measurements_per_generative_mode or {})
+        self.event_types_idxmap = dict(event_types_idxmap or {})
+
+        # ---- embeddings (config.py:575-600)
+        if do_split_embeddings:
+            for name, v in (("categorical_embedding_dim", categorical_embedding_dim),
+                            ("numerical_embedding_dim", numerical_embedding_dim)):
+                if not (type(v) is int and v > 0):
+                    raise ValueError(
+                        f"When do_split_embeddings={do_split_embeddings}, {name} must be a positive integer. "
+                        f"Got {v}."
+                    )
+        else:
+            if categorical_embedding_dim is not None:
+                _warn(f"categorical_embedding_dim is set to {categorical_embedding_dim} but "
+                      f"do_split_embeddings={do_split_embeddings}. Setting categorical_embedding_dim to None.")
+                categorical_embedding_dim = None
+            if numerical_embedding_dim is not None:
+                _warn(f"numerical_embedding_dim is set to {numerical_embedding_dim} but "
+                      f"do_split_embeddings={do_split_embeddings}. Setting numerical_embedding_dim to None.")
+                numerical_embedding_dim = None
+        self.do_split_embeddings = do_split_embeddings
+        self.categorical_embedding_dim = categorical_embedding_dim
+        self.numerical_embedding_dim = numerical_embedding_dim
+        self.static_embedding_mode = static_embedding_mode
+        self.static_embedding_weight = static_embedding_weight
+        self.dynamic_embedding_weight = dynamic_embedding_weight
+        self.categorical_embedding_weight = categorical_embedding_weight
+        self.numerical_embedding_weight = numerical_embedding_weight
+        self.do_normalize_by_measurement_index = do_normalize_by_measurement_index
+
+        # ---- structured processing mode (config.py:609-680)
+        mode = structured_event_processing_mode
+        if mode == StructuredEventProcessingMode.NESTED_ATTENTION:
+            missing = f"For a {mode} model, {{}} should not be None"
+            if do_full_block_in_seq_attention is None:
+                raise ValueError(missing.format("do_full_block_in_seq_attention"))
+            if do_full_block_in_dep_graph_attention is None:
+                raise ValueError(missing.format("do_full_block_in_dep_graph_attention"))
+            if measurements_per_dep_graph_level is None:
+                raise ValueError(missing.format("measurements_per_dep_graph_level"))
+            levels = []
+            for group in measurements_per_dep_graph_level:
+                out = []
+                for m in group:
+                    if isinstance(m, str):
+                        out.append(m)
+                    elif isinstance(m, (list, tuple)) and len(m) == 2 and isinstance(m[0], str):
+                        assert m[1] in MeasIndexGroupOptions.values()
+                        out.append((m[0], m[1]))
+                    else:
+                        raise ValueError(f"Invalid `measurements_per_dep_graph_level` entry {m}.")
+                levels.append(out)
+            measurements_per_dep_graph_level = levels
+        elif mode == StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT:
+            extra = f"For a {mode} model, {{}} is not used; got {{}}. Setting to None."
+            if measurements_per_dep_graph_level is not None:
+                _warn(extra.format("measurements_per_dep_graph_level", measurements_per_dep_graph_level))
+                measurements_per_dep_graph_level = None
+            if do_full_block_in_seq_attention is not None:
+                _warn(extra.format("do_full_block_in_seq_attention", do_full_block_in_seq_attention))
+                do_full_block_in_seq_attention = None
+            if do_full_block_in_dep_graph_attention is not None:
+                _warn(extra.format("do_full_block_in_dep_graph_attention", do_full_block_in_dep_graph_attention))
+                do_full_block_in_dep_graph_attention = None
+            if dep_graph_attention_types is not None:
+                _warn(extra.format("dep_graph_attention_types", dep_graph_attention_types))
+                dep_graph_attention_types = None
+            if dep_graph_window_size is not None:
+                _warn(extra.format("dep_graph_window_size", dep_graph_window_size))
+                dep_graph_window_size = None
+        else:
+            raise ValueError(
+                "`structured_event_processing_mode` must be a valid `StructuredEventProcessingMode` enum member "
+                f"({StructuredEventProcessingMode.values()}). Got {mode}."
+            )
+        self.structured_event_processing_mode = mode
+
+        # ---- sizes (config.py:682-701)
+        if head_dim is None and hidden_size is None:
+            raise ValueError("Must specify at least one of hidden size or head dim!")
+        if hidden_size is None:
+            hidden_size = head_dim * num_attention_heads
+        elif head_dim is None:
+            head_dim = hidden_size // num_attention_heads
+        if head_dim * num_attention_heads != hidden_size:
+            raise ValueError(
+                f"hidden_size must be divisible by num_attention_heads (got `hidden_size`: {hidden_size} "
+                f"and `num_attention_heads`: {num_attention_heads})."
+            )
+        if type(num_hidden_layers) is not int:
+            raise TypeError(f"num_hidden_layers must be an int! Got {type(num_hidden_layers)}.")
+        if num_hidden_layers <= 0:
+            raise ValueError(f"num_hidden_layers must be > 0! Got {num_hidden_layers}.")
+        self.num_hidden_layers = num_hidden_layers
+
+        # ---- attention layer types (config.py:703-742)
+        if seq_attention_types is None:
+            seq_attention_types = ["local", "global"]
+        self.seq_attention_types = seq_attention_types
+        self.seq_attention_layers = self.expand_attention_types_params(seq_attention_types)
+        if len(self.seq_attention_layers) != num_hidden_layers:
+            raise ValueError(
+                "Configuration for module is incorrect. It is required that `len(config.seq_attention_layers)` "
+                f"== `config.num_hidden_layers` but is `len(config.seq_attention_layers) = "
+                f"{len(self.seq_attention_layers)}`, `config.num_layers = {num_hidden_layers}`."
+            )
+        if mode != StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT:
+            if dep_graph_attention_types is None:
+                dep_graph_attention_types = "global"
+            dep_layers = self.expand_attention_types_params(dep_graph_attention_types)
+            if len(dep_layers) != num_hidden_layers:
+                raise ValueError(
+                    "Configuration for module is incorrect. It is required that "
+                    "`len(config.dep_graph_attention_layers)` == `config.num_hidden_layers` but is "
+                    f"`len(config.dep_graph_attention_layers) = {len(dep_layers)}`, "
+                    f"`config.num_layers = {num_hidden_layers}`."
+                )
+        else:
+            dep_layers = None
+        self.dep_graph_attention_types = dep_graph_attention_types
+        self.dep_graph_attention_layers = dep_layers
+        self.seq_window_size = seq_window_size
+        self.dep_graph_window_size = dep_graph_window_size
+
+        # ---- TTE head (config.py:744-795)
+        tte = TTE_generation_layer_type
+        if tte == TimeToEventGenerationHeadType.LOG_NORMAL_MIXTURE:
+            missing = f"For a {tte} model, {{}} should not be None"
+            if TTE_lognormal_generation_num_components is None:
+                raise ValueError(missing.format("TTE_lognormal_generation_num_components"))
+            if type(TTE_lognormal_generation_num_components) is not int:
+                raise TypeError(
+                    "`TTE_lognormal_generation_num_components` must be an int! "
+                    f"Got: {type(TTE_lognormal_generation_num_components)}."
+                )
+            if TTE_lognormal_generation_num_components <= 0:
+                raise ValueError(
+                    "`TTE_lognormal_generation_num_components` should be >0 "
+                    f"got {TTE_lognormal_generation_num_components}."
+                )
+            if mean_log_inter_event_time_min is None:
+                mean_log_inter_event_time_min = 0.0
+            if std_log_inter_event_time_min is None:
+                std_log_inter_event_time_min = 1.0
+        elif tte == TimeToEventGenerationHeadType.EXPONENTIAL:
+            extra = f"For a {tte} model, {{}} is not used; got {{}}. Setting to None."
+            if TTE_lognormal_generation_num_components is not None:
+                _warn(extra.format("TTE_lognormal_generation_num_components", TTE_lognormal_generation_num_components))
+                TTE_lognormal_generation_num_components = None
+            if mean_log_inter_event_time_min is not None:
+                _warn(extra.format("mean_log_inter_event_time_min", mean_log_inter_event_time_min))
+                mean_log_inter_event_time_min = None
+            if std_log_inter_event_time_min is not None:
+                _warn(extra.format("std_log_inter_event_time_min", std_log_inter_event_time_min))
+                std_log_inter_event_time_min = None
+        else:
+            raise ValueError(
+                "Invalid option for `TTE_generation_layer_type`. Must be in "
+                f"({TimeToEventGenerationHeadType.values()}). Got {tte}."
+            )
+        self.TTE_generation_layer_type = tte
+        self.TTE_lognormal_generation_num_components = TTE_lognormal_generation_num_components
+        self.mean_log_inter_event_time_min = mean_log_inter_event_time_min
+        self.std_log_inter_event_time_min = std_log_inter_event_time_min
+
+        self.init_std = init_std
+        self.max_seq_len = max_seq_len
+        self.measurements_per_dep_graph_level = measurements_per_dep_graph_level
+        # The reference sets this before calling PretrainedConfig.__init__, so an explicit `vocab_size=` kwarg
+        # (as its tests pass) wins (config.py:793).
+        self.vocab_size = max(sum(self.vocab_sizes_by_measurement.values()), 1)
+        self.head_dim = head_dim
+        self.hidden_size = hidden_size
+        self.num_attention_heads = num_attention_heads
+        self.attention_dropout = attention_dropout
+        self.input_dropout = input_dropout
+        self.resid_dropout = resid_dropout
+        self.intermediate_size = intermediate_size
+        self.layer_norm_epsilon = layer_norm_epsilon
+        self.activation_function = activation_function
+        self.do_full_block_in_seq_attention = do_full_block_in_seq_attention
+        self.do_full_block_in_dep_graph_attention = do_full_block_in_dep_graph_attention
+        self.use_cache = use_cache
+
+        assert not kwargs.get("is_encoder_decoder", False), "Can't be used in encoder/decoder mode!"
+        kwargs["is_encoder_decoder"] = False
+        super().__init__(**kwargs)
+
+    def measurements_for(self, modality: DataModality) -> list[str]:
+        return self.measurements_per_generative_mode.get(modality, [])
+
+    def expand_attention_types_params(self, attention_types) -> list[str]:
+        """``"global"`` → all layers; ``["global","local"]`` → alternate; ``[(types, n), …]`` → repeated runs."""
+        n = self.num_hidden_layers
+        if isinstance(attention_types, str):
+            return [attention_types] * n
+        if not isinstance(attention_types, list):
+            raise TypeError(f"Config Invalid {attention_types} ({type(attention_types)}) is wrong type!")
+        if isinstance(attention_types[0], str):
+            return (attention_types * n)[:n]
+        if isinstance(attention_types[0], (list, tuple)):
+            out = []
+            for sub, reps in attention_types:
+                out.extend(list(sub) * reps)
+            return out[:n]
+        raise TypeError(f"Config Invalid {attention_types} El 0 ({type(attention_types[0])}) is wrong type!")
+
+    def set_to_vocabulary(self, vocabulary_config: dict, max_seq_len: int | None = None,
+                          mean_log_inter_event_time_min: float | None = None,
+                          std_log_inter_event_time_min: float | None = None):
+        """The vocabulary part of ``set_to_dataset`` (``config.py:839-899``) from a ``vocabulary_config.json``
+        dict (the file the reference's ETL writes next to ``DL_reps``)."""
+        self.measurements_idxmap = dict(vocabulary_config["measurements_idxmap"])
+        mpg = dict(vocabulary_config["measurements_per_generative_mode"])
+        for k in DataModality.values():
+            mpg.setdefault(k, [])
+        self.measurements_per_generative_mode = mpg
+        self.event_types_idxmap = dict(vocabulary_config.get("event_types_idxmap", {}))
+        offsets = dict(vocabulary_config["vocab_offsets_by_measurement"])
+        sizes = dict(vocabulary_config["vocab_sizes_by_measurement"])
+        # VocabularyConfig.total_vocab_size (data/config.py:583-604), computed before size-1 fill-in.
+        total = sum(sizes.values()) + min(offsets.values()) + (len(offsets) - len(sizes))
+        for k in set(offsets) - set(sizes):
+            sizes[k] = 1
+        self.vocab_offsets_by_measurement = offsets
+        self.vocab_sizes_by_measurement = sizes
+        self.vocab_size = total
+        if max_seq_len is not None:
+            self.max_seq_len = max_seq_len
+        if self.TTE_generation_layer_type == TimeToEventGenerationHeadType.LOG_NORMAL_MIXTURE:
+            if mean_log_inter_event_time_min is not None:
+                self.mean_log_inter_event_time_min = mean_log_inter_event_time_min
+            if std_log_inter_event_time_min is not None:
+                self.std_log_inter_event_time_min = std_log_inter_event_time_min
+
+    def __eq__(self, other):
+        if not isinstance(other, PretrainedConfig):
+            return False
+        return PretrainedConfig.__eq__(self, other)
