@@ -1,0 +1,127 @@
+"""ctypes binding of the C ABI in ``include/esgpt_amd.h`` (libesgpt_amd.so, built in-tree for gfx950).
+
+This is the exact binding a maintainer would add on the reference side. The library is
+loaded after ``torch`` so that it shares torch's HIP runtime (both link ``libamdhip64.so.7``; the dynamic loader
+reuses the already-loaded copy), which makes torch's streams and allocations valid handles for the kernels.
+
+There is NO fallback: if the library is missing or no gfx950 device is visible, every product op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ESGPT_AMD_LIB", os.path.join(_HERE, "libesgpt_amd.so"))
+
+ESGPT_OK, ESGPT_ERR_INVALID_ARG, ESGPT_ERR_LAUNCH, ESGPT_ERR_UNSUPPORTED = 0, 1, 2, 3
+F32, BF16 = 0, 1
+FLAG_BAD_INDEX, FLAG_TTE_NAN, FLAG_TTE_NO_OBS, FLAG_BAD_LABEL = 1, 2, 4, 8
+EMB_NORMALIZE, EMB_STATIC, EMB_TIME, EMB_CUMSUM, EMB_TIME_ABS = 1, 2, 4, 8, 16
+BAG_JOINT, BAG_CAT, BAG_NUM = 0, 1, 2
+TERM_SINGLE, TERM_MULTI, TERM_MVREG, TERM_UVREG = 1, 2, 3, 4
+TTE_EXP, TTE_LNM = 1, 2
+MAX_TERMS = 16
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_int = ctypes.c_int
+_sz = ctypes.c_size_t
+
+
+class EsgptBatch(ctypes.Structure):
+    _fields_ = [
+        ("dyn_idx", _vp), ("dyn_meas", _vp), ("dyn_vals", _vp), ("dyn_vmask", _vp), ("event_mask", _vp),
+        ("time_delta", _vp), ("time_abs", _vp), ("st_idx", _vp), ("st_meas", _vp),
+        ("B", _i64), ("L", _i64), ("M", _i64), ("S", _i64),
+    ]
+
+
+class EsgptBuckets(ctypes.Structure):
+    _fields_ = [("G", _i64), ("cat_bits", ctypes.c_uint64 * 8), ("num_bits", ctypes.c_uint64 * 8)]
+
+
+class EsgptLossTerm(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("meas_idx", ctypes.c_int32), ("vocab_start", ctypes.c_int32),
+                ("vocab_end", ctypes.c_int32), ("col", ctypes.c_int32), ("obs_col", ctypes.c_int32),
+                ("level", ctypes.c_int32), ("pad", ctypes.c_int32)]
+
+
+class EsgptTTESpec(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("K", ctypes.c_int32), ("col", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("mean_log", _f32), ("std_log", _f32)]
+
+
+_PB = ctypes.POINTER(EsgptBatch)
+_PK = ctypes.POINTER(EsgptBuckets)
+
+SIGNATURES = {
+    "esgpt_version": (ctypes.c_char_p, []),
+    "esgpt_device_arch_ok": (_int, []),
+    "esgpt_embed_joint_fwd": (_int, [_PB, _PK, _vp, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),
+    "esgpt_embed_split_bags_fwd": (_int, [_PB, _PK, _vp, _i64, _vp, _i64, _i64, _int, _f32, _f32, _f32, _vp, _vp,
+                                          _vp]),
+    "esgpt_embed_epilogue_fwd": (_int, [_PB, _i64, _i64, _vp, _vp, _vp, _int, _vp, _vp]),
+    "esgpt_embed_epilogue_bwd": (_int, [_PB, _i64, _i64, _vp, _int, _vp, _vp]),
+    "esgpt_embed_bag_bwd_workspace": (_sz, [_PB, _i64, _i64, _i64]),
+    "esgpt_embed_bag_bwd": (_int, [_PB, _PK, _int, _int, _f32, _f32, _vp, _i64, _i64, _i64, _vp, _vp, _sz, _vp]),
+    "esgpt_attn_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                              _i64, _int, _vp]),
+    "esgpt_attn_bwd_workspace": (_sz, [_i64, _i64, _i64]),
+    "esgpt_attn_bwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                              _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp, _sz, _vp]),
+    "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),
+    "esgpt_output_loss": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
+                                 _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+}
+
+_lib = None
+
+
+class HipExtensionMissing(RuntimeError):
+    pass
+
+
+def load(require_device: bool = True):
+    """Returns the loaded library; raises loudly if it (or, with ``require_device``, a GPU) is unavailable."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipExtensionMissing(
+                f"eventstreamgpt_amd: HIP library not found at {LIB_PATH}. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C eventstreamgpt_amd/csrc`)."
+            )
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_device and not torch.cuda.is_available():
+        raise HipExtensionMissing("eventstreamgpt_amd: no HIP device visible; the product path has no CPU fallback.")
+    return _lib
+
+
+def check(status: int, what: str):
+    if status != ESGPT_OK:
+        names = {1: "invalid argument", 2: "launch failure", 3: "unsupported configuration"}
+        raise RuntimeError(f"eventstreamgpt_amd: {what} failed: {names.get(status, status)}")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError(f"eventstreamgpt_amd: unsupported activation dtype {dt}")

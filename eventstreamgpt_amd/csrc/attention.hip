@@ -1,0 +1,310 @@
+// Causal / local-window attention for gfx950 (InnerSelfAttention._attn, transformer.py:171-217).
+//
+// Two implementations behind one entry point:
+//   * attn_*_generic  — one lane per query (forward, dQ) or per key (dK/dV), f32 arithmetic, any head dim up to
+//     128, f32 or bf16 I/O. Lanes of a wave hold consecutive queries of one (batch, head), so every K/V (or Q/dO)
+//     row load in the key loop is wave-uniform (a broadcast). Used for the f32 parity mode and for the short
+//     dependency-graph sequences of the NA model (Lk = G + 1 <= 9), where a flash tile would be mostly padding.
+//   * attn_*_mfma (attention_mfma.hip) — bf16 v_mfma_f32_32x32x16_bf16 flash kernels for hd in {32, 64, 128}.
+//
+// Semantics (both): s_ij = q_i . k_j in f32 with NO 1/sqrt(hd) scaling; key j is visible to query i (at key
+// position p_i = i + Lk - Lq) iff j <= p_i, (local) p_i - j < window, and key_mask[j]; softmax in f32;
+// rows of padded queries (query_mask[i] == 0) are zeros and carry no gradient.
+#include "common.h"
+
+using namespace esgpt;
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ void load_row(const T* __restrict__ p, int hd, float* __restrict__ r, int HDP) {
+  for (int d = 0; d < HDP; ++d) r[d] = (d < hd) ? to_f32(p[d]) : 0.f;
+}
+
+template <typename T, int HDP>
+__global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ q, const T* __restrict__ k,
+                                                        const T* __restrict__ v, int64_t ld_in, int64_t tq,
+                                                        T* __restrict__ o, int64_t ld_o, float* __restrict__ lse,
+                                                        const uint8_t* __restrict__ kmask,
+                                                        const uint8_t* __restrict__ qmask, int64_t B, int64_t H,
+                                                        int64_t Lq, int64_t Lk, int hd, int64_t window) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = B * H * Lq;
+  if (tid >= total) return;
+  const int64_t qi = tid % Lq;
+  const int64_t bh = tid / Lq;
+  const int64_t h = bh % H, b = bh / H;
+  const int64_t pos = qi + (Lk - Lq);
+  const bool qvalid = qmask ? (qmask[b * Lq + qi] != 0) : true;
+
+  float qr[HDP], acc[HDP];
+  const T* qp = q + (b * tq + qi) * ld_in + h * hd;
+#pragma unroll
+  for (int d = 0; d < HDP; ++d) {
+    qr[d] = (d < hd) ? to_f32(qp[d]) : 0.f;
+    acc[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+  if (qvalid) {
+    for (int64_t j = jlo; j <= pos; ++j) {
+      if (kmask && !kmask[b * Lk + j]) continue;
+      const T* kp = k + (b * Lk + j) * ld_in + h * hd;
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < HDP; ++d)
+        if (d < hd) s = fmaf(qr[d], to_f32(kp[d]), s);
+      float p;
+      if (s > m) {
+        const float c = expf(m - s);  // m = -inf on the first key -> c = 0
+        l *= c;
+#pragma unroll
+        for (int d = 0; d < HDP; ++d) acc[d] *= c;
+        m = s;
+        p = 1.f;
+      } else {
+        p = expf(s - m);
+      }
+      l += p;
+      const T* vp = v + (b * Lk + j) * ld_in + h * hd;
+#pragma unroll
+      for (int d = 0; d < HDP; ++d)
+        if (d < hd) acc[d] = fmaf(p, to_f32(vp[d]), acc[d]);
+    }
+  }
+  const bool ok = qvalid && l > 0.f;
+  const float inv = ok ? 1.f / l : 0.f;
+  T* op = o + (b * Lq + qi) * ld_o + h * hd;
+#pragma unroll
+  for (int d = 0; d < HDP; ++d)
+    if (d < hd) op[d] = from_f32<T>(acc[d] * inv);
+  lse[bh * Lq + qi] = ok ? m + logf(l) : 0.f;
+}
+
+// dQ (and delta = rowsum(dO * O)) — one lane per query.
+template <typename T, int HDP>
+__global__ __launch_bounds__(256) void attn_bwd_dq_generic(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
+    const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
+    const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, int64_t ld_d,
+    float* __restrict__ delta, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = B * H * Lq;
+  if (tid >= total) return;
+  const int64_t qi = tid % Lq;
+  const int64_t bh = tid / Lq;
+  const int64_t h = bh % H, b = bh / H;
+  const int64_t pos = qi + (Lk - Lq);
+  const bool qvalid = qmask ? (qmask[b * Lq + qi] != 0) : true;
+  float qr[HDP], dor[HDP], acc[HDP];
+  const T* qp = q + (b * tq + qi) * ld_in + h * hd;
+  const T* dp_ = dout + (b * Lq + qi) * ld_do + h * hd;
+  const T* op = o + (b * Lq + qi) * ld_o + h * hd;
+  float dl = 0.f;
+#pragma unroll
+  for (int d = 0; d < HDP; ++d) {
+    qr[d] = (d < hd) ? to_f32(qp[d]) : 0.f;
+    dor[d] = (d < hd) ? to_f32(dp_[d]) : 0.f;
+    if (d < hd) dl = fmaf(dor[d], to_f32(op[d]), dl);
+    acc[d] = 0.f;
+  }
+  if (!qvalid) dl = 0.f;
+  delta[bh * Lq + qi] = dl;
+  const float ls = lse[bh * Lq + qi];
+  const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+  if (qvalid) {
+    for (int64_t j = jlo; j <= pos; ++j) {
+      if (kmask && !kmask[b * Lk + j]) continue;
+      const T* kp = k + (b * Lk + j) * ld_in + h * hd;
+      const T* vp = v + (b * Lk + j) * ld_in + h * hd;
+      float s = 0.f, dpv = 0.f;
+#pragma unroll
+      for (int d = 0; d < HDP; ++d) {
+        if (d < hd) {
+          s = fmaf(qr[d], to_f32(kp[d]), s);
+          dpv = fmaf(dor[d], to_f32(vp[d]), dpv);
+        }
+      }
+      const float p = expf(s - ls);
+      const float ds = p * (dpv - dl);
+#pragma unroll
+      for (int d = 0; d < HDP; ++d)
+        if (d < hd) acc[d] = fmaf(ds, to_f32(kp[d]), acc[d]);
+    }
+  }
+  T* dqp = dq + (b * tq + qi) * ld_d + h * hd;
+#pragma unroll
+  for (int d = 0; d < HDP; ++d)
+    if (d < hd) dqp[d] = from_f32<T>(acc[d]);
+}
+
+// dK, dV — one lane per key; loops over the queries that can see it.
+template <typename T, int HDP>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_generic(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
+    const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse, const float* __restrict__ delta,
+    const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dk, T* __restrict__ dv,
+    int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = B * H * Lk;
+  if (tid >= total) return;
+  const int64_t kj = tid % Lk;
+  const int64_t bh = tid / Lk;
+  const int64_t h = bh % H, b = bh / H;
+  const bool kvalid = kmask ? (kmask[b * Lk + kj] != 0) : true;
+  float kr[HDP], vr[HDP], dka[HDP], dva[HDP];
+  const T* kp = k + (b * Lk + kj) * ld_in + h * hd;
+  const T* vp = v + (b * Lk + kj) * ld_in + h * hd;
+#pragma unroll
+  for (int d = 0; d < HDP; ++d) {
+    kr[d] = (d < hd) ? to_f32(kp[d]) : 0.f;
+    vr[d] = (d < hd) ? to_f32(vp[d]) : 0.f;
+    dka[d] = 0.f;
+    dva[d] = 0.f;
+  }
+  const int64_t off = Lk - Lq;
+  // queries i with p_i = i + off in [kj, kj + window - 1] (local) or [kj, Lk-1] (global)
+  const int64_t ilo = max((int64_t)0, kj - off);
+  const int64_t ihi = (window > 0) ? min(Lq - 1, kj + window - 1 - off) : Lq - 1;
+  if (kvalid) {
+    for (int64_t i = ilo; i <= ihi; ++i) {
+      if (qmask && !qmask[b * Lq + i]) continue;
+      const T* qp = q + (b * tq + i) * ld_in + h * hd;
+      const T* dop = dout + (b * Lq + i) * ld_do + h * hd;
+      float s = 0.f, dpv = 0.f;
+#pragma unroll
+      for (int d = 0; d < HDP; ++d) {
+        if (d < hd) {
+          s = fmaf(to_f32(qp[d]), kr[d], s);
+          dpv = fmaf(to_f32(dop[d]), vr[d], dpv);
+        }
+      }
+      const float p = expf(s - lse[bh * Lq + i]);
+      const float ds = p * (dpv - delta[bh * Lq + i]);
+#pragma unroll
+      for (int d = 0; d < HDP; ++d) {
+        if (d < hd) {
+          dva[d] = fmaf(p, to_f32(dop[d]), dva[d]);
+          dka[d] = fmaf(ds, to_f32(qp[d]), dka[d]);
+        }
+      }
+    }
+  }
+  T* dkp = dk + (b * Lk + kj) * ld_d + h * hd;
+  T* dvp = dv + (b * Lk + kj) * ld_d + h * hd;
+#pragma unroll
+  for (int d = 0; d < HDP; ++d) {
+    if (d < hd) {
+      dkp[d] = from_f32<T>(dka[d]);
+      dvp[d] = from_f32<T>(dva[d]);
+    }
+  }
+}
+
+template <typename T>
+int launch_fwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o, float* lse,
+                       const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                       int64_t hd, int64_t window, hipStream_t st) {
+  const int64_t total = B * H * Lq;
+  dim3 grid((unsigned)cdiv(total, 256)), block(256);
+#define FWD(HDP)                                                                                                \
+  attn_fwd_generic<T, HDP><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (T*)o, ld_o, lse, \
+                                                   kmask, qmask, B, H, Lq, Lk, (int)hd, window)
+  if (hd <= 8) FWD(8);
+  else if (hd <= 16) FWD(16);
+  else if (hd <= 32) FWD(32);
+  else if (hd <= 64) FWD(64);
+  else FWD(128);
+#undef FWD
+  return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+}
+
+template <typename T>
+int launch_bwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
+                       const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask,
+                       void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                       int64_t hd, int64_t window, float* delta, hipStream_t st) {
+  dim3 gq((unsigned)cdiv(B * H * Lq, 256)), gk((unsigned)cdiv(B * H * Lk, 256)), block(256);
+#define BWD(HDP)                                                                                                   \
+  do {                                                                                                             \
+    attn_bwd_dq_generic<T, HDP><<<gq, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o,   \
+                                                      ld_o, (const T*)dout, ld_do, lse, kmask, qmask, (T*)dq, ld_d, \
+                                                      delta, B, H, Lq, Lk, (int)hd, window);                       \
+    attn_bwd_dkv_generic<T, HDP><<<gk, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq,          \
+                                                       (const T*)dout, ld_do, lse, delta, kmask, qmask, (T*)dk,     \
+                                                       (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window);               \
+  } while (0)
+  if (hd <= 8) BWD(8);
+  else if (hd <= 16) BWD(16);
+  else if (hd <= 32) BWD(32);
+  else if (hd <= 64) BWD(64);
+  else BWD(128);
+#undef BWD
+  return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+}
+
+}  // namespace
+
+// MFMA path (attention_mfma.hip).
+int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o, float* lse,
+                        const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                        int64_t hd, int64_t window, hipStream_t st);
+int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
+                        const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask,
+                        void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                        int64_t hd, int64_t window, float* delta, hipStream_t st);
+bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o);
+
+static int g_force_generic = -1;
+
+static bool force_generic() {
+  if (g_force_generic < 0) {
+    const char* e = getenv("ESGPT_ATTN_GENERIC");
+    g_force_generic = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_force_generic == 1;
+}
+
+extern "C" {
+
+int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
+                   float* lse,
+                   const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                   int64_t hd, int64_t window, int dtype, void* stream) {
+  ESGPT_REQUIRE(q && k && v && o && lse && hd > 0 && hd <= 128 && Lq <= Lk && Lq >= 0 && window >= 0 && tq >= Lq);
+  ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  if (B * H * Lq == 0) return ESGPT_OK;
+  hipStream_t st = as_stream(stream);
+  if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
+    return esgpt_attn_fwd_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window, st);
+  if (dtype == ESGPT_F32)
+    return launch_fwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
+                                     st);
+  return launch_fwd_generic<bf16>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window, st);
+}
+
+size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq) { return sizeof(float) * (size_t)(B * H * Lq); }
+
+int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                   int64_t ld_o,
+                   const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                   const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
+                   int64_t Lq, int64_t Lk, int64_t hd, int64_t window, int dtype, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  ESGPT_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv && hd > 0 && hd <= 128 && Lq <= Lk);
+  ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  ESGPT_REQUIRE(workspace && workspace_bytes >= esgpt_attn_bwd_workspace(B, H, Lq));
+  if (B * H * Lk == 0) return ESGPT_OK;
+  hipStream_t st = as_stream(stream);
+  float* delta = (float*)workspace;
+  if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
+    return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv, ld_dqkv, B,
+                               H, Lq, Lk, hd, window, delta, st);
+  if (dtype == ESGPT_F32)
+    return launch_bwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
+                                     ld_dqkv, B, H, Lq, Lk, hd, window, delta, st);
+  return launch_bwd_generic<bf16>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
+                                  ld_dqkv, B, H, Lq, Lk, hd, window, delta, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,329 @@
+"""Autograd wrappers around the C ABI (the PyTorch-ROCm custom-op layer).
+
+Each ``torch.autograd.Function`` launches the gfx950 kernels on torch's current HIP stream with raw device
+pointers; outputs and workspaces are allocated by torch (the library allocates nothing). Nothing here falls back
+to a CPU / ATen implementation: a missing library or a non-CUDA tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+from .data.types import PytorchBatch
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Batch view + device error word
+# ----------------------------------------------------------------------------------------------------------------
+class BatchView:
+    """Device-resident, kernel-ready view of a ``PytorchBatch`` (contiguous tensors of the ABI's dtypes)."""
+
+    def __init__(self, batch: PytorchBatch):
+        dev = batch.event_mask.device
+        if dev.type != "cuda":
+            raise L.HipExtensionMissing("eventstreamgpt_amd kernels need the batch on a HIP device (no CPU path).")
+
+        def c(t, dt):
+            return None if t is None else t.to(dtype=dt).contiguous()
+
+        self.event_mask = c(batch.event_mask, torch.bool)
+        self.time_delta = c(batch.time_delta, torch.float32)
+        self.time = c(batch.time, torch.float32)
+        self.dyn_idx = c(batch.dynamic_indices, torch.int64)
+        self.dyn_meas = c(batch.dynamic_measurement_indices, torch.int64)
+        self.dyn_vals = c(batch.dynamic_values, torch.float32)
+        self.dyn_vmask = c(batch.dynamic_values_mask, torch.bool)
+        self.st_idx = c(batch.static_indices, torch.int64)
+        self.st_meas = c(batch.static_measurement_indices, torch.int64)
+        B, Lq, M = self.dyn_idx.shape
+        S = 0 if self.st_idx is None else self.st_idx.shape[1]
+        self.B, self.L, self.M, self.S = B, Lq, M, S
+        self.struct = L.EsgptBatch(
+            L.ptr(self.dyn_idx), L.ptr(self.dyn_meas), L.ptr(self.dyn_vals), L.ptr(self.dyn_vmask),
+            L.ptr(self.event_mask), L.ptr(self.time_delta), L.ptr(self.time), L.ptr(self.st_idx),
+            L.ptr(self.st_meas), B, Lq, M, S,
+        )
+        self.ref = ctypes.byref(self.struct)
+
+
+def batch_view(batch: PytorchBatch) -> BatchView:
+    """Builds (and caches on the batch object) the kernel view. The cache is keyed on the tensor storages."""
+    key = (batch.event_mask.data_ptr(), batch.dynamic_indices.data_ptr(),
+           None if batch.time is None else batch.time.data_ptr())
+    v = getattr(batch, "_esgpt_view", None)
+    if v is None or v[0] != key:
+        v = (key, BatchView(batch))
+        object.__setattr__(batch, "_esgpt_view", v)
+    return v[1]
+
+
+_ERR: dict[int, torch.Tensor] = {}
+
+
+def err_word(device: torch.device) -> torch.Tensor:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    w = _ERR.get(idx)
+    if w is None:
+        w = torch.zeros(1, dtype=torch.int32, device=device)
+        _ERR[idx] = w
+    return w
+
+
+def check_errors(device: torch.device | None = None, n_total_embeddings: int | None = None):
+    """Reads (one host sync) and clears the device error word; raises the reference's exception for it."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    w = err_word(device)
+    code = int(w.item())
+    if code:
+        w.zero_()
+        if code & L.FLAG_BAD_INDEX:
+            raise AssertionError(f"Invalid embedding! index >= {n_total_embeddings}")
+        if code & L.FLAG_TTE_NO_OBS:
+            raise ValueError("No observed time-to-event for >= 1 patient in batch")
+        if code & L.FLAG_TTE_NAN:
+            raise ValueError("NaNs in TTE_LL")
+        if code & L.FLAG_BAD_LABEL:
+            raise IndexError("Target out of bounds in classification / regression labels")
+
+
+def buckets_struct(groups: list[list] | None):
+    """``split_by_measurement_indices`` → ``esgpt_buckets`` (None for the un-bucketed layer)."""
+    if groups is None:
+        return None
+    if len(groups) > 8:
+        raise ValueError("eventstreamgpt_amd supports at most 8 dependency-graph levels")
+    s = L.EsgptBuckets()
+    s.G = len(groups)
+    for g, group in enumerate(groups):
+        cb = nb = 0
+        for entry in group:
+            if isinstance(entry, (tuple, list)):
+                mi, mode = entry
+            else:
+                mi, mode = entry, "categorical_and_numerical"
+            mode = str(mode)
+            if not 0 <= mi < 64:
+                raise ValueError("eventstreamgpt_amd supports measurement indices < 64 in dependency-graph buckets")
+            if mode in ("categorical_and_numerical", "categorical_only"):
+                cb |= 1 << mi
+            if mode in ("categorical_and_numerical", "numerical_only"):
+                nb |= 1 << mi
+            if mode not in ("categorical_and_numerical", "categorical_only", "numerical_only"):
+                raise ValueError(f"Invalid group mode: {mode}")
+        s.cat_bits[g] = cb
+        s.num_bits[g] = nb
+    return s
+
+
+def _bref(bk):
+    return None if bk is None else ctypes.byref(bk)
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Embedding
+# ----------------------------------------------------------------------------------------------------------------
+@dataclass
+class EmbedSpec:
+    flags: int
+    static_w: float
+    dynamic_w: float
+    groups: object  # EsgptBuckets or None
+    G: int
+
+
+def _bag_bwd(bv, spec_groups, selector, flags, dyn_scale, static_scale, dsrc, ld, D, V, G):
+    lib = L.load()
+    dtable = torch.empty(V, D, dtype=torch.float32, device=dsrc.device)
+    nbytes = lib.esgpt_embed_bag_bwd_workspace(bv.ref, G, V, D)
+    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=dsrc.device)
+    L.check(lib.esgpt_embed_bag_bwd(bv.ref, _bref(spec_groups), selector, flags, dyn_scale, static_scale,
+                                    dsrc.data_ptr(), ld, D, V, dtable.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
+            "embed_bag_bwd")
+    return dtable
+
+
+def _epilogue_bwd(bv, G, D, dout, flags):
+    lib = L.load()
+    dy = torch.empty_like(dout)
+    L.check(lib.esgpt_embed_epilogue_bwd(bv.ref, G, D, dout.data_ptr(), flags, dy.data_ptr(), L.stream()),
+            "embed_epilogue_bwd")
+    return dy
+
+
+class JointEmbedFn(torch.autograd.Function):
+    """JOINT DataEmbeddingLayer (+ optional time encoding / NA cumsum) → f32 [B, L, G, D]."""
+
+    @staticmethod
+    def forward(ctx, table, bv: BatchView, spec: EmbedSpec, sin_div, cos_div):
+        lib = L.load()
+        V, D = table.shape
+        table = table.contiguous().float()
+        out = torch.empty(bv.B, bv.L, spec.G, D, dtype=torch.float32, device=table.device)
+        L.check(lib.esgpt_embed_joint_fwd(bv.ref, _bref(spec.groups), table.data_ptr(), V, D, L.ptr(sin_div),
+                                          L.ptr(cos_div), spec.flags, spec.static_w, spec.dynamic_w, out.data_ptr(),
+                                          err_word(table.device).data_ptr(), L.stream()), "embed_joint_fwd")
+        ctx.bv, ctx.spec, ctx.V, ctx.D = bv, spec, V, D
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        bv, spec, V, D = ctx.bv, ctx.spec, ctx.V, ctx.D
+        dout = dout.contiguous().float()
+        if spec.flags & L.EMB_CUMSUM:
+            dsrc = _epilogue_bwd(bv, spec.G, D, dout, spec.flags)
+        else:
+            dsrc = dout
+        static = bool(spec.flags & L.EMB_STATIC) and bv.S > 0
+        dyn_scale = spec.dynamic_w if static else 1.0
+        dtable = _bag_bwd(bv, spec.groups, L.BAG_JOINT, spec.flags, dyn_scale, spec.static_w, dsrc, D, D, V, spec.G)
+        return dtable, None, None, None, None
+
+
+class SplitBagsFn(torch.autograd.Function):
+    """SPLIT mode pre-projection bags: X [B*L*G, Dc+Dn] = [cat_scale*bag_c + static_scale*static_c, num_scale*bag_n]."""
+
+    @staticmethod
+    def forward(ctx, cat_table, num_table, bv: BatchView, spec: EmbedSpec, cat_scale, num_scale, static_scale):
+        lib = L.load()
+        V, Dc = cat_table.shape
+        Dn = num_table.shape[1]
+        cat_table = cat_table.contiguous().float()
+        num_table = num_table.contiguous().float()
+        x = torch.empty(bv.B * bv.L * spec.G, Dc + Dn, dtype=torch.float32, device=cat_table.device)
+        L.check(lib.esgpt_embed_split_bags_fwd(bv.ref, _bref(spec.groups), cat_table.data_ptr(), Dc,
+                                               num_table.data_ptr(), Dn, V, spec.flags, cat_scale, num_scale,
+                                               static_scale, x.data_ptr(), err_word(x.device).data_ptr(),
+                                               L.stream()), "embed_split_bags_fwd")
+        ctx.bv, ctx.spec, ctx.V, ctx.Dc, ctx.Dn = bv, spec, V, Dc, Dn
+        ctx.scales = (cat_scale, num_scale, static_scale)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        bv, spec, V, Dc, Dn = ctx.bv, ctx.spec, ctx.V, ctx.Dc, ctx.Dn
+        cat_scale, num_scale, static_scale = ctx.scales
+        dx = dx.contiguous().float()
+        flags = spec.flags
+        if static_scale == 0.0:
+            flags &= ~L.EMB_STATIC
+        dcat = _bag_bwd(bv, spec.groups, L.BAG_CAT, flags, cat_scale, static_scale, dx, Dc + Dn, Dc, V, spec.G)
+        dnum = _bag_bwd(bv, spec.groups, L.BAG_NUM, flags, num_scale, 0.0, dx[:, Dc:], Dc + Dn, Dn, V, spec.G)
+        return dcat, dnum, None, None, None, None, None
+
+
+class EmbedEpilogueFn(torch.autograd.Function):
+    """out[e,g] = mask_e * cumsum_g(y + time@g0) (flags select time / cumsum)."""
+
+    @staticmethod
+    def forward(ctx, y, bv: BatchView, G, flags, sin_div, cos_div):
+        lib = L.load()
+        D = y.shape[-1]
+        y = y.contiguous().float()
+        out = torch.empty(bv.B, bv.L, G, D, dtype=torch.float32, device=y.device)
+        L.check(lib.esgpt_embed_epilogue_fwd(bv.ref, G, D, y.data_ptr(), L.ptr(sin_div), L.ptr(cos_div), flags,
+                                             out.data_ptr(), L.stream()), "embed_epilogue_fwd")
+        ctx.bv, ctx.G, ctx.D, ctx.flags = bv, G, D, flags
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dy = _epilogue_bwd(ctx.bv, ctx.G, ctx.D, dout.contiguous().float(), ctx.flags)
+        return dy.view(-1, ctx.D), None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Attention
+# ----------------------------------------------------------------------------------------------------------------
+class AttentionFn(torch.autograd.Function):
+    """Packed-QKV causal/local attention. qkv: [Bs, T, 3D] (q | k | v), returns o: [Bs, T - skf, D]."""
+
+    @staticmethod
+    def forward(ctx, qkv, key_mask, query_mask, H: int, window: int, static_kv_first: bool):
+        lib = L.load()
+        qkv = qkv.contiguous()
+        Bs, T, D3 = qkv.shape
+        D = D3 // 3
+        hd = D // H
+        skf = 1 if static_kv_first else 0
+        Lk, Lq = T, T - skf
+        es = qkv.element_size()
+        base = qkv.data_ptr()
+        o = torch.empty(Bs, Lq, D, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(Bs, H, Lq, dtype=torch.float32, device=qkv.device)
+        L.check(lib.esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                                   lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask), Bs, H, Lq, Lk, hd, window,
+                                   L.dtype_code(qkv.dtype), L.stream()), "attn_fwd")
+        ctx.save_for_backward(qkv, o, lse, key_mask, query_mask)
+        ctx.cfg = (H, window, skf)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        lib = L.load()
+        qkv, o, lse, key_mask, query_mask = ctx.saved_tensors
+        H, window, skf = ctx.cfg
+        do = do.contiguous().to(qkv.dtype)
+        Bs, T, D3 = qkv.shape
+        D = D3 // 3
+        hd = D // H
+        Lk, Lq = T, T - skf
+        es = qkv.element_size()
+        dqkv = (torch.zeros if skf else torch.empty)(Bs, T, D3, dtype=qkv.dtype, device=qkv.device)
+        nbytes = lib.esgpt_attn_bwd_workspace(Bs, H, Lq)
+        ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=qkv.device)
+        base, dbase = qkv.data_ptr(), dqkv.data_ptr()
+        L.check(lib.esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                                   do.data_ptr(), D, lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask),
+                                   dbase + skf * D3 * es, dbase + D * es, dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd,
+                                   window, L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes, L.stream()), "attn_bwd")
+        return dqkv, None, None, None, None, None
+
+
+# ----------------------------------------------------------------------------------------------------------------
+# Output-layer losses
+# ----------------------------------------------------------------------------------------------------------------
+class OutputLossFn(torch.autograd.Function):
+    """Fused generative losses. Returns f32 [n_terms + 2] = per-term losses, -TTE_LL, total.
+
+    Only the total (last element) carries gradient; the per-term entries are for logging.
+    ``zt=None`` means the TTE parameters live in ``zc`` (CI: one fused head GEMM).
+    """
+
+    @staticmethod
+    def forward(ctx, zc, zt, zc_bias, bv: BatchView, terms, tte, shift: int, n_levels: int):
+        lib = L.load()
+        zc = zc.contiguous()
+        ldc = zc.shape[-1]
+        same = zt is None
+        zt_ = zc if same else zt.contiguous()
+        ldt = zt_.shape[-1]
+        if zc_bias is not None:
+            zc_bias = zc_bias.to(zc.dtype).contiguous()
+        n_terms = len(terms)
+        arr = (L.EsgptLossTerm * max(1, n_terms))(*terms)
+        dzc = torch.empty_like(zc)
+        dzt = dzc if same else torch.empty_like(zt_)
+        dbias = torch.empty(bv.B, ldc, dtype=torch.float32, device=zc.device) if shift else None
+        losses = torch.empty(n_terms + 2, dtype=torch.float32, device=zc.device)
+        nbytes = lib.esgpt_output_loss_workspace(bv.B, bv.L, n_terms)
+        ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=zc.device)
+        L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), ldc, n_levels, shift, L.ptr(zc_bias), zt_.data_ptr(),
+                                      ldt, L.dtype_code(zc.dtype), arr, n_terms, ctypes.byref(tte), dzc.data_ptr(),
+                                      dzt.data_ptr(), L.ptr(dbias), losses.data_ptr(), ws.data_ptr(), nbytes,
+                                      err_word(zc.device).data_ptr(), L.stream()), "output_loss")
+        ctx.same = same
+        ctx.has_bias = zc_bias is not None
+        ctx.save_for_backward(dzc, None if same else dzt, dbias)
+        return losses
+
+    @staticmethod
+    def backward(ctx, g):
+        dzc, dzt, dbias = ctx.saved_tensors
+        gt = g[-1].to(dzc.dtype)
+        d_zc = dzc * gt
+        d_zt = None if ctx.same else dzt * gt
+        d_bias = (dbias.sum(0) * g[-1]) if (ctx.has_bias and dbias is not None) else None
+        return d_zc, d_zt, d_bias, None, None, None, None, None

@@ -1,0 +1,60 @@
+"""``StructuredAttention`` — drop-in for ``EventStream/transformer/structured_attention.py:7-219`` (training path).
+
+Differences in mechanics (same results): padded events are NOT compacted out with boolean indexing (a device→host
+sync and data-dependent shapes in the reference, ``:87-96,158-165,186-193``); every (subject, event) runs through
+the dependency-graph module — its sequences are independent — and the outputs of padded events are zeroed, which
+is exactly what the reference's scatter into a zero tensor produces. This keeps the step shape-static (capturable
+into a HIP graph).
+"""
+from __future__ import annotations
+
+from typing import Any
+
+import torch
+
+
+class StructuredAttention(torch.nn.Module):
+    def __init__(self, seq_module: torch.nn.Module, dep_graph_module: torch.nn.Module):
+        super().__init__()
+        self.seq_module = seq_module
+        self.dep_graph_module = dep_graph_module
+
+    def forward(self, hidden_states: torch.Tensor, seq_attention_mask: torch.Tensor | None = None,
+                event_mask: torch.Tensor | None = None, seq_module_kwargs: dict[str, Any] | None = None,
+                dep_graph_module_kwargs: dict[str, Any] | None = None,
+                prepend_graph_with_history_embeddings: bool = True,
+                update_last_graph_el_to_history_embedding: bool = True):
+        if not (prepend_graph_with_history_embeddings and update_last_graph_el_to_history_embedding):
+            raise NotImplementedError("eventstreamgpt_amd: cached dependency-graph generation is out of scope")
+        seq_module_kwargs = dict(seq_module_kwargs or {})
+        dep_graph_module_kwargs = dict(dep_graph_module_kwargs or {})
+        bsz, seq_len, dep_graph_len, hidden_size = hidden_states.shape
+
+        kpm = event_mask
+        if kpm is None and seq_attention_mask is not None:
+            kpm = seq_attention_mask.reshape(bsz, -1) == 0
+        per_event = hidden_states[:, :, -1, :]
+        if event_mask is not None:
+            m3 = event_mask.unsqueeze(-1)
+            per_event = torch.where(m3, per_event, torch.zeros_like(per_event))
+        ctx = self.seq_module(per_event, key_padding_mask=kpm, **seq_module_kwargs)
+        seq_ret = None
+        if isinstance(ctx, tuple):
+            ctx, seq_ret = ctx
+        if event_mask is not None:
+            ctx = torch.where(m3, ctx, torch.zeros_like(ctx))
+
+        history = torch.cat((torch.zeros_like(ctx[:, :1, :]), ctx[:, :-1, :]), dim=1)
+        # [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i]: the last graph element is replaced by the contextualised
+        # event (structured_attention.py:125-149).
+        dep_graph_seq = torch.cat((history.unsqueeze(2), hidden_states[:, :, :-1, :], ctx.unsqueeze(2)), dim=2)
+        dep_graph_seq = dep_graph_seq.reshape(bsz * seq_len, dep_graph_len + 1, hidden_size)
+        out = self.dep_graph_module(dep_graph_seq, attention_mask=None, static_kv_first=True,
+                                    **dep_graph_module_kwargs)
+        dep_ret = None
+        if isinstance(out, tuple):
+            out, dep_ret = out
+        out = out.reshape(bsz, seq_len, dep_graph_len, hidden_size)
+        if event_mask is not None:
+            out = torch.where(event_mask[:, :, None, None], out, torch.zeros_like(out))
+        return out, {"seq_module": seq_ret, "dep_graph_module": dep_ret}

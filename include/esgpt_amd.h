@@ -1,0 +1,174 @@
+/*
+ * esgpt_amd.h — C ABI of the MI355X (gfx950) kernels behind eventstreamgpt_amd.
+ *
+ * The reference (Jwoo5/EventStreamGPT) is pure Python/PyTorch: its swap points are module classes, not an FFI.
+ * Each entry point below replaces the ATen ops inside one reference module method (cited per function); the
+ * Python side (eventstreamgpt_amd/_lib.py, ctypes) binds these symbols exactly as a maintainer would bind them
+ * from the reference (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers; sizes are int64; bool tensors are 1-byte (uint8) arrays.
+ *   - `stream` is a hipStream_t passed as void*. Every call is asynchronous and stream-ordered; no call
+ *     synchronises with the host, allocates, or frees. Callers own all outputs and workspaces.
+ *   - Return value: ESGPT_OK or an ESGPT_ERR_* code for invalid arguments / launch failures. Data-dependent
+ *     errors (out-of-range embedding index, NaN TTE log-likelihood, subject without observed TTE) are OR-ed
+ *     into the caller-provided device word `err` (ESGPT_FLAG_*); the Python wrapper reads it once per step and
+ *     raises the reference's exception type and message.
+ *   - dtype codes: ESGPT_F32 (float) or ESGPT_BF16 (bfloat16) for activation tensors; masters are f32.
+ */
+#ifndef ESGPT_AMD_H_
+#define ESGPT_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ESGPT_OK 0
+#define ESGPT_ERR_INVALID_ARG 1
+#define ESGPT_ERR_LAUNCH 2
+#define ESGPT_ERR_UNSUPPORTED 3
+
+#define ESGPT_F32 0
+#define ESGPT_BF16 1
+
+#define ESGPT_FLAG_BAD_INDEX 1    /* "Invalid embedding! {max} >= {V}"  (data_embedding_layer.py:485-488) */
+#define ESGPT_FLAG_TTE_NAN 2      /* "NaNs in TTE_LL"                    (model_output.py:1362-1363)     */
+#define ESGPT_FLAG_TTE_NO_OBS 4   /* "No observed time-to-event ..."     (model_output.py:1366-1367)     */
+
+/* embedding flags */
+#define ESGPT_EMB_NORMALIZE 1     /* do_normalize_by_measurement_index                                     */
+#define ESGPT_EMB_STATIC 2        /* StaticEmbeddingMode.SUM_ALL                                           */
+#define ESGPT_EMB_TIME 4          /* add TemporalPositionEncoding (at dependency-graph level 0)            */
+#define ESGPT_EMB_CUMSUM 8        /* NA input layer: cumulative sum over dependency-graph levels           */
+#define ESGPT_EMB_TIME_ABS 16     /* use batch.time instead of the exclusive cumsum of time_delta          */
+
+/* bag-backward selectors */
+#define ESGPT_BAG_JOINT 0         /* weight = (values_mask & num-bucket) ? value : 1                       */
+#define ESGPT_BAG_CAT 1           /* weight = cat-bucket ? 1 : 0                                           */
+#define ESGPT_BAG_NUM 2           /* weight = (values_mask & num-bucket) ? value : 0                       */
+
+/* Common batch view (PytorchBatch fields, data/types.py:86-163). */
+typedef struct {
+  const int64_t* dyn_idx;       /* [B,L,M] dynamic_indices                       */
+  const int64_t* dyn_meas;      /* [B,L,M] dynamic_measurement_indices           */
+  const float* dyn_vals;        /* [B,L,M] dynamic_values                        */
+  const uint8_t* dyn_vmask;     /* [B,L,M] dynamic_values_mask                   */
+  const uint8_t* event_mask;    /* [B,L]   event_mask                            */
+  const float* time_delta;      /* [B,L]   time_delta                            */
+  const float* time_abs;        /* [B,L]   time (optional, NULL)                 */
+  const int64_t* st_idx;        /* [B,S]   static_indices (optional)             */
+  const int64_t* st_meas;       /* [B,S]   static_measurement_indices (optional) */
+  int64_t B, L, M, S;
+} esgpt_batch;
+
+/* Dependency-graph buckets (split_by_measurement_indices, data_embedding_layer.py:505-561): bit k of
+ * cat_bits[g] / num_bits[g] is set when measurement index k belongs to bucket g categorically / numerically.
+ * G = 1 with all bits set reproduces the un-bucketed (CI) layer. Measurement indices must be < 64. */
+typedef struct {
+  int64_t G;
+  uint64_t cat_bits[8];
+  uint64_t num_bits[8];
+} esgpt_buckets;
+
+/* ---- Input layer ------------------------------------------------------------------------------------------
+ * JOINT mode, fully fused: DataEmbeddingLayer.forward (data_embedding_layer.py:609-708) with _joint_embed
+ * (:351-388), static SUM_ALL merge (:693-708), + TemporalPositionEncoding (transformer.py:594-619), event mask
+ * and (NA) the level-0 time add + cumsum over levels (transformer.py:926-936).
+ * out: f32 [B, L, G, D]. weights: static_w, dynamic_w already normalised as in data_embedding_layer.py:277-280. */
+int esgpt_embed_joint_fwd(const esgpt_batch* batch, const esgpt_buckets* buckets, const float* table,
+                          int64_t V, int64_t D, const float* sin_div, const float* cos_div, int flags,
+                          float static_w, float dynamic_w, float* out, int32_t* err, void* stream);
+
+/* SPLIT_CATEGORICAL_NUMERICAL mode, the gather part of _split_embed (:390-450) for every (event, bucket):
+ * x[e,g] = [cat_scale * bag_cat + static_scale * static_bag_cat , num_scale * bag_num]  (f32, [B*L*G, Dc+Dn]).
+ * The caller applies one GEMM with [cat_proj | num_proj] and then esgpt_embed_epilogue_fwd. */
+int esgpt_embed_split_bags_fwd(const esgpt_batch* batch, const esgpt_buckets* buckets, const float* cat_table,
+                               int64_t Dc, const float* num_table, int64_t Dn, int64_t V, int flags,
+                               float cat_scale, float num_scale, float static_scale, float* x, int32_t* err,
+                               void* stream);
+
+/* out[e,g] = mask_e * cumsum_g'<=g ( y[e,g'] + [g'==0] * time_enc(e) )  (CUMSUM flag; else no cumsum). */
+int esgpt_embed_epilogue_fwd(const esgpt_batch* batch, int64_t G, int64_t D, const float* y, const float* sin_div,
+                             const float* cos_div, int flags, float* out, void* stream);
+/* dy[e,g] = mask_e * sum_{g'>=g} dout[e,g'] (CUMSUM) or mask_e * dout[e,g]. */
+int esgpt_embed_epilogue_bwd(const esgpt_batch* batch, int64_t G, int64_t D, const float* dout, int flags,
+                             float* dy, void* stream);
+
+/* Table gradient of the bag sums (EmbeddingBag backward, atomic-free CSR form):
+ * dtable[v,:] = sum over entries (e,g,m) with index v of w(e,g,m) * dsrc[e*G+g, :]
+ *             + sum over static entries (b,s) of static_scale * w_s * sum_{e in b valid, g} dsrc[e*G+g, :].
+ * dsrc rows have leading dimension ld (elements); D columns are used. dtable: f32 [V, D], fully written. */
+size_t esgpt_embed_bag_bwd_workspace(const esgpt_batch* batch, int64_t G, int64_t V, int64_t D);
+int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, int selector, int flags,
+                        float dyn_scale, float static_scale, const float* dsrc, int64_t ld, int64_t D,
+                        int64_t V, float* dtable, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- Attention ---------------------------------------------------------------------------------------------
+ * InnerSelfAttention._attn (transformer.py:171-217): s = q.k (NO 1/sqrt(d) scaling), causal band (global, or
+ * local: 0 <= i-j < window; transformer.py:109-119), additive key-padding mask, softmax in f32, p.v.
+ * Element (b,t,h,d) of k/v lives at base + (b*Lk + t)*ld_in + h*hd + d, of q (and dq) at base + (b*tq + t)*ld_in
+ * + h*hd + d, of o/dout at base + (b*Lq + t)*ld_o + h*hd + d (q/k/v may alias one packed [.,3D] buffer).
+ * Query i sits at key position i + (Lk - Lq): static_kv_first (transformer.py:256-259) drops query 0, i.e. pass
+ * q = packed + ld_in, tq = Lk, Lq = Lk - 1 (the caller zero-fills the dq rows of token 0).
+ * Rows whose query is padded (query_mask == 0) are written as zeros (the reference zeroes them downstream,
+ * transformer.py:818-823). lse: f32 [B,H,Lq] (natural-log softmax normaliser, for the backward). */
+int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
+                   float* lse,
+                   const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
+                   int64_t Lk, int64_t hd, int64_t window, int dtype, void* stream);
+size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq);
+int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                   int64_t ld_o,
+                   const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                   const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
+                   int64_t Lq, int64_t Lk, int64_t hd, int64_t window, int dtype, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* ---- Output layer losses -----------------------------------------------------------------------------------
+ * GenerativeOutputLayerBase.get_{classification,regression,TTE}_outputs (model_output.py:1311-1721) with
+ * weighted_loss / safe_weighted_avg (utils.py:134-234), fused: one pass computes every per-event loss, the
+ * per-subject/per-term normalisers, the scalar losses and d(total loss)/d(logits). */
+#define ESGPT_TERM_SINGLE 1   /* CE(scores, label) + BCE(is_obs, has_label), masked by event & has_label     */
+#define ESGPT_TERM_MULTI 2    /* mean_j BCE(scores_j, multi_hot_j), masked by event                           */
+#define ESGPT_TERM_MVREG 3    /* safe_weighted_avg_m NLL(Normal(gathered)), masked by event & any(selected)    */
+#define ESGPT_TERM_UVREG 4    /* NLL(Normal) + BCE(is_obs, measured), masked by event & has_value             */
+#define ESGPT_TTE_EXP 1
+#define ESGPT_TTE_LNM 2
+
+typedef struct {
+  int32_t kind, meas_idx, vocab_start, vocab_end;
+  int32_t col;      /* first logit column of the term (scores / (mean,std) pairs)        */
+  int32_t obs_col;  /* is-observed logit column (SINGLE, UVREG), -1 otherwise             */
+  int32_t level;    /* content level (NA: dependency-graph level - 1); 0 for CI          */
+  int32_t pad;
+} esgpt_loss_term;
+
+typedef struct {
+  int32_t kind, K, col, pad;
+  float mean_log, std_log;
+} esgpt_tte_spec;
+
+#define ESGPT_MAX_TERMS 16
+
+/* zc: content logits, rows (b*L + l)*n_levels + level, leading dim ldc; `shift` = 1 (CI): position l reads
+ * row l-1 and position 0 reads `zc_bias` (the head bias: Linear(0) = bias). zt: TTE params, rows b*L+l.
+ * dzc/dzt: same layout/dtype as zc/zt, must be zero-filled by the caller; dbias: f32 [B, ldc] (position-0
+ * content grads, shift mode). losses: f32 [n_terms + 2] = per-term losses, -TTE_LL, total loss. */
+size_t esgpt_output_loss_workspace(int64_t B, int64_t L, int n_terms);
+int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int64_t n_levels, int shift,
+                      const void* zc_bias, const void* zt, int64_t ldt, int dtype, const esgpt_loss_term* terms,
+                      int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
+                      void* workspace, size_t workspace_bytes, int32_t* err, void* stream);
+
+/* ---- Misc ----------------------------------------------------------------------------------------------- */
+const char* esgpt_version(void);
+int esgpt_device_arch_ok(void); /* 1 if device 0 is gfx950 */
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ESGPT_AMD_H_ */

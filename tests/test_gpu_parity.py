@@ -1,0 +1,156 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and the CPU oracle.
+
+Tolerances (BASELINE.json north_star): f32 forward/backward <= 1e-5 relative on losses and encodings; gradients
+are compared with a max-abs-normalised error (<= 1e-4: different but valid f32 summation orders); bf16 losses
+<= 1e-2 relative.
+"""
+import pytest
+import torch
+
+import esgpt_oracle as O
+from helpers import CASES, load_case, rel_err
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _model(cfg):
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    if str(cfg.structured_event_processing_mode) == "conditionally_independent":
+        return CIPPTForGenerativeSequenceModeling(cfg)
+    return NAPPTForGenerativeSequenceModeling(cfg)
+
+
+@pytest.fixture(autouse=True)
+def _clean_errors():
+    from eventstreamgpt_amd.kernels import check_errors
+
+    yield
+    check_errors()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_model_matches_reference_f32(name):
+    fx, cfg, batch = load_case(name)
+    m = _model(cfg).to(DEV)
+    m.load_state_dict(fx["state_dict"])
+    m.train()
+    b = batch.to(DEV)
+    enc = m.encoder(b).last_hidden_state
+    assert rel_err(enc.detach().cpu(), fx["encoded"]) < 1e-5
+    out = m(b)
+    assert abs(out.loss.item() - fx["loss"].item()) <= 1e-5 * abs(fx["loss"].item())
+    for k, v in fx["classification"].items():
+        assert out.losses.classification[k].item() == pytest.approx(v.item(), rel=1e-5, abs=1e-6), k
+    for k, v in fx["regression"].items():
+        assert out.losses.regression[k].item() == pytest.approx(v.item(), rel=1e-5, abs=1e-6), k
+    assert out.losses.time_to_event.item() == pytest.approx(fx["tte_nll"].item(), rel=1e-5, abs=1e-6)
+    out.loss.backward()
+    named = dict(m.named_parameters())
+    for k, g in fx["grads"].items():
+        got = named[k].grad
+        assert got is not None, k
+        assert rel_err(got.cpu(), g) < 1e-4, (k, rel_err(got.cpu(), g))
+
+
+def _rand_qkv(B, T, H, hd, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(B, T, 3 * H * hd, generator=g) * 0.5).to(DEV, dtype)
+
+
+def _torch_attention(qkv, H, key_mask, window, skf):
+    """f32 PyTorch restatement of InnerSelfAttention._attn over packed qkv (the reference's math)."""
+    B, T, D3 = qkv.shape
+    D = D3 // 3
+    hd = D // H
+    q, k, v = qkv.float().split(D, -1)
+    q = q.view(B, T, H, hd).transpose(1, 2)
+    k = k.view(B, T, H, hd).transpose(1, 2)
+    v = v.view(B, T, H, hd).transpose(1, 2)
+    if skf:
+        q = q[:, :, 1:]
+    Lq, Lk = q.shape[2], T
+    s = q @ k.transpose(-1, -2)
+    band = O.causal_band(Lk, "local" if window else "global", window).to(qkv.device)[Lk - Lq:]
+    s = torch.where(band, s, torch.tensor(O.FMIN, device=qkv.device))
+    if key_mask is not None:
+        s = s + (1.0 - key_mask[:, None, None, :].float()) * O.FMIN
+    o = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, Lq, D)
+    if key_mask is not None and not skf:
+        o = torch.where(key_mask[..., None], o, torch.zeros_like(o))
+    return o
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(3, 37, 2, 16, 0, False), (2, 64, 4, 64, 0, False), (2, 70, 4, 64, 5, False),
+                                   (5, 9, 4, 8, 0, True), (4, 5, 2, 64, 2, True), (2, 256, 4, 64, 32, False)])
+def test_attention_kernel(shape, dtype):
+    from eventstreamgpt_amd.kernels import AttentionFn
+
+    B, T, H, hd, window, skf = shape
+    qkv = _rand_qkv(B, T, H, hd, dtype, seed=T * 7 + hd)
+    km = None
+    if not skf:
+        lens = torch.randint(max(1, T // 2), T + 1, (B,), generator=torch.Generator().manual_seed(1))
+        km = (torch.arange(T)[None] < lens[:, None])
+        km[-1] = torch.arange(T) >= (T - lens[-1])  # one left-padded subject
+        km = km.to(DEV)
+    x = qkv.clone().requires_grad_(True)
+    o = AttentionFn.apply(x, km, km, H, window, skf)
+    ref_in = qkv.float().clone().requires_grad_(True)
+    ref = _torch_attention(ref_in, H, km, window, skf)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(o.float().detach(), ref.detach()) < tol
+    go = torch.randn_like(ref)
+    if km is not None and not skf:
+        go = torch.where(km[..., None], go, torch.zeros_like(go))
+    o.backward(go.to(dtype))
+    ref.backward(go)
+    gtol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert rel_err(x.grad.float(), ref_in.grad) < gtol
+
+
+def test_embedding_c2_joint_matches_oracle():
+    """C2-sized JOINT input layer (synthetic batch): forward f32 within 1e-5, table gradient within 1e-5."""
+    from eventstreamgpt_amd.synthetic import CONFIGS
+    from eventstreamgpt_amd.transformer.transformer import ConditionallyIndependentPointProcessInputLayer
+
+    bc = CONFIGS["C2"]
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+    torch.manual_seed(0)
+    layer = ConditionallyIndependentPointProcessInputLayer(cfg).to(DEV)
+    batch = bc.batch(0)
+    out = layer(batch.to(DEV))
+    p = {"e." + k: v.detach().cpu().clone() for k, v in layer.state_dict().items()}
+    p["e.data_embedding_layer.embed_layer.weight"].requires_grad_(True)
+    ref = O.data_embedding(p, "e.data_embedding_layer.", O.emb_cfg(cfg), batch)
+    ref = ref + O.temporal_encoding(p, "e.time_embedding_layer.", batch, cfg.hidden_size)
+    ref = torch.where(batch.event_mask.unsqueeze(-1), ref, torch.zeros_like(ref))
+    assert rel_err(out.detach().cpu(), ref.detach()) < 1e-5
+    g = torch.randn_like(ref)
+    out.backward(g.to(DEV))
+    ref.backward(g)
+    assert rel_err(layer.data_embedding_layer.embed_layer.weight.grad.cpu(),
+                   p["e.data_embedding_layer.embed_layer.weight"].grad) < 1e-5
+
+
+@pytest.mark.parametrize("cfg_name", ["C2", "C5"])
+def test_full_step_bf16_matches_oracle(cfg_name):
+    """Full CI model at the config's real width on a reduced batch, bf16 autocast vs the f32 oracle:
+    loss within 1e-2 relative."""
+    from eventstreamgpt_amd.synthetic import CONFIGS
+
+    bc = CONFIGS[cfg_name]
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+    torch.manual_seed(0)
+    m = _model(cfg).to(DEV)
+    batch = bc.batch(0, batch_size=4)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = m(batch.to(DEV))
+    p = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    ref = O.model_losses(p, cfg, batch)
+    assert out.loss.item() == pytest.approx(ref["loss"].item(), rel=1e-2)
+    out.loss.backward()
