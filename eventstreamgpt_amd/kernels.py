@@ -16,6 +16,39 @@ from .data.types import PytorchBatch
 
 
 # ----------------------------------------------------------------------------------------------------------------
+# Optional per-launch timing (HIP events on the launching stream); used by bench.py's roofline measurement.
+# ----------------------------------------------------------------------------------------------------------------
+TIMING = {"enabled": False, "events": {}}
+
+
+class _timed:
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        if TIMING["enabled"]:
+            self.s = torch.cuda.Event(enable_timing=True)
+            self.e = torch.cuda.Event(enable_timing=True)
+            self.s.record()
+        return self
+
+    def __exit__(self, *a):
+        if TIMING["enabled"]:
+            self.e.record()
+            TIMING["events"].setdefault(self.name, []).append((self.s, self.e))
+
+
+def timing_summary() -> dict:
+    """{name: (n_launches, mean_ms)} of the recorded launches (synchronises)."""
+    torch.cuda.synchronize()
+    out = {}
+    for k, v in TIMING["events"].items():
+        ms = [s.elapsed_time(e) for s, e in v]
+        out[k] = (len(ms), sum(ms) / max(1, len(ms)))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------------------------
 # Batch view + device error word
 # ----------------------------------------------------------------------------------------------------------------
 class BatchView:
@@ -162,9 +195,11 @@ class JointEmbedFn(torch.autograd.Function):
         V, D = table.shape
         table = table.contiguous().float()
         out = torch.empty(bv.B, bv.L, spec.G, D, dtype=torch.float32, device=table.device)
-        L.check(lib.esgpt_embed_joint_fwd(bv.ref, _bref(spec.groups), table.data_ptr(), V, D, L.ptr(sin_div),
-                                          L.ptr(cos_div), spec.flags, spec.static_w, spec.dynamic_w, out.data_ptr(),
-                                          err_word(table.device).data_ptr(), L.stream()), "embed_joint_fwd")
+        with _timed("embed_joint_fwd"):
+            st = lib.esgpt_embed_joint_fwd(bv.ref, _bref(spec.groups), table.data_ptr(), V, D, L.ptr(sin_div),
+                                           L.ptr(cos_div), spec.flags, spec.static_w, spec.dynamic_w,
+                                           out.data_ptr(), err_word(table.device).data_ptr(), L.stream())
+        L.check(st, "embed_joint_fwd")
         ctx.bv, ctx.spec, ctx.V, ctx.D = bv, spec, V, D
         return out
 
@@ -178,7 +213,9 @@ class JointEmbedFn(torch.autograd.Function):
             dsrc = dout
         static = bool(spec.flags & L.EMB_STATIC) and bv.S > 0
         dyn_scale = spec.dynamic_w if static else 1.0
-        dtable = _bag_bwd(bv, spec.groups, L.BAG_JOINT, spec.flags, dyn_scale, spec.static_w, dsrc, D, D, V, spec.G)
+        with _timed("embed_joint_bwd"):
+            dtable = _bag_bwd(bv, spec.groups, L.BAG_JOINT, spec.flags, dyn_scale, spec.static_w, dsrc, D, D, V,
+                              spec.G)
         return dtable, None, None, None, None
 
 
@@ -253,9 +290,11 @@ class AttentionFn(torch.autograd.Function):
         base = qkv.data_ptr()
         o = torch.empty(Bs, Lq, D, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(Bs, H, Lq, dtype=torch.float32, device=qkv.device)
-        L.check(lib.esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
-                                   lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask), Bs, H, Lq, Lk, hd, window,
-                                   L.dtype_code(qkv.dtype), L.stream()), "attn_fwd")
+        with _timed("attn_fwd"):
+            st = lib.esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                                    lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask), Bs, H, Lq, Lk, hd, window,
+                                    L.dtype_code(qkv.dtype), L.stream())
+        L.check(st, "attn_fwd")
         ctx.save_for_backward(qkv, o, lse, key_mask, query_mask)
         ctx.cfg = (H, window, skf)
         return o
@@ -275,10 +314,12 @@ class AttentionFn(torch.autograd.Function):
         nbytes = lib.esgpt_attn_bwd_workspace(Bs, H, Lq)
         ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=qkv.device)
         base, dbase = qkv.data_ptr(), dqkv.data_ptr()
-        L.check(lib.esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
-                                   do.data_ptr(), D, lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask),
-                                   dbase + skf * D3 * es, dbase + D * es, dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd,
-                                   window, L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes, L.stream()), "attn_bwd")
+        with _timed("attn_bwd"):
+            st = lib.esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                                    do.data_ptr(), D, lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask),
+                                    dbase + skf * D3 * es, dbase + D * es, dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd,
+                                    window, L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes, L.stream())
+        L.check(st, "attn_bwd")
         return dqkv, None, None, None, None, None
 
 
@@ -310,10 +351,12 @@ class OutputLossFn(torch.autograd.Function):
         losses = torch.empty(n_terms + 2, dtype=torch.float32, device=zc.device)
         nbytes = lib.esgpt_output_loss_workspace(bv.B, bv.L, n_terms)
         ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=zc.device)
-        L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), ldc, n_levels, shift, L.ptr(zc_bias), zt_.data_ptr(),
-                                      ldt, L.dtype_code(zc.dtype), arr, n_terms, ctypes.byref(tte), dzc.data_ptr(),
-                                      dzt.data_ptr(), L.ptr(dbias), losses.data_ptr(), ws.data_ptr(), nbytes,
-                                      err_word(zc.device).data_ptr(), L.stream()), "output_loss")
+        with _timed("output_loss"):
+            st = lib.esgpt_output_loss(bv.ref, zc.data_ptr(), ldc, n_levels, shift, L.ptr(zc_bias), zt_.data_ptr(),
+                                       ldt, L.dtype_code(zc.dtype), arr, n_terms, ctypes.byref(tte), dzc.data_ptr(),
+                                       dzt.data_ptr(), L.ptr(dbias), losses.data_ptr(), ws.data_ptr(), nbytes,
+                                       err_word(zc.device).data_ptr(), L.stream())
+        L.check(st, "output_loss")
         ctx.same = same
         ctx.has_bias = zc_bias is not None
         ctx.save_for_backward(dzc, None if same else dzt, dbias)

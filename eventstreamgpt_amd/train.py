@@ -1,0 +1,149 @@
+"""Minimal Lightning-free training step (``generative_modeling.py:434-485``) for one GPU or DDP over RCCL.
+
+* loss = model(batch).loss (per-rank weighted_loss normalisation, exactly like the reference under DDP);
+* AdamW(lr=init_lr, weight_decay) + transformers' polynomial-decay-with-warmup schedule, stepped every step;
+* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Gradients live in one
+  flat f32 buffer (every ``param.grad`` is a view into it), all-reduced in buckets and divided by world size —
+  the DDP gradient-averaging semantics of the reference's Lightning trainer.
+* optional HIP-graph capture of forward+backward (static shapes; batches are copied into static buffers).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .data.types import PytorchBatch
+from .kernels import check_errors
+from .transformer.config import OptimizationConfig
+
+
+def poly_decay_lambda(warmup: int, total: int, power: float, init_lr: float, end_lr: float):
+    """``transformers.get_polynomial_decay_schedule_with_warmup`` as a multiplier of ``init_lr``."""
+
+    def f(step: int) -> float:
+        if step < warmup:
+            return float(step) / float(max(1, warmup))
+        if step > total:
+            return end_lr / init_lr
+        rem = 1 - (step - warmup) / (total - warmup)
+        return ((init_lr - end_lr) * rem**power + end_lr) / init_lr
+
+    return f
+
+
+class TrainStep:
+    def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
+                 bucket_mb: float = 25.0, use_graph: bool = False):
+        self.model = model
+        self.cfg = opt_cfg
+        self.dtype = compute_dtype
+        self.distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self.world = dist.get_world_size() if self.distributed else 1
+        params = [p for p in model.parameters() if p.requires_grad]
+        self.params = params
+        dev = params[0].device
+        n = sum(p.numel() for p in params)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in params:
+            p.grad = self.flat_grad[off: off + p.numel()].view_as(p)
+            off += p.numel()
+        # buckets in reverse parameter order (the last layers' gradients are final first)
+        self.buckets = []
+        lim = int(bucket_mb * 2**20 / 4)
+        end = n
+        while end > 0:
+            start = max(0, end - lim)
+            self.buckets.append((start, end))
+            end = start
+        fused = dev.type == "cuda"
+        self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay, fused=fused)
+        total = opt_cfg.max_training_steps or 1_000_000
+        warm = opt_cfg.lr_num_warmup_steps or 0
+        self.sched = torch.optim.lr_scheduler.LambdaLR(
+            self.opt, poly_decay_lambda(warm, total, opt_cfg.lr_decay_power, opt_cfg.init_lr, opt_cfg.end_lr))
+        self.use_graph = use_graph
+        self.graph = None
+        self.static_batch = None
+        self.static_loss = None
+
+    # --------------------------------------------------------------------------------------------------------
+    def _fwd_bwd(self, batch: PytorchBatch):
+        # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
+        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32,
+                            cache_enabled=not self.use_graph):
+            out = self.model(batch)
+        out.loss.backward()
+        return out.loss.detach()
+
+    def _allreduce(self):
+        if not self.distributed:
+            return
+        for s, e in self.buckets:
+            dist.all_reduce(self.flat_grad[s:e])
+        self.flat_grad.div_(self.world)
+
+    def _copy_into_static(self, batch: PytorchBatch):
+        for k, v in batch.as_dict().items():
+            getattr(self.static_batch, k).copy_(v, non_blocking=True)
+
+    def step(self, batch: PytorchBatch) -> torch.Tensor:
+        if not self.use_graph:
+            self.flat_grad.zero_()
+            loss = self._fwd_bwd(batch)
+        else:
+            if self.graph is None:
+                self._capture(batch)
+            self._copy_into_static(batch)
+            self.graph.replay()
+            loss = self.static_loss
+        self._allreduce()
+        self.opt.step()
+        self.sched.step()
+        return loss
+
+    def _capture(self, batch: PytorchBatch):
+        self.static_batch = PytorchBatch(**{k: v.clone() for k, v in batch.as_dict().items()})
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up allocator / lazy init outside the graph
+                self.flat_grad.zero_()
+                self._fwd_bwd(self.static_batch)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.flat_grad.zero_()
+            self.static_loss = self._fwd_bwd(self.static_batch)
+        torch.cuda.synchronize()
+
+    def check(self):
+        check_errors()
+
+
+def init_distributed():
+    """Initialises the process group from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
+    import os
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1, 0
+    rank = int(os.environ["RANK"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        backend = "nccl"
+    else:
+        backend = "gloo"
+    dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local
+
+
+def n_params(model) -> int:
+    return sum(p.numel() for p in model.parameters() if p.requires_grad)
+
+
+def grad_bytes(model) -> int:
+    return 4 * n_params(model)
+

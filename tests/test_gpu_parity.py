@@ -86,7 +86,9 @@ def _torch_attention(qkv, H, key_mask, window, skf):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(3, 37, 2, 16, 0, False), (2, 64, 4, 64, 0, False), (2, 70, 4, 64, 5, False),
-                                   (5, 9, 4, 8, 0, True), (4, 5, 2, 64, 2, True), (2, 256, 4, 64, 32, False)])
+                                   (5, 9, 4, 8, 0, True), (4, 5, 2, 64, 2, True), (2, 256, 4, 64, 32, False),
+                                   (2, 200, 2, 32, 0, False), (1, 130, 2, 128, 0, False), (1, 1024, 4, 64, 0, False),
+                                   (3, 17, 4, 64, 0, True)])
 def test_attention_kernel(shape, dtype):
     from eventstreamgpt_amd.kernels import AttentionFn
 
