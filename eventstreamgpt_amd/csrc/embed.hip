@@ -10,6 +10,8 @@
 // weights (bucket masks + measurement-index normalisation) in registers; the wave then streams the gathered
 // table rows, VEC floats per lane, accumulating every bucket in registers. Roofline: HBM/L2 gather-bound,
 // algorithmic bytes per event = nnz_e * D * 4 (rows, per occurrence) + M * 18 (index/meas/value/mask) + G*D*4.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace esgpt;
@@ -481,12 +483,34 @@ __device__ __forceinline__ bool bag_slot(const BagBwdArgs& a, int64_t slot, int6
   return true;
 }
 
-__global__ void bag_count_kernel(BagBwdArgs a, int64_t n_slots, int32_t* __restrict__ count) {
-  const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= n_slots) return;
-  int64_t v, src;
-  float w;
-  if (bag_slot(a, slot, v, w, src)) atomicAdd(count + v, 1);
+// Slot ranges: block i owns the contiguous slots [i*per, (i+1)*per) in both the count and the fill pass.
+constexpr int kBagBlocks = 256;
+constexpr int kLdsBins = 16384;  // vocabularies up to this size are histogrammed in LDS (2 x 64 KiB)
+
+// Per-block LDS histogram, then one global add per non-empty bin (hot rows such as event types would otherwise
+// serialise thousands of same-address atomics).
+template <bool LDS>
+__global__ __launch_bounds__(256) void bag_count_kernel(BagBwdArgs a, int64_t n_slots, int64_t per,
+                                                        int32_t* __restrict__ count) {
+  extern __shared__ int32_t s_hist[];
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n_slots, lo + per);
+  if (LDS) {
+    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x) s_hist[i] = 0;
+    __syncthreads();
+  }
+  for (int64_t slot = lo + threadIdx.x; slot < hi; slot += blockDim.x) {
+    int64_t v, src;
+    float w;
+    if (bag_slot(a, slot, v, w, src)) {
+      if (LDS) atomicAdd(s_hist + v, 1);
+      else atomicAdd(count + v, 1);
+    }
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x)
+      if (s_hist[i]) atomicAdd(count + i, s_hist[i]);
+  }
 }
 
 // Exclusive scan of count[0..V) into rowptr[0..V]; single workgroup of 1024 threads. Also zeroes cursor.
@@ -515,33 +539,61 @@ __global__ __launch_bounds__(1024) void bag_scan_kernel(const int32_t* __restric
   if (tid == 1023) rowptr[V] = s_part[1023];
 }
 
-__global__ void bag_fill_kernel(BagBwdArgs a, int64_t n_slots, const int32_t* __restrict__ rowptr,
-                                int32_t* __restrict__ cursor, int64_t* __restrict__ ent_src,
-                                float* __restrict__ ent_w, int32_t* __restrict__ ent_v) {
-  const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= n_slots) return;
-  int64_t v, src;
-  float w;
-  if (!bag_slot(a, slot, v, w, src)) return;
-  const int32_t pos = rowptr[v] + atomicAdd(cursor + v, 1);
-  ent_src[pos] = src;
-  ent_w[pos] = w;
-  ent_v[pos] = (int32_t)v;
+// Scatter into CSR order. LDS variant: block-local counts, one global cursor reservation per (block, bin), then
+// in-block ranks from LDS atomics.
+template <bool LDS>
+__global__ __launch_bounds__(256) void bag_fill_kernel(BagBwdArgs a, int64_t n_slots, int64_t per,
+                                                       const int32_t* __restrict__ rowptr,
+                                                       int32_t* __restrict__ cursor, int64_t* __restrict__ ent_src,
+                                                       float* __restrict__ ent_w, int32_t* __restrict__ ent_v) {
+  extern __shared__ int32_t s_mem[];
+  int32_t* s_cnt = s_mem;
+  int32_t* s_base = s_mem + a.V;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n_slots, lo + per);
+  if (LDS) {
+    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x) s_cnt[i] = 0;
+    __syncthreads();
+    for (int64_t slot = lo + threadIdx.x; slot < hi; slot += blockDim.x) {
+      int64_t v, src;
+      float w;
+      if (bag_slot(a, slot, v, w, src)) atomicAdd(s_cnt + v, 1);
+    }
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x) {
+      const int32_t c = s_cnt[i];
+      s_base[i] = c ? rowptr[i] + atomicAdd(cursor + i, c) : 0;
+      s_cnt[i] = 0;
+    }
+    __syncthreads();
+  }
+  for (int64_t slot = lo + threadIdx.x; slot < hi; slot += blockDim.x) {
+    int64_t v, src;
+    float w;
+    if (!bag_slot(a, slot, v, w, src)) continue;
+    const int32_t pos = LDS ? s_base[v] + atomicAdd(s_cnt + v, 1) : rowptr[v] + atomicAdd(cursor + v, 1);
+    ent_src[pos] = src;
+    ent_w[pos] = w;
+    ent_v[pos] = (int32_t)v;
+  }
 }
 
-// Subject sums of dsrc over valid events and all levels: sub[b, d].
-__global__ void bag_subject_sum_kernel(esgpt_batch bt, int64_t G, const float* __restrict__ dsrc, int64_t ld,
-                                       int64_t D, float* __restrict__ sub) {
-  const int64_t b = blockIdx.y;
-  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  float acc = 0.f;
-  for (int64_t l = 0; l < bt.L; ++l) {
-    const int64_t e = b * bt.L + l;
-    if (!bt.event_mask[e]) continue;
-    for (int64_t g = 0; g < G; ++g) acc += dsrc[(e * G + g) * ld + d];
+// Subject sums of dsrc over valid events and all levels: sub[b, d] (zeroed beforehand). Block (b, c) sums the
+// event chunk c of subject b for every column and adds it in.
+constexpr int kSubChunks = 8;
+__global__ __launch_bounds__(256) void bag_subject_sum_kernel(esgpt_batch bt, int64_t G, const float* __restrict__ dsrc,
+                                                              int64_t ld, int64_t D, float* __restrict__ sub) {
+  const int64_t b = blockIdx.x;
+  const int64_t per = (bt.L + kSubChunks - 1) / kSubChunks;
+  const int64_t l0 = blockIdx.y * per, l1 = min(bt.L, l0 + per);
+  for (int64_t d = threadIdx.x; d < D; d += blockDim.x) {
+    float acc = 0.f;
+    for (int64_t l = l0; l < l1; ++l) {
+      const int64_t e = b * bt.L + l;
+      if (!bt.event_mask[e]) continue;
+      for (int64_t g = 0; g < G; ++g) acc += dsrc[(e * G + g) * ld + d];
+    }
+    if (l1 > l0) atomicAdd(sub + b * D + d, acc);
   }
-  sub[b * D + d] = acc;
 }
 
 // One wave per chunk of kChunk sorted entries. Rows fully inside the chunk are stored; rows crossing a chunk
@@ -743,13 +795,27 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   if (hipMemsetAsync(dtable, 0, sizeof(float) * V * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   if (hipMemsetAsync(w.count, 0, sizeof(int32_t) * (V + 1), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   if (n_slots == 0) return ESGPT_OK;
-  const unsigned g_slots = (unsigned)cdiv(n_slots, 256);
-  bag_count_kernel<<<g_slots, 256, 0, st>>>(a, n_slots, w.count);
+  const int64_t nblk = std::min<int64_t>(kBagBlocks, cdiv(n_slots, 256));
+  const int64_t per = cdiv(n_slots, nblk);
+  // Dynamic LDS stays within the 64 KiB default: count needs 4 B/bin, fill 8 B/bin.
+  const bool lds = V <= kLdsBins;
+  const bool lds_fill = V <= kLdsBins / 2;
+  if (lds) {
+    bag_count_kernel<true><<<(unsigned)nblk, 256, sizeof(int32_t) * V, st>>>(a, n_slots, per, w.count);
+  } else {
+    bag_count_kernel<false><<<(unsigned)nblk, 256, 0, st>>>(a, n_slots, per, w.count);
+  }
   bag_scan_kernel<<<1, 1024, 0, st>>>(w.count, V, w.rowptr, w.cursor);
-  bag_fill_kernel<<<g_slots, 256, 0, st>>>(a, n_slots, w.rowptr, w.cursor, w.ent_src, w.ent_w, w.ent_v);
+  if (lds_fill) {
+    bag_fill_kernel<true><<<(unsigned)nblk, 256, 2 * sizeof(int32_t) * V, st>>>(a, n_slots, per, w.rowptr, w.cursor,
+                                                                               w.ent_src, w.ent_w, w.ent_v);
+  } else {
+    bag_fill_kernel<false><<<(unsigned)nblk, 256, 0, st>>>(a, n_slots, per, w.rowptr, w.cursor, w.ent_src, w.ent_w,
+                                                          w.ent_v);
+  }
   if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM) {
-    bag_subject_sum_kernel<<<dim3((unsigned)cdiv(D, 256), (unsigned)batch->B), 256, 0, st>>>(*batch, bk.G, dsrc, ld,
-                                                                                           D, w.sub);
+    if (hipMemsetAsync(w.sub, 0, sizeof(float) * batch->B * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    bag_subject_sum_kernel<<<dim3((unsigned)batch->B, kSubChunks), 256, 0, st>>>(*batch, bk.G, dsrc, ld, D, w.sub);
   }
   ESGPT_LAUNCH_CHECK();
   // The number of entries is data-dependent (not known on the host without a sync): launch for the upper bound;
