@@ -105,9 +105,8 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     bc = CONFIGS[args.config]
-    # Reference defaults keep dropout 0.1 on inputs/residuals; attention-probability dropout runs at 0.0 (the
-    # attention kernels do not implement it yet — DESIGN.md).
-    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.1, resid_dropout=0.1)
+    # Reference defaults: dropout 0.1 on inputs, residuals and attention probabilities (config.py:517-519).
+    cfg = bc.model_config(attention_dropout=0.1, input_dropout=0.1, resid_dropout=0.1)
     torch.manual_seed(0)
     from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
     from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
@@ -195,7 +194,7 @@ def main():
         "config": {"workload": f"{args.config}: {bc.name}", "model": "CIPPT" if "CI" in bc.name else "NAPPT",
                    "global_batch": bc.batch_size * world, "seq_len": bc.seq_len, "parallelism": f"dp{world}",
                    "events_per_step_per_gpu": round(sum(events) / n_batches, 1), "hip_graph": use_graph,
-                   "dropout": {"input": 0.1, "resid": 0.1, "attention": 0.0}},
+                   "dropout": {"input": 0.1, "resid": 0.1, "attention": 0.1}},
         "roofline": roofline,
         "roofline_aux": aux,
     }

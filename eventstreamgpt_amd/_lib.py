@@ -69,10 +69,10 @@ SIGNATURES = {
     "esgpt_embed_bag_bwd_workspace": (_sz, [_PB, _i64, _i64, _i64]),
     "esgpt_embed_bag_bwd": (_int, [_PB, _PK, _int, _int, _f32, _f32, _vp, _i64, _i64, _i64, _vp, _vp, _sz, _vp]),
     "esgpt_attn_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
-                              _i64, _int, _vp]),
+                              _i64, _f32, _vp, _int, _vp]),
     "esgpt_attn_bwd_workspace": (_sz, [_i64, _i64, _i64]),
     "esgpt_attn_bwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
-                              _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp, _sz, _vp]),
+                              _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _int, _vp, _sz, _vp]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),
     "esgpt_output_loss": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
                                  _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),

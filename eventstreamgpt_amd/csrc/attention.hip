@@ -8,17 +8,20 @@
 //   * attn_*_mfma (attention_mfma.hip) — bf16 v_mfma_f32_32x32x16_bf16 flash kernels for hd in {32, 64, 128}.
 //
 // Semantics (both): s_ij = q_i . k_j in f32 with NO 1/sqrt(hd) scaling; key j is visible to query i (at key
-// position p_i = i + Lk - Lq) iff j <= p_i, (local) p_i - j < window, and key_mask[j]; softmax in f32;
+// position p_i = i + Lk - Lq) iff j <= p_i, (local) p_i - j < window, and key_mask[j]; softmax in f32; the
+// attention-probability dropout of the reference (transformer.py:208, nn.Dropout on attn_weights) multiplies
+// p_ij by keep_ij / (1 - p) with keep regenerated from a counter hash of (seed, (bh*Lq + i)*Lk + j);
 // rows of padded queries (query_mask[i] == 0) are zeros and carry no gradient.
+#include <stdlib.h>
+
 #include "common.h"
 
 using namespace esgpt;
 
 namespace {
 
-template <typename T>
-__device__ __forceinline__ void load_row(const T* __restrict__ p, int hd, float* __restrict__ r, int HDP) {
-  for (int d = 0; d < HDP; ++d) r[d] = (d < hd) ? to_f32(p[d]) : 0.f;
+__device__ __forceinline__ uint64_t elem_index(int64_t bh, int64_t Lq, int64_t Lk, int64_t qi, int64_t kj) {
+  return ((uint64_t)(bh * Lq + qi)) * (uint64_t)Lk + (uint64_t)kj;
 }
 
 template <typename T, int HDP>
@@ -27,10 +30,12 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ q,
                                                         T* __restrict__ o, int64_t ld_o, float* __restrict__ lse,
                                                         const uint8_t* __restrict__ kmask,
                                                         const uint8_t* __restrict__ qmask, int64_t B, int64_t H,
-                                                        int64_t Lq, int64_t Lk, int hd, int64_t window) {
+                                                        int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
+                                                        const uint64_t* __restrict__ seed) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = B * H * Lq;
   if (tid >= total) return;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
   const int64_t qi = tid % Lq;
   const int64_t bh = tid / Lq;
   const int64_t h = bh % H, b = bh / H;
@@ -65,11 +70,12 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ q,
       } else {
         p = expf(s - m);
       }
-      l += p;
+      l += p;  // the softmax normaliser uses the undropped probabilities
+      const float pd = dr.p > 0.f ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, j)) : p;
       const T* vp = v + (b * Lk + j) * ld_in + h * hd;
 #pragma unroll
       for (int d = 0; d < HDP; ++d)
-        if (d < hd) acc[d] = fmaf(p, to_f32(vp[d]), acc[d]);
+        if (d < hd) acc[d] = fmaf(pd, to_f32(vp[d]), acc[d]);
     }
   }
   const bool ok = qvalid && l > 0.f;
@@ -81,16 +87,18 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ q,
   lse[bh * Lq + qi] = ok ? m + logf(l) : 0.f;
 }
 
-// dQ (and delta = rowsum(dO * O)) — one lane per query.
+// dQ (and delta = rowsum(dO * O)) — one lane per query. With dropout: dS = P o (dP_drop o keep / (1-p) - delta).
 template <typename T, int HDP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_generic(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
     const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, int64_t ld_d,
-    float* __restrict__ delta, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window) {
+    float* __restrict__ delta, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
+    const uint64_t* __restrict__ seed) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = B * H * Lq;
   if (tid >= total) return;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
   const int64_t qi = tid % Lq;
   const int64_t bh = tid / Lq;
   const int64_t h = bh % H, b = bh / H;
@@ -125,6 +133,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_generic(
           dpv = fmaf(dor[d], to_f32(vp[d]), dpv);
         }
       }
+      if (dr.p > 0.f) dpv *= dropout_mult(dr, elem_index(bh, Lq, Lk, qi, j));
       const float p = expf(s - ls);
       const float ds = p * (dpv - dl);
 #pragma unroll
@@ -144,10 +153,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
     const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse, const float* __restrict__ delta,
     const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dk, T* __restrict__ dv,
-    int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window) {
+    int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
+    const uint64_t* __restrict__ seed) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = B * H * Lk;
   if (tid >= total) return;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
   const int64_t kj = tid % Lk;
   const int64_t bh = tid / Lk;
   const int64_t h = bh % H, b = bh / H;
@@ -179,12 +190,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(
           dpv = fmaf(to_f32(dop[d]), vr[d], dpv);
         }
       }
+      const float keep = dr.p > 0.f ? dropout_mult(dr, elem_index(bh, Lq, Lk, i, kj)) : 1.f;
       const float p = expf(s - lse[bh * Lq + i]);
-      const float ds = p * (dpv - delta[bh * Lq + i]);
+      const float ds = p * (dpv * keep - delta[bh * Lq + i]);
+      const float pd = p * keep;
 #pragma unroll
       for (int d = 0; d < HDP; ++d) {
         if (d < hd) {
-          dva[d] = fmaf(p, to_f32(dop[d]), dva[d]);
+          dva[d] = fmaf(pd, to_f32(dop[d]), dva[d]);
           dka[d] = fmaf(ds, to_f32(qp[d]), dka[d]);
         }
       }
@@ -202,14 +215,14 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(
 }
 
 template <typename T>
-int launch_fwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o, float* lse,
-                       const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                       int64_t hd, int64_t window, hipStream_t st) {
+int launch_fwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
+                       float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
+                       int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st) {
   const int64_t total = B * H * Lq;
   dim3 grid((unsigned)cdiv(total, 256)), block(256);
-#define FWD(HDP)                                                                                                \
-  attn_fwd_generic<T, HDP><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (T*)o, ld_o, lse, \
-                                                   kmask, qmask, B, H, Lq, Lk, (int)hd, window)
+#define FWD(HDP)                                                                                                  \
+  attn_fwd_generic<T, HDP><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (T*)o, ld_o, \
+                                                   lse, kmask, qmask, B, H, Lq, Lk, (int)hd, window, drop_p, seed)
   if (hd <= 8) FWD(8);
   else if (hd <= 16) FWD(16);
   else if (hd <= 32) FWD(32);
@@ -220,19 +233,21 @@ int launch_fwd_generic(const void* q, const void* k, const void* v, int64_t ld_i
 }
 
 template <typename T>
-int launch_bwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
-                       const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask,
-                       void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                       int64_t hd, int64_t window, float* delta, hipStream_t st) {
+int launch_bwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                       int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
+                       const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
+                       int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                       float* delta, hipStream_t st) {
   dim3 gq((unsigned)cdiv(B * H * Lq, 256)), gk((unsigned)cdiv(B * H * Lk, 256)), block(256);
 #define BWD(HDP)                                                                                                   \
   do {                                                                                                             \
-    attn_bwd_dq_generic<T, HDP><<<gq, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o,   \
-                                                      ld_o, (const T*)dout, ld_do, lse, kmask, qmask, (T*)dq, ld_d, \
-                                                      delta, B, H, Lq, Lk, (int)hd, window);                       \
-    attn_bwd_dkv_generic<T, HDP><<<gk, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq,          \
+    attn_bwd_dq_generic<T, HDP><<<gq, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq,             \
+                                                      (const T*)o, ld_o, (const T*)dout, ld_do, lse, kmask, qmask,  \
+                                                      (T*)dq, ld_d, delta, B, H, Lq, Lk, (int)hd, window, drop_p,   \
+                                                      seed);                                                       \
+    attn_bwd_dkv_generic<T, HDP><<<gk, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq,           \
                                                        (const T*)dout, ld_do, lse, delta, kmask, qmask, (T*)dk,     \
-                                                       (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window);               \
+                                                       (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed);  \
   } while (0)
   if (hd <= 8) BWD(8);
   else if (hd <= 16) BWD(16);
@@ -246,13 +261,14 @@ int launch_bwd_generic(const void* q, const void* k, const void* v, int64_t ld_i
 }  // namespace
 
 // MFMA path (attention_mfma.hip).
-int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o, float* lse,
-                        const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                        int64_t hd, int64_t window, hipStream_t st);
-int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
-                        const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask,
-                        void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                        int64_t hd, int64_t window, float* delta, hipStream_t st);
+int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
+                        float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
+                        int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st);
+int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                        int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
+                        const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
+                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                        float* delta, hipStream_t st);
 bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o);
 
 static int g_force_generic = -1;
@@ -268,43 +284,46 @@ static bool force_generic() {
 extern "C" {
 
 int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
-                   float* lse,
-                   const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
-                   int64_t hd, int64_t window, int dtype, void* stream) {
+                   float* lse, const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
+                   int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
+                   void* stream) {
   ESGPT_REQUIRE(q && k && v && o && lse && hd > 0 && hd <= 128 && Lq <= Lk && Lq >= 0 && window >= 0 && tq >= Lq);
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   if (B * H * Lq == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
-    return esgpt_attn_fwd_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window, st);
+    return esgpt_attn_fwd_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
+                               dropout_p, seed, st);
   if (dtype == ESGPT_F32)
     return launch_fwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
-                                     st);
-  return launch_fwd_generic<bf16>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window, st);
+                                     dropout_p, seed, st);
+  return launch_fwd_generic<bf16>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
+                                  dropout_p, seed, st);
 }
 
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq) { return sizeof(float) * (size_t)(B * H * Lq); }
 
 int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
-                   int64_t ld_o,
-                   const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                   int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
                    const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
-                   int64_t Lq, int64_t Lk, int64_t hd, int64_t window, int dtype, void* workspace,
-                   size_t workspace_bytes, void* stream) {
+                   int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
+                   int dtype, void* workspace, size_t workspace_bytes, void* stream) {
   ESGPT_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv && hd > 0 && hd <= 128 && Lq <= Lk);
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   ESGPT_REQUIRE(workspace && workspace_bytes >= esgpt_attn_bwd_workspace(B, H, Lq));
   if (B * H * Lk == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   float* delta = (float*)workspace;
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
-    return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv, ld_dqkv, B,
-                               H, Lq, Lk, hd, window, delta, st);
+    return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
+                               ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);
   if (dtype == ESGPT_F32)
     return launch_bwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
-                                     ld_dqkv, B, H, Lq, Lk, hd, window, delta, st);
+                                     ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);
   return launch_bwd_generic<bf16>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
-                                  ld_dqkv, B, H, Lq, Lk, hd, window, delta, st);
+                                  ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);
 }
 
 }  // extern "C"

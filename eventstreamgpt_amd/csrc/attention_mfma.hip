@@ -91,6 +91,11 @@ __device__ __forceinline__ bool allowed(int key, int qpos, int window) {
   return key <= qpos && (window == 0 || qpos - key < window);
 }
 
+// Dropout element counter, identical to the generic kernels': (bh * Lq + q) * Lk + key.
+__device__ __forceinline__ uint64_t elem_index(int bh, int Lq, int Lk, int qi, int kj) {
+  return ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk + (uint64_t)kj;
+}
+
 // ------------------------------------------------------------------------------------------------------------
 template <int HD>
 __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __restrict__ q,
@@ -100,7 +105,8 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
                                                                float* __restrict__ lse,
                                                                const uint8_t* __restrict__ kmask,
                                                                const uint8_t* __restrict__ qmask, int H, int Lq,
-                                                               int Lk, int window) {
+                                                               int Lk, int window, float drop_p,
+                                                               const uint64_t* __restrict__ seed) {
   constexpr int NP = HD + 8, TP = ROWS + 4;
   __shared__ __attribute__((aligned(16))) __bf16 sK[ROWS * NP];
   __shared__ __attribute__((aligned(16))) __bf16 sVt[HD * TP];
@@ -109,6 +115,7 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
   const int qb = blockIdx.x * ROWS;
   const int qi = qb + wave * 32 + r;
@@ -178,8 +185,10 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = (s[c][i] == -INFINITY) ? 0.f : expf(s[c][i] - mnew);
-        s[c][i] = p;
-        rs += p;
+        rs += p;  // normaliser over undropped probabilities
+        s[c][i] = (dr.p > 0.f && p != 0.f)
+                      ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + 32 * c + acc_row(i, h)))
+                      : p;
       }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
@@ -224,7 +233,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_dq_mfma_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
-    __bf16* __restrict__ dq, int64_t ld_d, float* __restrict__ delta, int H, int Lq, int Lk, int window) {
+    __bf16* __restrict__ dq, int64_t ld_d, float* __restrict__ delta, int H, int Lq, int Lk, int window,
+    float drop_p, const uint64_t* __restrict__ seed) {
   constexpr int NP = HD + 8, TP = ROWS + 4;
   __shared__ __attribute__((aligned(16))) __bf16 sK[ROWS * NP];
   __shared__ __attribute__((aligned(16))) __bf16 sV[ROWS * NP];
@@ -234,6 +244,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_dq_mfma_kernel(
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
   const int qb = blockIdx.x * ROWS;
   const int qi = qb + wave * 32 + r;
@@ -301,7 +312,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_dq_mfma_kernel(
         const int kr = 32 * c + acc_row(i, h);
         const bool ok = qvalid && sKm[kr] && allowed(kt + kr, qpos, window);
         const float p = ok ? expf(st[i] - ls) : 0.f;
-        st[i] = p * (dpt[i] - dl);
+        const float keep = (dr.p > 0.f && ok) ? dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + kr)) : 1.f;
+        st[i] = p * (dpt[i] * keep - dl);
       }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
@@ -334,7 +346,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_dkv_mfma_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, const __bf16* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     const float* __restrict__ delta, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
-    __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d, int H, int Lq, int Lk, int window) {
+    __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d, int H, int Lq, int Lk, int window,
+    float drop_p, const uint64_t* __restrict__ seed) {
   constexpr int NP = HD + 8, TP = ROWS + 4;
   __shared__ __attribute__((aligned(16))) __bf16 sQ[ROWS * NP];
   __shared__ __attribute__((aligned(16))) __bf16 sD[ROWS * NP];
@@ -346,6 +359,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_dkv_mfma_kernel(
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
   const int kb = blockIdx.x * ROWS;
   const int kk = kb + wave * 32 + r;
@@ -406,8 +420,9 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_dkv_mfma_kernel(
         const int qpos = qt + qr + off;
         const bool ok = kvalid && sQm[qr] && allowed(kk, qpos, window);
         const float p = ok ? expf(s[i] - sL[qr]) : 0.f;
-        s[i] = p;
-        dp[i] = p * (dp[i] - sDl[qr]);
+        const float keep = (dr.p > 0.f && ok) ? dropout_mult(dr, elem_index(bh, Lq, Lk, qt + qr, kk)) : 1.f;
+        s[i] = p * keep;
+        dp[i] = p * (dp[i] * keep - sDl[qr]);
       }
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
@@ -453,48 +468,53 @@ bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, i
 template <int HD>
 static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, int64_t ld_in,
                        int64_t tq, void* o, int64_t ld_o, float* lse, const uint8_t* kmask, const uint8_t* qmask,
-                       int64_t H, int64_t Lq, int64_t Lk, int64_t window) {
+                       int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed) {
   attn_fwd_mfma_kernel<HD><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                                                            ld_in, tq, (__bf16*)o, ld_o, lse, kmask, qmask, (int)H,
-                                                           (int)Lq, (int)Lk, (int)window);
+                                                           (int)Lq, (int)Lk, (int)window, drop_p, seed);
 }
 
 template <int HD>
 static void launch_bwd(dim3 gq, dim3 gk, hipStream_t st, const void* q, const void* k, const void* v, int64_t ld_in,
                        int64_t tq, const void* o, int64_t ld_o, const void* dout, int64_t ld_do, const float* lse,
                        const uint8_t* kmask, const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d,
-                       int64_t H, int64_t Lq, int64_t Lk, int64_t window, float* delta) {
+                       int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed,
+                       float* delta) {
   attn_bwd_dq_mfma_kernel<HD><<<gq, dim3(THREADS), 0, st>>>(
       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
-      ld_do, lse, kmask, qmask, (__bf16*)dq, ld_d, delta, (int)H, (int)Lq, (int)Lk, (int)window);
+      ld_do, lse, kmask, qmask, (__bf16*)dq, ld_d, delta, (int)H, (int)Lq, (int)Lk, (int)window, drop_p, seed);
   attn_bwd_dkv_mfma_kernel<HD><<<gk, dim3(THREADS), 0, st>>>(
       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)dout, ld_do, lse, delta, kmask,
-      qmask, (__bf16*)dk, (__bf16*)dv, ld_d, (int)H, (int)Lq, (int)Lk, (int)window);
+      qmask, (__bf16*)dk, (__bf16*)dv, ld_d, (int)H, (int)Lq, (int)Lk, (int)window, drop_p, seed);
 }
 
 int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
                         float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
-                        int64_t Lk, int64_t hd, int64_t window, hipStream_t st) {
+                        int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st) {
   dim3 grid((unsigned)cdiv(Lq, ROWS), (unsigned)(B * H));
-  if (hd == 32) launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window);
-  else if (hd == 64) launch_fwd<64>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window);
-  else launch_fwd<128>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window);
+  if (hd == 32)
+    launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+  else if (hd == 64)
+    launch_fwd<64>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+  else
+    launch_fwd<128>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
   return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
 }
 
 int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                         int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
                         const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
-                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float* delta, hipStream_t st) {
+                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                        float* delta, hipStream_t st) {
   dim3 gq((unsigned)cdiv(Lq, ROWS), (unsigned)(B * H)), gk((unsigned)cdiv(Lk, ROWS), (unsigned)(B * H));
   if (hd == 32)
     launch_bwd<32>(gq, gk, st, q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, H, Lq,
-                   Lk, window, delta);
+                   Lk, window, drop_p, seed, delta);
   else if (hd == 64)
     launch_bwd<64>(gq, gk, st, q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, H, Lq,
-                   Lk, window, delta);
+                   Lk, window, drop_p, seed, delta);
   else
     launch_bwd<128>(gq, gk, st, q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, H, Lq,
-                    Lk, window, delta);
+                    Lk, window, drop_p, seed, delta);
   return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
 }

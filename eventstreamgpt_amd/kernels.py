@@ -274,11 +274,27 @@ class EmbedEpilogueFn(torch.autograd.Function):
 # ----------------------------------------------------------------------------------------------------------------
 # Attention
 # ----------------------------------------------------------------------------------------------------------------
+_SEEDS: dict[int, torch.Tensor] = {}
+
+
+def next_dropout_seed(device: torch.device) -> torch.Tensor:
+    """Device-side dropout seed: a per-device int64 counter advanced on the stream at every use (so HIP-graph
+    replays draw fresh masks); returns a snapshot tensor for the backward pass."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    c = _SEEDS.get(idx)
+    if c is None:
+        c = torch.full((1,), (torch.initial_seed() * 0x2545F491) & 0x7FFFFFFFFFFF, dtype=torch.int64, device=device)
+        _SEEDS[idx] = c
+    snap = c.clone()
+    c.add_(1)
+    return snap
+
+
 class AttentionFn(torch.autograd.Function):
     """Packed-QKV causal/local attention. qkv: [Bs, T, 3D] (q | k | v), returns o: [Bs, T - skf, D]."""
 
     @staticmethod
-    def forward(ctx, qkv, key_mask, query_mask, H: int, window: int, static_kv_first: bool):
+    def forward(ctx, qkv, key_mask, query_mask, H: int, window: int, static_kv_first: bool, dropout_p: float = 0.0):
         lib = L.load()
         qkv = qkv.contiguous()
         Bs, T, D3 = qkv.shape
@@ -290,20 +306,21 @@ class AttentionFn(torch.autograd.Function):
         base = qkv.data_ptr()
         o = torch.empty(Bs, Lq, D, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(Bs, H, Lq, dtype=torch.float32, device=qkv.device)
+        seed = next_dropout_seed(qkv.device) if dropout_p > 0 else None
         with _timed("attn_fwd"):
             st = lib.esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
                                     lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask), Bs, H, Lq, Lk, hd, window,
-                                    L.dtype_code(qkv.dtype), L.stream())
+                                    float(dropout_p), L.ptr(seed), L.dtype_code(qkv.dtype), L.stream())
         L.check(st, "attn_fwd")
-        ctx.save_for_backward(qkv, o, lse, key_mask, query_mask)
-        ctx.cfg = (H, window, skf)
+        ctx.save_for_backward(qkv, o, lse, key_mask, query_mask, seed)
+        ctx.cfg = (H, window, skf, float(dropout_p))
         return o
 
     @staticmethod
     def backward(ctx, do):
         lib = L.load()
-        qkv, o, lse, key_mask, query_mask = ctx.saved_tensors
-        H, window, skf = ctx.cfg
+        qkv, o, lse, key_mask, query_mask, seed = ctx.saved_tensors
+        H, window, skf, dropout_p = ctx.cfg
         do = do.contiguous().to(qkv.dtype)
         Bs, T, D3 = qkv.shape
         D = D3 // 3
@@ -318,9 +335,10 @@ class AttentionFn(torch.autograd.Function):
             st = lib.esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
                                     do.data_ptr(), D, lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask),
                                     dbase + skf * D3 * es, dbase + D * es, dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd,
-                                    window, L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes, L.stream())
+                                    window, dropout_p, L.ptr(seed), L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes,
+                                    L.stream())
         L.check(st, "attn_bwd")
-        return dqkv, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None
 
 
 # ----------------------------------------------------------------------------------------------------------------

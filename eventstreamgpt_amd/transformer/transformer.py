@@ -93,11 +93,6 @@ class InnerSelfAttention(nn.Module):
         _unsupported(output_attentions, "output_attentions")
         if head_mask is not None:
             raise NotImplementedError("eventstreamgpt_amd: head_mask is not supported")
-        if self.training and self.attn_dropout_p > 0:
-            raise NotImplementedError(
-                "eventstreamgpt_amd: attention-probability dropout is not implemented in the attention kernels "
-                "yet; set attention_dropout=0.0 (input/residual dropout are supported)."
-            )
         if key_padding_mask is None and attention_mask is not None:
             key_padding_mask = attention_mask.reshape(attention_mask.shape[0], -1) == 0
         w = torch.cat([self.q_proj.weight, self.k_proj.weight, self.v_proj.weight], dim=0)
@@ -106,7 +101,8 @@ class InnerSelfAttention(nn.Module):
         kpm = None if key_padding_mask is None else key_padding_mask.contiguous()
         # Query padding = key padding for self-attention over events (rows are zeroed downstream).
         qpm = None if (kpm is None or static_kv_first) else kpm
-        o = AttentionFn.apply(qkv, kpm, qpm, self.num_heads, window, static_kv_first)
+        p = self.attn_dropout_p if self.training else 0.0
+        o = AttentionFn.apply(qkv, kpm, qpm, self.num_heads, window, static_kv_first, p)
         out = self.resid_dropout(self.out_proj(o))
         return out, {"present_key_value": None}
 

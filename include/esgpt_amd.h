@@ -114,18 +114,21 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
  * Query i sits at key position i + (Lk - Lq): static_kv_first (transformer.py:256-259) drops query 0, i.e. pass
  * q = packed + ld_in, tq = Lk, Lq = Lk - 1 (the caller zero-fills the dq rows of token 0).
  * Rows whose query is padded (query_mask == 0) are written as zeros (the reference zeroes them downstream,
- * transformer.py:818-823). lse: f32 [B,H,Lq] (natural-log softmax normaliser, for the backward). */
+ * transformer.py:818-823). lse: f32 [B,H,Lq] (natural-log softmax normaliser, for the backward).
+ * Attention-probability dropout (transformer.py:208): dropout_p in [0,1); keep(b,h,i,j) is a counter hash of
+ * (*seed, (bh*Lq + i)*Lk + j) (device uint64, read at kernel start; the backward must see the same value). */
 int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
                    float* lse,
                    const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
-                   int64_t Lk, int64_t hd, int64_t window, int dtype, void* stream);
+                   int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
+                   void* stream);
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq);
 int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                    int64_t ld_o,
                    const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
                    const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
-                   int64_t Lq, int64_t Lk, int64_t hd, int64_t window, int dtype, void* workspace,
-                   size_t workspace_bytes, void* stream);
+                   int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
+                   int dtype, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- Output layer losses -----------------------------------------------------------------------------------
  * GenerativeOutputLayerBase.get_{classification,regression,TTE}_outputs (model_output.py:1311-1721) with

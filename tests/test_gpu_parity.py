@@ -156,3 +156,69 @@ def test_full_step_bf16_matches_oracle(cfg_name):
     ref = O.model_losses(p, cfg, batch)
     assert out.loss.item() == pytest.approx(ref["loss"].item(), rel=1e-2)
     out.loss.backward()
+
+
+def _np_keep(seed: int, B: int, H: int, Lq: int, Lk: int, p: float):
+    """Host restatement of the kernels' dropout keep-mask (splitmix64 of (seed, (bh*Lq+i)*Lk+j))."""
+    import numpy as np
+
+    with np.errstate(over="ignore"):
+        idx = np.arange(B * H * Lq * Lk, dtype=np.uint64)
+        z = np.uint64(seed) + (idx + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        h = (z >> np.uint64(32)).astype(np.uint64)
+    thresh = int(np.float32(p) * np.float32(4294967296.0))
+    return torch.from_numpy((h >= thresh).reshape(B, H, Lq, Lk))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 96, 4, 64, 0, False), (3, 40, 2, 16, 7, False), (4, 6, 2, 64, 0, True)])
+def test_attention_dropout(shape, dtype):
+    """Attention-probability dropout: kernels vs softmax -> mask/(1-p) -> P.V with the same counter-hash mask."""
+    from eventstreamgpt_amd import kernels as K
+    from eventstreamgpt_amd.kernels import AttentionFn
+
+    p = 0.2
+    B, T, H, hd, window, skf = shape
+    qkv = _rand_qkv(B, T, H, hd, dtype, seed=5 + T)
+    km = None
+    if not skf:
+        lens = torch.randint(max(1, T // 2), T + 1, (B,), generator=torch.Generator().manual_seed(3))
+        km = (torch.arange(T)[None] < lens[:, None]).to(DEV)
+    dev = torch.device(DEV)
+    idx = torch.cuda.current_device()
+    if idx not in K._SEEDS:
+        K.next_dropout_seed(dev)
+    seed = int(K._SEEDS[idx].item())
+    x = qkv.clone().requires_grad_(True)
+    o = AttentionFn.apply(x, km, km, H, window, skf, p)
+
+    Lq, Lk = T - (1 if skf else 0), T
+    keep = _np_keep(seed, B, H, Lq, Lk, p).to(DEV)
+    ref_in = qkv.float().clone().requires_grad_(True)
+    D = H * hd
+    q, k, v = ref_in.split(D, -1)
+    q = q.view(B, T, H, hd).transpose(1, 2)
+    k = k.view(B, T, H, hd).transpose(1, 2)
+    v = v.view(B, T, H, hd).transpose(1, 2)
+    if skf:
+        q = q[:, :, 1:]
+    s = q @ k.transpose(-1, -2)
+    band = O.causal_band(Lk, "local" if window else "global", window).to(DEV)[Lk - Lq:]
+    s = torch.where(band, s, torch.tensor(O.FMIN, device=DEV))
+    if km is not None:
+        s = s + (1.0 - km[:, None, None, :].float()) * O.FMIN
+    a = s.softmax(-1) * keep / (1 - p)
+    ref = (a @ v).transpose(1, 2).reshape(B, Lq, D)
+    if km is not None:
+        ref = torch.where(km[..., None], ref, torch.zeros_like(ref))
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(o.float().detach(), ref.detach()) < tol
+    go = torch.randn_like(ref)
+    if km is not None:
+        go = torch.where(km[..., None], go, torch.zeros_like(go))
+    o.backward(go.to(dtype))
+    ref.backward(go)
+    assert rel_err(x.grad.float(), ref_in.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
