@@ -73,6 +73,14 @@ SIGNATURES = {
     "esgpt_attn_bwd_workspace": (_sz, [_i64, _i64, _i64]),
     "esgpt_attn_bwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                               _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _int, _vp, _sz, _vp]),
+    "esgpt_residual_ln_partials": (_i64, [_i64]),
+    "esgpt_residual_ln_fwd": (_int, [_vp, _vp, _int, _vp, _vp, _f32, _vp, _vp, _vp, _f32, _i64, _i64, _vp, _vp, _int,
+                                     _vp, _vp, _vp]),
+    "esgpt_residual_ln_bwd": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i64, _i64, _vp, _vp, _int,
+                                     _vp, _vp, _vp]),
+    "esgpt_bias_act_fwd": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int, _vp]),
+    "esgpt_bias_act_partials": (_i64, [_i64]),
+    "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),
     "esgpt_output_loss": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
                                  _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),

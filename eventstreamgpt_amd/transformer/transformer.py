@@ -287,6 +287,17 @@ class ConditionallyIndependentPointProcessTransformer(StructuredTransformerPreTr
                 return_dict: bool | None = None):
         _unsupported(past is not None or bool(use_cache), "use_cache/past")
         _unsupported(bool(output_attentions), "output_attentions")
+        from ..fused import ci_encoder_fused, fused_supported
+
+        if (input_embeds is None and batch is not None and batch.event_mask is not None and not output_hidden_states
+                and fused_supported(self)):
+            il = self.input_layer
+            emb = il.data_embedding_layer.embed(batch, time_layer=il.time_embedding_layer).squeeze(2)
+            hidden = ci_encoder_fused(self, batch, emb, il.embedding_dropout.p)
+            if return_dict is False:
+                return (hidden,)
+            return TransformerOutputWithPast(last_hidden_state=hidden, past_key_values=None, hidden_states=None,
+                                             attentions=None)
         if input_embeds is None:
             assert batch is not None
             input_embeds = self.input_layer(batch)

@@ -166,6 +166,32 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
                       int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
                       void* workspace, size_t workspace_bytes, int32_t* err, void* stream);
 
+/* ---- Fused block elementwise stages ---------------------------------------------------------------------
+ * InnerBlock residual adds + resid_dropout + the CI encoder's per-block event mask + the following LayerNorm
+ * (transformer.py:350-461, 810-831) in one pass:
+ *   h = row_mask ? x + dropout(y + bias) : 0   (f32, x/y/bias/row_mask/h optional)
+ *   out = LayerNorm(h; ln_w, ln_b, eps)          (y_dtype / out_dtype: ESGPT_F32 or ESGPT_BF16); mean/rstd f32 [N].
+ * Backward: dh = row_mask ? dh_in + LN'(dout) : 0; dx = dh; dy = dropout'(dh); part: f32 workspace
+ * [esgpt_residual_ln_partials(N), 3, D]; sums: f32 [3, D] = (d ln_w, d ln_b, d bias). Dropout keep-mask as in
+ * attention, counter = row*D + col. */
+int64_t esgpt_residual_ln_partials(int64_t N);
+int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
+                          float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
+                          int64_t N, int64_t D, float* h, void* out, int out_dtype, float* mean, float* rstd,
+                          void* stream);
+int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, const float* h, const float* mean,
+                          const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
+                          const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
+                          float* sums, void* stream);
+/* g = act(f + bias) (InnerMLP c_fc bias + activation, transformer.py:378-391); act: 0 exact-erf GELU ("gelu"),
+ * 1 tanh GELU ("gelu_new"), 2 ReLU. Backward: dz = dg * act'(f + bias), dbias = column sums (part workspace
+ * f32 [esgpt_bias_act_partials(N), F]). */
+int esgpt_bias_act_fwd(const void* f, const float* bias, int act, int64_t N, int64_t F, void* g, int dtype,
+                       void* stream);
+int64_t esgpt_bias_act_partials(int64_t N);
+int esgpt_bias_act_bwd(const void* dg, const void* f, const float* bias, int act, int64_t N, int64_t F, void* dz,
+                       float* part, float* dbias, int dtype, void* stream);
+
 /* ---- Misc ----------------------------------------------------------------------------------------------- */
 const char* esgpt_version(void);
 int esgpt_device_arch_ok(void); /* 1 if device 0 is gfx950 */

@@ -32,8 +32,20 @@ def _clean_errors():
     check_errors()
 
 
+@pytest.fixture(params=[True, False], ids=["fused", "modules"])
+def fused_mode(request):
+    from eventstreamgpt_amd import fused
+
+    old = fused.ENABLED
+    fused.ENABLED = request.param
+    yield request.param
+    fused.ENABLED = old
+
+
 @pytest.mark.parametrize("name", CASES)
-def test_model_matches_reference_f32(name):
+def test_model_matches_reference_f32(name, fused_mode):
+    if not fused_mode and name.startswith("na_"):
+        pytest.skip("NA encoder has a single (module) path")
     fx, cfg, batch = load_case(name)
     m = _model(cfg).to(DEV)
     m.load_state_dict(fx["state_dict"])
@@ -222,3 +234,64 @@ def test_attention_dropout(shape, dtype):
     o.backward(go.to(dtype))
     ref.backward(go)
     assert rel_err(x.grad.float(), ref_in.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.0, 0.25])
+def test_residual_ln_kernel(dtype, p):
+    """ResidualLN (h = mask ? x + dropout(y + b) : 0; out = LN(h)) vs its PyTorch composition."""
+    from eventstreamgpt_amd import kernels as K
+    from eventstreamgpt_amd.fused import ResidualLNFn
+
+    g = torch.Generator().manual_seed(7)
+    N, D = 300, 256
+    x = torch.randn(N, D, generator=g).to(DEV)
+    y = torch.randn(N, D, generator=g).to(DEV, dtype)
+    b = torch.randn(D, generator=g).to(DEV)
+    w = (1 + 0.1 * torch.randn(D, generator=g)).to(DEV)
+    lb = (0.1 * torch.randn(D, generator=g)).to(DEV)
+    mask = (torch.rand(N, generator=g) > 0.2).to(DEV)
+    dev = torch.device(DEV)
+    idx = torch.cuda.current_device()
+    if idx not in K._SEEDS:
+        K.next_dropout_seed(dev)
+    seed = int(K._SEEDS[idx].item())
+    xs = [t.clone().requires_grad_(True) for t in (x, y, b, w, lb)]
+    h, out = ResidualLNFn.apply(xs[0], xs[1], xs[2], xs[3], xs[4], mask, p, 1e-5, dtype)
+    rs = [t.float().clone().requires_grad_(True) for t in (x, y, b, w, lb)]
+    keep = _np_keep(seed, 1, 1, N, D, p)[0, 0].to(DEV) if p > 0 else torch.ones(N, D, dtype=torch.bool, device=DEV)
+    t = (rs[1] + rs[2]) * keep / (1 - p)
+    hr = torch.where(mask[:, None], rs[0] + t, torch.zeros_like(rs[0]))
+    outr = F_layer_norm(hr, rs[3], rs[4])
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(h.detach(), hr.detach()) < 1e-5 * (1 if dtype == torch.float32 else 1e3)
+    assert rel_err(out.float().detach(), outr.detach()) < tol
+    gh = torch.randn(N, D, device=DEV)
+    go = torch.randn(N, D, device=DEV)
+    torch.autograd.backward([h, out], [gh, go.to(dtype)])
+    torch.autograd.backward([hr, outr], [gh, go.to(dtype).float()])
+    for a, r in zip(xs, rs):
+        assert rel_err(a.grad.float(), r.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+
+
+def F_layer_norm(h, w, b):
+    return torch.nn.functional.layer_norm(h, (h.shape[-1],), w, b, 1e-5)
+
+
+@pytest.mark.parametrize("act,name", [(0, "gelu"), (1, "gelu_new"), (2, "relu")])
+def test_bias_act_kernel(act, name):
+    from eventstreamgpt_amd.fused import BiasActFn
+
+    g = torch.Generator().manual_seed(11)
+    f = torch.randn(77, 1024, generator=g).to(DEV).requires_grad_(True)
+    b = torch.randn(1024, generator=g).to(DEV).requires_grad_(True)
+    out = BiasActFn.apply(f, b, act)
+    fr, br = f.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    z = fr + br
+    ref = {0: torch.nn.functional.gelu(z), 1: torch.nn.functional.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
+    assert rel_err(out.detach(), ref.detach()) < 1e-5
+    go = torch.randn_like(ref)
+    out.backward(go)
+    ref.backward(go)
+    assert rel_err(f.grad, fr.grad) < 1e-5
+    assert rel_err(b.grad, br.grad) < 1e-5
