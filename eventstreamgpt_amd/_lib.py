@@ -81,6 +81,8 @@ SIGNATURES = {
     "esgpt_bias_act_fwd": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int, _vp]),
     "esgpt_bias_act_partials": (_i64, [_i64]),
     "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),
+    "esgpt_column_sum_partials": (_i64, [_i64]),
+    "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),
     "esgpt_output_loss": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
                                  _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),

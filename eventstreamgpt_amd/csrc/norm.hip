@@ -4,24 +4,44 @@
 //   residual_ln_fwd   h   = rowmask ? x + dropout(y + bias) : 0          (f32 residual stream)
 //                     out = LayerNorm(h) * w + b                         (f32 or bf16: the next GEMM's operand)
 //   residual_ln_bwd   dh  = rowmask ? dh_in + LN'(dout) : 0 ; dx = dh ; dy = dropout'(dh)
-//                     per-block column partials of dgamma, dbeta, dbias
-//   bias_act_fwd/bwd  g = act(f + bias) (exact-erf GELU, tanh GELU or ReLU), dbias partials
+//                     per-block column partials of dgamma, dbeta, dbias -> colsum
+//   bias_act_fwd/bwd  g = act(f + bias) (exact-erf GELU, tanh GELU or ReLU), dbias partials -> colsum
 //
-// One wave per row (D <= 1024: each lane owns D/64 columns), statistics in registers (two-pass mean / variance,
-// biased variance as torch.nn.LayerNorm). HBM-bound: fwd reads x (4B), y (2-4B), writes h (4B) + out (2-4B) per
-// element; the backward reads dh_in, dout, h and writes dx, dy.
+// Layout: one wave per row; lane l owns the 4-column chunks {4l + 256k}, loaded as 16-B (f32) / 8-B (bf16)
+// vectors; statistics in registers (two-pass mean / variance, biased variance as torch.nn.LayerNorm).
+// HBM-bound: fwd reads x (4 B) + y (2-4 B), writes h (4 B) + out (2-4 B) per element.
 #include "common.h"
 
 using namespace esgpt;
 
 namespace {
 
-constexpr int kRowsPerWave = 4;
 constexpr int kWaves = 4;
-constexpr int kMaxPerLane = 16;  // D <= 1024
+constexpr int kMaxChunks = 4;      // 4-column chunks per lane: D <= 1024
+constexpr int kBwdRowsPerWave = 2;  // backward: rows per wave (fewer partial rows for the column sums)
 
-template <typename T>
-__device__ __forceinline__ float ld(const T* p, int64_t i) { return to_f32(p[i]); }
+struct V4 {
+  float v[4];
+};
+
+__device__ __forceinline__ V4 load4(const float* p) {
+  const float4 t = *reinterpret_cast<const float4*>(p);
+  return V4{{t.x, t.y, t.z, t.w}};
+}
+__device__ __forceinline__ V4 load4(const bf16* p) {
+  const uint2 t = *reinterpret_cast<const uint2*>(p);
+  return V4{{bf16_bits_to_f32((uint16_t)(t.x & 0xffff)), bf16_bits_to_f32((uint16_t)(t.x >> 16)),
+             bf16_bits_to_f32((uint16_t)(t.y & 0xffff)), bf16_bits_to_f32((uint16_t)(t.y >> 16))}};
+}
+__device__ __forceinline__ void store4(float* p, const V4& a) {
+  *reinterpret_cast<float4*>(p) = make_float4(a.v[0], a.v[1], a.v[2], a.v[3]);
+}
+__device__ __forceinline__ void store4(bf16* p, const V4& a) {
+  uint2 t;
+  t.x = (uint32_t)f32_to_bf16_bits(a.v[0]) | ((uint32_t)f32_to_bf16_bits(a.v[1]) << 16);
+  t.y = (uint32_t)f32_to_bf16_bits(a.v[2]) | ((uint32_t)f32_to_bf16_bits(a.v[3]) << 16);
+  *reinterpret_cast<uint2*>(p) = t;
+}
 
 __device__ __forceinline__ uint64_t drop_idx(int64_t row, int64_t D, int64_t col) { return (uint64_t)(row * D + col); }
 
@@ -36,51 +56,59 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
                                                               float* __restrict__ rstd_o) {
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int per = (int)((D + 63) / 64);
-  for (int rr = 0; rr < kRowsPerWave; ++rr) {
-    const int64_t row = ((int64_t)blockIdx.x * kWaves + wave) * kRowsPerWave + rr;
-    if (row >= N) return;
-    const bool keep_row = rmask == nullptr || rmask[row] != 0;
-    float v[kMaxPerLane];
-    float s = 0.f;
+  const int64_t row = (int64_t)blockIdx.x * kWaves + wave;
+  if (row >= N) return;
+  const bool keep_row = rmask == nullptr || rmask[row] != 0;
+  V4 v[kMaxChunks];
+  float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
-      const int64_t c = lane + 64 * k;
-      v[k] = 0.f;
-      if (k < per && c < D && keep_row) {
-        float a = x ? x[row * D + c] : 0.f;
-        if (y) {
-          float t = ld(y, row * D + c) + (bias ? bias[c] : 0.f);
-          if (dr.p > 0.f) t *= dropout_mult(dr, drop_idx(row, D, c));
-          a += t;
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int64_t c = 4 * lane + 256 * k;
+    v[k] = V4{{0.f, 0.f, 0.f, 0.f}};
+    if (c < D && keep_row) {
+      if (x) v[k] = load4(x + row * D + c);
+      if (y) {
+        V4 t = load4(y + row * D + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float u = t.v[j] + (bias ? bias[c + j] : 0.f);
+          if (dr.p > 0.f) u *= dropout_mult(dr, drop_idx(row, D, c + j));
+          v[k].v[j] += u;
         }
-        v[k] = a;
       }
-      s += v[k];
-    }
-    const float mean = wave_sum(s) / (float)D;
-    float q = 0.f;
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
-      const int64_t c = lane + 64 * k;
-      if (k < per && c < D) {
-        const float d = v[k] - mean;
+      for (int j = 0; j < 4; ++j) s += v[k].v[j];
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int64_t c = 4 * lane + 256 * k;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[k].v[j] - mean;
         q += d * d;
       }
     }
-    const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
-      const int64_t c = lane + 64 * k;
-      if (k < per && c < D) {
-        if (h) h[row * D + c] = v[k];
-        out[row * D + c] = from_f32<TO>((v[k] - mean) * rstd * w[c] + b[c]);
-      }
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int64_t c = 4 * lane + 256 * k;
+    if (c < D) {
+      if (h) store4(h + row * D + c, v[k]);
+      const V4 wv = load4(w + c), bv = load4(b + c);
+      V4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o.v[j] = (v[k].v[j] - mean) * rstd * wv.v[j] + bv.v[j];
+      store4(out + row * D + c, o);
     }
-    if (lane == 0) {
-      mean_o[row] = mean;
-      rstd_o[row] = rstd;
-    }
+  }
+  if (lane == 0) {
+    mean_o[row] = mean;
+    rstd_o[row] = rstd;
   }
 }
 
@@ -91,78 +119,109 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     const float* __restrict__ mean_i, const float* __restrict__ rstd_i, const float* __restrict__ w,
     const uint8_t* __restrict__ rmask, float drop_p, const uint64_t* __restrict__ seed, int64_t N, int64_t D,
     float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part) {
-  __shared__ float s_part[kWaves][3][256];
+  __shared__ float s_part[kWaves][3][4 * 64];
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int per = (int)((D + 63) / 64);
-  float pg[kMaxPerLane], pb[kMaxPerLane], py[kMaxPerLane];
+  V4 pg[kMaxChunks], pb[kMaxChunks], py[kMaxChunks], wv[kMaxChunks];
 #pragma unroll
-  for (int k = 0; k < kMaxPerLane; ++k) pg[k] = pb[k] = py[k] = 0.f;
-  for (int rr = 0; rr < kRowsPerWave; ++rr) {
-    const int64_t row = ((int64_t)blockIdx.x * kWaves + wave) * kRowsPerWave + rr;
+  for (int k = 0; k < kMaxChunks; ++k) {
+    pg[k] = pb[k] = py[k] = V4{{0.f, 0.f, 0.f, 0.f}};
+    const int64_t c = 4 * lane + 256 * k;
+    wv[k] = (c < D) ? load4(w + c) : V4{{0.f, 0.f, 0.f, 0.f}};
+  }
+  for (int rr = 0; rr < kBwdRowsPerWave; ++rr) {
+    const int64_t row = ((int64_t)blockIdx.x * kWaves + wave) * kBwdRowsPerWave + rr;
     if (row >= N) break;
     const float mean = mean_i[row], rstd = rstd_i[row];
     const bool keep_row = rmask == nullptr || rmask[row] != 0;
-    float xh[kMaxPerLane], g[kMaxPerLane];
+    V4 xh[kMaxChunks], g[kMaxChunks];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
-      const int64_t c = lane + 64 * k;
-      xh[k] = g[k] = 0.f;
-      if (k < per && c < D) {
-        const float dv = ld(dout, row * D + c);
-        xh[k] = (h[row * D + c] - mean) * rstd;
-        g[k] = dv * w[c];
-        pg[k] += dv * xh[k];
-        pb[k] += dv;
-        sg += g[k];
-        sgx += g[k] * xh[k];
+    for (int k = 0; k < kMaxChunks; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      xh[k] = g[k] = V4{{0.f, 0.f, 0.f, 0.f}};
+      if (c < D) {
+        const V4 dv = load4(dout + row * D + c);
+        const V4 hv = load4(h + row * D + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xh[k].v[j] = (hv.v[j] - mean) * rstd;
+          g[k].v[j] = dv.v[j] * wv[k].v[j];
+          pg[k].v[j] += dv.v[j] * xh[k].v[j];
+          pb[k].v[j] += dv.v[j];
+          sg += g[k].v[j];
+          sgx += g[k].v[j] * xh[k].v[j];
+        }
       }
     }
     sg = wave_sum(sg) / (float)D;
     sgx = wave_sum(sgx) / (float)D;
 #pragma unroll
-    for (int k = 0; k < kMaxPerLane; ++k) {
-      const int64_t c = lane + 64 * k;
-      if (k < per && c < D) {
-        float d = rstd * (g[k] - sg - xh[k] * sgx);
-        if (dh_in) d += dh_in[row * D + c];
-        if (!keep_row) d = 0.f;
-        if (dx) dx[row * D + c] = d;
+    for (int k = 0; k < kMaxChunks; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      if (c < D) {
+        V4 d;
+        const V4 din = dh_in ? load4(dh_in + row * D + c) : V4{{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float t = rstd * (g[k].v[j] - sg - xh[k].v[j] * sgx) + din.v[j];
+          d.v[j] = keep_row ? t : 0.f;
+        }
+        if (dx) store4(dx + row * D + c, d);
         if (dy) {
-          const float t = dr.p > 0.f ? d * dropout_mult(dr, drop_idx(row, D, c)) : d;
-          dy[row * D + c] = from_f32<TY>(t);
-          py[k] += t;
+          V4 e;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            e.v[j] = dr.p > 0.f ? d.v[j] * dropout_mult(dr, drop_idx(row, D, c + j)) : d.v[j];
+            py[k].v[j] += e.v[j];
+          }
+          store4(dy + row * D + c, e);
         }
       }
     }
   }
-  // combine the 4 waves' column partials, one row of partials per (block, quantity)
-  for (int k = 0; k < per; ++k) {
-    const int64_t c0 = 64 * k;
-    s_part[wave][0][lane] = pg[k];
-    s_part[wave][1][lane] = pb[k];
-    s_part[wave][2][lane] = py[k];
+  // combine the 4 waves' column partials
+#pragma unroll
+  for (int k = 0; k < kMaxChunks; ++k) {
+    const int64_t c0 = 256 * k;
+    if (c0 >= D) break;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s_part[wave][0][4 * lane + j] = pg[k].v[j];
+      s_part[wave][1][4 * lane + j] = pb[k].v[j];
+      s_part[wave][2][4 * lane + j] = py[k].v[j];
+    }
     __syncthreads();
-    if (wave == 0) {
-      for (int qd = 0; qd < 3; ++qd) {
-        const float t = s_part[0][qd][lane] + s_part[1][qd][lane] + s_part[2][qd][lane] + s_part[3][qd][lane];
-        if (c0 + lane < D) part[((int64_t)blockIdx.x * 3 + qd) * D + c0 + lane] = t;
+    for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
+      const int qd = i / 256, cc = i % 256;
+      if (c0 + cc < D) {
+        const float t = s_part[0][qd][cc] + s_part[1][qd][cc] + s_part[2][qd][cc] + s_part[3][qd][cc];
+        part[((int64_t)blockIdx.x * 3 + qd) * D + c0 + cc] = t;
       }
     }
     __syncthreads();
   }
 }
 
-// Column sums of part[nb, 3, D] -> sums[3, D] (deterministic: fixed block order).
-__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int64_t nb, int64_t Q, int64_t D,
-                                                     float* __restrict__ sums) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= Q * D) return;
-  const int64_t qd = i / D, c = i % D;
-  float s = 0.f;
-  for (int64_t b = 0; b < nb; ++b) s += part[(b * Q + qd) * D + c];
-  sums[i] = s;
+// sums[q, c] = sum_b part[b, q, c]. Block: 64 columns x 16 row groups (1024 threads); fixed order -> deterministic.
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int64_t nb, int64_t QD,
+                                                      float* __restrict__ sums) {
+  __shared__ float s[16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + cl;
+  float a = 0.f;
+  if (i < QD) {
+#pragma unroll 4
+    for (int64_t b = grp; b < nb; b += 16) a += part[b * QD + i];
+  }
+  s[grp][cl] = a;
+  __syncthreads();
+  if (grp == 0 && i < QD) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += s[g][cl];
+    sums[i] = t;
+  }
 }
 
 __device__ __forceinline__ float act_f(float z, int act) {
@@ -189,43 +248,76 @@ __device__ __forceinline__ float act_d(float z, int act) {
   return z > 0.f ? 1.f : 0.f;
 }
 
+// 4 consecutive elements per thread (F % 4 == 0).
 template <typename T>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__ f, const float* __restrict__ bias,
                                                            int act, int64_t N, int64_t F, T* __restrict__ g) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i >= N * F) return;
+  const int64_t c = i % F;
+  const V4 z = load4(f + i);
+  const V4 bv = load4(bias + c);
+  V4 o;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t j = i + k;
-    if (j < N * F) g[j] = from_f32<T>(act_f(to_f32(f[j]) + bias[j % F], act));
-  }
+  for (int j = 0; j < 4; ++j) o.v[j] = act_f(z.v[j] + bv.v[j], act);
+  store4(g + i, o);
 }
 
-// dz = dg * act'(f + bias); part[blockIdx.x, F] column partials of dz over this block's rows.
+// dz = dg * act'(f + bias); part[blockIdx.y, F] column partials of dz over this block's kActRows rows.
+// Block: 64 threads x 4 columns = 256 columns, 4 row groups (LDS combine); grid (F/256, N/kActRows).
 constexpr int kActRows = 32;
 template <typename T>
 __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__ dg, const T* __restrict__ f,
                                                            const float* __restrict__ bias, int act, int64_t N,
                                                            int64_t F, T* __restrict__ dz, float* __restrict__ part) {
-  const int64_t r0 = (int64_t)blockIdx.x * kActRows;
-  for (int64_t c = threadIdx.x; c < F; c += blockDim.x) {
-    float s = 0.f;
-    const float bc = bias[c];
-    for (int64_t r = r0; r < min(N, r0 + kActRows); ++r) {
-      const float z = to_f32(f[r * F + c]) + bc;
-      const float d = to_f32(dg[r * F + c]) * act_d(z, act);
-      dz[r * F + c] = from_f32<T>(d);
-      s += d;
+  __shared__ float s_part[4][256];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 256 + 4 * cl;
+  const int64_t r0 = (int64_t)blockIdx.y * kActRows, r1 = min(N, r0 + kActRows);
+  V4 s{{0.f, 0.f, 0.f, 0.f}};
+  if (c < F) {
+    const V4 bv = load4(bias + c);
+#pragma unroll 2
+    for (int64_t r = r0 + grp; r < r1; r += 4) {
+      const V4 z = load4(f + r * F + c);
+      const V4 d = load4(dg + r * F + c);
+      V4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o.v[j] = d.v[j] * act_d(z.v[j] + bv.v[j], act);
+        s.v[j] += o.v[j];
+      }
+      store4(dz + r * F + c, o);
     }
-    part[(int64_t)blockIdx.x * F + c] = s;
   }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) s_part[grp][4 * cl + j] = s.v[j];
+  __syncthreads();
+  const int64_t cc = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (cc < F)
+    part[(int64_t)blockIdx.y * F + cc] =
+        s_part[0][threadIdx.x] + s_part[1][threadIdx.x] + s_part[2][threadIdx.x] + s_part[3][threadIdx.x];
+}
+
+// part[blockIdx.y, c] = sum over this block's kColRows rows of x[:, c]; thread per column (coalesced along c).
+constexpr int kColRows = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void column_partial_kernel(const T* __restrict__ x, int64_t N, int64_t F,
+                                                             float* __restrict__ part) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= F) return;
+  const int64_t r0 = (int64_t)blockIdx.y * kColRows, r1 = min(N, r0 + kColRows);
+  float s = 0.f;
+#pragma unroll 8
+  for (int64_t r = r0; r < r1; ++r) s += to_f32(x[r * F + c]);
+  part[(int64_t)blockIdx.y * F + c] = s;
 }
 
 template <typename TY, typename TO>
 void launch_ln_fwd(const float* x, const void* y, const float* bias, const uint8_t* rmask, float p, const uint64_t* seed,
                    const float* w, const float* b, float eps, int64_t N, int64_t D, float* h, void* out, float* mean,
                    float* rstd, hipStream_t st) {
-  const unsigned grid = (unsigned)cdiv(N, kWaves * kRowsPerWave);
+  const unsigned grid = (unsigned)cdiv(N, kWaves);
   residual_ln_fwd_kernel<TY, TO><<<grid, 256, 0, st>>>(x, (const TY*)y, bias, rmask, p, seed, w, b, eps, N, D, h,
                                                        (TO*)out, mean, rstd);
 }
@@ -234,7 +326,7 @@ template <typename TY, typename TO>
 void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const float* mean, const float* rstd,
                    const float* w, const uint8_t* rmask, float p, const uint64_t* seed, int64_t N, int64_t D, float* dx,
                    void* dy, float* part, hipStream_t st) {
-  const unsigned grid = (unsigned)cdiv(N, kWaves * kRowsPerWave);
+  const unsigned grid = (unsigned)cdiv(N, kWaves * kBwdRowsPerWave);
   residual_ln_bwd_kernel<TY, TO><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, seed, N,
                                                        D, dx, (TY*)dy, part);
 }
@@ -243,13 +335,13 @@ void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const f
 
 extern "C" {
 
-int64_t esgpt_residual_ln_partials(int64_t N) { return cdiv(N, kWaves * kRowsPerWave); }
+int64_t esgpt_residual_ln_partials(int64_t N) { return cdiv(N, kWaves * kBwdRowsPerWave); }
 
 int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
                           float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
                           int64_t N, int64_t D, float* h, void* out, int out_dtype, float* mean, float* rstd,
                           void* stream) {
-  ESGPT_REQUIRE(ln_w && ln_b && out && mean && rstd && D > 0 && D <= 64 * kMaxPerLane && (x || y));
+  ESGPT_REQUIRE(ln_w && ln_b && out && mean && rstd && D > 0 && D % 4 == 0 && D <= 256 * kMaxChunks && (x || y));
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   if (N == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
@@ -270,7 +362,7 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
                           const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
                           const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
                           float* sums, void* stream) {
-  ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && sums && D > 0 && D <= 64 * kMaxPerLane);
+  ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && sums && D > 0 && D % 4 == 0 && D <= 256 * kMaxChunks);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   if (N == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
@@ -284,14 +376,14 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
   else launch_ln_bwd<bf16, bf16>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx, dy, part,
                                  st);
   const int64_t nb = esgpt_residual_ln_partials(N);
-  colsum_kernel<<<(unsigned)cdiv(3 * D, 256), 256, 0, st>>>(part, nb, 3, D, sums);
+  colsum_kernel<<<(unsigned)cdiv(3 * D, 64), 1024, 0, st>>>(part, nb, 3 * D, sums);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
 
 int esgpt_bias_act_fwd(const void* f, const float* bias, int act, int64_t N, int64_t F, void* g, int dtype,
                        void* stream) {
-  ESGPT_REQUIRE(f && bias && g && (dtype == ESGPT_F32 || dtype == ESGPT_BF16) && act >= 0 && act <= 2);
+  ESGPT_REQUIRE(f && bias && g && (dtype == ESGPT_F32 || dtype == ESGPT_BF16) && act >= 0 && act <= 2 && F % 4 == 0);
   if (N * F == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   const unsigned grid = (unsigned)cdiv(cdiv(N * F, 4), 256);
@@ -305,16 +397,36 @@ int64_t esgpt_bias_act_partials(int64_t N) { return cdiv(N, kActRows); }
 
 int esgpt_bias_act_bwd(const void* dg, const void* f, const float* bias, int act, int64_t N, int64_t F, void* dz,
                        float* part, float* dbias, int dtype, void* stream) {
-  ESGPT_REQUIRE(dg && f && bias && dz && part && dbias && (dtype == ESGPT_F32 || dtype == ESGPT_BF16));
+  ESGPT_REQUIRE(dg && f && bias && dz && part && dbias && (dtype == ESGPT_F32 || dtype == ESGPT_BF16) && F % 4 == 0);
   if (N * F == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
-  const unsigned grid = (unsigned)esgpt_bias_act_partials(N);
+  const int64_t nb = esgpt_bias_act_partials(N);
+  dim3 grid((unsigned)cdiv(F, 256), (unsigned)nb);
   if (dtype == ESGPT_F32)
     bias_act_bwd_kernel<float><<<grid, 256, 0, st>>>((const float*)dg, (const float*)f, bias, act, N, F, (float*)dz,
                                                      part);
   else
     bias_act_bwd_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)dg, (const bf16*)f, bias, act, N, F, (bf16*)dz, part);
-  colsum_kernel<<<(unsigned)cdiv(F, 256), 256, 0, st>>>(part, grid, 1, F, dbias);
+  colsum_kernel<<<(unsigned)cdiv(F, 64), 1024, 0, st>>>(part, nb, F, dbias);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int64_t esgpt_column_sum_partials(int64_t N) { return cdiv(N, kColRows); }
+
+int esgpt_column_sum(const void* x, int dtype, int64_t N, int64_t F, float* part, float* out, void* stream) {
+  ESGPT_REQUIRE(x && part && out && (dtype == ESGPT_F32 || dtype == ESGPT_BF16) && N >= 0 && F >= 0);
+  if (F == 0) return ESGPT_OK;
+  hipStream_t st = as_stream(stream);
+  if (N == 0) {
+    if (hipMemsetAsync(out, 0, F * sizeof(float), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    return ESGPT_OK;
+  }
+  const int64_t nb = esgpt_column_sum_partials(N);
+  dim3 grid((unsigned)cdiv(F, 256), (unsigned)nb);
+  if (dtype == ESGPT_F32) column_partial_kernel<float><<<grid, 256, 0, st>>>((const float*)x, N, F, part);
+  else column_partial_kernel<bf16><<<grid, 256, 0, st>>>((const bf16*)x, N, F, part);
+  colsum_kernel<<<(unsigned)cdiv(F, 64), 1024, 0, st>>>(part, nb, F, out);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

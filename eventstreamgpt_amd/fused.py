@@ -45,6 +45,7 @@ class ResidualLNFn(torch.autograd.Function):
                                            rstd.data_ptr(), L.stream())
         L.check(st, "residual_ln_fwd")
         ctx.save_for_backward(h, mean, rstd, ln_w, row_mask, seed)
+        ctx.set_materialize_grads(False)
         ctx.meta = (x is not None, y is not None, bias is not None, y_dtype, out_dtype, float(p))
         return h, out
 
@@ -117,35 +118,102 @@ ENABLED = True  # tests flip this to exercise the module-by-module path
 
 def fused_supported(encoder) -> bool:
     cfg = encoder.config
-    return ENABLED and cfg.activation_function in _ACTS and cfg.hidden_size <= 1024
+    return (ENABLED and cfg.activation_function in _ACTS and cfg.hidden_size <= 1024 and cfg.hidden_size % 4 == 0
+            and cfg.intermediate_size % 4 == 0)
+
+
+class WeightShadowFn(torch.autograd.Function):
+    """One cat + one cast of the block GEMM weights into a flat compute-dtype buffer, returned as per-layer views
+    (Wqkv, Wo, Wfc, Wproj); q, k, v are adjacent so the packed [3D, D] weight is a view. Backward gathers the view
+    gradients into one flat f32 buffer (one cat + one cast) and hands each parameter a view of it, instead of
+    autograd's per-slice zero-fill + add of the whole flat buffer."""
+
+    @staticmethod
+    def forward(ctx, dtype, n_layers: int, *ws):
+        flat = torch.cat([w.reshape(-1) for w in ws])
+        if dtype != torch.float32:
+            flat = flat.to(dtype)
+        shapes = [w.shape for w in ws]
+        outs, off = [], 0
+        for layer in range(n_layers):
+            q, k, v, o, fc, pj = shapes[6 * layer: 6 * layer + 6]
+            nqkv = q.numel() + k.numel() + v.numel()
+            outs.append(flat[off: off + nqkv].view(q[0] + k[0] + v[0], q[1]))
+            off += nqkv
+            for sh in (o, fc, pj):
+                outs.append(flat[off: off + sh.numel()].view(sh))
+                off += sh.numel()
+        ctx.shapes = shapes
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ref = next(g for g in gs if g is not None)
+        outs_numel = []
+        for layer in range(len(ctx.shapes) // 6):
+            q, k, v, o, fc, pj = ctx.shapes[6 * layer: 6 * layer + 6]
+            outs_numel += [q.numel() + k.numel() + v.numel(), o.numel(), fc.numel(), pj.numel()]
+        parts = [g.reshape(-1) if g is not None else torch.zeros(n, dtype=ref.dtype, device=ref.device)
+                 for g, n in zip(gs, outs_numel)]
+        gflat = torch.cat(parts)
+        if gflat.dtype != torch.float32:
+            gflat = gflat.float()
+        grads, off = [], 0
+        for sh in ctx.shapes:
+            grads.append(gflat[off: off + sh.numel()].view(sh))
+            off += sh.numel()
+        return (None, None, *grads)
 
 
 def weight_shadow(blocks, dtype):
-    """One cat (+ one cast) of every block GEMM weight; returns per-layer views (Wqkv, Wo, Wfc, Wproj)."""
-    ws, shapes = [], []
+    """Per-layer (Wqkv, Wo, Wfc, Wproj) compute-dtype views of one flat shadow of every block GEMM weight."""
+    ws = []
     for b in blocks:
         a = b.attn.attention
-        for w in (a.q_proj.weight, a.k_proj.weight, a.v_proj.weight, a.out_proj.weight, b.mlp.c_fc.weight,
-                  b.mlp.c_proj.weight):
-            ws.append(w.reshape(-1))
-            shapes.append(w.shape)
-    flat = torch.cat(ws)
-    if dtype != torch.float32:
-        flat = flat.to(dtype)
-    out, off, i = [], 0, 0
-    for _ in blocks:
-        start = off
-        views = []
-        for _k in range(6):
-            n = shapes[i].numel()
-            views.append(flat[off: off + n].view(shapes[i]))
-            off += n
-            i += 1
-        wq = views[0]
-        # q, k, v are adjacent in the flat buffer: the packed [3D, D] weight is a view, no extra copy.
-        wqkv = flat[start: start + 3 * wq.numel()].view(3 * wq.shape[0], wq.shape[1])
-        out.append((wqkv, views[3], views[4], views[5]))
-    return out
+        ws += [a.q_proj.weight, a.k_proj.weight, a.v_proj.weight, a.out_proj.weight, b.mlp.c_fc.weight,
+               b.mlp.c_proj.weight]
+    outs = WeightShadowFn.apply(dtype, len(blocks), *ws)
+    return [tuple(outs[4 * i: 4 * i + 4]) for i in range(len(blocks))]
+
+
+class LinearBiasFn(torch.autograd.Function):
+    """z = x @ wᵀ + b in x's dtype (bias in the GEMM epilogue); backward takes the bias gradient with the
+    column-sum kernel instead of torch's dim-0 reduction."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        dt = x.dtype
+        wd = w.to(dt)
+        z = F.linear(x, wd, b.to(dt))
+        ctx.save_for_backward(x, wd)
+        ctx.wdtype = w.dtype
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        lib = L.load()
+        x, wd = ctx.saved_tensors
+        dz = dz.contiguous()
+        N, Fo = dz.shape
+        dx = dz @ wd if ctx.needs_input_grad[0] else None
+        dw = (dz.t() @ x).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.needs_input_grad[2]:
+            part = torch.empty(lib.esgpt_column_sum_partials(N) * Fo, dtype=torch.float32, device=dz.device)
+            db = torch.empty(Fo, dtype=torch.float32, device=dz.device)
+            with _timed("column_sum"):
+                st = lib.esgpt_column_sum(dz.data_ptr(), L.dtype_code(dz.dtype), N, Fo, part.data_ptr(),
+                                          db.data_ptr(), L.stream())
+            L.check(st, "column_sum")
+        return dx, dw, db
+
+
+def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``F.linear(x, w, b)`` in the autocast compute dtype with the fused bias-gradient backward (2-D x)."""
+    dt = compute_dtype()
+    with torch.autocast("cuda", enabled=False):
+        return LinearBiasFn.apply(x.to(dt), w, b)
 
 
 def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: float):

@@ -2,9 +2,12 @@
 
 * loss = model(batch).loss (per-rank weighted_loss normalisation, exactly like the reference under DDP);
 * AdamW(lr=init_lr, weight_decay) + transformers' polynomial-decay-with-warmup schedule, stepped every step;
-* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Gradients live in one
-  flat f32 buffer (every ``param.grad`` is a view into it), all-reduced in buckets and divided by world size —
-  the DDP gradient-averaging semantics of the reference's Lightning trainer.
+* gradients are reset to ``None`` before each backward (Lightning's ``zero_grad(set_to_none=True)``), so autograd
+  hands each parameter its gradient without an accumulate-add; parameters without a gradient are skipped by
+  AdamW exactly as in the reference;
+* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Gradients are packed
+  into size-capped flat buckets, all-reduced and divided by world size (the DDP gradient-averaging semantics of
+  the reference's Lightning trainer); a parameter without a gradient contributes zeros.
 * optional HIP-graph capture of forward+backward (static shapes; batches are copied into static buffers).
 """
 from __future__ import annotations
@@ -42,20 +45,17 @@ class TrainStep:
         params = [p for p in model.parameters() if p.requires_grad]
         self.params = params
         dev = params[0].device
-        n = sum(p.numel() for p in params)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
-        for p in params:
-            p.grad = self.flat_grad[off: off + p.numel()].view_as(p)
-            off += p.numel()
-        # buckets in reverse parameter order (the last layers' gradients are final first)
-        self.buckets = []
+        # buckets of parameter indices in reverse order (the last layers' gradients are final first)
+        self.buckets, cur, size = [], [], 0
         lim = int(bucket_mb * 2**20 / 4)
-        end = n
-        while end > 0:
-            start = max(0, end - lim)
-            self.buckets.append((start, end))
-            end = start
+        for i in reversed(range(len(params))):
+            cur.append(i)
+            size += params[i].numel()
+            if size >= lim:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
         fused = dev.type == "cuda"
         self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay, fused=fused)
         total = opt_cfg.max_training_steps or 1_000_000
@@ -79,9 +79,16 @@ class TrainStep:
     def _allreduce(self):
         if not self.distributed:
             return
-        for s, e in self.buckets:
-            dist.all_reduce(self.flat_grad[s:e])
-        self.flat_grad.div_(self.world)
+        for idx in self.buckets:
+            ps = [self.params[i] for i in idx]
+            for p in ps:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            grads = [p.grad for p in ps]
+            flat = torch._utils._flatten_dense_tensors(grads)
+            dist.all_reduce(flat)
+            flat.div_(self.world)
+            torch._foreach_copy_(grads, torch._utils._unflatten_dense_tensors(flat, grads))
 
     def _copy_into_static(self, batch: PytorchBatch):
         for k, v in batch.as_dict().items():
@@ -89,7 +96,7 @@ class TrainStep:
 
     def step(self, batch: PytorchBatch) -> torch.Tensor:
         if not self.use_graph:
-            self.flat_grad.zero_()
+            self.opt.zero_grad(set_to_none=True)
             loss = self._fwd_bwd(batch)
         else:
             if self.graph is None:
@@ -108,13 +115,14 @@ class TrainStep:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):  # warm up allocator / lazy init outside the graph
-                self.flat_grad.zero_()
+                self.opt.zero_grad(set_to_none=True)
                 self._fwd_bwd(self.static_batch)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        # gradients are (re)allocated inside the capture from the graph's pool and stay static across replays
+        self.opt.zero_grad(set_to_none=True)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            self.flat_grad.zero_()
             self.static_loss = self._fwd_bwd(self.static_batch)
         torch.cuda.synchronize()
 

@@ -19,6 +19,7 @@ from transformers.utils import ModelOutput
 from .. import _lib as L
 from ..data.data_embedding_enums import MeasIndexGroupOptions
 from ..data.types import DataModality, PytorchBatch
+from ..fused import linear_bias
 from ..kernels import OutputLossFn, batch_view
 from .config import TimeToEventGenerationHeadType
 from .generative_layers import (
@@ -226,7 +227,7 @@ def fused_ci_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
     w = torch.cat([wc, layer.TTE_layer.proj.weight], 0)
     b = torch.cat([bc, layer.TTE_layer.proj.bias], 0)
     B, Lq, D = encoded.shape
-    z = torch.nn.functional.linear(encoded.reshape(B * Lq, D), w, b)
+    z = linear_bias(encoded.reshape(B * Lq, D), w, b)
     bv = batch_view(batch)
     losses = OutputLossFn.apply(z, None, b, bv, terms, layer._tte_spec(layer._layout["n_content"]), 1, 1)
     return losses, names
@@ -257,10 +258,10 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
     wc, bc = layer.content_weight()
     bv = batch_view(batch)
     if terms:
-        zc = torch.nn.functional.linear(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D), wc, bc)
+        zc = linear_bias(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D), wc, bc)
     else:
         zc = torch.zeros(1, 1, device=encoded.device, dtype=encoded.dtype)
-    zt = torch.nn.functional.linear(encoded[:, :, G - 1, :].reshape(B * Lq, D), layer.TTE_layer.proj.weight,
-                                    layer.TTE_layer.proj.bias)
+    zt = linear_bias(encoded[:, :, G - 1, :].reshape(B * Lq, D), layer.TTE_layer.proj.weight,
+                     layer.TTE_layer.proj.bias)
     losses = OutputLossFn.apply(zc, zt, None, bv, terms, layer._tte_spec(0), 0, max(1, G - 1))
     return losses, names

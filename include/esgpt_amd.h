@@ -173,7 +173,7 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
  *   out = LayerNorm(h; ln_w, ln_b, eps)          (y_dtype / out_dtype: ESGPT_F32 or ESGPT_BF16); mean/rstd f32 [N].
  * Backward: dh = row_mask ? dh_in + LN'(dout) : 0; dx = dh; dy = dropout'(dh); part: f32 workspace
  * [esgpt_residual_ln_partials(N), 3, D]; sums: f32 [3, D] = (d ln_w, d ln_b, d bias). Dropout keep-mask as in
- * attention, counter = row*D + col. */
+ * attention, counter = row*D + col. Requires D % 4 == 0, D <= 1024, 16-B aligned rows. */
 int64_t esgpt_residual_ln_partials(int64_t N);
 int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
                           float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
@@ -185,12 +185,17 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
                           float* sums, void* stream);
 /* g = act(f + bias) (InnerMLP c_fc bias + activation, transformer.py:378-391); act: 0 exact-erf GELU ("gelu"),
  * 1 tanh GELU ("gelu_new"), 2 ReLU. Backward: dz = dg * act'(f + bias), dbias = column sums (part workspace
- * f32 [esgpt_bias_act_partials(N), F]). */
+ * f32 [esgpt_bias_act_partials(N), F]). Requires F % 4 == 0. */
 int esgpt_bias_act_fwd(const void* f, const float* bias, int act, int64_t N, int64_t F, void* g, int dtype,
                        void* stream);
 int64_t esgpt_bias_act_partials(int64_t N);
 int esgpt_bias_act_bwd(const void* dg, const void* f, const float* bias, int act, int64_t N, int64_t F, void* dz,
                        float* part, float* dbias, int dtype, void* stream);
+/* out[c] = sum_r x[r, c] for x [N, F] (ESGPT_F32 / ESGPT_BF16): the bias gradient of a Linear whose output
+ * gradient is x (torch's dim-0 reduction of a bf16 matrix is ~20x off the HBM roofline). Fixed summation order
+ * (deterministic). part: f32 workspace [esgpt_column_sum_partials(N), F]. */
+int64_t esgpt_column_sum_partials(int64_t N);
+int esgpt_column_sum(const void* x, int dtype, int64_t N, int64_t F, float* part, float* out, void* stream);
 
 /* ---- Misc ----------------------------------------------------------------------------------------------- */
 const char* esgpt_version(void);

@@ -1,7 +1,7 @@
 """Data-parallel semantics of eventstreamgpt_amd.train.TrainStep on a 2-rank gloo (CPU) process group.
 
 Each rank computes its own per-rank loss (the reference's per-rank weighted_loss normalisation under DDP) on its
-own subjects; TrainStep all-reduces the flat gradient buffer (bucketed) and divides by the world size. The test
+own subjects; TrainStep all-reduces the gradients in flat buckets and divides by the world size. The test
 checks the updated parameters on both ranks against a single-process AdamW step on the mean of the per-rank
 gradients.
 """
@@ -51,7 +51,7 @@ def _worker(rank, world, port, q):
     torch.manual_seed(0)
     m = Toy()
     ts = TrainStep(m, OptimizationConfig(init_lr=0.1, lr_num_warmup_steps=0, max_training_steps=10),
-                   compute_dtype=torch.float32, bucket_mb=1e-4)  # tiny buckets: exercise several all-reduces
+                   compute_dtype=torch.float32, bucket_mb=2e-5)  # tiny buckets: exercise several all-reduces
     assert ts.distributed and len(ts.buckets) > 1
     ts.step(_data(rank))
     q.put((rank, {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}))  # by value, not shm

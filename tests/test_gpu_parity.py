@@ -236,15 +236,16 @@ def test_attention_dropout(shape, dtype):
     assert rel_err(x.grad.float(), ref_in.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
 
 
+@pytest.mark.parametrize("D", [64, 256, 1024])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("p", [0.0, 0.25])
-def test_residual_ln_kernel(dtype, p):
+def test_residual_ln_kernel(dtype, p, D):
     """ResidualLN (h = mask ? x + dropout(y + b) : 0; out = LN(h)) vs its PyTorch composition."""
     from eventstreamgpt_amd import kernels as K
     from eventstreamgpt_amd.fused import ResidualLNFn
 
     g = torch.Generator().manual_seed(7)
-    N, D = 300, 256
+    N = 300
     x = torch.randn(N, D, generator=g).to(DEV)
     y = torch.randn(N, D, generator=g).to(DEV, dtype)
     b = torch.randn(D, generator=g).to(DEV)
@@ -278,20 +279,60 @@ def F_layer_norm(h, w, b):
     return torch.nn.functional.layer_norm(h, (h.shape[-1],), w, b, 1e-5)
 
 
+@pytest.mark.parametrize("shape", [(77, 1024), (200, 36)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act,name", [(0, "gelu"), (1, "gelu_new"), (2, "relu")])
-def test_bias_act_kernel(act, name):
+def test_bias_act_kernel(act, name, dtype, shape):
     from eventstreamgpt_amd.fused import BiasActFn
 
     g = torch.Generator().manual_seed(11)
-    f = torch.randn(77, 1024, generator=g).to(DEV).requires_grad_(True)
-    b = torch.randn(1024, generator=g).to(DEV).requires_grad_(True)
+    N, Fd = shape
+    f = torch.randn(N, Fd, generator=g).to(DEV, dtype).requires_grad_(True)
+    b = torch.randn(Fd, generator=g).to(DEV).requires_grad_(True)
     out = BiasActFn.apply(f, b, act)
-    fr, br = f.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    fr, br = f.detach().float().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
     z = fr + br
     ref = {0: torch.nn.functional.gelu(z), 1: torch.nn.functional.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
-    assert rel_err(out.detach(), ref.detach()) < 1e-5
-    go = torch.randn_like(ref)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(out.detach().float(), ref.detach()) < tol
+    go = torch.randn(N, Fd, device=DEV).to(dtype)
     out.backward(go)
-    ref.backward(go)
-    assert rel_err(f.grad, fr.grad) < 1e-5
-    assert rel_err(b.grad, br.grad) < 1e-5
+    ref.backward(go.float())
+    assert rel_err(f.grad.float(), fr.grad) < tol
+    assert rel_err(b.grad, br.grad) < tol
+
+
+@pytest.mark.parametrize("N,Fd", [(1, 5), (64, 256), (1000, 1237), (8192, 1210)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_column_sum_kernel(N, Fd, dtype):
+    from eventstreamgpt_amd import _lib as L
+
+    lib = L.load()
+    x = torch.randn(N, Fd, generator=torch.Generator().manual_seed(N)).to(DEV, dtype)
+    part = torch.empty(lib.esgpt_column_sum_partials(N) * Fd, device=DEV)
+    out = torch.empty(Fd, device=DEV)
+    L.check(lib.esgpt_column_sum(x.data_ptr(), L.dtype_code(dtype), N, Fd, part.data_ptr(), out.data_ptr(),
+                                 L.stream()), "column_sum")
+    assert rel_err(out, x.double().sum(0).float()) < 1e-5
+
+
+def test_linear_bias_fn():
+    """LinearBiasFn (GEMM + bias epilogue, column-sum bias gradient) vs F.linear under bf16 autocast."""
+    from eventstreamgpt_amd.fused import linear_bias
+
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(513, 96, generator=g).to(DEV).requires_grad_(True)
+    w = torch.randn(301, 96, generator=g).to(DEV).requires_grad_(True)
+    b = torch.randn(301, generator=g).to(DEV).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        z = linear_bias(x, w, b)
+        xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+        zr = torch.nn.functional.linear(xr, wr, br)
+    assert z.dtype == zr.dtype == torch.bfloat16
+    assert rel_err(z.float(), zr.float()) < 1e-2
+    go = torch.randn(513, 301, device=DEV).bfloat16()
+    z.backward(go)
+    zr.backward(go)
+    for a, r in ((x, xr), (w, wr), (b, br)):
+        assert a.grad.dtype == r.grad.dtype
+        assert rel_err(a.grad.float(), r.grad.float()) < 1e-2
