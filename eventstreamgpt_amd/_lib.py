@@ -23,6 +23,7 @@ EMB_NORMALIZE, EMB_STATIC, EMB_TIME, EMB_CUMSUM, EMB_TIME_ABS = 1, 2, 4, 8, 16
 BAG_JOINT, BAG_CAT, BAG_NUM = 0, 1, 2
 TERM_SINGLE, TERM_MULTI, TERM_MVREG, TERM_UVREG = 1, 2, 3, 4
 TTE_EXP, TTE_LNM = 1, 2
+GEMM_K_CONTIG, GEMM_MN_CONTIG = 0, 1
 MAX_TERMS = 16
 
 _vp = ctypes.c_void_p
@@ -81,6 +82,9 @@ SIGNATURES = {
     "esgpt_bias_act_fwd": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int, _vp]),
     "esgpt_bias_act_partials": (_i64, [_i64]),
     "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),
+    "esgpt_gemm_workspace": (_sz, [_i64, _i64, _i64]),
+    "esgpt_gemm_bf16": (_int, [_int, _vp, _i64, _int, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _int, _int, _vp,
+                               _sz, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),

@@ -97,6 +97,38 @@ __device__ __forceinline__ uint64_t elem_index(int bh, int Lq, int Lk, int qi, i
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// V image row stride for ds_read_b64_tr_b16 (elements): 4 consecutive rows must land 16 dwords apart (mod 64)
+// so that a 32-lane half reading 4 rows x 32 columns touches all 64 banks once.
+template <int HD>
+struct VImg {
+  static constexpr int LD = (HD == 32) ? 32 : 160;
+};
+
+__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)p);
+}
+
+// K/V tile prefetch (global -> registers): 64 rows x HD, HD/16 16-byte chunks per thread per tensor.
+template <int HD>
+__device__ __forceinline__ void load_kv(const __bf16* __restrict__ kb, const __bf16* __restrict__ vb, int64_t ld,
+                                        int kt, int Lk, bf16x8 (&rk)[HD / 16], bf16x8 (&rv)[HD / 16]) {
+  constexpr int CH = HD / 8;
+#pragma unroll
+  for (int i = 0; i < HD / 16; ++i) {
+    const int c = threadIdx.x + THREADS * i;
+    const int row = c / CH, c8 = c % CH, gr = kt + row;
+    const bool ok = gr < Lk;
+    rk[i] = ok ? *reinterpret_cast<const bf16x8*>(kb + (int64_t)gr * ld + c8 * 8) : zero8();
+    rv[i] = ok ? *reinterpret_cast<const bf16x8*>(vb + (int64_t)gr * ld + c8 * 8) : zero8();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Forward. K is staged row-major (A operand of Sᵀ = K·Qᵀ by 16-B row reads); V row-major too, read as the
+// transposed A operand of Oᵀ += Vᵀ·Pᵀ with ds_read_b64_tr_b16 (no transposing LDS writes). The next K/V tile is
+// prefetched into registers while the current one is consumed. Key validity is a 64-bit ballot per tile; tiles
+// that are fully valid and fully inside the causal / local band skip the per-element masks. Softmax in the exp2
+// domain (v_exp_f32).
 template <int HD>
 __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __restrict__ q,
                                                                const __bf16* __restrict__ k,
@@ -107,11 +139,10 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
                                                                const uint8_t* __restrict__ qmask, int H, int Lq,
                                                                int Lk, int window, float drop_p,
                                                                const uint64_t* __restrict__ seed) {
-  constexpr int NP = HD + 8, TP = ROWS + 4;
+  constexpr int NP = HD + 8, VLD = VImg<HD>::LD;
+  constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
   __shared__ __attribute__((aligned(16))) __bf16 sK[ROWS * NP];
-  __shared__ __attribute__((aligned(16))) __bf16 sVt[HD * TP];
-  __shared__ uint8_t sKm[ROWS];
-  __shared__ int sAny;
+  __shared__ __attribute__((aligned(16))) __bf16 sV[ROWS * VLD];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
@@ -122,6 +153,8 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
   const bool qin = qi < Lq;
   const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
   const int qpos = qi + off;
+  const int qlo_w = qb + wave * 32 + off;                // smallest query position of this wave
+  const int qhi_w = min(qb + wave * 32 + 31, Lq - 1) + off;  // largest
 
   bf16x8 qf[HD / 16];
   const __bf16* qrow = q + ((int64_t)b * tq + qi) * ld_in + hh * HD;
@@ -132,29 +165,36 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
   f32x16 oacc[HD / 32];
 #pragma unroll
   for (int dt = 0; dt < HD / 32; ++dt) oacc[dt] = zero16();
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;  // running max (log2 domain) and normaliser
 
   const int qhi = min(Lq, qb + ROWS) - 1;
   const int kmax = min(Lk - 1, qhi + off);
   const int kmin = window ? max(0, qb + off - window + 1) : 0;
   const __bf16* kbase = k + (int64_t)b * Lk * ld_in + hh * HD;
   const __bf16* vbase = v + (int64_t)b * Lk * ld_in + hh * HD;
+  const uint8_t* kmb = kmask ? kmask + (int64_t)b * Lk : nullptr;
 
-  for (int kt = (kmin / ROWS) * ROWS; kt <= kmax; kt += ROWS) {
+  bf16x8 rk[HD / 16], rv[HD / 16];
+  int kt = (kmin / ROWS) * ROWS;
+  load_kv<HD>(kbase, vbase, ld_in, kt, Lk, rk, rv);
+  bool kok = kt + lane < Lk && (kmb == nullptr || kmb[kt + lane] != 0);
+  for (; kt <= kmax; kt += ROWS) {
+    const uint64_t kbits = __ballot(kok);  // identical in both waves (same 64 keys)
     __syncthreads();
-    if (tid == 0) sAny = 0;
-    __syncthreads();
-    if (tid < ROWS) {
-      const int key = kt + tid;
-      const uint8_t ok = key < Lk && (kmask == nullptr || kmask[(int64_t)b * Lk + key] != 0);
-      sKm[tid] = ok;
-      if (ok) sAny = 1;
+    if (kbits) {
+#pragma unroll
+      for (int i = 0; i < HD / 16; ++i) {
+        const int c = tid + THREADS * i, row = c / (HD / 8), c8 = c % (HD / 8);
+        *reinterpret_cast<bf16x8*>(sK + row * NP + c8 * 8) = rk[i];
+        *reinterpret_cast<bf16x8*>(sV + row * VLD + c8 * 8) = rv[i];
+      }
     }
     __syncthreads();
-    if (!sAny) continue;  // fully padded key tile
-    stage_rows<HD>(kbase, ld_in, kt, Lk, sK, nullptr);
-    stage_rows<HD>(vbase, ld_in, kt, Lk, nullptr, sVt);
-    __syncthreads();
+    if (kt + ROWS <= kmax) {
+      load_kv<HD>(kbase, vbase, ld_in, kt + ROWS, Lk, rk, rv);
+      kok = kt + ROWS + lane < Lk && (kmb == nullptr || kmb[kt + ROWS + lane] != 0);
+    }
+    if (!kbits) continue;  // fully padded key tile
 
     f32x16 s[2];
 #pragma unroll
@@ -166,25 +206,37 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
         s[c] = mfma(a, qf[t], s[c]);
       }
     }
+    const bool full = kbits == ~0ull && kt + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - kt < window);
     float mt = -INFINITY;
+    if (full) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kr = 32 * c + acc_row(i, h);
-        const bool ok = qvalid && sKm[kr] && allowed(kt + kr, qpos, window);
-        s[c][i] = ok ? s[c][i] : -INFINITY;
-        mt = fmaxf(mt, s[c][i]);
-      }
+        for (int i = 0; i < 16; ++i) {
+          s[c][i] *= kLog2e;
+          mt = fmaxf(mt, s[c][i]);
+        }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int kr = 32 * c + acc_row(i, h);
+          const bool ok = qvalid && ((kbits >> kr) & 1ull) && allowed(kt + kr, qpos, window);
+          s[c][i] = ok ? s[c][i] * kLog2e : -INFINITY;
+          mt = fmaxf(mt, s[c][i]);
+        }
+    }
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float mnew = fmaxf(m, mt);
-    const float alpha = (mnew == -INFINITY) ? 1.f : expf(m - mnew);
+    const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+    const float msub = (mnew == -INFINITY) ? 0.f : mnew;
     float rs = 0.f;
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = (s[c][i] == -INFINITY) ? 0.f : expf(s[c][i] - mnew);
+        const float p = __builtin_amdgcn_exp2f(s[c][i] - msub);  // exp2(-inf) = 0
         rs += p;  // normaliser over undropped probabilities
         s[c][i] = (dr.p > 0.f && p != 0.f)
                       ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + 32 * c + acc_row(i, h)))
@@ -197,14 +249,22 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
     for (int dt = 0; dt < HD / 32; ++dt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+    // Vᵀ fragment by transposed reads: lane group g (16 lanes) reads keys 16ss + 4(g>>1) + {0..3} (+8) of
+    // columns 32dt + 16(g&1) + {0..15}; the lane receives its column r, in the accumulator's permuted key order.
+    const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int ss = 0; ss < 2; ++ss) {
         const bf16x8 pf = acc_frag(s[c], ss);
+        const int row0 = 32 * c + 16 * ss + 4 * (g >> 1) + q4;
 #pragma unroll
         for (int dt = 0; dt < HD / 32; ++dt) {
-          const bf16x8 vf = perm_frag(sVt, TP, 32 * dt + r, 32 * c, ss, h);
+          const __bf16* vp = sV + row0 * VLD + 32 * dt + 16 * (g & 1) + 4 * p4;
+          const bf16x4 lo = tr_read(vp), hi = tr_read(vp + 8 * VLD);
+          bf16x8 vf;
+          vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
+          vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
           oacc[dt] = mfma(vf, pf, oacc[dt]);
         }
       }
@@ -217,13 +277,13 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
 #pragma unroll
     for (int dt = 0; dt < HD / 32; ++dt)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
+      for (int gg = 0; gg < 4; ++gg) {
         bf16x4 w;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (__bf16)(oacc[dt][4 * g + j] * inv);
-        *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * g + 4 * h) = w;
+        for (int j = 0; j < 4; ++j) w[j] = (__bf16)(oacc[dt][4 * gg + j] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * gg + 4 * h) = w;
       }
-    if (h == 0) lse[(int64_t)bh * Lq + qi] = ok ? m + logf(l) : 0.f;
+    if (h == 0) lse[(int64_t)bh * Lq + qi] = ok ? m * kLn2 + logf(l) : 0.f;
   }
 }
 

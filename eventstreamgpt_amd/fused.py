@@ -122,98 +122,131 @@ def fused_supported(encoder) -> bool:
             and cfg.intermediate_size % 4 == 0)
 
 
-class WeightShadowFn(torch.autograd.Function):
-    """One cat + one cast of the block GEMM weights into a flat compute-dtype buffer, returned as per-layer views
-    (Wqkv, Wo, Wfc, Wproj); q, k, v are adjacent so the packed [3D, D] weight is a view. Backward gathers the view
-    gradients into one flat f32 buffer (one cat + one cast) and hands each parameter a view of it, instead of
-    autograd's per-slice zero-fill + add of the whole flat buffer."""
+# ----------------------------------------------------------------------------------------------------------------
+# Projection GEMMs (csrc/gemm.hip): y = x·Wᵀ (+ b), dx = dy·W, dW = dyᵀ·x written straight to f32
+# ----------------------------------------------------------------------------------------------------------------
+def _gemm(a, a_layout: int, lda: int, b, b_layout: int, ldb: int, M: int, N: int, K: int, out, bias=None,
+          accumulate: bool = False):
+    lib = L.load()
+    nbytes = lib.esgpt_gemm_workspace(M, N, K)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device) if nbytes else None
+    with _timed("gemm"):
+        st = lib.esgpt_gemm_bf16(a_layout, a.data_ptr(), lda, b_layout, b.data_ptr(), ldb, M, N, K, L.ptr(bias),
+                                 out.data_ptr(), out.stride(0), L.dtype_code(out.dtype), int(accumulate), L.ptr(ws),
+                                 nbytes, L.stream())
+    L.check(st, "gemm")
+    return out
+
+
+def gemm_supported(n_tokens: int, d_in: int, d_out: int) -> bool:
+    """Shape constraints of esgpt_gemm_bf16 for the fwd / dx / dW products of one projection."""
+    return n_tokens % 8 == 0 and d_in % 8 == 0 and d_out % 8 == 0
+
+
+def linear_fwd(x, w, bias=None):
+    """y[N, out] = x[N, in] · w[out, in]ᵀ (+ bias f32), bf16."""
+    N, din = x.shape
+    y = torch.empty(N, w.shape[0], dtype=x.dtype, device=x.device)
+    return _gemm(x, L.GEMM_K_CONTIG, din, w, L.GEMM_K_CONTIG, din, N, w.shape[0], din, y, bias)
+
+
+def linear_dx(dy, w):
+    """dx[N, in] = dy[N, out] · w[out, in], bf16."""
+    N, dout = dy.shape
+    dx = torch.empty(N, w.shape[1], dtype=dy.dtype, device=dy.device)
+    return _gemm(dy, L.GEMM_K_CONTIG, dout, w, L.GEMM_MN_CONTIG, w.shape[1], N, w.shape[1], dout, dx)
+
+
+def linear_dw(dy, x):
+    """dW[out, in] = dy[N, out]ᵀ · x[N, in] in f32 (the parameters' dtype; no bf16 rounding of the gradient)."""
+    N, dout = dy.shape
+    din = x.shape[1]
+    dw = torch.empty(dout, din, dtype=torch.float32, device=dy.device)
+    return _gemm(dy, L.GEMM_MN_CONTIG, dout, x, L.GEMM_MN_CONTIG, din, dout, din, N, dw)
+
+
+def column_sum(x):
+    lib = L.load()
+    N, Fo = x.shape
+    part = torch.empty(lib.esgpt_column_sum_partials(N) * Fo, dtype=torch.float32, device=x.device)
+    out = torch.empty(Fo, dtype=torch.float32, device=x.device)
+    with _timed("column_sum"):
+        st = lib.esgpt_column_sum(x.data_ptr(), L.dtype_code(x.dtype), N, Fo, part.data_ptr(), out.data_ptr(),
+                                  L.stream())
+    L.check(st, "column_sum")
+    return out
+
+
+class ProjFn(torch.autograd.Function):
+    """y = x · w_lpᵀ (+ bias) where ``w_lp`` is a no-grad bf16 shadow of the row-concatenation of ``params`` (f32).
+    Backward: dx = dy · w_lp, and dW = dyᵀ · x computed directly in f32 and handed to each parameter as a row
+    slice; dbias by the column-sum kernel. No bf16 gradient round trip, no cast/accumulate kernels."""
 
     @staticmethod
-    def forward(ctx, dtype, n_layers: int, *ws):
-        flat = torch.cat([w.reshape(-1) for w in ws])
-        if dtype != torch.float32:
-            flat = flat.to(dtype)
-        shapes = [w.shape for w in ws]
-        outs, off = [], 0
-        for layer in range(n_layers):
-            q, k, v, o, fc, pj = shapes[6 * layer: 6 * layer + 6]
-            nqkv = q.numel() + k.numel() + v.numel()
-            outs.append(flat[off: off + nqkv].view(q[0] + k[0] + v[0], q[1]))
-            off += nqkv
-            for sh in (o, fc, pj):
-                outs.append(flat[off: off + sh.numel()].view(sh))
-                off += sh.numel()
-        ctx.shapes = shapes
-        ctx.set_materialize_grads(False)
-        return tuple(outs)
+    def forward(ctx, x, w_lp, bias, *params):
+        x = x.contiguous()
+        y = linear_fwd(x, w_lp, bias)
+        ctx.save_for_backward(x, w_lp)
+        ctx.rows = [p.shape[0] for p in params]
+        ctx.has_bias = bias is not None
+        return y
 
     @staticmethod
-    def backward(ctx, *gs):
-        ref = next(g for g in gs if g is not None)
-        outs_numel = []
-        for layer in range(len(ctx.shapes) // 6):
-            q, k, v, o, fc, pj = ctx.shapes[6 * layer: 6 * layer + 6]
-            outs_numel += [q.numel() + k.numel() + v.numel(), o.numel(), fc.numel(), pj.numel()]
-        parts = [g.reshape(-1) if g is not None else torch.zeros(n, dtype=ref.dtype, device=ref.device)
-                 for g, n in zip(gs, outs_numel)]
-        gflat = torch.cat(parts)
-        if gflat.dtype != torch.float32:
-            gflat = gflat.float()
-        grads, off = [], 0
-        for sh in ctx.shapes:
-            grads.append(gflat[off: off + sh.numel()].view(sh))
-            off += sh.numel()
-        return (None, None, *grads)
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = linear_dx(dy, w) if ctx.needs_input_grad[0] else None
+        dw = linear_dw(dy, x)
+        grads = list(torch.split(dw, ctx.rows, 0))
+        db = column_sum(dy) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        return (dx, None, db, *grads)
 
 
+def proj(x, w_lp, bias, params):
+    """Projection through the HIP GEMM when the shapes allow it, else ``F.linear`` on the (differentiable)
+    compute-dtype weights."""
+    if w_lp is not None and w_lp.dtype == torch.bfloat16 and gemm_supported(x.shape[0], x.shape[1], w_lp.shape[0]):
+        return ProjFn.apply(x.to(torch.bfloat16), w_lp, bias, *params)
+    w = params[0] if len(params) == 1 else torch.cat(list(params), 0)
+    dt = x.dtype
+    return F.linear(x, w.to(dt), None if bias is None else bias.to(dt))
+
+
+@torch.no_grad()
 def weight_shadow(blocks, dtype):
-    """Per-layer (Wqkv, Wo, Wfc, Wproj) compute-dtype views of one flat shadow of every block GEMM weight."""
+    """One cat + one cast of every block GEMM weight into a flat compute-dtype buffer (no autograd: the gradients
+    come from ProjFn straight into the f32 parameters). Returns per-layer (Wqkv, Wo, Wfc, Wproj) views; q, k, v
+    are adjacent, so the packed [3D, D] weight is a view."""
     ws = []
     for b in blocks:
         a = b.attn.attention
         ws += [a.q_proj.weight, a.k_proj.weight, a.v_proj.weight, a.out_proj.weight, b.mlp.c_fc.weight,
                b.mlp.c_proj.weight]
-    outs = WeightShadowFn.apply(dtype, len(blocks), *ws)
-    return [tuple(outs[4 * i: 4 * i + 4]) for i in range(len(blocks))]
+    flat = torch.cat([w.reshape(-1) for w in ws]).to(dtype)
+    out, off = [], 0
+    for i in range(len(blocks)):
+        q, k, v, o, fc, pj = ws[6 * i: 6 * i + 6]
+        nqkv = q.numel() + k.numel() + v.numel()
+        views = [flat[off: off + nqkv].view(q.shape[0] + k.shape[0] + v.shape[0], q.shape[1])]
+        off += nqkv
+        for w in (o, fc, pj):
+            views.append(flat[off: off + w.numel()].view(w.shape))
+            off += w.numel()
+        out.append(tuple(views))
+    return out
 
 
-class LinearBiasFn(torch.autograd.Function):
-    """z = x @ wᵀ + b in x's dtype (bias in the GEMM epilogue); backward takes the bias gradient with the
-    column-sum kernel instead of torch's dim-0 reduction."""
-
-    @staticmethod
-    def forward(ctx, x, w, b):
-        dt = x.dtype
-        wd = w.to(dt)
-        z = F.linear(x, wd, b.to(dt))
-        ctx.save_for_backward(x, wd)
-        ctx.wdtype = w.dtype
-        return z
-
-    @staticmethod
-    def backward(ctx, dz):
-        lib = L.load()
-        x, wd = ctx.saved_tensors
-        dz = dz.contiguous()
-        N, Fo = dz.shape
-        dx = dz @ wd if ctx.needs_input_grad[0] else None
-        dw = (dz.t() @ x).to(ctx.wdtype) if ctx.needs_input_grad[1] else None
-        db = None
-        if ctx.needs_input_grad[2]:
-            part = torch.empty(lib.esgpt_column_sum_partials(N) * Fo, dtype=torch.float32, device=dz.device)
-            db = torch.empty(Fo, dtype=torch.float32, device=dz.device)
-            with _timed("column_sum"):
-                st = lib.esgpt_column_sum(dz.data_ptr(), L.dtype_code(dz.dtype), N, Fo, part.data_ptr(),
-                                          db.data_ptr(), L.stream())
-            L.check(st, "column_sum")
-        return dx, dw, db
-
-
-def linear_bias(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``F.linear(x, w, b)`` in the autocast compute dtype with the fused bias-gradient backward (2-D x)."""
+def linear_bias(x: torch.Tensor, params, biases) -> torch.Tensor:
+    """Head projection: x · [params]ᵀ + [biases] in the autocast compute dtype (2-D x). ``params`` / ``biases``
+    are lists of the modules' weights and biases, row-concatenated."""
     dt = compute_dtype()
+    b = torch.cat(list(biases), 0) if len(biases) > 1 else biases[0]
     with torch.autocast("cuda", enabled=False):
-        return LinearBiasFn.apply(x.to(dt), w, b)
+        if dt == torch.bfloat16:
+            with torch.no_grad():
+                w_lp = torch.cat([p.detach() for p in params], 0).to(dt)
+            return proj(x.to(dt), w_lp, b, params)
+        return proj(x.to(dt), None, b, params)
 
 
 def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: float):
@@ -232,7 +265,7 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
     eps = float(cfg.layer_norm_epsilon)
     act = _ACTS[cfg.activation_function]
     blocks = list(encoder.h)
-    weights = weight_shadow(blocks, dt)
+    weights = weight_shadow(blocks, dt) if dt == torch.bfloat16 else [(None,) * 4] * len(blocks)
     ln0 = blocks[0].attn.layer_norm
     h, ln = ResidualLNFn.apply(None, input_embeds.reshape(N, D).float().contiguous(), None, ln0.weight, ln0.bias,
                                None, p_in, eps, dt)
@@ -240,15 +273,15 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
         for i, blk in enumerate(blocks):
             att = blk.attn.attention
             wqkv, wo, wfc, wpj = weights[i]
-            qkv = F.linear(ln, wqkv).view(B, Lq, 3 * D)
+            qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight)).view(B, Lq, 3 * D)
             window = att.window_size if att.attention_type == "local" else 0
             o = AttentionFn.apply(qkv, em, em, att.num_heads, window, False, p_att)
-            y = F.linear(o.view(N, D), wo)
+            y = proj(o.view(N, D), wo, None, (att.out_proj.weight,))
             h1, ln2 = ResidualLNFn.apply(h, y, att.out_proj.bias, blk.layer_norm.weight, blk.layer_norm.bias, None,
                                          p_res, eps, dt)
-            f = F.linear(ln2, wfc)
+            f = proj(ln2, wfc, None, (blk.mlp.c_fc.weight,))
             g = BiasActFn.apply(f, blk.mlp.c_fc.bias, act)
-            y2 = F.linear(g, wpj)
+            y2 = proj(g, wpj, None, (blk.mlp.c_proj.weight,))
             nxt = blocks[i + 1].attn.layer_norm if i + 1 < len(blocks) else encoder.ln_f
             h, ln = ResidualLNFn.apply(h1, y2, blk.mlp.c_proj.bias, nxt.weight, nxt.bias, rows, p_res, eps, dt)
     return ln.view(B, Lq, D)

@@ -223,11 +223,10 @@ def fused_ci_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
         layer._layout = layer._build_layout()
     terms, names = layer._terms_for(all_classification_measurements(layer),
                                     all_regression_measurements(layer.config), 0)
-    wc, bc = layer.content_weight()
-    w = torch.cat([wc, layer.TTE_layer.proj.weight], 0)
-    b = torch.cat([bc, layer.TTE_layer.proj.bias], 0)
+    mods = layer._content_modules() + [layer.TTE_layer.proj]
     B, Lq, D = encoded.shape
-    z = linear_bias(encoded.reshape(B * Lq, D), w, b)
+    z = linear_bias(encoded.reshape(B * Lq, D), [m.weight for m in mods], [m.bias for m in mods])
+    b = torch.cat([m.bias for m in mods], 0)
     bv = batch_view(batch)
     losses = OutputLossFn.apply(z, None, b, bv, terms, layer._tte_spec(layer._layout["n_content"]), 1, 1)
     return losses, names
@@ -255,13 +254,14 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
             seen.add(nn_)
             terms.append(tt)
             names.append(nn_)
-    wc, bc = layer.content_weight()
+    mods = layer._content_modules()
     bv = batch_view(batch)
     if terms:
-        zc = linear_bias(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D), wc, bc)
+        zc = linear_bias(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D), [m.weight for m in mods],
+                         [m.bias for m in mods])
     else:
         zc = torch.zeros(1, 1, device=encoded.device, dtype=encoded.dtype)
-    zt = linear_bias(encoded[:, :, G - 1, :].reshape(B * Lq, D), layer.TTE_layer.proj.weight,
-                     layer.TTE_layer.proj.bias)
+    zt = linear_bias(encoded[:, :, G - 1, :].reshape(B * Lq, D), [layer.TTE_layer.proj.weight],
+                     [layer.TTE_layer.proj.bias])
     losses = OutputLossFn.apply(zc, zt, None, bv, terms, layer._tte_spec(0), 0, max(1, G - 1))
     return losses, names

@@ -321,18 +321,81 @@ def test_linear_bias_fn():
     from eventstreamgpt_amd.fused import linear_bias
 
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(513, 96, generator=g).to(DEV).requires_grad_(True)
-    w = torch.randn(301, 96, generator=g).to(DEV).requires_grad_(True)
-    b = torch.randn(301, generator=g).to(DEV).requires_grad_(True)
+    x = torch.randn(512, 96, generator=g).to(DEV).requires_grad_(True)
+    w = torch.randn(304, 96, generator=g).to(DEV).requires_grad_(True)
+    b = torch.randn(304, generator=g).to(DEV).requires_grad_(True)
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        z = linear_bias(x, w, b)
+        z = linear_bias(x, [w], [b])
         xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
         zr = torch.nn.functional.linear(xr, wr, br)
     assert z.dtype == zr.dtype == torch.bfloat16
     assert rel_err(z.float(), zr.float()) < 1e-2
-    go = torch.randn(513, 301, device=DEV).bfloat16()
+    go = torch.randn(512, 304, device=DEV).bfloat16()
     z.backward(go)
     zr.backward(go)
     for a, r in ((x, xr), (w, wr), (b, br)):
         assert a.grad.dtype == r.grad.dtype
         assert rel_err(a.grad.float(), r.grad.float()) < 1e-2
+
+
+GEMM_SHAPES = [(8192, 768, 256), (8192, 256, 1024), (256, 256, 8192), (1232, 256, 8192), (104, 40, 24),
+               (336, 1232, 256), (8, 8, 8), (520, 136, 72)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+@pytest.mark.parametrize("a_kc", [True, False])
+@pytest.mark.parametrize("b_kc", [True, False])
+def test_gemm_kernel(M, N, K, a_kc, b_kc):
+    """esgpt_gemm_bf16 for every operand layout vs an f64 matmul of the same bf16 values: bf16 / f32 outputs,
+    bias, accumulate, split-K (the dW-shaped cases) and ragged tails."""
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.fused import _gemm
+
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    b = torch.randn(K, N, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    ref = a.double() @ b.double()
+    # operand storage per layout
+    a_st = a.contiguous() if a_kc else a.t().contiguous()  # K-contig: [M][K]; M-contig: [K][M]
+    b_st = b.t().contiguous() if b_kc else b.contiguous()  # K-contig: [N][K]; N-contig: [K][N]
+    lda = K if a_kc else M
+    ldb = K if b_kc else N
+    A, Bm = a_st.to(DEV), b_st.to(DEV)
+    la = L.GEMM_K_CONTIG if a_kc else L.GEMM_MN_CONTIG
+    lb = L.GEMM_K_CONTIG if b_kc else L.GEMM_MN_CONTIG
+    scale = ref.abs().max().item() if K else 1.0
+    c32 = torch.full((M, N), float("nan"), device=DEV)
+    _gemm(A, la, max(lda, 8), Bm, lb, max(ldb, 8), M, N, K, c32)
+    assert ((c32.double().cpu() - ref).abs().max() / max(scale, 1e-6)).item() < 1e-5
+    cb = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    _gemm(A, la, max(lda, 8), Bm, lb, max(ldb, 8), M, N, K, cb, bias=bias.to(DEV))
+    refb = ref + bias.double()
+    assert ((cb.double().cpu() - refb).abs().max() / refb.abs().max()).item() < 1e-2
+    acc = torch.randn(M, N, generator=g).to(DEV)
+    want = acc.double().cpu() + refb
+    _gemm(A, la, max(lda, 8), Bm, lb, max(ldb, 8), M, N, K, acc, bias=bias.to(DEV), accumulate=True)
+    assert ((acc.double().cpu() - want).abs().max() / want.abs().max()).item() < 1e-5
+
+
+def test_proj_fn_grads():
+    """ProjFn (HIP fwd / dx / f32 dW, packed q|k|v parameters) vs F.linear on the same bf16 values."""
+    from eventstreamgpt_amd.fused import proj
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1024, 64, generator=g).to(DEV).bfloat16().requires_grad_(True)
+    ps = [torch.randn(n, 64, generator=g).to(DEV).requires_grad_(True) for n in (64, 64, 32)]
+    with torch.no_grad():
+        w_lp = torch.cat(ps, 0).bfloat16()
+    y = proj(x, w_lp, None, ps)
+    xr = x.detach().float().requires_grad_(True)
+    wr = w_lp.float().requires_grad_(True)
+    yr = xr @ wr.t()
+    assert rel_err(y.float(), yr) < 1e-2
+    go = torch.randn(1024, 160, device=DEV).bfloat16()
+    y.backward(go)
+    yr.backward(go.float())
+    assert rel_err(x.grad.float(), xr.grad) < 1e-2
+    gw = torch.cat([p.grad for p in ps], 0)
+    assert gw.dtype == torch.float32
+    assert rel_err(gw, wr.grad) < 1e-4

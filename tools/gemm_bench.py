@@ -41,3 +41,16 @@ for lib in ("cublaslt", "cublas"):
         except Exception:  # noqa: BLE001
             pass
         print(lib, (out, inn), "  ".join(f"{k} {v:6.1f}us ({fl / v / 1e6:5.0f}TF)" for k, v in r.items()), flush=True)
+
+# the HIP projection GEMM (csrc/gemm.hip) on the same shapes
+import os, sys  # noqa: E401,E402
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from eventstreamgpt_amd.fused import linear_dw, linear_dx, linear_fwd  # noqa: E402
+
+for out, inn in SHAPES:
+    x = torch.randn(N, inn, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(out, inn, device="cuda", dtype=torch.bfloat16)
+    dy = torch.randn(N, out, device="cuda", dtype=torch.bfloat16)
+    fl = 2 * N * out * inn
+    r = {"fwd": t(lambda: linear_fwd(x, w)), "dX": t(lambda: linear_dx(dy, w)), "dW f32": t(lambda: linear_dw(dy, x))}
+    print("hip", (out, inn), "  ".join(f"{k} {v:6.1f}us ({fl / v / 1e6:5.0f}TF)" for k, v in r.items()), flush=True)
