@@ -100,4 +100,9 @@ static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Zero-fills `bytes` bytes at `p` on `st` with a kernel (misc.hip). Used instead of hipMemsetAsync so that every
+// reset is an ordinary kernel node when the caller captures the stream into a HIP graph (memset nodes captured
+// from this library were observed not to re-run on graph replay). Returns hipSuccess or the launch error.
+hipError_t zero_async(void* p, size_t bytes, hipStream_t st);
+
 }  // namespace esgpt

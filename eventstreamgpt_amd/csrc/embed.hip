@@ -792,8 +792,8 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   hipStream_t st = as_stream(stream);
   BagBwdArgs a{*batch, bk, selector, flags, dyn_scale, static_scale, V};
   const int64_t n_slots = batch->B * batch->L * bk.G * batch->M + batch->B * batch->S;
-  if (hipMemsetAsync(dtable, 0, sizeof(float) * V * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if (hipMemsetAsync(w.count, 0, sizeof(int32_t) * (V + 1), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  if (zero_async(dtable, sizeof(float) * V * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  if (zero_async(w.count, sizeof(int32_t) * (V + 1), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   if (n_slots == 0) return ESGPT_OK;
   const int64_t nblk = std::min<int64_t>(kBagBlocks, cdiv(n_slots, 256));
   const int64_t per = cdiv(n_slots, nblk);
@@ -814,7 +814,7 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
                                                           w.ent_v);
   }
   if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM) {
-    if (hipMemsetAsync(w.sub, 0, sizeof(float) * batch->B * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    if (zero_async(w.sub, sizeof(float) * batch->B * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
     bag_subject_sum_kernel<<<dim3((unsigned)batch->B, kSubChunks), 256, 0, st>>>(*batch, bk.G, dsrc, ld, D, w.sub);
   }
   ESGPT_LAUNCH_CHECK();

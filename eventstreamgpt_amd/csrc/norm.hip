@@ -419,7 +419,7 @@ int esgpt_column_sum(const void* x, int dtype, int64_t N, int64_t F, float* part
   if (F == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   if (N == 0) {
-    if (hipMemsetAsync(out, 0, F * sizeof(float), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    if (zero_async(out, F * sizeof(float), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
     return ESGPT_OK;
   }
   const int64_t nb = esgpt_column_sum_partials(N);
