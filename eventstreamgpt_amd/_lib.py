@@ -61,6 +61,8 @@ _PK = ctypes.POINTER(EsgptBuckets)
 
 SIGNATURES = {
     "esgpt_version": (ctypes.c_char_p, []),
+    "esgpt_adamw_chunk": (_i64, []),
+    "esgpt_adamw": (_int, [_vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i64, _vp]),
     "esgpt_device_arch_ok": (_int, []),
     "esgpt_embed_joint_fwd": (_int, [_PB, _PK, _vp, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_embed_split_bags_fwd": (_int, [_PB, _PK, _vp, _i64, _vp, _i64, _i64, _int, _f32, _f32, _f32, _vp, _vp,
@@ -83,8 +85,8 @@ SIGNATURES = {
     "esgpt_bias_act_partials": (_i64, [_i64]),
     "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),
     "esgpt_gemm_workspace": (_sz, [_i64, _i64, _i64]),
-    "esgpt_gemm_bf16": (_int, [_int, _vp, _i64, _int, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i64, _int, _int, _vp,
-                               _sz, _vp]),
+    "esgpt_gemm_bf16": (_int, [_int, _vp, _i64, _int, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _int, _int,
+                               _vp, _sz, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),

@@ -16,6 +16,8 @@
 // MFMA v_mfma_f32_32x32x16_bf16; 4 waves as 2x2, each wave (BM/2)x(BN/2); register-staged global->LDS with the
 // next k-tile's loads in flight during the current tile's MFMAs.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -35,6 +37,11 @@ constexpr int NS = 3;          // register stages: NS-1 k-tiles in flight while 
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const __bf16 a = (__bf16)lo, b = (__bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
 
 __device__ __forceinline__ bf16x8 zero8() {
@@ -120,16 +127,28 @@ struct Tile {
   }
 };
 
-// C = A·B (+ bias) for one BMxBN tile over k in [z*kchunk, min(K, (z+1)*kchunk)).
+// XCD-aware tile order: the hardware deals consecutive workgroup ids round-robin over the 8 XCDs (each with its
+// own L2), so id -> (xcd = id % 8, slot = id / 8) is remapped (bijectively) to a linear tile index that gives every
+// XCD a contiguous run of tiles. The n-tile index runs fastest, so the tiles of one XCD share A row-blocks in L2.
+__device__ __forceinline__ int xcd_remap(int id, int nwg) {
+  const int q = nwg >> 3, rr = nwg & 7, xcd = id & 7, slot = id >> 3;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+}
+
+// C = alpha · (A·B) (+ bias) for one BMxBN tile over k in [z*kchunk, min(K, (z+1)*kchunk)).
 // OUT_F32: C f32 (accumulate: C += …); else bf16. Split-K callers pass C = slab z (ldc = N) and no bias.
 // Pipeline: NS register stages (loads for k-tile i+NS-1 are issued before k-tile i is written to LDS) and two LDS
 // buffers (one barrier per k-tile: a buffer is rewritten only after every wave passed the next barrier).
+// The MFMAs compute the tile transposed (A-operand = B fragment, B-operand = A fragment), so that a lane owns one
+// output ROW m and its registers hold columns n = (e&3) + 8(e>>2) + 4h: four consecutive columns per register
+// group. The epilogue then stores 16 B per lane (f32: one group; bf16: two groups joined across the half-waves
+// with v_permlane32_swap), 8x fewer store instructions than one 2-byte store per element.
 template <bool AKC, bool BKC, int WM, int WN, bool OUT_F32>
 __global__ __launch_bounds__(THREADS) void gemm_kernel(const __bf16* __restrict__ A, int64_t lda,
                                                        const __bf16* __restrict__ B, int64_t ldb, int M, int N,
                                                        int K, int kchunk, const float* __restrict__ bias,
-                                                       void* __restrict__ Cv, int64_t ldc, int64_t slab_stride,
-                                                       int accumulate) {
+                                                       const float* __restrict__ alpha, void* __restrict__ Cv,
+                                                       int64_t ldc, int64_t slab_stride, int accumulate) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   using TA = Tile<AKC, BM>;
   using TB = Tile<BKC, BN>;
@@ -137,8 +156,12 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(const __bf16* __restrict_
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kb = blockIdx.z * kchunk, ke = min(K, kb + kchunk);
+  const int tn = gridDim.x, tm = gridDim.y;
+  const int nwg = tn * tm * gridDim.z;
+  const int lin = xcd_remap(blockIdx.x + tn * (blockIdx.y + tm * blockIdx.z), nwg);
+  const int bx = lin % tn, by = (lin / tn) % tm, bz = lin / (tn * tm);
+  const int m0 = by * BM, n0 = bx * BN;
+  const int kb = bz * kchunk, ke = min(K, kb + kchunk);
   const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
 
   f32x16 acc[WM][WN];
@@ -167,7 +190,7 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(const __bf16* __restrict_
 #pragma unroll
       for (int ii = 0; ii < WM; ++ii)
 #pragma unroll
-        for (int j = 0; j < WN; ++j) acc[ii][j] = mfma(af[ii], bfr[j], acc[ii][j]);
+        for (int j = 0; j < WN; ++j) acc[ii][j] = mfma(bfr[j], af[ii], acc[ii][j]);
     }
   };
   // Loads are unconditional (clamped addresses; tiles past the end are zeroed at the LDS write), so the stage
@@ -191,44 +214,90 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(const __bf16* __restrict_
   for (int st = 0; st < NS - 1; ++st)
     if (i0 + st < nk) consume(st, i0 + st);
 
-  // Epilogue: register e of tile (i, j) holds row (e&3) + 8(e>>2) + 4h, column r.
-  char* Cb = reinterpret_cast<char*>(Cv) + (int64_t)blockIdx.z * slab_stride * (OUT_F32 ? 4 : 2);
+  // Epilogue. Lane: row m0 + wm*32*WM + 32i + r; register group g of tile (i, j): columns
+  // n0 + wn*32*WN + 32j + 8g + 4h + {0..3}. N is a multiple of 8 (bf16) / 4 (f32): a group is in or out whole.
+  const float al = alpha ? *alpha : 1.f;
+  char* Cb = reinterpret_cast<char*>(Cv) + (int64_t)bz * slab_stride * (OUT_F32 ? 4 : 2);
 #pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int col = n0 + wn * 32 * WN + 32 * j + r;
-    const bool cok = col < N;
-    const float bc = (bias && cok) ? bias[col] : 0.f;
+  for (int i = 0; i < WM; ++i) {
+    const int row = m0 + wm * 32 * WM + 32 * i + r;
+    const bool rok = row < M;
 #pragma unroll
-    for (int i = 0; i < WM; ++i)
+    for (int j = 0; j < WN; ++j) {
+      const int cb = n0 + wn * 32 * WN + 32 * j;
+      float v[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * 32 * WM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (!cok || row >= M) continue;
-        const float v = acc[i][j][e] + bc;
-        if (OUT_F32) {
-          float* c = reinterpret_cast<float*>(Cb) + (int64_t)row * ldc + col;
-          *c = accumulate ? *c + v : v;
-        } else {
-          reinterpret_cast<__bf16*>(Cb)[(int64_t)row * ldc + col] = (__bf16)v;
+      for (int g = 0; g < 4; ++g) {
+        const int c = cb + 8 * g + 4 * h;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (bias && c < N) bv = *reinterpret_cast<const float4*>(bias + c);
+        v[4 * g + 0] = acc[i][j][4 * g + 0] * al + bv.x;
+        v[4 * g + 1] = acc[i][j][4 * g + 1] * al + bv.y;
+        v[4 * g + 2] = acc[i][j][4 * g + 2] * al + bv.z;
+        v[4 * g + 3] = acc[i][j][4 * g + 3] * al + bv.w;
+      }
+      if (OUT_F32) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = cb + 8 * g + 4 * h;
+          if (!rok || c >= N) continue;
+          float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(Cb) + (int64_t)row * ldc + c);
+          float4 w = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+          if (accumulate) {
+            const float4 o = *p;
+            w.x += o.x; w.y += o.y; w.z += o.z; w.w += o.w;
+          }
+          *p = w;
+        }
+      } else {
+        uint32_t d[4][2];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
+          d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g += 2) {
+          // lanes 0-31: columns 8g..8g+7 (own group g | upper half's group g);
+          // lanes 32-63: columns 8g+8..8g+15 (lower half's group g+1 | own group g+1)
+#pragma unroll
+          for (int w = 0; w < 2; ++w) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(d[g][w], d[g + 1][w], false, false);
+            d[g][w] = sw[0];
+            d[g + 1][w] = sw[1];
+          }
+          const int c = cb + 8 * g + 8 * h;
+          if (rok && c < N)
+            *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(Cb) + (int64_t)row * ldc + c) =
+                make_uint4(d[g][0], d[g][1], d[g + 1][0], d[g + 1][1]);
         }
       }
+    }
   }
 }
 
-// out[m, n] (=, or += when accumulate) sum_z slab[z, m, n] + bias[n]; fixed summation order.
+// out[m, n] (=, or += when accumulate) sum_z slab[z, m, n] + bias[n]; fixed summation order; 4 columns per thread.
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N,
                                                             const float* __restrict__ bias, void* __restrict__ C,
                                                             int64_t ldc, int out_bf16, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)M * N) return;
-  const int64_t row = i / N, col = i % N;
-  float s = bias ? bias[col] : 0.f;
-  for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * M * N + i];
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= (int64_t)M * N) return;
+  const int64_t row = i4 / N, col = i4 % N;
+  float4 s = bias ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int z = 0; z < splits; ++z) {
+    const float4 x = *reinterpret_cast<const float4*>(slab + (int64_t)z * M * N + i4);
+    s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+  }
   if (out_bf16) {
-    reinterpret_cast<__bf16*>(C)[row * ldc + col] = (__bf16)s;
+    *reinterpret_cast<uint2*>(reinterpret_cast<__bf16*>(C) + row * ldc + col) =
+        make_uint2(pack_bf16x2(s.x, s.y), pack_bf16x2(s.z, s.w));
   } else {
-    float* c = reinterpret_cast<float*>(C) + row * ldc + col;
-    *c = accumulate ? *c + s : s;
+    float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + row * ldc + col);
+    if (accumulate) {
+      const float4 o = *c;
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
+    *c = s;
   }
 }
 
@@ -240,15 +309,24 @@ Plan plan(int64_t M, int64_t N, int64_t K) {
   constexpr int64_t kTarget = 240;  // workgroups wanted (256 CUs, one resident tile each is already MFMA-bound)
   Plan p{2, 2, 1, (int)(cdiv(K, BK) * BK)};
   if (K == 0) return p;
-  if (cdiv(M, 128) * cdiv(N, 128) >= kTarget) return p;
-  if (cdiv(M, 128) * cdiv(N, 64) >= kTarget) {
-    p.wn = 1;
-    return p;
+  if (const char* e = getenv("ESGPT_GEMM_PLAN")) {  // tuning hook: "wm,wn,splits"
+    int wm = 2, wn = 2, sp = 1;
+    if (sscanf(e, "%d,%d,%d", &wm, &wn, &sp) == 3 && wm >= 1 && wm <= 2 && wn >= 1 && wn <= 2 && sp >= 1) {
+      p.wm = wm;
+      p.wn = wn;
+      const int64_t kchunk = cdiv(cdiv(K, sp), BK) * BK;
+      p.splits = (int)cdiv(K, kchunk);
+      p.kchunk = (int)kchunk;
+      return p;
+    }
   }
+  // Measured on MI355X at the C2 step's shapes (tools/gemm_sweep.py): 64x64 tiles beat 128x64 / 128x128 for the
+  // short-K (256, 1024) projections — more resident workgroups per CU hide the load/store latency that dominates
+  // at these sizes. Long-K (dW, K = tokens) products with few tiles split K to about two workgroups per CU.
   p.wm = p.wn = 1;
   const int64_t tiles = cdiv(M, 64) * cdiv(N, 64);
   if (tiles >= kTarget) return p;
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(kTarget / tiles, K / 256));
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(2 * kTarget / tiles, K / 512));
   const int64_t kchunk = cdiv(cdiv(K, splits), BK) * BK;
   p.splits = (int)cdiv(K, kchunk);
   p.kchunk = (int)kchunk;
@@ -257,28 +335,29 @@ Plan plan(int64_t M, int64_t N, int64_t K) {
 
 template <bool AKC, bool BKC, bool F32>
 void launch(const Plan& p, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
-            const float* bias, void* C, int64_t ldc, int64_t slab_stride, int accumulate, hipStream_t st) {
+            const float* bias, const float* alpha, void* C, int64_t ldc, int64_t slab_stride, int accumulate,
+            hipStream_t st) {
   const int BM = 64 * p.wm, BN = 64 * p.wn;
   dim3 grid((unsigned)cdiv(N, BN), (unsigned)cdiv(M, BM), (unsigned)p.splits);
   if (p.wm == 2 && p.wn == 2)
-    gemm_kernel<AKC, BKC, 2, 2, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, C, ldc,
-                                                                slab_stride, accumulate);
+    gemm_kernel<AKC, BKC, 2, 2, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, alpha, C,
+                                                                ldc, slab_stride, accumulate);
   else if (p.wm == 2)
-    gemm_kernel<AKC, BKC, 2, 1, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, C, ldc,
-                                                                slab_stride, accumulate);
+    gemm_kernel<AKC, BKC, 2, 1, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, alpha, C,
+                                                                ldc, slab_stride, accumulate);
   else
-    gemm_kernel<AKC, BKC, 1, 1, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, C, ldc,
-                                                                slab_stride, accumulate);
+    gemm_kernel<AKC, BKC, 1, 1, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, alpha, C,
+                                                                ldc, slab_stride, accumulate);
 }
 
 template <bool F32>
 void launch_any(bool akc, bool bkc, const Plan& p, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M,
-                int N, int K, const float* bias, void* C, int64_t ldc, int64_t slab_stride, int accumulate,
-                hipStream_t st) {
-  if (akc && bkc) launch<true, true, F32>(p, A, lda, B, ldb, M, N, K, bias, C, ldc, slab_stride, accumulate, st);
-  else if (akc) launch<true, false, F32>(p, A, lda, B, ldb, M, N, K, bias, C, ldc, slab_stride, accumulate, st);
-  else if (bkc) launch<false, true, F32>(p, A, lda, B, ldb, M, N, K, bias, C, ldc, slab_stride, accumulate, st);
-  else launch<false, false, F32>(p, A, lda, B, ldb, M, N, K, bias, C, ldc, slab_stride, accumulate, st);
+                int N, int K, const float* bias, const float* alpha, void* C, int64_t ldc, int64_t slab_stride,
+                int accumulate, hipStream_t st) {
+  if (akc && bkc) launch<true, true, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
+  else if (akc) launch<true, false, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
+  else if (bkc) launch<false, true, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
+  else launch<false, false, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
 }
 
 }  // namespace
@@ -291,8 +370,8 @@ size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K) {
 }
 
 int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, const void* B, int64_t ldb, int64_t M,
-                    int64_t N, int64_t K, const float* bias, void* C, int64_t ldc, int c_dtype, int accumulate,
-                    void* workspace, size_t workspace_bytes, void* stream) {
+                    int64_t N, int64_t K, const float* bias, const float* alpha, void* C, int64_t ldc, int c_dtype,
+                    int accumulate, void* workspace, size_t workspace_bytes, void* stream) {
   ESGPT_REQUIRE(A && B && C && M >= 0 && N >= 0 && K >= 0);
   ESGPT_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31));
   ESGPT_REQUIRE(c_dtype == ESGPT_F32 || (c_dtype == ESGPT_BF16 && !accumulate));
@@ -303,6 +382,10 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   ESGPT_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0);
   ESGPT_REQUIRE((akc || M % 8 == 0) && (bkc || N % 8 == 0));
   ESGPT_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
+  // 16-B epilogue stores: whole 8-column (bf16) / 4-column (f32) groups, 16-B aligned rows.
+  const int cgrp = c_dtype == ESGPT_F32 ? 4 : 8;
+  ESGPT_REQUIRE(N % cgrp == 0 && ldc % cgrp == 0 && ((uintptr_t)C % 16) == 0);
+  ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   if (M == 0 || N == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   const Plan p = plan(M, N, K);  // K == 0: one split, the k-loop is empty and C = bias (or C += bias)
@@ -312,13 +395,13 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   if (p.splits > 1) {
     ESGPT_REQUIRE(workspace && workspace_bytes >= sizeof(float) * (size_t)p.splits * M * N);
     float* slab = reinterpret_cast<float*>(workspace);
-    launch_any<true>(akc, bkc, p, a, lda, b, ldb, M, N, K, nullptr, slab, N, M * N, 0, st);
-    splitk_reduce_kernel<<<(unsigned)cdiv(M * N, 256), 256, 0, st>>>(slab, p.splits, (int)M, (int)N, bias, C, ldc,
+    launch_any<true>(akc, bkc, p, a, lda, b, ldb, M, N, K, nullptr, alpha, slab, N, M * N, 0, st);
+    splitk_reduce_kernel<<<(unsigned)cdiv(M * N / 4, 256), 256, 0, st>>>(slab, p.splits, (int)M, (int)N, bias, C, ldc,
                                                                       f32 ? 0 : 1, accumulate);
   } else if (f32) {
-    launch_any<true>(akc, bkc, p, a, lda, b, ldb, M, N, K, bias, C, ldc, 0, accumulate, st);
+    launch_any<true>(akc, bkc, p, a, lda, b, ldb, M, N, K, bias, alpha, C, ldc, 0, accumulate, st);
   } else {
-    launch_any<false>(akc, bkc, p, a, lda, b, ldb, M, N, K, bias, C, ldc, 0, 0, st);
+    launch_any<false>(akc, bkc, p, a, lda, b, ldb, M, N, K, bias, alpha, C, ldc, 0, 0, st);
   }
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;

@@ -413,7 +413,7 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
   float* contrib = (float*)((char*)workspace + align_up(sizeof(int32_t) * B * (ESGPT_MAX_TERMS + 1)));
   const size_t esz = dtype == ESGPT_F32 ? 4 : 2;
   if (n_terms > 0 && zero_async(dzc, esz * B * L * n_levels * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if (zero_async(dzt, esz * B * L * ldt, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  if ((dzt != dzc || n_terms == 0) && zero_async(dzt, esz * B * L * ldt, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   if (shift && zero_async(dbias, sizeof(float) * B * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   count_kernel<<<(unsigned)B, 256, 0, st>>>(*batch, T, counts, err);
   const int64_t n_rows = B * (L + shift);

@@ -1,4 +1,5 @@
-// Version / device probes of the C ABI.
+// Version / device probes of the C ABI, the zero-fill helper and the fused AdamW step.
+#include <math.h>
 #include <string.h>
 
 #include "common.h"
@@ -15,6 +16,48 @@ __global__ __launch_bounds__(256) void zero_kernel(uint8_t* __restrict__ p, size
   for (size_t j = i; j < n16; j += stride) body[j] = make_uint4(0u, 0u, 0u, 0u);
   uint8_t* t = p + head + 16 * n16;
   for (size_t j = i; j < tail; j += stride) t[j] = 0;
+}
+// AdamW (torch.optim.AdamW, decoupled weight decay) over a table of tensors. Block b updates elements
+// [start, start + kAdamChunk) of tensor (blocks[b] >> 40) where start = blocks[b] & (2^40 - 1).
+constexpr int kAdamChunk = 4096;
+
+__global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __restrict__ table,
+                                                    const int64_t* __restrict__ blocks, float lr, float beta1,
+                                                    float beta2, float eps, float wd, float step_size,
+                                                    float bc2_sqrt) {
+  const int64_t e = blocks[blockIdx.x];
+  const esgpt_adam_tensor t = table[e >> 40];
+  const int64_t start = e & ((1ll << 40) - 1);
+  const int64_t end = start + kAdamChunk < t.n ? start + kAdamChunk : t.n;
+  const float decay = 1.f - lr * wd;
+  auto upd = [&](float& p, float g, float& m, float& v) {
+    p *= decay;
+    m = beta1 * m + (1.f - beta1) * g;
+    v = beta2 * v + (1.f - beta2) * g * g;
+    p -= step_size * m / (sqrtf(v) / bc2_sqrt + eps);
+  };
+  const bool vec = ((reinterpret_cast<uintptr_t>(t.p) | reinterpret_cast<uintptr_t>(t.g) |
+                     reinterpret_cast<uintptr_t>(t.m) | reinterpret_cast<uintptr_t>(t.v)) & 15) == 0;
+  if (vec) {
+    const int64_t n4 = (end - start) / 4;
+    for (int64_t j = threadIdx.x; j < n4; j += blockDim.x) {
+      const int64_t i = start + 4 * j;
+      float4 p = *reinterpret_cast<float4*>(t.p + i);
+      const float4 g = *reinterpret_cast<const float4*>(t.g + i);
+      float4 m = *reinterpret_cast<float4*>(t.m + i);
+      float4 v = *reinterpret_cast<float4*>(t.v + i);
+      upd(p.x, g.x, m.x, v.x);
+      upd(p.y, g.y, m.y, v.y);
+      upd(p.z, g.z, m.z, v.z);
+      upd(p.w, g.w, m.w, v.w);
+      *reinterpret_cast<float4*>(t.p + i) = p;
+      *reinterpret_cast<float4*>(t.m + i) = m;
+      *reinterpret_cast<float4*>(t.v + i) = v;
+    }
+    for (int64_t i = start + 4 * n4 + threadIdx.x; i < end; i += blockDim.x) upd(t.p[i], t.g[i], t.m[i], t.v[i]);
+  } else {
+    for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) upd(t.p[i], t.g[i], t.m[i], t.v[i]);
+  }
 }
 }  // namespace
 
@@ -35,6 +78,20 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
 extern "C" {
 
 const char* esgpt_version(void) { return "eventstreamgpt_amd 0.1.0 (gfx950)"; }
+
+int64_t esgpt_adamw_chunk(void) { return esgpt::kAdamChunk; }
+
+int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, float lr, float beta1,
+                float beta2, float eps, float weight_decay, int64_t step, void* stream) {
+  ESGPT_REQUIRE(table && blocks && n_blocks >= 0 && step >= 1);
+  if (n_blocks == 0) return ESGPT_OK;
+  const double bc1 = 1.0 - pow((double)beta1, (double)step), bc2 = 1.0 - pow((double)beta2, (double)step);
+  esgpt::adamw_kernel<<<(unsigned)n_blocks, 256, 0, esgpt::as_stream(stream)>>>(table, blocks, lr, beta1, beta2, eps,
+                                                                   weight_decay, (float)(lr / bc1),
+                                                                   (float)sqrt(bc2));
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
 
 int esgpt_device_arch_ok(void) {
   hipDeviceProp_t prop;

@@ -18,7 +18,9 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib as L
-from .kernels import AttentionFn, _timed, next_dropout_seed
+import ctypes
+
+from .kernels import AttentionFn, _timed, err_word, next_dropout_seed
 
 _ACTS = {"gelu": 0, "gelu_new": 1, "gelu_pytorch_tanh": 1, "gelu_fast": 1, "relu": 2}
 
@@ -126,13 +128,13 @@ def fused_supported(encoder) -> bool:
 # Projection GEMMs (csrc/gemm.hip): y = x·Wᵀ (+ b), dx = dy·W, dW = dyᵀ·x written straight to f32
 # ----------------------------------------------------------------------------------------------------------------
 def _gemm(a, a_layout: int, lda: int, b, b_layout: int, ldb: int, M: int, N: int, K: int, out, bias=None,
-          accumulate: bool = False):
+          accumulate: bool = False, alpha=None):
     lib = L.load()
     nbytes = lib.esgpt_gemm_workspace(M, N, K)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device) if nbytes else None
     with _timed("gemm"):
         st = lib.esgpt_gemm_bf16(a_layout, a.data_ptr(), lda, b_layout, b.data_ptr(), ldb, M, N, K, L.ptr(bias),
-                                 out.data_ptr(), out.stride(0), L.dtype_code(out.dtype), int(accumulate), L.ptr(ws),
+                                 L.ptr(alpha), out.data_ptr(), out.stride(0), L.dtype_code(out.dtype), int(accumulate), L.ptr(ws),
                                  nbytes, L.stream())
     L.check(st, "gemm")
     return out
@@ -247,6 +249,120 @@ def linear_bias(x: torch.Tensor, params, biases) -> torch.Tensor:
                 w_lp = torch.cat([p.detach() for p in params], 0).to(dt)
             return proj(x.to(dt), w_lp, b, params)
         return proj(x.to(dt), None, b, params)
+
+
+_ZPAD: dict = {}
+
+
+def _pad_rows(ts, mult: int = 8):
+    """Row-concatenation of ``ts`` (same dtype / trailing dim) padded with zero rows to a multiple of ``mult``
+    (one cat kernel; the zero block is cached)."""
+    n = sum(t.shape[0] for t in ts)
+    pad = (-n) % mult
+    if pad:
+        t0 = ts[0]
+        key = (pad, tuple(t0.shape[1:]), t0.dtype, t0.device)
+        z = _ZPAD.get(key)
+        if z is None:
+            z = torch.zeros((pad,) + tuple(t0.shape[1:]), dtype=t0.dtype, device=t0.device)
+            _ZPAD[key] = z
+        ts = list(ts) + [z]
+    return torch.cat(list(ts), 0) if len(ts) > 1 else ts[0]
+
+
+class HeadLossFn(torch.autograd.Function):
+    """bf16 generative heads + fused losses in one autograd node (model_output.py:1253-1721 through
+    ``OutputLossFn``'s kernel): z = x · W_padᵀ + b_pad with the HIP GEMM (the head's output columns padded to a
+    multiple of 8 with zero weights), the loss kernel computes the losses AND d(loss)/dz, and the backward scales
+    every gradient by the incoming d(total) straight from device memory (the GEMM's alpha pointer) — no logits-
+    sized scaling pass, no host sync. ``xt`` / TTE params are None when the TTE columns are part of the content
+    head (CI). Returns f32 [n_terms + 2] like ``OutputLossFn``."""
+
+    @staticmethod
+    def forward(ctx, xc, xt, bv, terms, tte, shift: int, n_levels: int, n_cw: int, n_tw: int, *wb):
+        lib = L.load()
+        cw, cb = wb[:n_cw], wb[n_cw: 2 * n_cw]
+        tw, tb = wb[2 * n_cw: 2 * n_cw + n_tw], wb[2 * n_cw + n_tw:]
+        with torch.no_grad():
+            wc = _pad_rows([w.detach() for w in cw]).to(torch.bfloat16)
+            bc = _pad_rows([b.detach().float() for b in cb]).contiguous()
+            zc = linear_fwd(xc, wc, bc)
+            if n_tw:
+                wt = _pad_rows([w.detach() for w in tw]).to(torch.bfloat16)
+                bt = _pad_rows([b.detach().float() for b in tb]).contiguous()
+                zt = linear_fwd(xt, wt, bt)
+            else:
+                wt = bt = zt = None
+        zc_bias = bc.to(torch.bfloat16) if shift else None
+        n_terms = len(terms)
+        arr = (L.EsgptLossTerm * max(1, n_terms))(*terms)
+        zt_ = zc if zt is None else zt
+        dzc = torch.empty_like(zc)
+        dzt = dzc if zt is None else torch.empty_like(zt)
+        dbias = torch.empty(bv.B, zc.shape[1], dtype=torch.float32, device=zc.device) if shift else None
+        losses = torch.empty(n_terms + 2, dtype=torch.float32, device=zc.device)
+        nbytes = lib.esgpt_output_loss_workspace(bv.B, bv.L, n_terms)
+        ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=zc.device)
+        with _timed("output_loss"):
+            st = lib.esgpt_output_loss(bv.ref, zc.data_ptr(), zc.shape[1], n_levels, shift, L.ptr(zc_bias),
+                                       zt_.data_ptr(), zt_.shape[1], L.BF16, arr, n_terms, ctypes.byref(tte),
+                                       dzc.data_ptr(), dzt.data_ptr(), L.ptr(dbias), losses.data_ptr(), ws.data_ptr(),
+                                       nbytes, err_word(zc.device).data_ptr(), L.stream())
+        L.check(st, "output_loss")
+        ctx.save_for_backward(xc, xt, wc, wt, dzc, None if zt is None else dzt, dbias)
+        ctx.rows = ([w.shape[0] for w in cw], [w.shape[0] for w in tw])
+        ctx.n = (n_cw, n_tw)
+        return losses
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, xt, wc, wt, dzc, dzt, dbias = ctx.saved_tensors
+        n_cw, n_tw = ctx.n
+        rows_c, rows_t = ctx.rows
+        g = g.contiguous()
+        alpha = g[-1:]  # d(total): read by the GEMMs from device memory
+        dxc = _gemm(dzc, L.GEMM_K_CONTIG, dzc.shape[1], wc, L.GEMM_MN_CONTIG, wc.shape[1], dzc.shape[0],
+                    wc.shape[1], dzc.shape[1], torch.empty(dzc.shape[0], wc.shape[1], dtype=dzc.dtype,
+                                                           device=dzc.device), alpha=alpha)
+        dwc = _gemm(dzc, L.GEMM_MN_CONTIG, dzc.shape[1], xc, L.GEMM_MN_CONTIG, xc.shape[1], dzc.shape[1],
+                    xc.shape[1], dzc.shape[0], torch.empty(dzc.shape[1], xc.shape[1], dtype=torch.float32,
+                                                           device=dzc.device), alpha=alpha)
+        dbc = column_sum(dzc)
+        if dbias is not None:
+            dbc = dbc + dbias.sum(0)
+        dbc = dbc * alpha
+        n_real_c = sum(rows_c)
+        gw_c = list(torch.split(dwc[:n_real_c], rows_c, 0))
+        gb_c = list(torch.split(dbc[:n_real_c], rows_c, 0))
+        dxt, gw_t, gb_t = None, [], []
+        if n_tw:
+            dxt = _gemm(dzt, L.GEMM_K_CONTIG, dzt.shape[1], wt, L.GEMM_MN_CONTIG, wt.shape[1], dzt.shape[0],
+                        wt.shape[1], dzt.shape[1], torch.empty(dzt.shape[0], wt.shape[1], dtype=dzt.dtype,
+                                                               device=dzt.device), alpha=alpha)
+            dwt = _gemm(dzt, L.GEMM_MN_CONTIG, dzt.shape[1], xt, L.GEMM_MN_CONTIG, xt.shape[1], dzt.shape[1],
+                        xt.shape[1], dzt.shape[0], torch.empty(dzt.shape[1], xt.shape[1], dtype=torch.float32,
+                                                               device=dzt.device), alpha=alpha)
+            dbt = column_sum(dzt) * alpha
+            n_real_t = sum(rows_t)
+            gw_t = list(torch.split(dwt[:n_real_t], rows_t, 0))
+            gb_t = list(torch.split(dbt[:n_real_t], rows_t, 0))
+        return (dxc, dxt, None, None, None, None, None, None, None, *gw_c, *gb_c, *gw_t, *gb_t)
+
+
+def head_losses(xc, xt, bv, terms, tte, shift, n_levels, cmods, tmods):
+    """Generative heads + losses through ``HeadLossFn`` (bf16 compute) — None if the shapes do not fit the HIP
+    GEMM (the caller then uses the module-by-module path)."""
+    D = xc.shape[1]
+    if compute_dtype() != torch.bfloat16 or D % 8 or xc.shape[0] % 8 or (xt is not None and xt.shape[0] % 8):
+        return None
+    cw = [m.weight for m in cmods]
+    cb = [m.bias for m in cmods]
+    tw = [m.weight for m in tmods]
+    tb = [m.bias for m in tmods]
+    xc = xc.to(torch.bfloat16).contiguous()
+    xt = None if xt is None else xt.to(torch.bfloat16).contiguous()
+    with torch.autocast("cuda", enabled=False):
+        return HeadLossFn.apply(xc, xt, bv, terms, tte, shift, n_levels, len(cw), len(tw), *cw, *cb, *tw, *tb)
 
 
 def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: float):

@@ -275,19 +275,56 @@ class EmbedEpilogueFn(torch.autograd.Function):
 # Attention
 # ----------------------------------------------------------------------------------------------------------------
 _SEEDS: dict[int, torch.Tensor] = {}
+_BANKS: dict[int, dict] = {}
+SEED_BANK_SLOTS = 256
 
 
-def next_dropout_seed(device: torch.device) -> torch.Tensor:
-    """Device-side dropout seed: a per-device int64 counter advanced on the stream at every use (so HIP-graph
-    replays draw fresh masks); returns a snapshot tensor for the backward pass."""
+def _seed_counter(device: torch.device) -> torch.Tensor:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     c = _SEEDS.get(idx)
     if c is None:
         c = torch.full((1,), (torch.initial_seed() * 0x2545F491) & 0x7FFFFFFFFFFF, dtype=torch.int64, device=device)
         _SEEDS[idx] = c
+    return c
+
+
+def begin_dropout_step(device: torch.device) -> None:
+    """Refreshes the per-step seed bank on the stream (two small kernels per training step): slot i of the bank
+    = counter + i, then counter += slots. Until the next call, ``next_dropout_seed`` hands out slots of the bank
+    (no kernel per dropout site); under HIP-graph capture the refresh is part of the graph, so every replay draws
+    fresh masks. Without a bank (eager use outside a step) every call clones and advances the counter."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    c = _seed_counter(device)
+    bank = _BANKS.get(idx)
+    if bank is None:
+        bank = {"buf": torch.empty(SEED_BANK_SLOTS, dtype=torch.int64, device=device),
+                "ar": torch.arange(SEED_BANK_SLOTS, dtype=torch.int64, device=device), "next": 0}
+        _BANKS[idx] = bank
+    torch.add(bank["ar"], c, out=bank["buf"])
+    c.add_(SEED_BANK_SLOTS)
+    bank["next"] = 0
+
+
+def next_dropout_seed(device: torch.device) -> torch.Tensor:
+    """Device-side dropout seed (a 1-element int64 tensor that stays valid for the backward pass)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    bank = _BANKS.get(idx)
+    if bank is not None and bank["next"] < SEED_BANK_SLOTS:
+        i = bank["next"]
+        bank["next"] = i + 1
+        return bank["buf"][i: i + 1]
+    c = _seed_counter(device)
     snap = c.clone()
     c.add_(1)
     return snap
+
+
+def end_dropout_step(device: torch.device) -> None:
+    """Closes the bank (later calls fall back to per-call seeds until the next ``begin_dropout_step``)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    bank = _BANKS.get(idx)
+    if bank is not None:
+        bank["next"] = SEED_BANK_SLOTS
 
 
 class AttentionFn(torch.autograd.Function):

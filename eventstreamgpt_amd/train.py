@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 
 from .data.types import PytorchBatch
-from .kernels import check_errors
+from .kernels import begin_dropout_step, check_errors, end_dropout_step
 from .transformer.config import OptimizationConfig
 
 
@@ -32,6 +32,74 @@ def poly_decay_lambda(warmup: int, total: int, power: float, init_lr: float, end
         return ((init_lr - end_lr) * rem**power + end_lr) / init_lr
 
     return f
+
+
+class FusedAdamW:
+    """``torch.optim.AdamW`` (default betas / eps, decoupled weight decay; ``generative_modeling.py:460-466``) as ONE
+    gfx950 kernel launch per step over every parameter (csrc/misc.hip ``esgpt_adamw``), instead of torch's
+    multi-tensor launches. Parameters whose ``.grad`` is None are skipped, like torch. The tensor table (device
+    pointers of p / grad / exp_avg / exp_avg_sq) is rebuilt only when a gradient's storage changes (never under
+    HIP-graph replay, where gradients live in the graph's pool)."""
+
+    def __init__(self, params, lr: float, weight_decay: float = 0.01, betas=(0.9, 0.999), eps: float = 1e-8):
+        from . import _lib as L
+
+        self.L = L
+        self.lib = L.load()
+        self.params = list(params)
+        self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, betas, eps
+        self.exp_avg = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
+        self.exp_avg_sq = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
+        self.steps = [0] * len(self.params)
+        self._key = None
+        self._table = self._blocks = None
+        self._active = []
+
+    def zero_grad(self, set_to_none: bool = True):
+        for p in self.params:
+            p.grad = None
+
+    def _plan(self):
+        items = [i for i, p in enumerate(self.params) if p.grad is not None]
+        for i in items:
+            g = self.params[i].grad
+            if not (g.is_contiguous() and g.dtype == torch.float32 and self.params[i].is_contiguous()):
+                raise RuntimeError("FusedAdamW needs contiguous f32 parameters and gradients")
+        key = tuple((i, self.params[i].grad.data_ptr()) for i in items)
+        if key == self._key:
+            return
+        chunk = int(self.lib.esgpt_adamw_chunk())
+        rows, blocks = [], []
+        for t, i in enumerate(items):
+            p = self.params[i]
+            rows.append([p.data_ptr(), p.grad.data_ptr(), self.exp_avg[i].data_ptr(), self.exp_avg_sq[i].data_ptr(),
+                         p.numel()])
+            blocks += [(t << 40) | s for s in range(0, p.numel(), chunk)]
+        dev = self.params[0].device
+        self._table = torch.tensor(rows, dtype=torch.int64).to(dev)
+        self._blocks = torch.tensor(blocks, dtype=torch.int64).to(dev)
+        self._key = key
+        self._active = items
+
+    @torch.no_grad()
+    def step(self, lr: float | None = None):
+        self._plan()
+        if not self._active:
+            return
+        # torch keeps one step counter per parameter; they advance together for parameters updated every step
+        step = self.steps[self._active[0]] + 1
+        for i in self._active:
+            self.steps[i] += 1
+        b1, b2 = self.betas
+        self.L.check(self.lib.esgpt_adamw(self._table.data_ptr(), self._blocks.data_ptr(), self._blocks.numel(),
+                                          float(self.lr if lr is None else lr), b1, b2, self.eps,
+                                          self.weight_decay, step, self.L.stream()), "adamw")
+
+    def state_dict(self):
+        return {"state": {i: {"step": self.steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}
+                          for i in range(len(self.params))},
+                "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
+                                  "weight_decay": self.weight_decay}]}
 
 
 class TrainStep:
@@ -56,12 +124,16 @@ class TrainStep:
                 cur, size = [], 0
         if cur:
             self.buckets.append(cur)
-        fused = dev.type == "cuda"
-        self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay, fused=fused)
         total = opt_cfg.max_training_steps or 1_000_000
         warm = opt_cfg.lr_num_warmup_steps or 0
-        self.sched = torch.optim.lr_scheduler.LambdaLR(
-            self.opt, poly_decay_lambda(warm, total, opt_cfg.lr_decay_power, opt_cfg.init_lr, opt_cfg.end_lr))
+        self.lr_lambda = poly_decay_lambda(warm, total, opt_cfg.lr_decay_power, opt_cfg.init_lr, opt_cfg.end_lr)
+        self.sched_step = 0  # LambdaLR semantics: the first optimizer step uses lambda(0)
+        if dev.type == "cuda":
+            self.opt = FusedAdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
+            self.sched = None
+        else:
+            self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
+            self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, self.lr_lambda)
         self.use_graph = use_graph
         self.graph = None
         self.static_batch = None
@@ -70,10 +142,15 @@ class TrainStep:
     # --------------------------------------------------------------------------------------------------------
     def _fwd_bwd(self, batch: PytorchBatch):
         # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
+        dev = self.params[0].device
+        if dev.type == "cuda":
+            begin_dropout_step(dev)
         with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32,
                             cache_enabled=not self.use_graph):
             out = self.model(batch)
         out.loss.backward()
+        if dev.type == "cuda":
+            end_dropout_step(dev)
         return out.loss.detach()
 
     def _allreduce(self):
@@ -105,8 +182,12 @@ class TrainStep:
             self.graph.replay()
             loss = self.static_loss
         self._allreduce()
-        self.opt.step()
-        self.sched.step()
+        if self.sched is None:
+            self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step))
+        else:
+            self.opt.step()
+            self.sched.step()
+        self.sched_step += 1
         return loss
 
     def _capture(self, batch: PytorchBatch):

@@ -19,7 +19,7 @@ from transformers.utils import ModelOutput
 from .. import _lib as L
 from ..data.data_embedding_enums import MeasIndexGroupOptions
 from ..data.types import DataModality, PytorchBatch
-from ..fused import linear_bias
+from ..fused import head_losses, linear_bias
 from ..kernels import OutputLossFn, batch_view
 from .config import TimeToEventGenerationHeadType
 from .generative_layers import (
@@ -225,10 +225,14 @@ def fused_ci_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
                                     all_regression_measurements(layer.config), 0)
     mods = layer._content_modules() + [layer.TTE_layer.proj]
     B, Lq, D = encoded.shape
+    bv = batch_view(batch)
+    tte = layer._tte_spec(layer._layout["n_content"])
+    fused = head_losses(encoded.reshape(B * Lq, D), None, bv, terms, tte, 1, 1, mods, [])
+    if fused is not None:
+        return fused, names
     z = linear_bias(encoded.reshape(B * Lq, D), [m.weight for m in mods], [m.bias for m in mods])
     b = torch.cat([m.bias for m in mods], 0)
-    bv = batch_view(batch)
-    losses = OutputLossFn.apply(z, None, b, bv, terms, layer._tte_spec(layer._layout["n_content"]), 1, 1)
+    losses = OutputLossFn.apply(z, None, b, bv, terms, tte, 1, 1)
     return losses, names
 
 
@@ -256,6 +260,12 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
             names.append(nn_)
     mods = layer._content_modules()
     bv = batch_view(batch)
+    if terms:
+        fused = head_losses(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D),
+                            encoded[:, :, G - 1, :].reshape(B * Lq, D), bv, terms, layer._tte_spec(0), 0,
+                            max(1, G - 1), mods, [layer.TTE_layer.proj])
+        if fused is not None:
+            return fused, names
     if terms:
         zc = linear_bias(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D), [m.weight for m in mods],
                          [m.bias for m in mods])

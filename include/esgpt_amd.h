@@ -198,20 +198,38 @@ int64_t esgpt_column_sum_partials(int64_t N);
 int esgpt_column_sum(const void* x, int dtype, int64_t N, int64_t F, float* part, float* out, void* stream);
 
 /* ---- Projection GEMM -------------------------------------------------------------------------------------
- * C[M, N] = A · B (+ bias[n]) with bf16 operands and f32 accumulation (the q/k/v/out, c_fc/c_proj and head
+ * C[M, N] = alpha · (A · B) (+ bias[n]) with bf16 operands and f32 accumulation (the q/k/v/out, c_fc/c_proj and head
  * projections and their input / weight gradients, transformer.py:133-163, 378-391). Operand layouts:
  *   A: ESGPT_GEMM_K_CONTIG  A[m][k] = a[m*lda + k]     ESGPT_GEMM_MN_CONTIG  A[m][k] = a[k*lda + m]
  *   B: ESGPT_GEMM_K_CONTIG  B[k][n] = b[n*ldb + k]     ESGPT_GEMM_MN_CONTIG  B[k][n] = b[k*ldb + n]
  * so y = x·Wᵀ is (K, K), dx = dy·W is (K, MN) and dW = dyᵀ·x is (MN, MN). c_dtype ESGPT_BF16 or ESGPT_F32;
- * accumulate (f32 only): C += A·B (+ bias). Requires K, lda, ldb multiples of 8, the MN-contig extents multiples
- * of 8 and 16-B aligned A, B. Workspace: f32 split-K slabs, esgpt_gemm_workspace(M, N, K) bytes (0 = none). The
+ * accumulate (f32 only): C += alpha·A·B (+ bias). alpha: optional DEVICE pointer to one f32 (NULL = 1), read at
+ * run time (e.g. the incoming gradient of a loss, without a host sync or a separate scaling kernel). Requires K,
+ * lda, ldb multiples of 8, the MN-contig extents multiples of 8, 16-B aligned A, B, C (and bias), and N, ldc
+ * multiples of 8 (bf16 C) / 4 (f32 C). Workspace: f32 split-K slabs, esgpt_gemm_workspace(M, N, K) bytes (0 = none). The
  * split-K reduction runs in a fixed order: results are deterministic. */
 #define ESGPT_GEMM_K_CONTIG 0
 #define ESGPT_GEMM_MN_CONTIG 1
 size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K);
 int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, const void* B, int64_t ldb, int64_t M,
-                    int64_t N, int64_t K, const float* bias, void* C, int64_t ldc, int c_dtype, int accumulate,
-                    void* workspace, size_t workspace_bytes, void* stream);
+                    int64_t N, int64_t K, const float* bias, const float* alpha, void* C, int64_t ldc, int c_dtype,
+                    int accumulate, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- Optimizer ------------------------------------------------------------------------------------------
+ * Fused AdamW step (torch.optim.AdamW semantics: decoupled weight decay, bias-corrected moments;
+ * generative_modeling.py:460-485 configure_optimizers) over many parameter tensors in ONE launch.
+ * table: device array of esgpt_adam_tensor; blocks: device array of (tensor index << 40 | first element), one
+ * entry per esgpt_adamw_chunk() elements of each tensor. step = the 1-based optimizer step (bias corrections). */
+typedef struct esgpt_adam_tensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  int64_t n;
+} esgpt_adam_tensor;
+int64_t esgpt_adamw_chunk(void);
+int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, float lr, float beta1,
+                float beta2, float eps, float weight_decay, int64_t step, void* stream);
 
 /* ---- Misc ----------------------------------------------------------------------------------------------- */
 const char* esgpt_version(void);
