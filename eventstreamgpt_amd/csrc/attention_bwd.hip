@@ -1,0 +1,432 @@
+// bf16 MFMA attention backward for gfx950 (InnerSelfAttention._attn, transformer.py:171-217): ONE kernel computes
+// dQ, dK and dV with no atomics when a (batch, head) has at most 256 keys (every C1/C2/C4 sequence), and adds dQ with
+// f32 atomics into a workspace otherwise (one conversion pass at the end).
+//
+// Work decomposition: one 512-thread workgroup = 8 waves = 256 keys of one (batch, head); wave w owns keys
+// 32w .. 32w+31 of the block (K, V fragments in registers, dKᵀ / dVᵀ accumulators in registers). The workgroup
+// sweeps the query tiles that can see its keys (causal / local window bounds), QT queries at a time:
+//   stage Q, dO (row-major LDS images) and the per-query constants lse, δ = rowsum(dO∘O) (δ computed here from
+//   dO and O: no separate pass, no δ buffer);
+//   per wave and 32-query slice:   S  = Q·Kᵀ − lse      (accumulator initialised to −lse: P = exp(S) directly)
+//                                  dP = dO·Vᵀ − δ       (initialised to −δ)
+//                                  (key on the MFMA lane: both accumulators are the B operands of the next two)
+//                                  dVᵀ += dOᵀ·(P∘Z),  dKᵀ += Qᵀ·dS,  dS = P∘(Z∘dP̃ − δ)   (Z = dropout keep/scale)
+//   dS crosses LDS once ([key][q] image, 8-byte stores), then dQ = dS·K for the tile over all 256 keys, one 32x32
+//   output tile per wave (K image [key][d] read transposed).
+// Fragment conventions (v_mfma_f32_32x32x16_bf16): lane l = (r = l&31, h = l>>5); A[row r][k = 8h+j],
+// B[k = 8h+j][col r]; C reg i = row (i&3) + 8(i>>2) + 4h, col r. An accumulator used as a B operand supplies k-step
+// s element j = row 16s + 8(j>>2) + 4h + (j&3) (permuted); the A operand is then read in that order.
+// Roofline: MFMA-bound at large L; algorithmic FLOPs 8·H·hd·T (T = allowed (q, k) pairs; recompute not counted).
+#include "common.h"
+
+using namespace esgpt;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#ifdef ESGPT_STAMPS
+__device__ uint64_t g_stamps[64];
+#define STAMP(i)                                                                              \
+  do {                                                                                        \
+    if (blockIdx.x == 0 && blockIdx.y == 5 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STAMP(i)
+#endif
+
+constexpr int KB = 256;      // keys per workgroup
+constexpr int NW = 8;        // waves
+constexpr int THREADS = 64 * NW;
+
+__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 zero8() {
+  bf16x8 z;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.f;
+  return z;
+}
+
+__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)p);
+}
+
+__device__ __forceinline__ bf16x8 join(bf16x4 lo, bf16x4 hi) {
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+// Accumulator registers 8s..8s+7 -> bf16 operand fragment (permuted k order).
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (__bf16)x[8 * s + j];
+  return f;
+}
+
+__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  const __bf16 a = (__bf16)lo, b = (__bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+// Stores the 32 accumulator-row values of one lane's column (x[i] = row acc_row(i, h)) as bf16 into
+// dst[0 .. 31] with 16-B stores: register groups g and g+1 are joined across the half-waves with
+// v_permlane32_swap (lanes 0-31 end up with rows 8g..8g+7, lanes 32-63 with rows 8g+8..8g+15).
+__device__ __forceinline__ void store_col32(__bf16* dst, const f32x16& x, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; g += 2) {
+    uint32_t a0 = pack2(x[4 * g], x[4 * g + 1]), a1 = pack2(x[4 * g + 2], x[4 * g + 3]);
+    uint32_t b0 = pack2(x[4 * g + 4], x[4 * g + 5]), b1 = pack2(x[4 * g + 6], x[4 * g + 7]);
+    const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    *reinterpret_cast<uint4*>(dst + 8 * g + 8 * h) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  }
+}
+
+// LDS images with W bf16 columns per row, unpadded, 16-B chunks XOR-swizzled per row so that BOTH access kinds
+// are bank-conflict free: 16-B row reads (ds_read_b128: lane r reads row r, one chunk; 16-lane groups
+// {0-3,12-15,20-27} / {4-11,16-19,28-31}) and transposed reads (ds_read_b64_tr_b16: a 32-lane half reads 4
+// consecutive rows x 32 columns), plus 8-B stores of 16 consecutive rows at one column.
+//   W = 32  (64-B rows):  chunk ^ ((row >> 2) & 3)
+//   W = 64  (128-B rows): chunk ^ g(row >> 1),  g(m) = ((m & 1) << 2) | ((m >> 1) & 3)
+//   W = 128 (256-B rows): chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))
+// off(row, col) is an element offset; col % 4 == 0 (8-B accesses stay inside one chunk).
+template <int W>
+struct Img {
+  __device__ __forceinline__ static int off(int row, int col) {
+    int sw;
+    if (W == 32) sw = (row >> 2) & 3;
+    else if (W == 64) sw = (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+    else sw = ((row & 3) << 2) | ((row >> 2) & 3);
+    return row * W + (((col >> 3) ^ sw) << 3) + (col & 7);
+  }
+};
+
+template <int HD>
+struct Cfg {
+  static constexpr int QT = HD == 128 ? 32 : 64;  // queries per tile
+  static constexpr int LDS_BYTES = 2 * (KB * HD + 2 * QT * HD + KB * QT) + 8 * QT;
+};
+
+template <int HD, bool DROP>
+__global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
+    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
+    int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
+    const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
+    __bf16* __restrict__ dq, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d,
+    float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed) {
+  constexpr int QT = Cfg<HD>::QT;
+  using IQ = Img<HD>;  // Q, dO, K images: [row][HD]
+  using IS = Img<QT>;  // dS image: [key][QT]
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  __bf16* sK = reinterpret_cast<__bf16*>(smem_raw);
+  __bf16* sQ = sK + KB * HD;
+  __bf16* sD = sQ + QT * HD;
+  __bf16* sS = sD + QT * HD;
+  float* sL = reinterpret_cast<float*>(sS + KB * QT);
+  float* sDl = sL + QT;
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;  // transposed-read lane roles
+  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
+  const int off = Lk - Lq;
+  const int kb0 = blockIdx.x * KB;
+  const int kw0 = kb0 + 32 * wave;  // this wave's first key
+  const int key = kw0 + r;
+  const bool kvalid = key < Lk && (kmask == nullptr || kmask[(int64_t)b * Lk + key] != 0);
+  STAMP(0);
+
+  // ---- own keys: K / V fragments (B operands of S and dP) ----
+  bf16x8 kf[HD / 16], vf[HD / 16];
+  {
+    const int kk = min(key, Lk - 1);
+    const __bf16* krow = k + ((int64_t)b * Lk + kk) * ld_in + hh * HD;
+    const __bf16* vrow = v + ((int64_t)b * Lk + kk) * ld_in + hh * HD;
+#pragma unroll
+    for (int t = 0; t < HD / 16; ++t) {
+      kf[t] = key < Lk ? *reinterpret_cast<const bf16x8*>(krow + 16 * t + 8 * h) : zero8();
+      vf[t] = key < Lk ? *reinterpret_cast<const bf16x8*>(vrow + 16 * t + 8 * h) : zero8();
+    }
+  }
+  // ---- K image of the whole key block for dQ = dS·K ----
+  for (int c = tid; c < KB * HD / 8; c += THREADS) {
+    const int row = c / (HD / 8), c8 = c % (HD / 8), kr = kb0 + row;
+    bf16x8 val = zero8();
+    if (kr < Lk) val = *reinterpret_cast<const bf16x8*>(k + ((int64_t)b * Lk + kr) * ld_in + hh * HD + c8 * 8);
+    *reinterpret_cast<bf16x8*>(sK + IQ::off(row, c8 * 8)) = val;
+  }
+
+  f32x16 dka[HD / 32], dva[HD / 32];
+#pragma unroll
+  for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dka[dt][i] = dva[dt][i] = 0.f;
+
+  const int kbend = min(Lk, kb0 + KB) - 1;  // last key of the block
+  const int qlo = max(0, kb0 - off);
+  const int qhi = window ? min(Lq - 1, kbend + window - 1 - off) : Lq - 1;
+  const bool direct = dq32 == nullptr;  // this workgroup holds every key of the (batch, head)
+
+  // Query-tile prefetch: one 16-B chunk of Q, dO and O per thread (QT*HD/8 <= THREADS chunks per tile), plus the
+  // row's lse / validity for the chunk-0 thread. Issued one tile ahead, written to LDS at the top of the tile.
+  constexpr int NCHUNK = QT * HD / 8;
+  const bool stager = tid < NCHUNK;  // whole waves (NCHUNK is a multiple of 64)
+  const int srow = tid / (HD / 8), sc8 = tid % (HD / 8);
+  bf16x8 pq = zero8(), pd = zero8(), po = zero8();
+  float pl = INFINITY;
+  auto prefetch = [&](int q0) {
+    const int qi = q0 + srow;
+    const bool in = stager && qi < Lq;
+    pq = pd = po = zero8();
+    pl = INFINITY;
+    if (in) {
+      pq = *reinterpret_cast<const bf16x8*>(q + ((int64_t)b * tq + qi) * ld_in + hh * HD + sc8 * 8);
+      pd = *reinterpret_cast<const bf16x8*>(dout + ((int64_t)b * Lq + qi) * ld_do + hh * HD + sc8 * 8);
+      po = *reinterpret_cast<const bf16x8*>(o + ((int64_t)b * Lq + qi) * ld_o + hh * HD + sc8 * 8);
+      if (sc8 == 0 && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0)) pl = lse[(int64_t)bh * Lq + qi];
+    }
+  };
+  int q0 = (qlo / QT) * QT;
+  if (q0 <= qhi) prefetch(q0);
+  STAMP(1);
+  int it = 0;
+
+  for (; q0 <= qhi; q0 += QT, ++it) {
+    __syncthreads();  // the previous tile's reads of sQ / sD / sS are done
+    STAMP(2 + 6 * it);
+    if (stager) {
+      *reinterpret_cast<bf16x8*>(sQ + IQ::off(srow, sc8 * 8)) = pq;
+      *reinterpret_cast<bf16x8*>(sD + IQ::off(srow, sc8 * 8)) = pd;
+      float dl = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl = fmaf((float)pd[j], (float)po[j], dl);
+      // δ: sum over the HD/8 consecutive threads of the row (rows never straddle a wave)
+#pragma unroll
+      for (int o2 = 1; o2 < HD / 8; o2 <<= 1) dl += __shfl_xor(dl, o2, 64);
+      if (sc8 == 0) {
+        sL[srow] = pl;  // +inf for invalid / missing queries: P = exp(S - inf) = 0 for the row
+        sDl[srow] = pl == INFINITY ? 0.f : dl;
+      }
+    }
+    __syncthreads();
+    STAMP(3 + 6 * it);
+    if (q0 + QT <= qhi) prefetch(q0 + QT);  // in flight during this tile's MFMAs
+
+    // ---- per wave: S, dP, dV, dK for its 32 keys over the tile's queries ----
+#pragma unroll
+    for (int qs = 0; qs < QT / 32; ++qs) {
+      const int qa = q0 + 32 * qs;  // first query of the slice
+      const int qpos_lo = qa + off, qpos_hi = min(qa + 31, Lq - 1) + off;
+      const bool any = qa < Lq && qpos_hi >= kw0 && kw0 < Lk && (window == 0 || qpos_lo - (kw0 + 31) < window);
+      f32x16 s, dp;
+      if (any) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = 32 * qs + acc_row(i, h);
+          s[i] = -sL[row];
+          dp[i] = -sDl[row];
+        }
+#pragma unroll
+        for (int t = 0; t < HD / 16; ++t) {
+          const bf16x8 qa8 = *reinterpret_cast<const bf16x8*>(sQ + IQ::off(32 * qs + r, 16 * t + 8 * h));
+          const bf16x8 da8 = *reinterpret_cast<const bf16x8*>(sD + IQ::off(32 * qs + r, 16 * t + 8 * h));
+          s = mfma(qa8, kf[t], s);
+          dp = mfma(da8, vf[t], dp);
+        }
+        constexpr float kLog2e = 1.4426950408889634f;
+        // fully visible slice: every key of the wave valid and inside the causal / local band of every query
+        const bool full = __ballot(kvalid) == ~0ull && qpos_lo >= kw0 + 31 && (window == 0 || qpos_hi - kw0 < window);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int ql = 32 * qs + acc_row(i, h);
+          const int qpos = q0 + ql + off;
+          const float e = __builtin_amdgcn_exp2f(s[i] * kLog2e);
+          const bool ok = full | (kvalid & (key <= qpos) & ((window == 0) | (qpos - key < window)));
+          const float p = ok ? e : 0.f;
+          if (DROP) {
+            const float z = dropout_mult(dr, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)(q0 + ql)) * (uint64_t)Lk +
+                                                 (uint64_t)key);
+            const float dl = sDl[ql];
+            s[i] = p * z;                          // P∘Z (feeds dV)
+            dp[i] = p * (z * (dp[i] + dl) - dl);   // dS
+          } else {
+            s[i] = p;
+            dp[i] = p * dp[i];
+          }
+        }
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pf = acc_frag(s, ss);
+          const bf16x8 dsf = acc_frag(dp, ss);
+          const int row0 = 32 * qs + 16 * ss + 4 * (g >> 1) + q4;
+#pragma unroll
+          for (int dt = 0; dt < HD / 32; ++dt) {
+            const int col = 32 * dt + 16 * (g & 1) + 4 * p4;
+            const bf16x8 dof = join(tr_read(sD + IQ::off(row0, col)), tr_read(sD + IQ::off(row0 + 8, col)));
+            dva[dt] = mfma(dof, pf, dva[dt]);
+            const bf16x8 qf = join(tr_read(sQ + IQ::off(row0, col)), tr_read(sQ + IQ::off(row0 + 8, col)));
+            dka[dt] = mfma(qf, dsf, dka[dt]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dp[i] = 0.f;
+      }
+      // dS -> LDS [key][q] (4 consecutive queries per register group: one 8-byte store each)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        bf16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (__bf16)dp[4 * gg + j];
+        *reinterpret_cast<bf16x4*>(sS + IS::off(32 * wave + r, 32 * qs + 8 * gg + 4 * h)) = w;
+      }
+    }
+    STAMP(4 + 6 * it);
+    __syncthreads();
+    STAMP(5 + 6 * it);
+
+    // ---- dQ[q][d] = Σ_key dS[q][key] · K[key][d] for the tile: one 32x32 output tile per wave ----
+    constexpr int NT = (QT / 32) * (HD / 32);
+    if (wave < NT) {
+      const int qsub = wave % (QT / 32), dsub = wave / (QT / 32);
+      const int qpos_max = min(q0 + QT - 1, Lq - 1) + off;
+      const int nkeys = min(min(kbend, qpos_max) - kb0 + 1, KB);  // keys past the causal bound contribute 0
+      f32x16 acc;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+      if (direct) {
+        // dQᵀ[d][q] = Kᵀ·dSᵀ: the query on the lane, 16-B row stores of the bf16 result
+        for (int t = 0; t < (nkeys + 15) / 16; ++t) {
+          const int kr = 16 * t + 8 * (g >> 1) + q4;
+          const int qc = 32 * qsub + 16 * (g & 1) + 4 * p4, dc = 32 * dsub + 16 * (g & 1) + 4 * p4;
+          const bf16x8 af = join(tr_read(sS + IS::off(kr, qc)), tr_read(sS + IS::off(kr + 4, qc)));
+          const bf16x8 bf = join(tr_read(sK + IQ::off(kr, dc)), tr_read(sK + IQ::off(kr + 4, dc)));
+          acc = mfma(bf, af, acc);
+        }
+        const int qi = q0 + 32 * qsub + r;
+        STAMP(6 + 6 * it);
+        if (qi < Lq) store_col32(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + 32 * dsub, acc, h);
+        STAMP(7 + 6 * it);
+      } else {
+        // dQ[q][d] = dS·K: the head dim on the lane, so that each f32 atomic instruction adds two 128-B rows
+        for (int t = 0; t < (nkeys + 15) / 16; ++t) {
+          const int kr = 16 * t + 8 * (g >> 1) + q4;
+          const int qc = 32 * qsub + 16 * (g & 1) + 4 * p4, dc = 32 * dsub + 16 * (g & 1) + 4 * p4;
+          const bf16x8 af = join(tr_read(sS + IS::off(kr, qc)), tr_read(sS + IS::off(kr + 4, qc)));
+          const bf16x8 bf = join(tr_read(sK + IQ::off(kr, dc)), tr_read(sK + IQ::off(kr + 4, dc)));
+          acc = mfma(af, bf, acc);
+        }
+        const int d = 32 * dsub + r;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int qi = q0 + 32 * qsub + acc_row(i, h);
+          if (qi < Lq) atomicAdd(dq32 + ((int64_t)bh * Lq + qi) * HD + d, acc[i]);
+        }
+      }
+    }
+  }
+
+  STAMP(40);
+  // ---- dK, dV (every key belongs to exactly one workgroup): 16-B row stores ----
+  if (key < Lk) {
+    __bf16* ko = dk + ((int64_t)b * Lk + key) * ld_d + hh * HD;
+    __bf16* vo = dv + ((int64_t)b * Lk + key) * ld_d + hh * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt) {
+      store_col32(ko + 32 * dt, dka[dt], h);
+      store_col32(vo + 32 * dt, dva[dt], h);
+    }
+  }
+  STAMP(41);
+}
+
+// dq (bf16, rows strided by tq) <- dq32 (f32 [B*H, Lq, HD])
+template <int HD>
+__global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ dq32, __bf16* __restrict__ dq,
+                                                         int64_t ld_d, int64_t tq, int H, int Lq, int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int64_t e = 4 * i;
+  const int d = (int)(e % HD);
+  const int64_t rowi = e / HD;  // (bh, qi)
+  const int qi = (int)(rowi % Lq);
+  const int64_t bh = rowi / Lq;
+  const int b = (int)(bh / H), hh = (int)(bh % H);
+  const float4 x = *reinterpret_cast<const float4*>(dq32 + e);
+  bf16x4 w;
+  w[0] = (__bf16)x.x; w[1] = (__bf16)x.y; w[2] = (__bf16)x.z; w[3] = (__bf16)x.w;
+  *reinterpret_cast<bf16x4*>(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + d) = w;
+}
+
+template <int HD>
+int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
+           const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask, void* dq,
+           void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t window,
+           float drop_p, const uint64_t* seed, float* dq32, hipStream_t st) {
+  constexpr int lds = Cfg<HD>::LDS_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)attn_bwd_kernel<HD, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds) != hipSuccess ||
+        hipFuncSetAttribute((const void*)attn_bwd_kernel<HD, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds) != hipSuccess)
+      return ESGPT_ERR_LAUNCH;
+    attr = true;
+  }
+  const int nkb = (int)cdiv(Lk, KB);
+  float* acc = nkb > 1 ? dq32 : nullptr;
+  if (acc && zero_async(acc, sizeof(float) * (size_t)(B * H * Lq * HD), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  const dim3 grid((unsigned)nkb, (unsigned)(B * H));
+  if (drop_p > 0.f)
+    attn_bwd_kernel<HD, true><<<grid, THREADS, lds, st>>>(
+        (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
+        ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,
+        (int)window, drop_p, seed);
+  else
+    attn_bwd_kernel<HD, false><<<grid, THREADS, lds, st>>>(
+        (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
+        ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,
+        (int)window, drop_p, seed);
+  if (acc) {
+    const int64_t n4 = B * H * Lq * HD / 4;
+    dq_convert_kernel<HD><<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(acc, (__bf16*)dq, ld_d, tq, (int)H, (int)Lq, n4);
+  }
+  return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+}
+
+}  // namespace
+
+#ifdef ESGPT_STAMPS
+extern "C" int esgpt_debug_stamps(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(uint64_t) * 64) == hipSuccess ? 0 : 1;
+}
+#endif
+
+size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
+  return Lk > KB ? sizeof(float) * (size_t)(B * H * Lq * hd) : 0;
+}
+
+int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                        int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
+                        const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
+                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                        float* dq32, hipStream_t st) {
+  if (hd == 32)
+    return launch<32>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
+                      window, drop_p, seed, dq32, st);
+  if (hd == 64)
+    return launch<64>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
+                      window, drop_p, seed, dq32, st);
+  return launch<128>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
+                     window, drop_p, seed, dq32, st);
+}

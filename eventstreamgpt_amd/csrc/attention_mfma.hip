@@ -33,6 +33,24 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 
 __device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  const __bf16 a = (__bf16)lo, b = (__bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+
+// Stores one lane's 32 accumulator-row values (x[i] = row acc_row(i, h)) as bf16 into dst[0 .. 31] with 16-B
+// stores, joining register groups g, g+1 across the half-waves with v_permlane32_swap.
+__device__ __forceinline__ void store_col32(__bf16* dst, const f32x16& x, int h) {
+#pragma unroll
+  for (int g = 0; g < 4; g += 2) {
+    uint32_t a0 = pack2(x[4 * g], x[4 * g + 1]), a1 = pack2(x[4 * g + 2], x[4 * g + 3]);
+    uint32_t b0 = pack2(x[4 * g + 4], x[4 * g + 5]), b1 = pack2(x[4 * g + 6], x[4 * g + 7]);
+    const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+    *reinterpret_cast<uint4*>(dst + 8 * g + 8 * h) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  }
+}
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -129,7 +147,7 @@ __device__ __forceinline__ void load_kv(const __bf16* __restrict__ kb, const __b
 // prefetched into registers while the current one is consumed. Key validity is a 64-bit ballot per tile; tiles
 // that are fully valid and fully inside the causal / local band skip the per-element masks. Softmax in the exp2
 // domain (v_exp_f32).
-template <int HD>
+template <int HD, bool DROP>
 __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __restrict__ q,
                                                                const __bf16* __restrict__ k,
                                                                const __bf16* __restrict__ v, int64_t ld_in, int64_t tq,
@@ -238,9 +256,7 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(s[c][i] - msub);  // exp2(-inf) = 0
         rs += p;  // normaliser over undropped probabilities
-        s[c][i] = (dr.p > 0.f && p != 0.f)
-                      ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + 32 * c + acc_row(i, h)))
-                      : p;
+        s[c][i] = DROP ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + 32 * c + acc_row(i, h))) : p;
       }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
@@ -275,245 +291,12 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
   if (qin) {
     __bf16* orow = o + ((int64_t)b * Lq + qi) * ld_o + hh * HD;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
+    for (int dt = 0; dt < HD / 32; ++dt) {
 #pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        bf16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (__bf16)(oacc[dt][4 * gg + j] * inv);
-        *reinterpret_cast<bf16x4*>(orow + 32 * dt + 8 * gg + 4 * h) = w;
-      }
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= inv;
+      store_col32(orow + 32 * dt, oacc[dt], h);
+    }
     if (h == 0) lse[(int64_t)bh * Lq + qi] = ok ? m * kLn2 + logf(l) : 0.f;
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------
-template <int HD>
-__global__ __launch_bounds__(THREADS) void attn_bwd_dq_mfma_kernel(
-    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
-    int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
-    const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
-    __bf16* __restrict__ dq, int64_t ld_d, float* __restrict__ delta, int H, int Lq, int Lk, int window,
-    float drop_p, const uint64_t* __restrict__ seed) {
-  constexpr int NP = HD + 8, TP = ROWS + 4;
-  __shared__ __attribute__((aligned(16))) __bf16 sK[ROWS * NP];
-  __shared__ __attribute__((aligned(16))) __bf16 sV[ROWS * NP];
-  __shared__ __attribute__((aligned(16))) __bf16 sKt[HD * TP];
-  __shared__ uint8_t sKm[ROWS];
-  __shared__ int sAny;
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
-  const DropoutSpec dr = make_dropout(drop_p, seed);
-  const int off = Lk - Lq;
-  const int qb = blockIdx.x * ROWS;
-  const int qi = qb + wave * 32 + r;
-  const bool qin = qi < Lq;
-  const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
-  const int qpos = qi + off;
-
-  bf16x8 qf[HD / 16], df[HD / 16];
-  const __bf16* qrow = q + ((int64_t)b * tq + qi) * ld_in + hh * HD;
-  const __bf16* drow = dout + ((int64_t)b * Lq + qi) * ld_do + hh * HD;
-  const __bf16* orow = o + ((int64_t)b * Lq + qi) * ld_o + hh * HD;
-  float dl = 0.f;
-#pragma unroll
-  for (int t = 0; t < HD / 16; ++t) {
-    qf[t] = qin ? *reinterpret_cast<const bf16x8*>(qrow + 16 * t + 8 * h) : zero8();
-    df[t] = qin ? *reinterpret_cast<const bf16x8*>(drow + 16 * t + 8 * h) : zero8();
-    if (qin) {
-      const bf16x8 of = *reinterpret_cast<const bf16x8*>(orow + 16 * t + 8 * h);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dl = fmaf((float)df[t][j], (float)of[j], dl);
-    }
-  }
-  dl += __shfl_xor(dl, 32, 64);
-  if (!qvalid) dl = 0.f;
-  if (qin && h == 0) delta[(int64_t)bh * Lq + qi] = dl;
-  const float ls = qvalid ? lse[(int64_t)bh * Lq + qi] : 0.f;
-
-  f32x16 dqa[HD / 32];
-#pragma unroll
-  for (int dt = 0; dt < HD / 32; ++dt) dqa[dt] = zero16();
-
-  const int qhi = min(Lq, qb + ROWS) - 1;
-  const int kmax = min(Lk - 1, qhi + off);
-  const int kmin = window ? max(0, qb + off - window + 1) : 0;
-  const __bf16* kbase = k + (int64_t)b * Lk * ld_in + hh * HD;
-  const __bf16* vbase = v + (int64_t)b * Lk * ld_in + hh * HD;
-
-  for (int kt = (kmin / ROWS) * ROWS; kt <= kmax; kt += ROWS) {
-    __syncthreads();
-    if (tid == 0) sAny = 0;
-    __syncthreads();
-    if (tid < ROWS) {
-      const int key = kt + tid;
-      const uint8_t ok = key < Lk && (kmask == nullptr || kmask[(int64_t)b * Lk + key] != 0);
-      sKm[tid] = ok;
-      if (ok) sAny = 1;
-    }
-    __syncthreads();
-    if (!sAny) continue;
-    stage_rows<HD>(kbase, ld_in, kt, Lk, sK, sKt);
-    stage_rows<HD>(vbase, ld_in, kt, Lk, sV, nullptr);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      f32x16 st = zero16(), dpt = zero16();
-#pragma unroll
-      for (int t = 0; t < HD / 16; ++t) {
-        const bf16x8 ka = *reinterpret_cast<const bf16x8*>(sK + (32 * c + r) * NP + 16 * t + 8 * h);
-        const bf16x8 va = *reinterpret_cast<const bf16x8*>(sV + (32 * c + r) * NP + 16 * t + 8 * h);
-        st = mfma(ka, qf[t], st);
-        dpt = mfma(va, df[t], dpt);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int kr = 32 * c + acc_row(i, h);
-        const bool ok = qvalid && sKm[kr] && allowed(kt + kr, qpos, window);
-        const float p = ok ? expf(st[i] - ls) : 0.f;
-        const float keep = (dr.p > 0.f && ok) ? dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + kr)) : 1.f;
-        st[i] = p * (dpt[i] * keep - dl);
-      }
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 dsf = acc_frag(st, ss);
-#pragma unroll
-        for (int dt = 0; dt < HD / 32; ++dt) {
-          const bf16x8 kf = perm_frag(sKt, TP, 32 * dt + r, 32 * c, ss, h);
-          dqa[dt] = mfma(kf, dsf, dqa[dt]);
-        }
-      }
-    }
-  }
-  if (qin) {
-    __bf16* out = dq + ((int64_t)b * tq + qi) * ld_d + hh * HD;
-#pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (__bf16)dqa[dt][4 * g + j];
-        *reinterpret_cast<bf16x4*>(out + 32 * dt + 8 * g + 4 * h) = w;
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------
-template <int HD>
-__global__ __launch_bounds__(THREADS) void attn_bwd_dkv_mfma_kernel(
-    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
-    int64_t tq, const __bf16* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
-    const float* __restrict__ delta, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
-    __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d, int H, int Lq, int Lk, int window,
-    float drop_p, const uint64_t* __restrict__ seed) {
-  constexpr int NP = HD + 8, TP = ROWS + 4;
-  __shared__ __attribute__((aligned(16))) __bf16 sQ[ROWS * NP];
-  __shared__ __attribute__((aligned(16))) __bf16 sD[ROWS * NP];
-  __shared__ __attribute__((aligned(16))) __bf16 sQt[HD * TP];
-  __shared__ __attribute__((aligned(16))) __bf16 sDt[HD * TP];
-  __shared__ float sL[ROWS], sDl[ROWS];
-  __shared__ uint8_t sQm[ROWS];
-  __shared__ int sAny;
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
-  const DropoutSpec dr = make_dropout(drop_p, seed);
-  const int off = Lk - Lq;
-  const int kb = blockIdx.x * ROWS;
-  const int kk = kb + wave * 32 + r;
-  const bool kin = kk < Lk;
-  const bool kvalid = kin && (kmask == nullptr || kmask[(int64_t)b * Lk + kk] != 0);
-
-  bf16x8 kf[HD / 16], vf[HD / 16];
-  const __bf16* krow = k + ((int64_t)b * Lk + kk) * ld_in + hh * HD;
-  const __bf16* vrow = v + ((int64_t)b * Lk + kk) * ld_in + hh * HD;
-#pragma unroll
-  for (int t = 0; t < HD / 16; ++t) {
-    kf[t] = kin ? *reinterpret_cast<const bf16x8*>(krow + 16 * t + 8 * h) : zero8();
-    vf[t] = kin ? *reinterpret_cast<const bf16x8*>(vrow + 16 * t + 8 * h) : zero8();
-  }
-  f32x16 dka[HD / 32], dva[HD / 32];
-#pragma unroll
-  for (int dt = 0; dt < HD / 32; ++dt) {
-    dka[dt] = zero16();
-    dva[dt] = zero16();
-  }
-
-  const int khi = min(Lk, kb + ROWS) - 1;
-  const int qmin = max(0, kb - off);
-  const int qmax = window ? min(Lq - 1, khi + window - 1 - off) : Lq - 1;
-  const __bf16* qbase = q + (int64_t)b * tq * ld_in + hh * HD;
-  const __bf16* dbase = dout + (int64_t)b * Lq * ld_do + hh * HD;
-
-  for (int qt = (qmin / ROWS) * ROWS; qt <= qmax; qt += ROWS) {
-    __syncthreads();
-    if (tid == 0) sAny = 0;
-    __syncthreads();
-    if (tid < ROWS) {
-      const int qq = qt + tid;
-      const uint8_t ok = qq < Lq && (qmask == nullptr || qmask[(int64_t)b * Lq + qq] != 0);
-      sQm[tid] = ok;
-      sL[tid] = ok ? lse[(int64_t)bh * Lq + qq] : 0.f;
-      sDl[tid] = ok ? delta[(int64_t)bh * Lq + qq] : 0.f;
-      if (ok) sAny = 1;
-    }
-    __syncthreads();
-    if (!sAny) continue;
-    stage_rows<HD>(qbase, ld_in, qt, Lq, sQ, sQt);
-    stage_rows<HD>(dbase, ld_do, qt, Lq, sD, sDt);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      f32x16 s = zero16(), dp = zero16();
-#pragma unroll
-      for (int t = 0; t < HD / 16; ++t) {
-        const bf16x8 qa = *reinterpret_cast<const bf16x8*>(sQ + (32 * c + r) * NP + 16 * t + 8 * h);
-        const bf16x8 da = *reinterpret_cast<const bf16x8*>(sD + (32 * c + r) * NP + 16 * t + 8 * h);
-        s = mfma(qa, kf[t], s);
-        dp = mfma(da, vf[t], dp);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int qr = 32 * c + acc_row(i, h);
-        const int qpos = qt + qr + off;
-        const bool ok = kvalid && sQm[qr] && allowed(kk, qpos, window);
-        const float p = ok ? expf(s[i] - sL[qr]) : 0.f;
-        const float keep = (dr.p > 0.f && ok) ? dropout_mult(dr, elem_index(bh, Lq, Lk, qt + qr, kk)) : 1.f;
-        s[i] = p * keep;
-        dp[i] = p * (dp[i] * keep - sDl[qr]);
-      }
-#pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const bf16x8 pf = acc_frag(s, ss);
-        const bf16x8 dsf = acc_frag(dp, ss);
-#pragma unroll
-        for (int dt = 0; dt < HD / 32; ++dt) {
-          const bf16x8 da = perm_frag(sDt, TP, 32 * dt + r, 32 * c, ss, h);
-          dva[dt] = mfma(da, pf, dva[dt]);
-          const bf16x8 qa = perm_frag(sQt, TP, 32 * dt + r, 32 * c, ss, h);
-          dka[dt] = mfma(qa, dsf, dka[dt]);
-        }
-      }
-    }
-  }
-  if (kin) {
-    __bf16* ko = dk + ((int64_t)b * Lk + kk) * ld_d + hh * HD;
-    __bf16* vo = dv + ((int64_t)b * Lk + kk) * ld_d + hh * HD;
-#pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        bf16x4 wk, wv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          wk[j] = (__bf16)dka[dt][4 * g + j];
-          wv[j] = (__bf16)dva[dt][4 * g + j];
-        }
-        *reinterpret_cast<bf16x4*>(ko + 32 * dt + 8 * g + 4 * h) = wk;
-        *reinterpret_cast<bf16x4*>(vo + 32 * dt + 8 * g + 4 * h) = wv;
-      }
   }
 }
 
@@ -529,23 +312,15 @@ template <int HD>
 static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, int64_t ld_in,
                        int64_t tq, void* o, int64_t ld_o, float* lse, const uint8_t* kmask, const uint8_t* qmask,
                        int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed) {
-  attn_fwd_mfma_kernel<HD><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+  if (drop_p > 0.f)
+    attn_fwd_mfma_kernel<HD, true><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k,
+                                                                    (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o,
+                                                                    lse, kmask, qmask, (int)H, (int)Lq, (int)Lk,
+                                                                    (int)window, drop_p, seed);
+  else
+  attn_fwd_mfma_kernel<HD, false><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                                                            ld_in, tq, (__bf16*)o, ld_o, lse, kmask, qmask, (int)H,
                                                            (int)Lq, (int)Lk, (int)window, drop_p, seed);
-}
-
-template <int HD>
-static void launch_bwd(dim3 gq, dim3 gk, hipStream_t st, const void* q, const void* k, const void* v, int64_t ld_in,
-                       int64_t tq, const void* o, int64_t ld_o, const void* dout, int64_t ld_do, const float* lse,
-                       const uint8_t* kmask, const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d,
-                       int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed,
-                       float* delta) {
-  attn_bwd_dq_mfma_kernel<HD><<<gq, dim3(THREADS), 0, st>>>(
-      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
-      ld_do, lse, kmask, qmask, (__bf16*)dq, ld_d, delta, (int)H, (int)Lq, (int)Lk, (int)window, drop_p, seed);
-  attn_bwd_dkv_mfma_kernel<HD><<<gk, dim3(THREADS), 0, st>>>(
-      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)dout, ld_do, lse, delta, kmask,
-      qmask, (__bf16*)dk, (__bf16*)dv, ld_d, (int)H, (int)Lq, (int)Lk, (int)window, drop_p, seed);
 }
 
 int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
@@ -558,23 +333,5 @@ int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
     launch_fwd<64>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
   else
     launch_fwd<128>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
-  return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
-}
-
-int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
-                        int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
-                        const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
-                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
-                        float* delta, hipStream_t st) {
-  dim3 gq((unsigned)cdiv(Lq, ROWS), (unsigned)(B * H)), gk((unsigned)cdiv(Lk, ROWS), (unsigned)(B * H));
-  if (hd == 32)
-    launch_bwd<32>(gq, gk, st, q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, H, Lq,
-                   Lk, window, drop_p, seed, delta);
-  else if (hd == 64)
-    launch_bwd<64>(gq, gk, st, q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, H, Lq,
-                   Lk, window, drop_p, seed, delta);
-  else
-    launch_bwd<128>(gq, gk, st, q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, H, Lq,
-                    Lk, window, drop_p, seed, delta);
   return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
 }

@@ -66,25 +66,36 @@ __device__ __forceinline__ void set_err(int32_t* err, int code) {
   if (err) atomicOr(err, code);
 }
 
-// Attention-probability dropout: a counter-based hash (splitmix64 finaliser) of (seed, element index), so the
-// forward and backward regenerate the same keep-mask without storing it. keep <=> hash >= p * 2^32.
+// Dropout (attention probabilities, residual / input): a counter-based hash of (seed, element index), so the
+// forward and backward regenerate the same keep-mask without storing it. 32-bit arithmetic only (no 64-bit
+// multiplies in the hot loops): key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)) once per kernel, then per
+// element h = mix32(idx_lo ^ key ^ idx_hi * 0x9E3779B9) ("lowbias32" finaliser); keep <=> h >= p * 2^32.
 struct DropoutSpec {
   float p;          // drop probability (0 = off)
   float scale;      // 1 / (1 - p)
   uint32_t thresh;  // p * 2^32
-  uint64_t seed;
+  uint32_t key;
 };
 
-__host__ __device__ __forceinline__ uint32_t dropout_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t dropout_key(uint64_t seed) {
+  return mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) ^ 0x9E3779B9u));
+}
+
+__host__ __device__ __forceinline__ uint32_t dropout_hash(uint32_t key, uint64_t idx) {
+  return mix32((uint32_t)idx ^ key ^ ((uint32_t)(idx >> 32) * 0x9E3779B9u));
 }
 
 __device__ __forceinline__ float dropout_mult(const DropoutSpec& d, uint64_t idx) {
-  return (dropout_hash(d.seed, idx) >= d.thresh) ? d.scale : 0.f;
+  return (dropout_hash(d.key, idx) >= d.thresh) ? d.scale : 0.f;
 }
 
 __device__ __forceinline__ DropoutSpec make_dropout(float p, const uint64_t* seed_ptr) {
@@ -92,7 +103,7 @@ __device__ __forceinline__ DropoutSpec make_dropout(float p, const uint64_t* see
   d.p = p;
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   d.thresh = p > 0.f ? (uint32_t)fminf(p * 4294967296.f, 4294967295.f) : 0u;
-  d.seed = (p > 0.f && seed_ptr) ? *seed_ptr : 0ull;
+  d.key = dropout_key((p > 0.f && seed_ptr) ? *seed_ptr : 0ull);
   return d;
 }
 

@@ -365,7 +365,7 @@ class AttentionFn(torch.autograd.Function):
         Lk, Lq = T, T - skf
         es = qkv.element_size()
         dqkv = (torch.zeros if skf else torch.empty)(Bs, T, D3, dtype=qkv.dtype, device=qkv.device)
-        nbytes = lib.esgpt_attn_bwd_workspace(Bs, H, Lq)
+        nbytes = lib.esgpt_attn_bwd_workspace(Bs, H, Lq, Lk, hd)
         ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=qkv.device)
         base, dbase = qkv.data_ptr(), dqkv.data_ptr()
         with _timed("attn_bwd"):

@@ -122,7 +122,7 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
                    int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
                    void* stream);
-size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq);
+size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
 int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                    int64_t ld_o,
                    const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,

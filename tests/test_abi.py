@@ -42,7 +42,8 @@ def test_workspace_queries_without_gpu():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("library not built")
     lib = _lib.load(require_device=False)
-    assert lib.esgpt_attn_bwd_workspace(2, 4, 256) == 4 * 2 * 4 * 256
+    assert lib.esgpt_attn_bwd_workspace(2, 4, 256, 256, 64) == 4 * 2 * 4 * 256
+    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 64) == 4 * 2 * 4 * 512 * 64
     b = _lib.EsgptBatch()
     b.B, b.L, b.M, b.S = 32, 256, 16, 2
     assert lib.esgpt_embed_bag_bwd_workspace(ctypes.byref(b), 1, 1210, 256) > 32 * 256 * 16 * 16

@@ -170,17 +170,29 @@ def test_full_step_bf16_matches_oracle(cfg_name):
     out.loss.backward()
 
 
+def _np_mix32(x):
+    import numpy as np
+
+    x = x.astype(np.uint64) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x7FEB352D)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(15)
+    x = (x * np.uint64(0x846CA68B)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    return x
+
+
 def _np_keep(seed: int, B: int, H: int, Lq: int, Lk: int, p: float):
-    """Host restatement of the kernels' dropout keep-mask (splitmix64 of (seed, (bh*Lq+i)*Lk+j))."""
+    """Host restatement of the kernels' dropout keep-mask (csrc/common.h dropout_hash: lowbias32 of
+    idx_lo ^ key ^ idx_hi * 0x9E3779B9, key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)), idx = (bh*Lq+i)*Lk+j)."""
     import numpy as np
 
     with np.errstate(over="ignore"):
+        key = _np_mix32(np.uint64(seed & 0xFFFFFFFF) ^ _np_mix32(np.uint64(((seed >> 32) ^ 0x9E3779B9) & 0xFFFFFFFF)))
         idx = np.arange(B * H * Lq * Lk, dtype=np.uint64)
-        z = np.uint64(seed) + (idx + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
-        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        z = z ^ (z >> np.uint64(31))
-        h = (z >> np.uint64(32)).astype(np.uint64)
+        lo = idx & np.uint64(0xFFFFFFFF)
+        hi = ((idx >> np.uint64(32)) * np.uint64(0x9E3779B9)) & np.uint64(0xFFFFFFFF)
+        h = _np_mix32(lo ^ key ^ hi)
     thresh = int(np.float32(p) * np.float32(4294967296.0))
     return torch.from_numpy((h >= thresh).reshape(B, H, Lq, Lk))
 
