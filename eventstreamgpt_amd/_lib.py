@@ -85,8 +85,13 @@ SIGNATURES = {
     "esgpt_bias_act_partials": (_i64, [_i64]),
     "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),
     "esgpt_gemm_workspace": (_sz, [_i64, _i64, _i64]),
+    "esgpt_gemm_counters": (_i64, [_i64, _i64]),
     "esgpt_gemm_bf16": (_int, [_int, _vp, _i64, _int, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _int, _int,
-                               _vp, _sz, _vp]),
+                               _vp, _sz, _vp, _vp]),
+    "esgpt_linear_fwd": (_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _vp, _i64, _vp]),
+    "esgpt_linear_bwd_workspace": (_sz, [_i64, _i64, _i64, _int]),
+    "esgpt_linear_bwd": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64, _vp,
+                                _vp, _vp, _sz, _vp, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),

@@ -1,22 +1,25 @@
 // bf16 MFMA tile GEMM for the training step's projections (the InnerAttention q/k/v/out projections, the InnerMLP
 // c_fc/c_proj and the generative heads: transformer.py:133-163, 378-391; generative_layers.py) on gfx950.
 //
-//   C[M, N] = A · B (+ bias[n]),   bf16 operands, f32 accumulation, C bf16 or f32.
+//   C[M, N] = alpha · A · B (+ bias[n]) (+ epilogue),   bf16 operands, f32 accumulation, C bf16 or f32.
 //
-// The step's shapes are skinny: M = B·L tokens (8192 for the C2 workload) with N, K in {256 … 1232}, and the
-// weight gradients are [out, in] products with K = tokens. Library kernels pick 64x64 tiles with no K split for
-// the latter (64 workgroups on a 256-CU part); here the decomposition is chosen for the chip: 128x128 / 128x64 /
-// 64x64 tiles, and split-K into f32 slabs plus a fixed-order reduce (deterministic) when there are too few tiles.
+// The step's shapes are skinny: M = B·L tokens (8192 for the C2 workload) with N, K in {256 … 1624}, and the
+// weight gradients are [out, in] products with K = tokens. Tiles are 64x64 (4 waves of 32x32; measured best at
+// these sizes: more resident workgroups hide the load / store latency that dominates). Products with few tiles or
+// a long K split K into f32 slabs that the LAST-arriving workgroup of each tile sums in a fixed order (agent-scope
+// release / acquire ticket, cdna_hip_programming.md's in-launch split-K recipe; deterministic, no second launch).
+// Epilogues fuse what the step needs around a GEMM: bias + activation (c_fc: stores the pre-activation too), the
+// activation gradient (c_proj's dX), a device-side alpha (the incoming loss gradient) and the bias gradient
+// Σ_k A[m][k] as one extra MFMA against a ones operand. A projection's whole backward (dX = dY·W, dW = dYᵀ·X,
+// db = Σ dY) is ONE grouped launch.
 //
 // Operand layouts (both supported for either operand, so fwd, dX and dW need no transposed copies):
 //   A "K-contig": A[m][k] = a[m*lda + k]   LDS image [rows][BK + 8], fragments by 16-B row reads
-//   A "M-contig": A[m][k] = a[k*lda + m]   LDS image [BK][160], fragments by ds_read_b64_tr_b16 (hardware
-//                                          transpose; row stride = 16 dwords mod 64 -> conflict-free reads)
+//   A "M-contig": A[m][k] = a[k*lda + m]   LDS image [BK][96], fragments by ds_read_b64_tr_b16 (hardware
+//                                          transpose; row stride = 48 dwords -> conflict-free reads)
 //   B likewise with n in place of m ("K-contig": B[k][n] = b[n*ldb + k], "N-contig": B[k][n] = b[k*ldb + n]).
-// MFMA v_mfma_f32_32x32x16_bf16; 4 waves as 2x2, each wave (BM/2)x(BN/2); register-staged global->LDS with the
-// next k-tile's loads in flight during the current tile's MFMAs.
+// MFMA v_mfma_f32_32x32x16_bf16; register-staged global->LDS with NS-1 k-tiles in flight during the MFMAs.
 #include <algorithm>
-#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -34,6 +37,7 @@ constexpr int BK = 64;
 constexpr int KC_LD = BK + 8;  // K-contig image row stride (elements)
 constexpr int THREADS = 256;
 constexpr int NS = 3;          // register stages: NS-1 k-tiles in flight while one is written to LDS
+constexpr int TILE = 64;
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -64,10 +68,10 @@ struct Tile {
   __device__ __forceinline__ static void coords(int i, int& a, int& b) {
     const int c = threadIdx.x + THREADS * i;
     if (KC) {
-      a = c >> 3;          // row
-      b = (c & 7) * 8;     // k
+      a = c >> 3;             // row
+      b = (c & 7) * 8;        // k
     } else {
-      a = c / (R / 8);     // k-row
+      a = c / (R / 8);        // k-row
       b = (c % (R / 8)) * 8;  // column
     }
   }
@@ -127,237 +131,358 @@ struct Tile {
   }
 };
 
-// XCD-aware tile order: the hardware deals consecutive workgroup ids round-robin over the 8 XCDs (each with its
-// own L2), so id -> (xcd = id % 8, slot = id / 8) is remapped (bijectively) to a linear tile index that gives every
-// XCD a contiguous run of tiles. The n-tile index runs fastest, so the tiles of one XCD share A row-blocks in L2.
+// XCD-aware order: the hardware deals consecutive workgroup ids round-robin over the 8 XCDs (each with its own
+// L2), so id -> (xcd = id % 8, slot = id / 8) is remapped (bijectively) to a linear index that gives every XCD a
+// contiguous run. The split index runs fastest (the slabs of a tile are written and reduced on one XCD), then
+// the n-tile (the tiles of one XCD share A row-blocks in L2).
 __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   const int q = nwg >> 3, rr = nwg & 7, xcd = id & 7, slot = id >> 3;
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
 }
 
-// C = alpha · (A·B) (+ bias) for one BMxBN tile over k in [z*kchunk, min(K, (z+1)*kchunk)).
-// OUT_F32: C f32 (accumulate: C += …); else bf16. Split-K callers pass C = slab z (ldc = N) and no bias.
-// Pipeline: NS register stages (loads for k-tile i+NS-1 are issued before k-tile i is written to LDS) and two LDS
-// buffers (one barrier per k-tile: a buffer is rewritten only after every wave passed the next barrier).
-// The MFMAs compute the tile transposed (A-operand = B fragment, B-operand = A fragment), so that a lane owns one
-// output ROW m and its registers hold columns n = (e&3) + 8(e>>2) + 4h: four consecutive columns per register
-// group. The epilogue then stores 16 B per lane (f32: one group; bf16: two groups joined across the half-waves
-// with v_permlane32_swap), 8x fewer store instructions than one 2-byte store per element.
-template <bool AKC, bool BKC, int WM, int WN, bool OUT_F32>
-__global__ __launch_bounds__(THREADS) void gemm_kernel(const __bf16* __restrict__ A, int64_t lda,
-                                                       const __bf16* __restrict__ B, int64_t ldb, int M, int N,
-                                                       int K, int kchunk, const float* __restrict__ bias,
-                                                       const float* __restrict__ alpha, void* __restrict__ Cv,
-                                                       int64_t ldc, int64_t slab_stride, int accumulate) {
-  constexpr int BM = 64 * WM, BN = 64 * WN;
-  using TA = Tile<AKC, BM>;
-  using TB = Tile<BKC, BN>;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * (TA::kElems + TB::kElems)];
+enum : int { EPI_STORE = 0, EPI_BIAS_ACT = 1, EPI_ACT_GRAD = 2 };
 
+// One GEMM problem of a (possibly grouped) launch.
+struct Prob {
+  const __bf16* A;
+  const __bf16* B;
+  int64_t lda, ldb;
+  int M, N, K;
+  int tm, tn, splits, kchunk;  // tile grid and split-K
+  int wg0;                     // first (remapped) workgroup index of this problem in the launch
+  void* C;
+  int64_t ldc;
+  int out_f32, accumulate;
+  const float* bias;   // [N] f32 (or null)
+  const float* alpha;  // device scalar (or null = 1)
+  int epi, act;        // epilogue kind; activation (0 erf-GELU, 1 tanh-GELU, 2 ReLU)
+  const __bf16* aux;   // EPI_ACT_GRAD: pre-activation [M][ld_aux]
+  __bf16* aux_out;     // EPI_BIAS_ACT: pre-activation output [M][ld_aux]
+  int64_t ld_aux;
+  float* rowsum;       // optional [M] f32: alpha · Σ_k A[m][k] (the bias gradient of a dW product)
+  float* slab;         // split-K: f32 [splits][M][N] (+ [splits][M] row sums)
+  int* counters;       // split-K: one zeroed ticket per tile (left zeroed)
+};
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  if (act == 0) return 0.5f * z * (1.f + erff(z * 0.70710678118654752440f));
+  if (act == 1) {
+    const float k = 0.79788456080286535588f;
+    return 0.5f * z * (1.f + tanhf(k * (z + 0.044715f * z * z * z)));
+  }
+  return z > 0.f ? z : 0.f;
+}
+
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == 0) {
+    const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752440f));
+    const float pdf = 0.39894228040143267794f * expf(-0.5f * z * z);
+    return cdf + z * pdf;
+  }
+  if (act == 1) {
+    const float k = 0.79788456080286535588f;
+    const float u = k * (z + 0.044715f * z * z * z);
+    const float t = tanhf(u);
+    return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * z * z);
+  }
+  return z > 0.f ? 1.f : 0.f;
+}
+
+__device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+constexpr int kMaxTileElems =
+    Tile<false, TILE>::kElems > Tile<true, TILE>::kElems ? Tile<false, TILE>::kElems : Tile<true, TILE>::kElems;
+constexpr int LDS_ELEMS = 4 * kMaxTileElems;  // two buffers x (A + B); also holds the reducer flag
+
+// One 64x64 output tile (4 waves as 2x2 of 32x32) of problem p; `lin` = the tile's index within the problem.
+// The MFMAs compute the tile transposed (A-operand = B fragment, B-operand = A fragment) so that a lane owns one
+// output ROW m and its registers hold columns n = (e&3) + 8(e>>2) + 4h: the epilogue stores 16 B per lane.
+template <bool AKC, bool BKC>
+__device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) {
+  using TA = Tile<AKC, TILE>;
+  using TB = Tile<BKC, TILE>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int tn = gridDim.x, tm = gridDim.y;
-  const int nwg = tn * tm * gridDim.z;
-  const int lin = xcd_remap(blockIdx.x + tn * (blockIdx.y + tm * blockIdx.z), nwg);
-  const int bx = lin % tn, by = (lin / tn) % tm, bz = lin / (tn * tm);
-  const int m0 = by * BM, n0 = bx * BN;
-  const int kb = bz * kchunk, ke = min(K, kb + kchunk);
+  const int bz = lin % p.splits, tile = lin / p.splits;
+  const int bx = tile % p.tn, by = tile / p.tn;
+  const int M = p.M, N = p.N;
+  const int m0 = by * TILE, n0 = bx * TILE;
+  const int kb = bz * p.kchunk, ke = min(p.K, kb + p.kchunk);
   const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+  const __bf16* __restrict__ A = p.A;
+  const __bf16* __restrict__ B = p.B;
+  const bool want_rs = p.rowsum != nullptr && bx == 0 && wn == 0;  // wave-uniform
 
-  f32x16 acc[WM][WN];
+  f32x16 acc, racc;
 #pragma unroll
-  for (int i = 0; i < WM; ++i)
+  for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
+  bf16x8 ones;
 #pragma unroll
-    for (int j = 0; j < WN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
   bf16x8 ra[NS][TA::kChunks], rb[NS][TB::kChunks];
-  // Consumes k-tile `i` from register stage `st`: write to LDS buffer i&1, one barrier, MFMAs.
   auto consume = [&](int st, int i) {
-    __bf16* sA = smem + (i & 1) * (TA::kElems + TB::kElems);
-    __bf16* sB = sA + TA::kElems;
+    __bf16* sA = smem + (i & 1) * 2 * kMaxTileElems;
+    __bf16* sB = sA + kMaxTileElems;
     TA::store(sA, ra[st], m0, M, kb + i * BK, ke);
     TB::store(sB, rb[st], n0, N, kb + i * BK, ke);
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < BK / 16; ++t) {
-      bf16x8 af[WM], bfr[WN];
-#pragma unroll
-      for (int ii = 0; ii < WM; ++ii) af[ii] = TA::frag(sA, wm * 32 * WM + 32 * ii, t);
-#pragma unroll
-      for (int j = 0; j < WN; ++j) bfr[j] = TB::frag(sB, wn * 32 * WN + 32 * j, t);
-#pragma unroll
-      for (int ii = 0; ii < WM; ++ii)
-#pragma unroll
-        for (int j = 0; j < WN; ++j) acc[ii][j] = mfma(bfr[j], af[ii], acc[ii][j]);
+      const bf16x8 af = TA::frag(sA, wm * 32, t);
+      const bf16x8 bfr = TB::frag(sB, wn * 32, t);
+      acc = mfma(bfr, af, acc);
+      if (want_rs) racc = mfma(ones, af, racc);
     }
   };
-  // Loads are unconditional (clamped addresses; tiles past the end are zeroed at the LDS write), so the stage
-  // registers are never merged across branches and the compiler keeps the vmcnt waits counted.
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {
-    TA::load(ra[st], A, lda, m0, M, kb + st * BK, ke);
-    TB::load(rb[st], B, ldb, n0, N, kb + st * BK, ke);
+    TA::load(ra[st], A, p.lda, m0, M, kb + st * BK, ke);
+    TB::load(rb[st], B, p.ldb, n0, N, kb + st * BK, ke);
   }
   int i0 = 0;
   for (; i0 + NS <= nk; i0 += NS) {
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
-      TA::load(ra[(st + NS - 1) % NS], A, lda, m0, M, kb + (i0 + st + NS - 1) * BK, ke);
-      TB::load(rb[(st + NS - 1) % NS], B, ldb, n0, N, kb + (i0 + st + NS - 1) * BK, ke);
+      TA::load(ra[(st + NS - 1) % NS], A, p.lda, m0, M, kb + (i0 + st + NS - 1) * BK, ke);
+      TB::load(rb[(st + NS - 1) % NS], B, p.ldb, n0, N, kb + (i0 + st + NS - 1) * BK, ke);
       consume(st, i0 + st);
     }
   }
-  // tail: fewer than NS k-tiles left, already resident in stages 0 .. nk-i0-1
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st)
     if (i0 + st < nk) consume(st, i0 + st);
 
-  // Epilogue. Lane: row m0 + wm*32*WM + 32i + r; register group g of tile (i, j): columns
-  // n0 + wn*32*WN + 32j + 8g + 4h + {0..3}. N is a multiple of 8 (bf16) / 4 (f32): a group is in or out whole.
-  const float al = alpha ? *alpha : 1.f;
-  char* Cb = reinterpret_cast<char*>(Cv) + (int64_t)bz * slab_stride * (OUT_F32 ? 4 : 2);
-#pragma unroll
-  for (int i = 0; i < WM; ++i) {
-    const int row = m0 + wm * 32 * WM + 32 * i + r;
-    const bool rok = row < M;
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int cb = n0 + wn * 32 * WN + 32 * j;
-      float v[16];
+  const int row = m0 + wm * 32 + r;
+  const bool rok = row < M;
+  const int cb = n0 + wn * 32;
+
+  // ---- split-K: slab, ticket, the last arriver reduces in z order (agent-scope release / acquire) ----
+  if (p.splits > 1) {
+    float* slab = p.slab + (size_t)bz * M * N;
+    if (rok) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = cb + 8 * g + 4 * h;
-        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (bias && c < N) bv = *reinterpret_cast<const float4*>(bias + c);
-        v[4 * g + 0] = acc[i][j][4 * g + 0] * al + bv.x;
-        v[4 * g + 1] = acc[i][j][4 * g + 1] * al + bv.y;
-        v[4 * g + 2] = acc[i][j][4 * g + 2] * al + bv.z;
-        v[4 * g + 3] = acc[i][j][4 * g + 3] * al + bv.w;
+        if (c < N)
+          *reinterpret_cast<float4*>(slab + (int64_t)row * N + c) =
+              make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
       }
-      if (OUT_F32) {
+      if (want_rs && h == 0) p.slab[(size_t)p.splits * M * N + (size_t)bz * M + row] = racc[0];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's slab stores have completed (and the LDS tiles are no longer read)
+    int* flag = reinterpret_cast<int*>(smem);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == p.splits - 1;
+      if (last) {
+        __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
+    for (int z = 0; z < p.splits; ++z) {
+      const float* sz = p.slab + (size_t)z * M * N;
+      if (rok) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int c = cb + 8 * g + 4 * h;
-          if (!rok || c >= N) continue;
-          float4* p = reinterpret_cast<float4*>(reinterpret_cast<float*>(Cb) + (int64_t)row * ldc + c);
-          float4 w = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
-          if (accumulate) {
-            const float4 o = *p;
-            w.x += o.x; w.y += o.y; w.z += o.z; w.w += o.w;
+          if (c < N) {
+            const float4 x = *reinterpret_cast<const float4*>(sz + (int64_t)row * N + c);
+            acc[4 * g] += x.x;
+            acc[4 * g + 1] += x.y;
+            acc[4 * g + 2] += x.z;
+            acc[4 * g + 3] += x.w;
           }
-          *p = w;
         }
-      } else {
-        uint32_t d[4][2];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
-          d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; g += 2) {
-          // lanes 0-31: columns 8g..8g+7 (own group g | upper half's group g);
-          // lanes 32-63: columns 8g+8..8g+15 (lower half's group g+1 | own group g+1)
-#pragma unroll
-          for (int w = 0; w < 2; ++w) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(d[g][w], d[g + 1][w], false, false);
-            d[g][w] = sw[0];
-            d[g + 1][w] = sw[1];
-          }
-          const int c = cb + 8 * g + 8 * h;
-          if (rok && c < N)
-            *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(Cb) + (int64_t)row * ldc + c) =
-                make_uint4(d[g][0], d[g][1], d[g + 1][0], d[g + 1][1]);
-        }
+        if (want_rs) racc[0] += p.slab[(size_t)p.splits * M * N + (size_t)z * M + row];
       }
     }
   }
+
+  // ---- epilogue: lane = row, register group g = columns cb + 8g + 4h + {0..3} ----
+  const float al = p.alpha ? *p.alpha : 1.f;
+  if (want_rs && rok && h == 0) p.rowsum[row] = racc[0] * al;
+  float v[16];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int c = cb + 8 * g + 4 * h;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p.bias && c < N) bv = *reinterpret_cast<const float4*>(p.bias + c);
+    v[4 * g + 0] = acc[4 * g + 0] * al + bv.x;
+    v[4 * g + 1] = acc[4 * g + 1] * al + bv.y;
+    v[4 * g + 2] = acc[4 * g + 2] * al + bv.z;
+    v[4 * g + 3] = acc[4 * g + 3] * al + bv.w;
+  }
+  if (p.out_f32) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = cb + 8 * g + 4 * h;
+      if (!rok || c >= N) continue;
+      float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)row * p.ldc + c);
+      float4 w = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+      if (p.accumulate) {
+        const float4 o = *q;
+        w.x += o.x;
+        w.y += o.y;
+        w.z += o.z;
+        w.w += o.w;
+      }
+      *q = w;
+    }
+    return;
+  }
+  if (p.epi == EPI_ACT_GRAD) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = cb + 8 * g + 4 * h;
+      if (rok && c < N) {
+        const uint2 f = *reinterpret_cast<const uint2*>(p.aux + (int64_t)row * p.ld_aux + c);
+        v[4 * g + 0] *= act_grad(bf16_lo(f.x), p.act);
+        v[4 * g + 1] *= act_grad(bf16_hi(f.x), p.act);
+        v[4 * g + 2] *= act_grad(bf16_lo(f.y), p.act);
+        v[4 * g + 3] *= act_grad(bf16_hi(f.y), p.act);
+      }
+    }
+  }
+  uint32_t d[4][2];
+  if (p.epi == EPI_BIAS_ACT) {
+    // store the pre-activation (bf16: the value the activation and its gradient see), then activate it
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
+      d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
+      v[4 * g + 0] = act_fwd(bf16_lo(d[g][0]), p.act);
+      v[4 * g + 1] = act_fwd(bf16_hi(d[g][0]), p.act);
+      v[4 * g + 2] = act_fwd(bf16_lo(d[g][1]), p.act);
+      v[4 * g + 3] = act_fwd(bf16_hi(d[g][1]), p.act);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      const auto s0 = __builtin_amdgcn_permlane32_swap(d[g][0], d[g + 1][0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(d[g][1], d[g + 1][1], false, false);
+      const int c = cb + 8 * g + 8 * h;
+      if (rok && c < N)
+        *reinterpret_cast<uint4*>(p.aux_out + (int64_t)row * p.ld_aux + c) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
+    d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
+  }
+#pragma unroll
+  for (int g = 0; g < 4; g += 2) {
+    // lanes 0-31: columns 8g..8g+7 (own group g | upper half's group g);
+    // lanes 32-63: columns 8g+8..8g+15 (lower half's group g+1 | own group g+1)
+    const auto s0 = __builtin_amdgcn_permlane32_swap(d[g][0], d[g + 1][0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(d[g][1], d[g + 1][1], false, false);
+    const int c = cb + 8 * g + 8 * h;
+    if (rok && c < N)
+      *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(p.C) + (int64_t)row * p.ldc + c) =
+          make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  }
 }
 
-// out[m, n] (=, or += when accumulate) sum_z slab[z, m, n] + bias[n]; fixed summation order; 4 columns per thread.
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slab, int splits, int M, int N,
-                                                            const float* __restrict__ bias, void* __restrict__ C,
-                                                            int64_t ldc, int out_bf16, int accumulate) {
-  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i4 >= (int64_t)M * N) return;
-  const int64_t row = i4 / N, col = i4 % N;
-  float4 s = bias ? *reinterpret_cast<const float4*>(bias + col) : make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int z = 0; z < splits; ++z) {
-    const float4 x = *reinterpret_cast<const float4*>(slab + (int64_t)z * M * N + i4);
-    s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
-  }
-  if (out_bf16) {
-    *reinterpret_cast<uint2*>(reinterpret_cast<__bf16*>(C) + row * ldc + col) =
-        make_uint2(pack_bf16x2(s.x, s.y), pack_bf16x2(s.z, s.w));
-  } else {
-    float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + row * ldc + col);
-    if (accumulate) {
-      const float4 o = *c;
-      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
-    }
-    *c = s;
-  }
+template <bool AKC, bool BKC>
+__global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[LDS_ELEMS];
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  gemm_tile<AKC, BKC>(p, lin, smem);
+}
+
+// A projection's backward in one launch: problem 0 = dX (A = dY K-contig, B = W N-contig), problem 1 = dW (A = dYᵀ
+// M-contig, B = X N-contig, + the bias gradient). Workgroups [0, p1.wg0) belong to problem 0.
+__global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[LDS_ELEMS];
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  if (lin < p1.wg0)
+    gemm_tile<true, false>(p0, lin, smem);
+  else
+    gemm_tile<false, false>(p1, lin - p1.wg0, smem);
 }
 
 struct Plan {
-  int wm, wn, splits, kchunk;
+  int splits, kchunk;
 };
 
-Plan plan(int64_t M, int64_t N, int64_t K) {
-  constexpr int64_t kTarget = 240;  // workgroups wanted (256 CUs, one resident tile each is already MFMA-bound)
-  Plan p{2, 2, 1, (int)(cdiv(K, BK) * BK)};
-  if (K == 0) return p;
-  if (const char* e = getenv("ESGPT_GEMM_PLAN")) {  // tuning hook: "wm,wn,splits"
-    int wm = 2, wn = 2, sp = 1;
-    if (sscanf(e, "%d,%d,%d", &wm, &wn, &sp) == 3 && wm >= 1 && wm <= 2 && wn >= 1 && wn <= 2 && sp >= 1) {
-      p.wm = wm;
-      p.wn = wn;
-      const int64_t kchunk = cdiv(cdiv(K, sp), BK) * BK;
-      p.splits = (int)cdiv(K, kchunk);
-      p.kchunk = (int)kchunk;
-      return p;
-    }
+// Split-K: enough workgroups for `target` (<= 0: never split), and no workgroup walks more than kMaxChunk of K
+// (a long K is one long serial chain: 8192 tokens = 128 k-tiles), never below 256 of K per split.
+constexpr int64_t kMaxChunk = 1024;
+constexpr int64_t kTarget = 480;  // about two resident 64x64 tiles per CU
+
+Plan plan(int64_t M, int64_t N, int64_t K, int64_t target) {
+  Plan p{1, (int)(cdiv(K, BK) * BK)};
+  if (K == 0 || target <= 0) return p;
+  int64_t splits = 1;
+  if (const char* e = getenv("ESGPT_GEMM_SPLITS")) {  // tuning hook
+    splits = std::max<int64_t>(1, atoi(e));
+  } else {
+    const int64_t tiles = cdiv(M, TILE) * cdiv(N, TILE);
+    if (tiles < target) splits = cdiv(target, tiles);
+    splits = std::max<int64_t>(splits, K / kMaxChunk);
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, K / 256));
   }
-  // Measured on MI355X at the C2 step's shapes (tools/gemm_sweep.py): 64x64 tiles beat 128x64 / 128x128 for the
-  // short-K (256, 1024) projections — more resident workgroups per CU hide the load/store latency that dominates
-  // at these sizes. Long-K (dW, K = tokens) products with few tiles split K to about two workgroups per CU.
-  p.wm = p.wn = 1;
-  const int64_t tiles = cdiv(M, 64) * cdiv(N, 64);
-  if (tiles >= kTarget) return p;
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(2 * kTarget / tiles, K / 512));
   const int64_t kchunk = cdiv(cdiv(K, splits), BK) * BK;
   p.splits = (int)cdiv(K, kchunk);
   p.kchunk = (int)kchunk;
   return p;
 }
 
-template <bool AKC, bool BKC, bool F32>
-void launch(const Plan& p, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M, int N, int K,
-            const float* bias, const float* alpha, void* C, int64_t ldc, int64_t slab_stride, int accumulate,
-            hipStream_t st) {
-  const int BM = 64 * p.wm, BN = 64 * p.wn;
-  dim3 grid((unsigned)cdiv(N, BN), (unsigned)cdiv(M, BM), (unsigned)p.splits);
-  if (p.wm == 2 && p.wn == 2)
-    gemm_kernel<AKC, BKC, 2, 2, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, alpha, C,
-                                                                ldc, slab_stride, accumulate);
-  else if (p.wm == 2)
-    gemm_kernel<AKC, BKC, 2, 1, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, alpha, C,
-                                                                ldc, slab_stride, accumulate);
-  else
-    gemm_kernel<AKC, BKC, 1, 1, F32><<<grid, THREADS, 0, st>>>(A, lda, B, ldb, M, N, K, p.kchunk, bias, alpha, C,
-                                                                ldc, slab_stride, accumulate);
+Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K, void* C,
+               int64_t ldc, int out_f32, int accumulate, const float* bias, const float* alpha, int64_t target) {
+  Prob p{};
+  p.A = reinterpret_cast<const __bf16*>(A);
+  p.B = reinterpret_cast<const __bf16*>(B);
+  p.lda = lda;
+  p.ldb = ldb;
+  p.M = (int)M;
+  p.N = (int)N;
+  p.K = (int)K;
+  p.tm = (int)cdiv(M, TILE);
+  p.tn = (int)cdiv(N, TILE);
+  const Plan pl = plan(M, N, K, target);
+  p.splits = pl.splits;
+  p.kchunk = pl.kchunk;
+  p.C = C;
+  p.ldc = ldc;
+  p.out_f32 = out_f32;
+  p.accumulate = accumulate;
+  p.bias = bias;
+  p.alpha = alpha;
+  return p;
 }
 
-template <bool F32>
-void launch_any(bool akc, bool bkc, const Plan& p, const __bf16* A, int64_t lda, const __bf16* B, int64_t ldb, int M,
-                int N, int K, const float* bias, const float* alpha, void* C, int64_t ldc, int64_t slab_stride,
-                int accumulate, hipStream_t st) {
-  if (akc && bkc) launch<true, true, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
-  else if (akc) launch<true, false, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
-  else if (bkc) launch<false, true, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
-  else launch<false, false, F32>(p, A, lda, B, ldb, M, N, K, bias, alpha, C, ldc, slab_stride, accumulate, st);
+size_t slab_bytes(int64_t splits, int64_t M, int64_t N) {
+  return splits > 1 ? sizeof(float) * ((size_t)splits * M * N + (size_t)splits * M) : 0;
+}
+
+int n_wg(const Prob& p) { return p.tm * p.tn * p.splits; }
+
+// Shared argument checks of a bf16 product with a 16-B epilogue (K > 0: an empty reduction is the caller's case).
+bool shapes_ok(bool akc, bool bkc, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N,
+               int64_t K, const void* C, int64_t ldc, bool f32) {
+  if (!(A && B && C && M >= 0 && N >= 0 && K > 0)) return false;
+  if (!(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31))) return false;
+  if (!(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0)) return false;
+  if (!((akc || M % 8 == 0) && (bkc || N % 8 == 0))) return false;
+  if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16)) return false;
+  const int cgrp = f32 ? 4 : 8;
+  return N % cgrp == 0 && ldc % cgrp == 0;
+}
+
+// Tile count of the dX product (what the grouped launch already puts on the chip): the dW split targets the rest.
+int64_t dw_target(bool has_dx, int64_t T, int64_t in) {
+  return has_dx ? std::max<int64_t>(64, kTarget - cdiv(T, TILE) * cdiv(in, TILE)) : kTarget;
 }
 
 }  // namespace
@@ -365,43 +490,99 @@ void launch_any(bool akc, bool bkc, const Plan& p, const __bf16* A, int64_t lda,
 extern "C" {
 
 size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K) {
-  const Plan p = plan(M, N, K);
-  return p.splits > 1 ? sizeof(float) * (size_t)p.splits * M * N : 0;
+  return slab_bytes(plan(M, N, K, kTarget).splits, M, N);
 }
+
+int64_t esgpt_gemm_counters(int64_t M, int64_t N) { return cdiv(M, TILE) * cdiv(N, TILE); }
 
 int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, const void* B, int64_t ldb, int64_t M,
                     int64_t N, int64_t K, const float* bias, const float* alpha, void* C, int64_t ldc, int c_dtype,
-                    int accumulate, void* workspace, size_t workspace_bytes, void* stream) {
-  ESGPT_REQUIRE(A && B && C && M >= 0 && N >= 0 && K >= 0);
-  ESGPT_REQUIRE(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31));
+                    int accumulate, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream) {
   ESGPT_REQUIRE(c_dtype == ESGPT_F32 || (c_dtype == ESGPT_BF16 && !accumulate));
   const bool akc = a_layout == ESGPT_GEMM_K_CONTIG, bkc = b_layout == ESGPT_GEMM_K_CONTIG;
   ESGPT_REQUIRE(akc || a_layout == ESGPT_GEMM_MN_CONTIG);
   ESGPT_REQUIRE(bkc || b_layout == ESGPT_GEMM_MN_CONTIG);
-  // 16-B vector loads: the contiguous extent and every row start must be 8-element aligned.
-  ESGPT_REQUIRE(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0);
-  ESGPT_REQUIRE((akc || M % 8 == 0) && (bkc || N % 8 == 0));
-  ESGPT_REQUIRE(((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
-  // 16-B epilogue stores: whole 8-column (bf16) / 4-column (f32) groups, 16-B aligned rows.
-  const int cgrp = c_dtype == ESGPT_F32 ? 4 : 8;
-  ESGPT_REQUIRE(N % cgrp == 0 && ldc % cgrp == 0 && ((uintptr_t)C % 16) == 0);
+  const bool f32 = c_dtype == ESGPT_F32;
+  ESGPT_REQUIRE(shapes_ok(akc, bkc, A, lda, B, ldb, M, N, K, C, ldc, f32));
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   if (M == 0 || N == 0) return ESGPT_OK;
-  hipStream_t st = as_stream(stream);
-  const Plan p = plan(M, N, K);  // K == 0: one split, the k-loop is empty and C = bias (or C += bias)
-  const __bf16* a = reinterpret_cast<const __bf16*>(A);
-  const __bf16* b = reinterpret_cast<const __bf16*>(B);
-  const bool f32 = c_dtype == ESGPT_F32;
+  Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget);
   if (p.splits > 1) {
-    ESGPT_REQUIRE(workspace && workspace_bytes >= sizeof(float) * (size_t)p.splits * M * N);
-    float* slab = reinterpret_cast<float*>(workspace);
-    launch_any<true>(akc, bkc, p, a, lda, b, ldb, M, N, K, nullptr, alpha, slab, N, M * N, 0, st);
-    splitk_reduce_kernel<<<(unsigned)cdiv(M * N / 4, 256), 256, 0, st>>>(slab, p.splits, (int)M, (int)N, bias, C, ldc,
-                                                                      f32 ? 0 : 1, accumulate);
-  } else if (f32) {
-    launch_any<true>(akc, bkc, p, a, lda, b, ldb, M, N, K, bias, alpha, C, ldc, 0, accumulate, st);
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N) && counters);
+    p.slab = reinterpret_cast<float*>(workspace);
+    p.counters = counters;
+  }
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)n_wg(p));
+  if (akc && bkc) gemm_kernel<true, true><<<grid, THREADS, 0, st>>>(p);
+  else if (akc) gemm_kernel<true, false><<<grid, THREADS, 0, st>>>(p);
+  else if (bkc) gemm_kernel<false, true><<<grid, THREADS, 0, st>>>(p);
+  else gemm_kernel<false, false><<<grid, THREADS, 0, st>>>(p);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64_t in, int64_t out,
+                     const float* bias, int act, void* pre, void* y, int64_t ldy, void* stream) {
+  ESGPT_REQUIRE(shapes_ok(true, true, x, ldx, w, in, T, out, in, y, ldy, false));
+  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2));
+  ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
+  ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
+  if (T == 0 || out == 0) return ESGPT_OK;
+  Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 0, 0, bias, nullptr, 0);  // never split
+  if (act >= 0) {
+    p.epi = EPI_BIAS_ACT;
+    p.act = act;
+    p.aux_out = reinterpret_cast<__bf16*>(pre);
+    p.ld_aux = ldy;
+  }
+  gemm_kernel<true, true><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx) {
+  return slab_bytes(plan(out, in, T, dw_target(has_dx != 0, T, in)).splits, out, in);
+}
+
+int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
+                     int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
+                     int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
+                     void* stream) {
+  ESGPT_REQUIRE(dy && x && w && dw && T >= 0 && in >= 0 && out >= 0);
+  hipStream_t st = as_stream(stream);
+  if (in == 0 || out == 0) return ESGPT_OK;
+  if (T == 0) {  // empty batch: zero weight / bias gradients, nothing else
+    if (zero_async(dw, sizeof(float) * out * in, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    if (db && zero_async(db, sizeof(float) * out, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    return ESGPT_OK;
+  }
+  ESGPT_REQUIRE(shapes_ok(false, false, dy, lddy, x, ldx, out, in, T, dw, in, true));
+  const bool has_dx = dx != nullptr;
+  if (has_dx) ESGPT_REQUIRE(shapes_ok(true, false, dy, lddy, w, in, T, in, out, dx, lddx, false));
+  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
+  Prob p0{};
+  if (has_dx) {
+    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0);
+    if (act >= 0) {
+      p0.epi = EPI_ACT_GRAD;
+      p0.act = act;
+      p0.aux = reinterpret_cast<const __bf16*>(pre);
+      p0.ld_aux = ldpre;
+    }
+  }
+  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in));
+  p1.rowsum = db;
+  if (p1.splits > 1) {
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in) && counters);
+    p1.slab = reinterpret_cast<float*>(workspace);
+    p1.counters = counters;
+  }
+  if (has_dx) {
+    p1.wg0 = n_wg(p0);
+    gemm_bwd_pair_kernel<<<dim3((unsigned)(n_wg(p0) + n_wg(p1))), THREADS, 0, st>>>(p0, p1);
   } else {
-    launch_any<false>(akc, bkc, p, a, lda, b, ldb, M, N, K, bias, alpha, C, ldc, 0, 0, st);
+    gemm_kernel<false, false><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
   }
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;

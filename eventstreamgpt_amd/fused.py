@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from . import _lib as L
 import ctypes
 
-from .kernels import AttentionFn, _timed, err_word, next_dropout_seed
+from .kernels import AttentionFn, _timed, err_word, next_dropout_seed, tickets
 
 _ACTS = {"gelu": 0, "gelu_new": 1, "gelu_pytorch_tanh": 1, "gelu_fast": 1, "relu": 2}
 
@@ -125,17 +125,21 @@ def fused_supported(encoder) -> bool:
 
 
 # ----------------------------------------------------------------------------------------------------------------
-# Projection GEMMs (csrc/gemm.hip): y = x·Wᵀ (+ b), dx = dy·W, dW = dyᵀ·x written straight to f32
+# Projection GEMMs (csrc/gemm.hip): y = x·Wᵀ (+ b) [+ act], and one grouped launch per projection backward
+# (dx = dy·W [· act'], dW = dyᵀ·x and db = Σ dy written straight to f32)
 # ----------------------------------------------------------------------------------------------------------------
 def _gemm(a, a_layout: int, lda: int, b, b_layout: int, ldb: int, M: int, N: int, K: int, out, bias=None,
           accumulate: bool = False, alpha=None):
     lib = L.load()
     nbytes = lib.esgpt_gemm_workspace(M, N, K)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=a.device) if nbytes else None
+    cnt = tickets(a.device)
+    if nbytes and lib.esgpt_gemm_counters(M, N) > cnt.numel():
+        raise RuntimeError("eventstreamgpt_amd: GEMM tile grid exceeds the ticket array")
     with _timed("gemm"):
         st = lib.esgpt_gemm_bf16(a_layout, a.data_ptr(), lda, b_layout, b.data_ptr(), ldb, M, N, K, L.ptr(bias),
-                                 L.ptr(alpha), out.data_ptr(), out.stride(0), L.dtype_code(out.dtype), int(accumulate), L.ptr(ws),
-                                 nbytes, L.stream())
+                                 L.ptr(alpha), out.data_ptr(), out.stride(0), L.dtype_code(out.dtype),
+                                 int(accumulate), L.ptr(ws), nbytes, cnt.data_ptr(), L.stream())
     L.check(st, "gemm")
     return out
 
@@ -167,6 +171,45 @@ def linear_dw(dy, x):
     return _gemm(dy, L.GEMM_MN_CONTIG, dout, x, L.GEMM_MN_CONTIG, din, dout, din, N, dw)
 
 
+def linear_fwd_act(x, w, bias, act: int):
+    """(pre, y): pre = x · wᵀ + bias (bf16) and y = act(pre) — c_fc with its bias and activation in the GEMM
+    epilogue (the pre-activation is kept for the backward)."""
+    lib = L.load()
+    T, din = x.shape
+    dout = w.shape[0]
+    pre = torch.empty(T, dout, dtype=x.dtype, device=x.device)
+    y = torch.empty_like(pre)
+    with _timed("gemm"):
+        st = lib.esgpt_linear_fwd(x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout, L.ptr(bias), int(act),
+                                  pre.data_ptr(), y.data_ptr(), y.stride(0), L.stream())
+    L.check(st, "linear_fwd")
+    return pre, y
+
+
+def linear_bwd(dy, x, w, alpha=None, act: int = -1, pre=None, need_dx: bool = True, need_db: bool = False):
+    """One launch for the backward of y = x · wᵀ: dx = alpha·dy·w [· act'(pre)] (bf16), dw = alpha·dyᵀ·x (f32) and
+    db = alpha·Σ_rows dy (f32). ``alpha``: optional device scalar. Returns (dx | None, dw, db | None)."""
+    lib = L.load()
+    T, dout = dy.shape
+    din = x.shape[1]
+    dev = dy.device
+    dw = torch.empty(dout, din, dtype=torch.float32, device=dev)
+    dx = torch.empty(T, din, dtype=dy.dtype, device=dev) if need_dx else None
+    db = torch.empty(dout, dtype=torch.float32, device=dev) if need_db else None
+    nbytes = lib.esgpt_linear_bwd_workspace(T, din, dout, int(need_dx))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev) if nbytes else None
+    cnt = tickets(dev)
+    if nbytes and lib.esgpt_gemm_counters(dout, din) > cnt.numel():
+        raise RuntimeError("eventstreamgpt_amd: GEMM tile grid exceeds the ticket array")
+    with _timed("gemm"):
+        st = lib.esgpt_linear_bwd(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
+                                  L.ptr(alpha), int(act), L.ptr(pre), 0 if pre is None else pre.stride(0), L.ptr(dx),
+                                  0 if dx is None else dx.stride(0), dw.data_ptr(), L.ptr(db), L.ptr(ws), nbytes,
+                                  cnt.data_ptr(), L.stream())
+    L.check(st, "linear_bwd")
+    return dx, dw, db
+
+
 def column_sum(x):
     lib = L.load()
     N, Fo = x.shape
@@ -181,8 +224,8 @@ def column_sum(x):
 
 class ProjFn(torch.autograd.Function):
     """y = x · w_lpᵀ (+ bias) where ``w_lp`` is a no-grad bf16 shadow of the row-concatenation of ``params`` (f32).
-    Backward: dx = dy · w_lp, and dW = dyᵀ · x computed directly in f32 and handed to each parameter as a row
-    slice; dbias by the column-sum kernel. No bf16 gradient round trip, no cast/accumulate kernels."""
+    Backward: one grouped launch for dx = dy · w_lp, dW = dyᵀ · x (directly in f32, handed to each parameter as a
+    row slice) and dbias (a row sum inside the dW product). No bf16 gradient round trip, no cast kernels."""
 
     @staticmethod
     def forward(ctx, x, w_lp, bias, *params):
@@ -196,11 +239,9 @@ class ProjFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
-        dy = dy.contiguous()
-        dx = linear_dx(dy, w) if ctx.needs_input_grad[0] else None
-        dw = linear_dw(dy, x)
+        need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        dx, dw, db = linear_bwd(dy.contiguous(), x, w, need_dx=ctx.needs_input_grad[0], need_db=need_db)
         grads = list(torch.split(dw, ctx.rows, 0))
-        db = column_sum(dy) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
         return (dx, None, db, *grads)
 
 
@@ -212,6 +253,40 @@ def proj(x, w_lp, bias, params):
     w = params[0] if len(params) == 1 else torch.cat(list(params), 0)
     dt = x.dtype
     return F.linear(x, w.to(dt), None if bias is None else bias.to(dt))
+
+
+class MLPFn(torch.autograd.Function):
+    """InnerMLP (transformer.py:378-391) up to c_proj's bias: y = act(x · W_fcᵀ + b_fc) · W_projᵀ in two GEMM
+    launches (c_fc's bias + activation in its epilogue; the bf16 pre-activation is kept) and two grouped backward
+    launches (c_proj: d(pre) = (dy · W_proj) · act'(pre) in the dX epilogue, + dW_proj; c_fc: dx + dW_fc + db_fc as a
+    row sum inside its dW product). c_proj's bias and the residual dropout belong to the following ResidualLNFn.
+    ``w_fc`` / ``w_pj`` are the bf16 shadows; the f32 parameters ``p_fc`` / ``p_pj`` receive the gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w_fc, w_pj, b_fc, act: int, p_fc, p_pj):
+        x = x.contiguous()
+        pre, g = linear_fwd_act(x, w_fc, b_fc, act)
+        y = linear_fwd(g, w_pj)
+        ctx.save_for_backward(x, w_fc, w_pj, pre, g)
+        ctx.act = act
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w_fc, w_pj, pre, g = ctx.saved_tensors
+        dz, dw_pj, _ = linear_bwd(dy.contiguous(), g, w_pj, act=ctx.act, pre=pre)
+        dx, dw_fc, db_fc = linear_bwd(dz, x, w_fc, need_dx=ctx.needs_input_grad[0], need_db=True)
+        return dx, None, None, db_fc, None, dw_fc, dw_pj
+
+
+def mlp(x, w_fc, w_pj, fc, pj, act: int):
+    """InnerMLP without c_proj's bias: ``MLPFn`` when the bf16 GEMM shapes allow it, else proj + BiasActFn + proj."""
+    if (w_fc is not None and w_fc.dtype == torch.bfloat16
+            and gemm_supported(x.shape[0], x.shape[1], w_fc.shape[0])):
+        return MLPFn.apply(x.to(torch.bfloat16), w_fc, w_pj, fc.bias, act, fc.weight, pj.weight)
+    f = proj(x, w_fc, None, (fc.weight,))
+    g = BiasActFn.apply(f, fc.bias, act)
+    return proj(g, w_pj, None, (pj.weight,))
 
 
 @torch.no_grad()
@@ -321,28 +396,15 @@ class HeadLossFn(torch.autograd.Function):
         rows_c, rows_t = ctx.rows
         g = g.contiguous()
         alpha = g[-1:]  # d(total): read by the GEMMs from device memory
-        dxc = _gemm(dzc, L.GEMM_K_CONTIG, dzc.shape[1], wc, L.GEMM_MN_CONTIG, wc.shape[1], dzc.shape[0],
-                    wc.shape[1], dzc.shape[1], torch.empty(dzc.shape[0], wc.shape[1], dtype=dzc.dtype,
-                                                           device=dzc.device), alpha=alpha)
-        dwc = _gemm(dzc, L.GEMM_MN_CONTIG, dzc.shape[1], xc, L.GEMM_MN_CONTIG, xc.shape[1], dzc.shape[1],
-                    xc.shape[1], dzc.shape[0], torch.empty(dzc.shape[1], xc.shape[1], dtype=torch.float32,
-                                                           device=dzc.device), alpha=alpha)
-        dbc = column_sum(dzc)
+        dxc, dwc, dbc = linear_bwd(dzc, xc, wc, alpha=alpha, need_db=True)
         if dbias is not None:
-            dbc = dbc + dbias.sum(0)
-        dbc = dbc * alpha
+            dbc = dbc + dbias.sum(0) * alpha
         n_real_c = sum(rows_c)
         gw_c = list(torch.split(dwc[:n_real_c], rows_c, 0))
         gb_c = list(torch.split(dbc[:n_real_c], rows_c, 0))
         dxt, gw_t, gb_t = None, [], []
         if n_tw:
-            dxt = _gemm(dzt, L.GEMM_K_CONTIG, dzt.shape[1], wt, L.GEMM_MN_CONTIG, wt.shape[1], dzt.shape[0],
-                        wt.shape[1], dzt.shape[1], torch.empty(dzt.shape[0], wt.shape[1], dtype=dzt.dtype,
-                                                               device=dzt.device), alpha=alpha)
-            dwt = _gemm(dzt, L.GEMM_MN_CONTIG, dzt.shape[1], xt, L.GEMM_MN_CONTIG, xt.shape[1], dzt.shape[1],
-                        xt.shape[1], dzt.shape[0], torch.empty(dzt.shape[1], xt.shape[1], dtype=torch.float32,
-                                                               device=dzt.device), alpha=alpha)
-            dbt = column_sum(dzt) * alpha
+            dxt, dwt, dbt = linear_bwd(dzt, xt, wt, alpha=alpha, need_db=True)
             n_real_t = sum(rows_t)
             gw_t = list(torch.split(dwt[:n_real_t], rows_t, 0))
             gb_t = list(torch.split(dbt[:n_real_t], rows_t, 0))
@@ -395,9 +457,7 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
             y = proj(o.view(N, D), wo, None, (att.out_proj.weight,))
             h1, ln2 = ResidualLNFn.apply(h, y, att.out_proj.bias, blk.layer_norm.weight, blk.layer_norm.bias, None,
                                          p_res, eps, dt)
-            f = proj(ln2, wfc, None, (blk.mlp.c_fc.weight,))
-            g = BiasActFn.apply(f, blk.mlp.c_fc.bias, act)
-            y2 = proj(g, wpj, None, (blk.mlp.c_proj.weight,))
+            y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, act)
             nxt = blocks[i + 1].attn.layer_norm if i + 1 < len(blocks) else encoder.ln_f
             h, ln = ResidualLNFn.apply(h1, y2, blk.mlp.c_proj.bias, nxt.weight, nxt.bias, rows, p_res, eps, dt)
     return ln.view(B, Lq, D)

@@ -105,6 +105,22 @@ def err_word(device: torch.device) -> torch.Tensor:
     return w
 
 
+_TICKETS: dict[int, torch.Tensor] = {}
+TICKETS_LEN = 1 << 16
+
+
+def tickets(device: torch.device) -> torch.Tensor:
+    """Per-device int32 counters of the kernels' in-launch last-arriver reductions (split-K GEMM tiles, column
+    sums). Zeroed once here; every launch leaves the counters it used at zero. The launches that use them are
+    stream-ordered (one stream per device in the training step)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    t = _TICKETS.get(idx)
+    if t is None:
+        t = torch.zeros(TICKETS_LEN, dtype=torch.int32, device=torch.device("cuda", idx))
+        _TICKETS[idx] = t
+    return t
+
+
 def check_errors(device: torch.device | None = None, n_total_embeddings: int | None = None):
     """Reads (one host sync) and clears the device error word; raises the reference's exception for it."""
     device = device or torch.device("cuda", torch.cuda.current_device())

@@ -204,16 +204,36 @@ int esgpt_column_sum(const void* x, int dtype, int64_t N, int64_t F, float* part
  *   B: ESGPT_GEMM_K_CONTIG  B[k][n] = b[n*ldb + k]     ESGPT_GEMM_MN_CONTIG  B[k][n] = b[k*ldb + n]
  * so y = x·Wᵀ is (K, K), dx = dy·W is (K, MN) and dW = dyᵀ·x is (MN, MN). c_dtype ESGPT_BF16 or ESGPT_F32;
  * accumulate (f32 only): C += alpha·A·B (+ bias). alpha: optional DEVICE pointer to one f32 (NULL = 1), read at
- * run time (e.g. the incoming gradient of a loss, without a host sync or a separate scaling kernel). Requires K,
- * lda, ldb multiples of 8, the MN-contig extents multiples of 8, 16-B aligned A, B, C (and bias), and N, ldc
- * multiples of 8 (bf16 C) / 4 (f32 C). Workspace: f32 split-K slabs, esgpt_gemm_workspace(M, N, K) bytes (0 = none). The
- * split-K reduction runs in a fixed order: results are deterministic. */
+ * run time (e.g. the incoming gradient of a loss, without a host sync or a separate scaling kernel). Requires K > 0,
+ * K, lda, ldb multiples of 8, the MN-contig extents multiples of 8, 16-B aligned A, B, C (and bias), and N, ldc
+ * multiples of 8 (bf16 C) / 4 (f32 C). Split-K: f32 slabs in `workspace` (esgpt_gemm_workspace(M, N, K) bytes, 0 =
+ * none needed) and one int32 ticket per output tile in `counters` (esgpt_gemm_counters(M, N) entries, zeroed once
+ * by the caller; every launch leaves them zeroed; launches sharing a counter array must be stream-ordered). The
+ * last workgroup of each tile sums the slabs in a fixed order inside the same launch: results are deterministic. */
 #define ESGPT_GEMM_K_CONTIG 0
 #define ESGPT_GEMM_MN_CONTIG 1
 size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K);
+int64_t esgpt_gemm_counters(int64_t M, int64_t N);
 int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, const void* B, int64_t ldb, int64_t M,
                     int64_t N, int64_t K, const float* bias, const float* alpha, void* C, int64_t ldc, int c_dtype,
-                    int accumulate, void* workspace, size_t workspace_bytes, void* stream);
+                    int accumulate, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream);
+/* Linear layer y = x·wᵀ (nn.Linear: w [out, in] bf16 row-major, x [T, in] bf16 with row stride ldx) in the layouts
+ * above:
+ *   esgpt_linear_fwd: y = x·wᵀ + bias (f32 [out], optional). With act >= 0 (0 exact-erf GELU, 1 tanh GELU, 2 ReLU)
+ *     the bf16 pre-activation goes to `pre` and y = act(pre): InnerMLP's c_fc + activation (transformer.py:
+ *     378-391) in one launch. y and pre: [T, out], row stride ldy.
+ *   esgpt_linear_bwd: ONE launch for dx = alpha·dy·w (bf16 [T, in]; times act'(pre) when act >= 0, i.e. the
+ *     gradient w.r.t. the pre-activation of an input x = act(pre)), dw = alpha·dyᵀ·x (f32 [out, in]) and
+ *     db = alpha·Σ_rows dy (f32 [out], optional). dx = NULL skips the input gradient. Split-K workspace:
+ *     esgpt_linear_bwd_workspace(T, in, out, dx != NULL) bytes; counters as for esgpt_gemm_bf16 with
+ *     esgpt_gemm_counters(out, in) entries. T == 0 zero-fills dw and db. */
+int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64_t in, int64_t out,
+                     const float* bias, int act, void* pre, void* y, int64_t ldy, void* stream);
+size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx);
+int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
+                     int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
+                     int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
+                     void* stream);
 
 /* ---- Optimizer ------------------------------------------------------------------------------------------
  * Fused AdamW step (torch.optim.AdamW semantics: decoupled weight decay, bias-corrected moments;

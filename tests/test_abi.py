@@ -48,6 +48,10 @@ def test_workspace_queries_without_gpu():
     b.B, b.L, b.M, b.S = 32, 256, 16, 2
     assert lib.esgpt_embed_bag_bwd_workspace(ctypes.byref(b), 1, 1210, 256) > 32 * 256 * 16 * 16
     assert lib.esgpt_output_loss_workspace(32, 256, 5) > 0
+    # GEMM split-K plans: forward products never split; weight gradients split the token dimension
+    assert lib.esgpt_gemm_counters(8192, 1624) == 128 * 26
+    assert lib.esgpt_linear_bwd_workspace(8192, 256, 256, 1) == 4 * (8 * 256 * 256 + 8 * 256)
+    assert lib.esgpt_linear_bwd_workspace(64, 256, 256, 1) == 0
 
 
 def test_product_path_fails_loudly_without_gpu():

@@ -390,6 +390,93 @@ def test_gemm_kernel(M, N, K, a_kc, b_kc):
     assert ((acc.double().cpu() - want).abs().max() / want.abs().max()).item() < 1e-5
 
 
+def _act_ref(z, act):
+    F = torch.nn.functional
+    return {0: F.gelu(z), 1: F.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
+
+
+@pytest.mark.parametrize("T,din,dout", [(8192, 256, 1024), (520, 136, 72), (8, 8, 8)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_linear_fwd_act(T, din, dout, act):
+    """c_fc epilogue: pre = x·wᵀ + b (bf16) and y = act(pre) vs f64 references."""
+    from eventstreamgpt_amd.fused import linear_fwd_act
+
+    g = torch.Generator().manual_seed(T + din + act)
+    x = torch.randn(T, din, generator=g).bfloat16()
+    w = (0.1 * torch.randn(dout, din, generator=g)).bfloat16()
+    b = torch.randn(dout, generator=g)
+    pre, y = linear_fwd_act(x.to(DEV), w.to(DEV), b.to(DEV), act)
+    pre_ref = x.double() @ w.double().t() + b.double()
+    assert rel_err(pre.cpu(), pre_ref) < 1e-2
+    # the activation of the stored (bf16) pre-activation
+    assert rel_err(y.cpu(), _act_ref(pre.double().cpu(), act)) < 1e-2
+
+
+@pytest.mark.parametrize("T,din,dout", [(8192, 256, 256), (8192, 1024, 256), (8192, 256, 1624), (520, 136, 72),
+                                        (8, 8, 8), (0, 64, 32)])
+@pytest.mark.parametrize("act", [-1, 0, 2])
+@pytest.mark.parametrize("need_dx", [True, False])
+def test_linear_bwd(T, din, dout, act, need_dx):
+    """Grouped projection backward (dx [· act'], f32 dW with in-launch split-K tickets, row-sum bias gradient,
+    device alpha) vs f64 references; the ticket counters are left zeroed."""
+    from eventstreamgpt_amd.fused import linear_bwd, tickets
+
+    if act >= 0 and not need_dx:
+        pytest.skip("the activation gradient belongs to dx")
+    g = torch.Generator().manual_seed(T * 3 + din + dout + act)
+    dy = torch.randn(T, dout, generator=g).bfloat16()
+    x = torch.randn(T, din, generator=g).bfloat16()
+    w = torch.randn(dout, din, generator=g).bfloat16()
+    pre = torch.randn(T, din, generator=g).bfloat16() if act >= 0 else None
+    alpha = torch.tensor([0.75])
+    dx, dw, db = linear_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), alpha=alpha.to(DEV), act=act,
+                            pre=None if pre is None else pre.to(DEV), need_dx=need_dx, need_db=True)
+    dwr = 0.75 * (dy.double().t() @ x.double())
+    dbr = 0.75 * dy.double().sum(0)
+    if T == 0:
+        assert not dw.cpu().any() and not db.cpu().any()
+    else:
+        assert rel_err(dw.cpu(), dwr) < 1e-5
+        assert rel_err(db.cpu(), dbr) < 1e-5
+    if need_dx:
+        dxr = 0.75 * (dy.double() @ w.double())
+        if act >= 0:
+            z = pre.double().requires_grad_(True)
+            dxr = dxr * torch.autograd.grad(_act_ref(z, act).sum(), z)[0]
+        if T:
+            assert rel_err(dx.cpu(), dxr) < 1e-2
+    else:
+        assert dx is None
+    assert int(tickets(torch.device(DEV)).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("act", [0, 1])
+def test_mlp_fn_grads(act):
+    """MLPFn (c_fc bias + GELU epilogue, c_proj, grouped backward with the activation gradient in c_proj's dX
+    epilogue) vs an f32 torch reference on the same bf16 values."""
+    from eventstreamgpt_amd.fused import mlp
+
+    g = torch.Generator().manual_seed(9 + act)
+    T, D, Fd = 1024, 64, 256
+    fc, pj = torch.nn.Linear(D, Fd).to(DEV), torch.nn.Linear(Fd, D).to(DEV)
+    with torch.no_grad():
+        fc.bias.copy_(0.5 * torch.randn(Fd, generator=g))
+        wfc, wpj = fc.weight.bfloat16(), pj.weight.bfloat16()
+    x = torch.randn(T, D, generator=g).to(DEV).bfloat16().requires_grad_(True)
+    y = mlp(x, wfc, wpj, fc, pj, act)
+    xr = x.detach().float().requires_grad_(True)
+    wfr, wpr = wfc.float().requires_grad_(True), wpj.float().requires_grad_(True)
+    bfr = fc.bias.detach().clone().requires_grad_(True)
+    yr = _act_ref(xr @ wfr.t() + bfr, act) @ wpr.t()
+    assert rel_err(y.float(), yr) < 2e-2
+    go = torch.randn(T, D, device=DEV).bfloat16()
+    y.backward(go)
+    yr.backward(go.float())
+    for a, r in ((x.grad.float(), xr.grad), (fc.weight.grad, wfr.grad), (fc.bias.grad, bfr.grad),
+                 (pj.weight.grad, wpr.grad)):
+        assert rel_err(a, r) < 2e-2
+
+
 def test_proj_fn_grads():
     """ProjFn (HIP fwd / dx / f32 dW, packed q|k|v parameters) vs F.linear on the same bf16 values."""
     from eventstreamgpt_amd.fused import proj
