@@ -149,7 +149,7 @@ struct Prob {
   int64_t lda, ldb;
   int M, N, K;
   int tm, tn, splits, kchunk;  // tile grid and split-K
-  int wg0;                     // first (remapped) workgroup index of this problem in the launch
+  int wg0;                     // grouped launch: first workgroup id of this problem
   void* C;
   int64_t ldc;
   int out_f32, accumulate;
@@ -258,32 +258,38 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   const bool rok = row < M;
   const int cb = n0 + wn * 32;
 
-  // ---- split-K: slab, ticket, the last arriver reduces in z order (agent-scope release / acquire) ----
+  // ---- split-K: slab, ticket, the last arriver reduces in z order ----
+  // Hand-off in its write-through form (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms): every slab
+  // store is an sc1 (write-through) store, every storing wave drains it (vmcnt(0)) before the workgroup barrier and
+  // one agent-scope ticket add; the workgroup whose add comes last reads every slab with sc1 loads. No L2
+  // write-back fence: with the grouped dX product streaming its output through the same L2s, buffer_wbl2 per
+  // workgroup serialised on the dirty lines of the whole XCD.
   if (p.splits > 1) {
-    float* slab = p.slab + (size_t)bz * M * N;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(p.slab, (short)0, 0x7fffffff, 0x00020000);
+    constexpr int kSC1 = 16;  // cache policy: sc1
+    const int rs_base = p.splits * M * N;  // row-sum slabs follow the tile slabs
     if (rok) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = cb + 8 * g + 4 * h;
-        if (c < N)
-          *reinterpret_cast<float4*>(slab + (int64_t)row * N + c) =
-              make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+        if (c < N) {
+          const u32x4 w = {__float_as_uint(acc[4 * g]), __float_as_uint(acc[4 * g + 1]),
+                           __float_as_uint(acc[4 * g + 2]), __float_as_uint(acc[4 * g + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(w, rs, 4 * (bz * M * N + row * N + c), 0, kSC1);
+        }
       }
-      if (want_rs && h == 0) p.slab[(size_t)p.splits * M * N + (size_t)bz * M + row] = racc[0];
+      if (want_rs && h == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(racc[0]), rs, 4 * (rs_base + bz * M + row), 0, kSC1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave's slab stores have completed (and the LDS tiles are no longer read)
+    __syncthreads();  // every wave's slab stores have drained (and the LDS tiles are no longer read)
     int* flag = reinterpret_cast<int*>(smem);
     if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == p.splits - 1;
-      if (last) {
-        __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last;
     }
     __syncthreads();
@@ -291,20 +297,20 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
     for (int z = 0; z < p.splits; ++z) {
-      const float* sz = p.slab + (size_t)z * M * N;
       if (rok) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int c = cb + 8 * g + 4 * h;
           if (c < N) {
-            const float4 x = *reinterpret_cast<const float4*>(sz + (int64_t)row * N + c);
-            acc[4 * g] += x.x;
-            acc[4 * g + 1] += x.y;
-            acc[4 * g + 2] += x.z;
-            acc[4 * g + 3] += x.w;
+            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (z * M * N + row * N + c), 0, kSC1);
+            acc[4 * g] += __uint_as_float(x[0]);
+            acc[4 * g + 1] += __uint_as_float(x[1]);
+            acc[4 * g + 2] += __uint_as_float(x[2]);
+            acc[4 * g + 3] += __uint_as_float(x[3]);
           }
         }
-        if (want_rs) racc[0] += p.slab[(size_t)p.splits * M * N + (size_t)z * M + row];
+        if (want_rs)
+          racc[0] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (rs_base + z * M + row), 0, kSC1));
       }
     }
   }
@@ -401,14 +407,16 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
 }
 
 // A projection's backward in one launch: problem 0 = dX (A = dY K-contig, B = W N-contig), problem 1 = dW (A = dYᵀ
-// M-contig, B = X N-contig, + the bias gradient). Workgroups [0, p1.wg0) belong to problem 0.
+// M-contig, B = X N-contig, + the bias gradient). The dW workgroups (the long K = tokens chains) take the first
+// p0.wg0 workgroup ids, so the dispatcher deals them round-robin over all 8 XCDs first and the short dX tiles
+// fill in behind them; each problem keeps its own XCD-aware order within its id range.
 __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[LDS_ELEMS];
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  if (lin < p1.wg0)
-    gemm_tile<true, false>(p0, lin, smem);
+  const int id = blockIdx.x, n1 = p0.wg0;
+  if (id < n1)
+    gemm_tile<false, false>(p1, xcd_remap(id, n1), smem);
   else
-    gemm_tile<false, false>(p1, lin - p1.wg0, smem);
+    gemm_tile<true, false>(p0, xcd_remap(id - n1, gridDim.x - n1), smem);
 }
 
 struct Plan {
@@ -509,6 +517,7 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget);
   if (p.splits > 1) {
     ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N) && counters);
+    ESGPT_REQUIRE(slab_bytes(p.splits, M, N) < (1ull << 31));  // 32-bit buffer offsets
     p.slab = reinterpret_cast<float*>(workspace);
     p.counters = counters;
   }
@@ -549,10 +558,11 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
                      int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
                      int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
                      void* stream) {
-  ESGPT_REQUIRE(dy && x && w && dw && T >= 0 && in >= 0 && out >= 0);
+  ESGPT_REQUIRE(T >= 0 && in >= 0 && out >= 0);
   hipStream_t st = as_stream(stream);
   if (in == 0 || out == 0) return ESGPT_OK;
-  if (T == 0) {  // empty batch: zero weight / bias gradients, nothing else
+  ESGPT_REQUIRE(dw != nullptr);
+  if (T == 0) {  // empty batch (the operands may be empty allocations): zero weight / bias gradients
     if (zero_async(dw, sizeof(float) * out * in, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
     if (db && zero_async(db, sizeof(float) * out, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
     return ESGPT_OK;
@@ -575,11 +585,12 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
   p1.rowsum = db;
   if (p1.splits > 1) {
     ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in) && counters);
+    ESGPT_REQUIRE(slab_bytes(p1.splits, out, in) < (1ull << 31));  // 32-bit buffer offsets
     p1.slab = reinterpret_cast<float*>(workspace);
     p1.counters = counters;
   }
   if (has_dx) {
-    p1.wg0 = n_wg(p0);
+    p0.wg0 = n_wg(p1);
     gemm_bwd_pair_kernel<<<dim3((unsigned)(n_wg(p0) + n_wg(p1))), THREADS, 0, st>>>(p0, p1);
   } else {
     gemm_kernel<false, false><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
