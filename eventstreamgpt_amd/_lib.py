@@ -79,8 +79,9 @@ SIGNATURES = {
     "esgpt_residual_ln_partials": (_i64, [_i64]),
     "esgpt_residual_ln_fwd": (_int, [_vp, _vp, _int, _vp, _vp, _f32, _vp, _vp, _vp, _f32, _i64, _i64, _vp, _vp, _int,
                                      _vp, _vp, _vp]),
+    "esgpt_residual_ln_counters": (_i64, [_i64]),
     "esgpt_residual_ln_bwd": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i64, _i64, _vp, _vp, _int,
-                                     _vp, _vp, _vp]),
+                                     _vp, _vp, _vp, _vp]),
     "esgpt_bias_act_fwd": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int, _vp]),
     "esgpt_bias_act_partials": (_i64, [_i64]),
     "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),

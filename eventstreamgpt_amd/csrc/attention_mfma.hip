@@ -1,18 +1,18 @@
-// bf16 MFMA flash attention for gfx950 (InnerSelfAttention._attn, transformer.py:171-217), hd in {32, 64, 128}.
+// bf16 MFMA flash attention forward for gfx950 (InnerSelfAttention._attn, transformer.py:171-217), hd in {32, 64,
+// 128}; the fused backward (dQ, dK, dV in one kernel) is attention_bwd.hip.
 //
-// All three kernels use v_mfma_f32_32x32x16_bf16 and keep one sequence index on the MFMA lane so that the
-// per-row softmax statistics are lane-local (no cross-lane row reductions beyond one xor-32 exchange):
-//   forward   Sᵀ[key][q] = K·Qᵀ  (A = K rows from LDS, B = Q fragments in registers)
-//             Oᵀ[d][q]  += Vᵀ·Pᵀ (A = Vᵀ tile in LDS read in the permuted key order, B = P straight from the
-//                                 Sᵀ accumulator registers converted to bf16 — no LDS round trip for P)
-//   dQ        Sᵀ, dPᵀ = V·dOᵀ, dSᵀ = Pᵀ∘(dPᵀ−δ), dQᵀ += Kᵀ·dSᵀ          (q on the lane; writes δ = rowsum(dO∘O))
-//   dK/dV     S = Q·Kᵀ, dP = dO·Vᵀ, dVᵀ += dOᵀ·P, dKᵀ += Qᵀ·dS           (key on the lane; reads δ)
+// v_mfma_f32_32x32x16_bf16 with the query on the MFMA lane, so the per-row softmax statistics are lane-local (no
+// cross-lane row reductions beyond one xor-32 exchange):
+//   Sᵀ[key][q] = K·Qᵀ  (A = K rows from LDS, B = Q fragments in registers)
+//   Oᵀ[d][q]  += Vᵀ·Pᵀ (A = Vᵀ tile in LDS read in the permuted key order, B = P straight from the Sᵀ accumulator
+//                       registers converted to bf16 — no LDS round trip for P)
 // Fragment maps (gfx950, 32x32x16 bf16): lane l = (r = l&31, h = l>>5); A[row r][k = 8h+j], B[k = 8h+j][col r];
 // C/D reg i holds row (i&3) + 8(i>>2) + 4h, col r. An accumulator used as the next B operand supplies, for k-step s,
 // element j of half h = row 16s + 8(j>>2) + 4h + (j&3); the A operand is read from LDS in that same key order.
 //
-// Work decomposition: one 128-thread workgroup (2 waves x 32 rows) per 64-row block of one (batch, head);
-// K/V (or Q/dO) tiles of 64 rows are staged in LDS. Causal / local-window / fully-padded key tiles are skipped.
+// Work decomposition (forward): one 256-thread workgroup per 64-query block of one (batch, head), two waves per
+// query half splitting its key tiles by parity; K/V tiles of 64 rows are staged in LDS in pairs. Causal /
+// local-window / fully-padded key tiles are skipped.
 // Roofline: MFMA-bound at large L (algorithmic FLOPs: fwd 4*H*hd*T, bwd 8*H*hd*T, T = allowed (q,k) pairs).
 #include "common.h"
 
@@ -25,7 +25,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int ROWS = 64;   // rows per workgroup block and per staged tile
-constexpr int THREADS = 128;
+constexpr int THREADS = 256;  // forward workgroup: 4 waves
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -85,26 +85,6 @@ __device__ __forceinline__ bf16x8 perm_frag(const __bf16* T, int ld, int row, in
   return f;
 }
 
-// Stages a [ROWS][HD] block of rows (row stride ld_g elements in global) into LDS: natural layout N[row][HD+8]
-// (optional) and transposed layout Tt[d][ROWS+4] (optional). Rows >= n_rows are zero.
-template <int HD>
-__device__ __forceinline__ void stage_rows(const __bf16* __restrict__ g, int64_t ld_g, int row0, int n_rows,
-                                           __bf16* N, __bf16* Tt) {
-  constexpr int CH = HD / 8;
-  constexpr int NP = HD + 8, TP = ROWS + 4;
-  for (int c = threadIdx.x; c < ROWS * CH; c += THREADS) {
-    const int row = c / CH, c8 = c % CH;
-    const int gr = row0 + row;
-    bf16x8 val = zero8();
-    if (gr < n_rows) val = *reinterpret_cast<const bf16x8*>(g + (int64_t)gr * ld_g + c8 * 8);
-    if (N) *reinterpret_cast<bf16x8*>(N + row * NP + c8 * 8) = val;
-    if (Tt) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Tt[(c8 * 8 + j) * TP + row] = val[j];
-    }
-  }
-}
-
 __device__ __forceinline__ bool allowed(int key, int qpos, int window) {
   return key <= qpos && (window == 0 || qpos - key < window);
 }
@@ -126,29 +106,17 @@ __device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)p);
 }
 
-// K/V tile prefetch (global -> registers): 64 rows x HD, HD/16 16-byte chunks per thread per tensor.
-template <int HD>
-__device__ __forceinline__ void load_kv(const __bf16* __restrict__ kb, const __bf16* __restrict__ vb, int64_t ld,
-                                        int kt, int Lk, bf16x8 (&rk)[HD / 16], bf16x8 (&rv)[HD / 16]) {
-  constexpr int CH = HD / 8;
-#pragma unroll
-  for (int i = 0; i < HD / 16; ++i) {
-    const int c = threadIdx.x + THREADS * i;
-    const int row = c / CH, c8 = c % CH, gr = kt + row;
-    const bool ok = gr < Lk;
-    rk[i] = ok ? *reinterpret_cast<const bf16x8*>(kb + (int64_t)gr * ld + c8 * 8) : zero8();
-    rv[i] = ok ? *reinterpret_cast<const bf16x8*>(vb + (int64_t)gr * ld + c8 * 8) : zero8();
-  }
-}
-
 // ------------------------------------------------------------------------------------------------------------
-// Forward. K is staged row-major (A operand of Sᵀ = K·Qᵀ by 16-B row reads); V row-major too, read as the
-// transposed A operand of Oᵀ += Vᵀ·Pᵀ with ds_read_b64_tr_b16 (no transposing LDS writes). The next K/V tile is
-// prefetched into registers while the current one is consumed. Key validity is a 64-bit ballot per tile; tiles
-// that are fully valid and fully inside the causal / local band skip the per-element masks. Softmax in the exp2
-// domain (v_exp_f32).
+// Forward. One 256-thread workgroup (4 waves) per 64-query block of one (batch, head): wave w owns queries
+// 32·(w&1) .. +31 of the block and the 64-key tiles of parity w>>1 (tiles t, t+128, … and t+64, t+192, …), so two
+// waves walk the causal key range of each query half in parallel (half the serial chain of a 2-wave block) and
+// merge their online-softmax states (max, sum, O) through LDS at the end. K is staged row-major (A operand of
+// Sᵀ = K·Qᵀ by 16-B row reads); V row-major too, read as the transposed A operand of Oᵀ += Vᵀ·Pᵀ with
+// ds_read_b64_tr_b16 (no transposing LDS writes). The next pair of K/V tiles is prefetched into registers while the
+// current pair is consumed. Key validity is a 64-bit ballot per tile; tiles that are fully valid and fully inside the
+// causal / local band skip the per-element masks. Softmax in the exp2 domain (v_exp_f32).
 template <int HD, bool DROP>
-__global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __restrict__ q,
+__global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kernel(const __bf16* __restrict__ q,
                                                                const __bf16* __restrict__ k,
                                                                const __bf16* __restrict__ v, int64_t ld_in, int64_t tq,
                                                                __bf16* __restrict__ o, int64_t ld_o,
@@ -158,21 +126,28 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
                                                                int Lk, int window, float drop_p,
                                                                const uint64_t* __restrict__ seed) {
   constexpr int NP = HD + 8, VLD = VImg<HD>::LD;
+  constexpr int CH = HD / 8;                        // 16-B chunks per row
+  constexpr int NLD = 2 * ROWS * CH / THREADS;      // chunks per thread and tensor for a pair of tiles
   constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
-  __shared__ __attribute__((aligned(16))) __bf16 sK[ROWS * NP];
-  __shared__ __attribute__((aligned(16))) __bf16 sV[ROWS * VLD];
+  // [2 tiles][ROWS][NP] K and [2 tiles][ROWS][VLD] V images; the K image doubles as the merge buffer at the end
+  __shared__ __attribute__((aligned(16))) __bf16 sK[2 * ROWS * NP];
+  __shared__ __attribute__((aligned(16))) __bf16 sV[2 * ROWS * VLD];
+  static_assert(sizeof(__bf16) * 2 * ROWS * NP >= sizeof(float) * (2 * (HD / 32) * 16 * 64 + 4 * 64), "merge");
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int qh = wave & 1, kp = wave >> 1;
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
   const int qb = blockIdx.x * ROWS;
-  const int qi = qb + wave * 32 + r;
+  const int qi = qb + qh * 32 + r;
   const bool qin = qi < Lq;
   const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
   const int qpos = qi + off;
-  const int qlo_w = qb + wave * 32 + off;                // smallest query position of this wave
-  const int qhi_w = min(qb + wave * 32 + 31, Lq - 1) + off;  // largest
+  const int qlo_w = qb + qh * 32 + off;                      // smallest query position of this wave
+  const int qhi_w = min(qb + qh * 32 + 31, Lq - 1) + off;    // largest
+  const __bf16* myK = sK + kp * ROWS * NP;
+  const __bf16* myV = sV + kp * ROWS * VLD;
 
   bf16x8 qf[HD / 16];
   const __bf16* qrow = q + ((int64_t)b * tq + qi) * ld_in + hh * HD;
@@ -192,27 +167,41 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
   const __bf16* vbase = v + (int64_t)b * Lk * ld_in + hh * HD;
   const uint8_t* kmb = kmask ? kmask + (int64_t)b * Lk : nullptr;
 
-  bf16x8 rk[HD / 16], rv[HD / 16];
-  int kt = (kmin / ROWS) * ROWS;
-  load_kv<HD>(kbase, vbase, ld_in, kt, Lk, rk, rv);
-  bool kok = kt + lane < Lk && (kmb == nullptr || kmb[kt + lane] != 0);
-  for (; kt <= kmax; kt += ROWS) {
-    const uint64_t kbits = __ballot(kok);  // identical in both waves (same 64 keys)
-    __syncthreads();
-    if (kbits) {
+  // pair of tiles (keys kt .. kt+127) -> registers; rows past kmax (never visible to this block) are zeros
+  bf16x8 rk[NLD], rv[NLD];
+  auto load_pair = [&](int kt) {
 #pragma unroll
-      for (int i = 0; i < HD / 16; ++i) {
-        const int c = tid + THREADS * i, row = c / (HD / 8), c8 = c % (HD / 8);
-        *reinterpret_cast<bf16x8*>(sK + row * NP + c8 * 8) = rk[i];
-        *reinterpret_cast<bf16x8*>(sV + row * VLD + c8 * 8) = rv[i];
-      }
+    for (int i = 0; i < NLD; ++i) {
+      const int c = tid + THREADS * i, row = c / CH, c8 = c % CH, gr = kt + row;
+      const bool ok = gr <= kmax;
+      rk[i] = ok ? *reinterpret_cast<const bf16x8*>(kbase + (int64_t)gr * ld_in + c8 * 8) : zero8();
+      rv[i] = ok ? *reinterpret_cast<const bf16x8*>(vbase + (int64_t)gr * ld_in + c8 * 8) : zero8();
+    }
+  };
+  auto key_ok = [&](int kt) {
+    const int key = kt + ROWS * kp + lane;
+    return key <= kmax && (kmb == nullptr || kmb[key] != 0);
+  };
+
+  int kt = (kmin / ROWS) * ROWS;
+  load_pair(kt);
+  bool kok = key_ok(kt);
+  for (; kt <= kmax; kt += 2 * ROWS) {
+    const int t0 = kt + ROWS * kp;          // this wave's tile
+    const uint64_t kbits = __ballot(kok);   // 0 when the tile lies past kmax
+    __syncthreads();                        // the previous pair's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = tid + THREADS * i, row = c / CH, c8 = c % CH;
+      *reinterpret_cast<bf16x8*>(sK + row * NP + c8 * 8) = rk[i];
+      *reinterpret_cast<bf16x8*>(sV + row * VLD + c8 * 8) = rv[i];
     }
     __syncthreads();
-    if (kt + ROWS <= kmax) {
-      load_kv<HD>(kbase, vbase, ld_in, kt + ROWS, Lk, rk, rv);
-      kok = kt + ROWS + lane < Lk && (kmb == nullptr || kmb[kt + ROWS + lane] != 0);
+    if (kt + 2 * ROWS <= kmax) {
+      load_pair(kt + 2 * ROWS);
+      kok = key_ok(kt + 2 * ROWS);
     }
-    if (!kbits) continue;  // fully padded key tile
+    if (!kbits) continue;  // fully padded (or absent) key tile
 
     f32x16 s[2];
 #pragma unroll
@@ -220,11 +209,11 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
       s[c] = zero16();
 #pragma unroll
       for (int t = 0; t < HD / 16; ++t) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(sK + (32 * c + r) * NP + 16 * t + 8 * h);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(myK + (32 * c + r) * NP + 16 * t + 8 * h);
         s[c] = mfma(a, qf[t], s[c]);
       }
     }
-    const bool full = kbits == ~0ull && kt + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - kt < window);
+    const bool full = kbits == ~0ull && t0 + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - t0 < window);
     float mt = -INFINITY;
     if (full) {
 #pragma unroll
@@ -240,7 +229,7 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int kr = 32 * c + acc_row(i, h);
-          const bool ok = qvalid && ((kbits >> kr) & 1ull) && allowed(kt + kr, qpos, window);
+          const bool ok = qvalid && ((kbits >> kr) & 1ull) && allowed(t0 + kr, qpos, window);
           s[c][i] = ok ? s[c][i] * kLog2e : -INFINITY;
           mt = fmaxf(mt, s[c][i]);
         }
@@ -256,7 +245,7 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(s[c][i] - msub);  // exp2(-inf) = 0
         rs += p;  // normaliser over undropped probabilities
-        s[c][i] = DROP ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kt + 32 * c + acc_row(i, h))) : p;
+        s[c][i] = DROP ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, t0 + 32 * c + acc_row(i, h))) : p;
       }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
@@ -276,7 +265,7 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
         const int row0 = 32 * c + 16 * ss + 4 * (g >> 1) + q4;
 #pragma unroll
         for (int dt = 0; dt < HD / 32; ++dt) {
-          const __bf16* vp = sV + row0 * VLD + 32 * dt + 16 * (g & 1) + 4 * p4;
+          const __bf16* vp = myV + row0 * VLD + 32 * dt + 16 * (g & 1) + 4 * p4;
           const bf16x4 lo = tr_read(vp), hi = tr_read(vp + 8 * VLD);
           bf16x8 vf;
           vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
@@ -284,6 +273,35 @@ __global__ __launch_bounds__(THREADS) void attn_fwd_mfma_kernel(const __bf16* __
           oacc[dt] = mfma(vf, pf, oacc[dt]);
         }
       }
+  }
+
+  // ---- merge the two key parities of each query half (the odd-parity wave hands its state over in LDS) ----
+  __syncthreads();  // every wave is done with the K / V images
+  float* cO = reinterpret_cast<float*>(sK);   // [qh][HD/32][16][64]
+  float* cM = cO + 2 * (HD / 32) * 16 * 64;   // [qh][64]
+  float* cL = cM + 2 * 64;
+  if (kp == 1) {
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) cO[((qh * (HD / 32) + dt) * 16 + i) * 64 + lane] = oacc[dt][i];
+    cM[qh * 64 + lane] = m;
+    cL[qh * 64 + lane] = l;
+  }
+  __syncthreads();
+  if (kp == 1) return;
+  {
+    const float m1 = cM[qh * 64 + lane], l1 = cL[qh * 64 + lane];
+    const float mm = fmaxf(m, m1);
+    const float a0 = (m == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m - mm);
+    const float a1 = (m1 == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m1 - mm);
+    l = l * a0 + l1 * a1;
+    m = mm;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        oacc[dt][i] = oacc[dt][i] * a0 + cO[((qh * (HD / 32) + dt) * 16 + i) * 64 + lane] * a1;
   }
 
   const bool ok = qvalid && l > 0.f;

@@ -107,6 +107,31 @@ __device__ __forceinline__ DropoutSpec make_dropout(float p, const uint64_t* see
   return d;
 }
 
+// In-launch last-arriver ticket, write-through form (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms):
+// the handed-off bytes are stored with sc1 stores (st_wt) and read back with sc1 loads (ld_wt); every thread calls
+// this after its stores; each wave drains them, the workgroup barrier orders them before ONE agent-scope ticket add,
+// and the workgroup whose add comes last — of the `expected` ones sharing `counter` — gets true and resets the
+// counter for the next launch. No L2 write-back fence (buffer_wbl2 would write back every dirty line of the XCD's
+// L2, which the streaming kernels around it keep full). `flag`: one int of the caller's LDS.
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool last_arrival(int32_t* counter, int expected, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == expected - 1;
+    if (last) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }

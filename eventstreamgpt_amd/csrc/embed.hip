@@ -596,9 +596,18 @@ __global__ __launch_bounds__(256) void bag_subject_sum_kernel(esgpt_batch bt, in
   }
 }
 
-// One wave per chunk of kChunk sorted entries. Rows fully inside the chunk are stored; rows crossing a chunk
-// boundary are accumulated with f32 atomics (at most two per chunk). dtable is zeroed beforehand.
+// One wave per chunk of kChunk sorted entries. Lanes 0..n-1 load the chunk's entries (coalesced); the wave then
+// walks them in groups of kGroup with the group's gathered gradient rows in flight together (the entry fields are
+// wave-uniform via readlane). Rows fully inside the chunk are stored; a row that continues into a neighbouring
+// chunk (at most the first and the last run) is added with f32 atomics. dtable is zeroed beforehand.
 constexpr int kChunk = 32;
+constexpr int kGroup = 8;
+
+__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 
 template <int VEC>
 __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_t* __restrict__ rowptr,
@@ -614,51 +623,74 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
   const int64_t lo = chunk * kChunk;
   const int64_t n_ent = rowptr[V];
   if (lo >= n_ent) return;
-  const int64_t hi = min(n_ent, lo + kChunk);
-  for (int64_t d0 = lane * VEC; d0 < D; d0 += 64 * VEC) {
+  const int n = (int)min<int64_t>(kChunk, n_ent - lo);
+  int32_t my_v = -1;
+  int64_t my_s = 0;
+  float my_w = 0.f;
+  if (lane < n) {
+    my_v = ent_v[lo + lane];
+    my_s = ent_src[lo + lane];
+    my_w = ent_w[lo + lane];
+  }
+  // the chunk's first / last run continues into the previous / next chunk when those entries share its row
+  const int32_t prev_v = lo > 0 ? ent_v[lo - 1] : -1;
+  const int32_t next_v = lo + n < n_ent ? ent_v[lo + n] : -1;
+  for (int64_t base = 0; base < D; base += 64 * VEC) {
+    const int64_t d0 = base + (int64_t)lane * VEC;
+    const bool dok = d0 < D;  // VEC == 4 only when D % 4 == 0
     float acc[VEC];
 #pragma unroll
-    for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
-    int32_t cur = ent_v[lo];
-    for (int64_t p = lo; p < hi; ++p) {
-      const int32_t v = ent_v[p];
-      if (v != cur) {
-        const bool interior = rowptr[cur] >= lo && rowptr[cur + 1] <= hi;
-        float* dst = dtable + (int64_t)cur * D + d0;
+    for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+    int32_t cur = __builtin_amdgcn_readlane(my_v, 0);
+    bool head = true;  // the current run starts at the chunk's first entry
+    auto flush = [&](bool tail) {
+      const bool shared = (head && prev_v == cur) || (tail && next_v == cur);
+      float* dst = dtable + (int64_t)cur * D + d0;
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-          if (d0 + k < D) {
-            if (interior) dst[k] = acc[k];
-            else atomicAdd(dst + k, acc[k]);
-          }
-          acc[k] = 0.f;
+      for (int k = 0; k < VEC; ++k) {
+        if (dok && (VEC == 4 || d0 + k < D)) {
+          if (shared) atomicAdd(dst + k, acc[k]);
+          else dst[k] = acc[k];
         }
-        cur = v;
+        acc[k] = 0.f;
       }
-      const int64_t s = ent_src[p];
-      const float w = ent_w[p];
-      const float* row = (s >= 0) ? dsrc + s * ld : sub + (-1 - s) * D;
-      if (VEC == 4 && d0 + 3 < D && (s >= 0 ? (ld % 4 == 0) : true)) {
-        const float4 x = *reinterpret_cast<const float4*>(row + d0);
-        acc[0] = fmaf(w, x.x, acc[0]);
-        acc[1] = fmaf(w, x.y, acc[1]);
-        acc[2] = fmaf(w, x.z, acc[2]);
-        acc[3] = fmaf(w, x.w, acc[3]);
-      } else {
+    };
+    for (int p0 = 0; p0 < n; p0 += kGroup) {
+      float x[kGroup][VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k)
-          if (d0 + k < D) acc[k] = fmaf(w, row[d0 + k], acc[k]);
+      for (int j = 0; j < kGroup; ++j) {
+        const int p = min(p0 + j, n - 1);
+        const int64_t s = readlane64(my_s, p);
+        const float* row = s >= 0 ? dsrc + s * ld : sub + (-1 - s) * D;
+        if (VEC == 4) {
+          float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (dok) t = *reinterpret_cast<const float4*>(row + d0);
+          x[j][0] = t.x;
+          x[j][1] = t.y;
+          x[j][2] = t.z;
+          x[j][3] = t.w;
+        } else {
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) x[j][k] = (d0 + k < D) ? row[d0 + k] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const int p = p0 + j;
+        if (p < n) {
+          const int32_t v = __builtin_amdgcn_readlane(my_v, p);
+          if (v != cur) {
+            flush(false);
+            cur = v;
+            head = false;
+          }
+          const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), p));
+#pragma unroll
+          for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, x[j][k], acc[k]);
+        }
       }
     }
-    const bool interior = rowptr[cur] >= lo && rowptr[cur + 1] <= hi;
-    float* dst = dtable + (int64_t)cur * D + d0;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      if (d0 + k < D) {
-        if (interior) dst[k] = acc[k];
-        else atomicAdd(dst + k, acc[k]);
-      }
-    }
+    flush(true);
   }
 }
 

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void count_kernel(esgpt_batch bt, Terms terms,
 }
 
 // ------------------------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, bool RMW>
 __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms, esgpt_tte_spec tte,
                                                     const T* __restrict__ zc, int64_t ldc, int64_t n_levels, int shift,
                                                     const T* __restrict__ zc_bias, const T* __restrict__ zt,
@@ -178,9 +178,13 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
       const bool mk = term_mask(tm, E, (int)M, ev);
       const int32_t cnt = cnt_b[t];
       const float scale = (mk && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
+      // Gradient columns: with disjoint term columns (checked on the host) every column of a row has exactly one
+      // writer, so the zero-filled buffer is stored to without a read; otherwise read-modify-write. The bias row
+      // (shift mode) is this wave's own f32 row.
       auto put = [&](int64_t col, float g) {
-        if (gF) gF[col] += g;  // bias row: several terms never share a column, += keeps it generic
-        else gT[col] = from_f32<T>(to_f32(gT[col]) + g);
+        if (gF) gF[col] += g;
+        else if (RMW) gT[col] = from_f32<T>(to_f32(gT[col]) + g);
+        else gT[col] = from_f32<T>(g);
       };
       float ell = 0.f;
       if (tm.kind == ESGPT_TERM_SINGLE) {
@@ -217,13 +221,19 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
         }
       } else if (tm.kind == ESGPT_TERM_MULTI) {
         const int n = tm.vocab_end - tm.vocab_start;
+        // lane m < M holds entry m's label within this term (-1: another measurement); labels are broadcast
+        // with readlane (wave-uniform m) instead of re-reading the staged entries per column
+        const int my_lab = (lane < M && E.meas[lane] == tm.meas_idx) ? (int)(E.idx[lane] - tm.vocab_start) : -1;
         float acc = 0.f;
-        for (int j = lane; j < n; j += 64) {
+        for (int j0 = 0; j0 < n; j0 += 64) {
+          const int j = j0 + lane;
           bool y = false;
-          for (int m = 0; m < M; ++m) y |= (E.meas[m] == tm.meas_idx) && (E.idx[m] - tm.vocab_start == j);
-          const float x = to_f32(zrow[tm.col + j]);
-          acc += bce_logits(x, y ? 1.f : 0.f);
-          if (scale != 0.f) put(tm.col + j, scale / (float)n * (sigmoidf_(x) - (y ? 1.f : 0.f)));
+          for (int m = 0; m < M; ++m) y |= __builtin_amdgcn_readlane(my_lab, m) == j;
+          if (j < n) {
+            const float x = to_f32(zrow[tm.col + j]);
+            acc += bce_logits(x, y ? 1.f : 0.f);
+            if (scale != 0.f) put(tm.col + j, scale / (float)n * (sigmoidf_(x) - (y ? 1.f : 0.f)));
+          }
         }
         ell = wave_sum(acc) / (float)n;
       } else if (tm.kind == ESGPT_TERM_MVREG) {
@@ -358,27 +368,59 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Deterministic sums of the per-row contributions: every thread accumulates all terms over its rows, then wave
+// sums and a fixed-order sum over the 16 waves.
 __global__ __launch_bounds__(1024) void reduce_kernel(const float* __restrict__ contrib, int64_t n_rows, int NT,
                                                       float* __restrict__ losses) {
-  __shared__ float s[1024];
-  float total = 0.f;
-  for (int t = 0; t <= NT; ++t) {
-    float a = 0.f;
-    for (int64_t i = threadIdx.x; i < n_rows; i += 1024) a += contrib[(int64_t)t * n_rows + i];
-    s[threadIdx.x] = a;
-    __syncthreads();
-    for (int o = 512; o > 0; o >>= 1) {
-      if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
-      __syncthreads();
+  __shared__ float s[16][ESGPT_MAX_TERMS + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float a[ESGPT_MAX_TERMS + 1];
+#pragma unroll
+  for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) a[t] = 0.f;
+  for (int64_t i = threadIdx.x; i < n_rows; i += 1024) {
+#pragma unroll
+    for (int t = 0; t <= ESGPT_MAX_TERMS; ++t)
+      if (t <= NT) a[t] += contrib[(int64_t)t * n_rows + i];
+  }
+#pragma unroll
+  for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) {
+    if (t <= NT) {
+      const float v = wave_sum(a[t]);
+      if (lane == 0) s[wave][t] = v;
     }
-    if (threadIdx.x == 0) {
-      const float v = (t < NT) ? s[0] : -s[0];  // last slot: -TTE_LL
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float total = 0.f;
+    for (int t = 0; t <= NT; ++t) {
+      float v = 0.f;
+      for (int w = 0; w < 16; ++w) v += s[w][t];
+      v = (t < NT) ? v : -v;  // last slot: -TTE_LL
       losses[t] = v;
       total += v;
     }
-    __syncthreads();
+    losses[NT + 1] = total;
   }
-  if (threadIdx.x == 0) losses[NT + 1] = total;
+}
+
+// True when no two terms write the same gradient column of one logit row (the event kernel then stores instead of
+// read-modify-writing). Columns per term: SINGLE [col, col+n) + obs_col; MULTI [col, col+n); MVREG [col, col+2n);
+// UVREG [col, col+2) + obs_col. Terms of different levels write different rows.
+bool disjoint_columns(const esgpt_loss_term* terms, int n_terms, int shift) {
+  int64_t lo[2 * ESGPT_MAX_TERMS], hi[2 * ESGPT_MAX_TERMS];
+  int lvl[2 * ESGPT_MAX_TERMS], k = 0;
+  for (int i = 0; i < n_terms; ++i) {
+    const esgpt_loss_term& t = terms[i];
+    const int64_t n = t.vocab_end - t.vocab_start;
+    const int64_t w = t.kind == ESGPT_TERM_MVREG ? 2 * n : t.kind == ESGPT_TERM_UVREG ? 2 : n;
+    const int level = shift ? 0 : t.level;
+    lo[k] = t.col, hi[k] = t.col + w, lvl[k++] = level;
+    if (t.kind == ESGPT_TERM_SINGLE || t.kind == ESGPT_TERM_UVREG) lo[k] = t.obs_col, hi[k] = t.obs_col + 1, lvl[k++] = level;
+  }
+  for (int a = 0; a < k; ++a)
+    for (int b = a + 1; b < k; ++b)
+      if (lvl[a] == lvl[b] && lo[a] < hi[b] && lo[b] < hi[a]) return false;
+  return true;
 }
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -418,14 +460,17 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
   count_kernel<<<(unsigned)B, 256, 0, st>>>(*batch, T, counts, err);
   const int64_t n_rows = B * (L + shift);
   const unsigned grid = (unsigned)cdiv(n_rows, kWaves);
-  if (dtype == ESGPT_F32)
-    event_kernel<float><<<grid, 256, 0, st>>>(*batch, T, *tte, (const float*)zc, ldc, n_levels, shift,
-                                              (const float*)zc_bias, (const float*)zt, ldt, (float*)dzc, (float*)dzt,
-                                              dbias, counts, contrib, n_rows, err);
-  else
-    event_kernel<bf16><<<grid, 256, 0, st>>>(*batch, T, *tte, (const bf16*)zc, ldc, n_levels, shift,
-                                             (const bf16*)zc_bias, (const bf16*)zt, ldt, (bf16*)dzc, (bf16*)dzt, dbias,
-                                             counts, contrib, n_rows, err);
+  const bool rmw = !disjoint_columns(terms, n_terms, shift);
+#define LAUNCH_EV(TT, RMW)                                                                                        \
+  event_kernel<TT, RMW><<<grid, 256, 0, st>>>(*batch, T, *tte, (const TT*)zc, ldc, n_levels, shift,               \
+                                              (const TT*)zc_bias, (const TT*)zt, ldt, (TT*)dzc, (TT*)dzt, dbias,  \
+                                              counts, contrib, n_rows, err)
+  if (dtype == ESGPT_F32) {
+    if (rmw) LAUNCH_EV(float, true); else LAUNCH_EV(float, false);
+  } else {
+    if (rmw) LAUNCH_EV(bf16, true); else LAUNCH_EV(bf16, false);
+  }
+#undef LAUNCH_EV
   reduce_kernel<<<1, 1024, 0, st>>>(contrib, n_rows, n_terms, losses);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;

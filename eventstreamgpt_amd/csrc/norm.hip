@@ -4,12 +4,14 @@
 //   residual_ln_fwd   h   = rowmask ? x + dropout(y + bias) : 0          (f32 residual stream)
 //                     out = LayerNorm(h) * w + b                         (f32 or bf16: the next GEMM's operand)
 //   residual_ln_bwd   dh  = rowmask ? dh_in + LN'(dout) : 0 ; dx = dh ; dy = dropout'(dh)
-//                     per-block column partials of dgamma, dbeta, dbias -> colsum
+//                     + the column sums dgamma, dbeta, dbias in the same launch (last-arriver tickets)
 //   bias_act_fwd/bwd  g = act(f + bias) (exact-erf GELU, tanh GELU or ReLU), dbias partials -> colsum
 //
-// Layout: one wave per row; lane l owns the 4-column chunks {4l + 256k}, loaded as 16-B (f32) / 8-B (bf16)
-// vectors; statistics in registers (two-pass mean / variance, biased variance as torch.nn.LayerNorm).
-// HBM-bound: fwd reads x (4 B) + y (2-4 B), writes h (4 B) + out (2-4 B) per element.
+// Layout: one wave per row; lane l owns the 4-column chunks {4l + 256k}, k < KC = ceil(D / 256) (a template
+// parameter: registers sized for the row), loaded as 16-B (f32) / 8-B (bf16) vectors; statistics in registers
+// (two-pass mean / variance, biased variance as torch.nn.LayerNorm).
+// HBM-bound: fwd reads x (4 B) + y (2-4 B), writes h (4 B) + out (2-4 B) per element; bwd reads dout (2-4 B), h
+// (4 B), dh_in (4 B) and writes dx (4 B) + dy (2-4 B) per element.
 #include "common.h"
 
 using namespace esgpt;
@@ -17,8 +19,9 @@ using namespace esgpt;
 namespace {
 
 constexpr int kWaves = 4;
-constexpr int kMaxChunks = 4;      // 4-column chunks per lane: D <= 1024
-constexpr int kBwdRowsPerWave = 2;  // backward: rows per wave (fewer partial rows for the column sums)
+constexpr int kMaxChunks = 4;       // 4-column chunks per lane: D <= 1024
+constexpr int kBwdRowsPerWave = 4;  // backward: rows per wave, every load issued before the row reductions
+constexpr int kGroupBlocks = 32;    // backward column sums: blocks per first-level group
 
 struct V4 {
   float v[4];
@@ -43,9 +46,11 @@ __device__ __forceinline__ void store4(bf16* p, const V4& a) {
   *reinterpret_cast<uint2*>(p) = t;
 }
 
+__device__ __forceinline__ V4 zero4() { return V4{{0.f, 0.f, 0.f, 0.f}}; }
+
 __device__ __forceinline__ uint64_t drop_idx(int64_t row, int64_t D, int64_t col) { return (uint64_t)(row * D + col); }
 
-template <typename TY, typename TO>
+template <typename TY, typename TO, int KC>
 __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __restrict__ x, const TY* __restrict__ y,
                                                               const float* __restrict__ bias,
                                                               const uint8_t* __restrict__ rmask, float drop_p,
@@ -59,12 +64,12 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
   const int64_t row = (int64_t)blockIdx.x * kWaves + wave;
   if (row >= N) return;
   const bool keep_row = rmask == nullptr || rmask[row] != 0;
-  V4 v[kMaxChunks];
+  V4 v[KC];
   float s = 0.f;
 #pragma unroll
-  for (int k = 0; k < kMaxChunks; ++k) {
+  for (int k = 0; k < KC; ++k) {
     const int64_t c = 4 * lane + 256 * k;
-    v[k] = V4{{0.f, 0.f, 0.f, 0.f}};
+    v[k] = zero4();
     if (c < D && keep_row) {
       if (x) v[k] = load4(x + row * D + c);
       if (y) {
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
   const float mean = wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
-  for (int k = 0; k < kMaxChunks; ++k) {
+  for (int k = 0; k < KC; ++k) {
     const int64_t c = 4 * lane + 256 * k;
     if (c < D) {
 #pragma unroll
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
   }
   const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
 #pragma unroll
-  for (int k = 0; k < kMaxChunks; ++k) {
+  for (int k = 0; k < KC; ++k) {
     const int64_t c = 4 * lane + 256 * k;
     if (c < D) {
       if (h) store4(h + row * D + c, v[k]);
@@ -112,43 +117,88 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
   }
 }
 
-// Backward. part: f32 [gridDim.x, 3, D] column partials (dgamma, dbeta, dbias) of this block's rows.
-template <typename TY, typename TO>
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSC1 = 16;  // buffer cache policy: sc1 (write-through stores, L1-bypassing loads)
+
+// Four consecutive columns summed over n partial rows (float index base + j * stride), in row order, with
+// kGroupBlocks write-through loads in flight at a time.
+__device__ __forceinline__ u32x4 ordered_sum4(__amdgpu_buffer_rsrc_t rs, int base, int stride, int n) {
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < n; j0 += kGroupBlocks) {
+    u32x4 v[kGroupBlocks];
+#pragma unroll
+    for (int j = 0; j < kGroupBlocks; ++j)
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (base + min(j0 + j, n - 1) * stride), 0, kSC1);
+#pragma unroll
+    for (int j = 0; j < kGroupBlocks; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) t[c] += j0 + j < n ? __uint_as_float(v[j][c]) : 0.f;
+  }
+  return u32x4{__float_as_uint(t[0]), __float_as_uint(t[1]), __float_as_uint(t[2]), __float_as_uint(t[3])};
+}
+
+// Backward. Each wave owns kBwdRowsPerWave consecutive rows and issues every load of them before the row
+// reductions. Column partials (dgamma, dbeta, dbias) of the block's rows go to part[blockIdx.x][3][D]; the last
+// block to finish in each group of kGroupBlocks sums its group's partials into part[nb + group], and the last group
+// sums those into sums[3][D]: fixed order (deterministic), no second launch, counters left at zero.
+template <typename TY, typename TO, int KC>
 __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     const float* __restrict__ dh_in, const TO* __restrict__ dout, const float* __restrict__ h,
     const float* __restrict__ mean_i, const float* __restrict__ rstd_i, const float* __restrict__ w,
     const uint8_t* __restrict__ rmask, float drop_p, const uint64_t* __restrict__ seed, int64_t N, int64_t D,
-    float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part) {
+    float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part, float* __restrict__ sums,
+    int32_t* __restrict__ counters) {
+  constexpr int R = kBwdRowsPerWave;
   __shared__ float s_part[kWaves][3][4 * 64];
   const DropoutSpec dr = make_dropout(drop_p, seed);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0x7fffffff, 0x00020000);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  V4 pg[kMaxChunks], pb[kMaxChunks], py[kMaxChunks], wv[kMaxChunks];
+  V4 pg[KC], pb[KC], py[KC], wv[KC];
 #pragma unroll
-  for (int k = 0; k < kMaxChunks; ++k) {
-    pg[k] = pb[k] = py[k] = V4{{0.f, 0.f, 0.f, 0.f}};
+  for (int k = 0; k < KC; ++k) {
+    pg[k] = pb[k] = py[k] = zero4();
     const int64_t c = 4 * lane + 256 * k;
-    wv[k] = (c < D) ? load4(w + c) : V4{{0.f, 0.f, 0.f, 0.f}};
+    wv[k] = (c < D) ? load4(w + c) : zero4();
   }
-  for (int rr = 0; rr < kBwdRowsPerWave; ++rr) {
-    const int64_t row = ((int64_t)blockIdx.x * kWaves + wave) * kBwdRowsPerWave + rr;
-    if (row >= N) break;
-    const float mean = mean_i[row], rstd = rstd_i[row];
-    const bool keep_row = rmask == nullptr || rmask[row] != 0;
-    V4 xh[kMaxChunks], g[kMaxChunks];
+  // ---- every load of the wave's rows first (rows past N clamped to a valid row, results dropped) ----
+  const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * R;
+  V4 dv[R][KC], hv[R][KC], di[R][KC];
+  float mean[R], rstd[R];
+  bool keep[R];
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int64_t row = min(row0 + rr, N - 1);
+    mean[rr] = mean_i[row];
+    rstd[rr] = rstd_i[row];
+    keep[rr] = rmask == nullptr || rmask[row] != 0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      dv[rr][k] = hv[rr][k] = di[rr][k] = zero4();
+      if (c < D) {
+        dv[rr][k] = load4(dout + row * D + c);
+        hv[rr][k] = load4(h + row * D + c);
+        if (dh_in) di[rr][k] = load4(dh_in + row * D + c);
+      }
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int64_t row = row0 + rr;
+    if (row >= N) break;  // wave-uniform
+    V4 xh[KC], g[KC];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
-    for (int k = 0; k < kMaxChunks; ++k) {
+    for (int k = 0; k < KC; ++k) {
       const int64_t c = 4 * lane + 256 * k;
-      xh[k] = g[k] = V4{{0.f, 0.f, 0.f, 0.f}};
+      xh[k] = g[k] = zero4();
       if (c < D) {
-        const V4 dv = load4(dout + row * D + c);
-        const V4 hv = load4(h + row * D + c);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          xh[k].v[j] = (hv.v[j] - mean) * rstd;
-          g[k].v[j] = dv.v[j] * wv[k].v[j];
-          pg[k].v[j] += dv.v[j] * xh[k].v[j];
-          pb[k].v[j] += dv.v[j];
+          xh[k].v[j] = (hv[rr][k].v[j] - mean[rr]) * rstd[rr];
+          g[k].v[j] = dv[rr][k].v[j] * wv[k].v[j];
+          pg[k].v[j] += dv[rr][k].v[j] * xh[k].v[j];
+          pb[k].v[j] += dv[rr][k].v[j];
           sg += g[k].v[j];
           sgx += g[k].v[j] * xh[k].v[j];
         }
@@ -157,15 +207,14 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     sg = wave_sum(sg) / (float)D;
     sgx = wave_sum(sgx) / (float)D;
 #pragma unroll
-    for (int k = 0; k < kMaxChunks; ++k) {
+    for (int k = 0; k < KC; ++k) {
       const int64_t c = 4 * lane + 256 * k;
       if (c < D) {
         V4 d;
-        const V4 din = dh_in ? load4(dh_in + row * D + c) : V4{{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float t = rstd * (g[k].v[j] - sg - xh[k].v[j] * sgx) + din.v[j];
-          d.v[j] = keep_row ? t : 0.f;
+          const float t = rstd[rr] * (g[k].v[j] - sg - xh[k].v[j] * sgx) + di[rr][k].v[j];
+          d.v[j] = keep[rr] ? t : 0.f;
         }
         if (dx) store4(dx + row * D + c, d);
         if (dy) {
@@ -180,9 +229,9 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
       }
     }
   }
-  // combine the 4 waves' column partials
+  // ---- combine the 4 waves' column partials ----
 #pragma unroll
-  for (int k = 0; k < kMaxChunks; ++k) {
+  for (int k = 0; k < KC; ++k) {
     const int64_t c0 = 256 * k;
     if (c0 >= D) break;
 #pragma unroll
@@ -192,14 +241,35 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
       s_part[wave][2][4 * lane + j] = py[k].v[j];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 3 * 256; i += blockDim.x) {
-      const int qd = i / 256, cc = i % 256;
+    if (threadIdx.x < 3 * 64) {
+      const int qd = threadIdx.x / 64, cc = 4 * (threadIdx.x % 64);
       if (c0 + cc < D) {
-        const float t = s_part[0][qd][cc] + s_part[1][qd][cc] + s_part[2][qd][cc] + s_part[3][qd][cc];
-        part[((int64_t)blockIdx.x * 3 + qd) * D + c0 + cc] = t;
+        u32x4 t;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          t[j] = __float_as_uint(s_part[0][qd][cc + j] + s_part[1][qd][cc + j] + s_part[2][qd][cc + j] +
+                                 s_part[3][qd][cc + j]);
+        __builtin_amdgcn_raw_buffer_store_b128(t, rs, 4 * (int)(((int64_t)blockIdx.x * 3 + qd) * D + c0 + cc), 0,
+                                               kSC1);
       }
     }
     __syncthreads();
+  }
+  // ---- column sums: two ticket levels ----
+  const int nb = gridDim.x, QD = 3 * (int)D;
+  const int grp = blockIdx.x / kGroupBlocks, ngrp = (nb + kGroupBlocks - 1) / kGroupBlocks;
+  const int b0 = grp * kGroupBlocks, gsz = min(kGroupBlocks, nb - b0);
+  int* flag = reinterpret_cast<int*>(&s_part[0][0][0]);
+  if (!last_arrival(counters + grp, gsz, flag)) return;
+  const int part2 = nb * QD;  // second-level partials follow the block partials (float index)
+  for (int i = 4 * threadIdx.x; i < QD; i += 4 * blockDim.x)
+    __builtin_amdgcn_raw_buffer_store_b128(ordered_sum4(rs, b0 * QD + i, QD, gsz), rs, 4 * (part2 + grp * QD + i), 0,
+                                           kSC1);
+  if (!last_arrival(counters + ngrp, ngrp, flag)) return;
+  for (int i = 4 * threadIdx.x; i < QD; i += 4 * blockDim.x) {
+    const u32x4 t = ordered_sum4(rs, part2 + i, QD, ngrp);
+    *reinterpret_cast<float4*>(sums + i) =
+        make_float4(__uint_as_float(t[0]), __uint_as_float(t[1]), __uint_as_float(t[2]), __uint_as_float(t[3]));
   }
 }
 
@@ -318,24 +388,45 @@ void launch_ln_fwd(const float* x, const void* y, const float* bias, const uint8
                    const float* w, const float* b, float eps, int64_t N, int64_t D, float* h, void* out, float* mean,
                    float* rstd, hipStream_t st) {
   const unsigned grid = (unsigned)cdiv(N, kWaves);
-  residual_ln_fwd_kernel<TY, TO><<<grid, 256, 0, st>>>(x, (const TY*)y, bias, rmask, p, seed, w, b, eps, N, D, h,
-                                                       (TO*)out, mean, rstd);
+#define LN_FWD(KC)                                                                                                \
+  residual_ln_fwd_kernel<TY, TO, KC><<<grid, 256, 0, st>>>(x, (const TY*)y, bias, rmask, p, seed, w, b, eps, N, D, h, \
+                                                           (TO*)out, mean, rstd)
+  switch (cdiv(D, 256)) {
+    case 1: LN_FWD(1); break;
+    case 2: LN_FWD(2); break;
+    case 3: LN_FWD(3); break;
+    default: LN_FWD(4); break;
+  }
+#undef LN_FWD
 }
 
 template <typename TY, typename TO>
 void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const float* mean, const float* rstd,
                    const float* w, const uint8_t* rmask, float p, const uint64_t* seed, int64_t N, int64_t D, float* dx,
-                   void* dy, float* part, hipStream_t st) {
+                   void* dy, float* part, float* sums, int32_t* counters, hipStream_t st) {
   const unsigned grid = (unsigned)cdiv(N, kWaves * kBwdRowsPerWave);
-  residual_ln_bwd_kernel<TY, TO><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, seed, N,
-                                                       D, dx, (TY*)dy, part);
+#define LN_BWD(KC)                                                                                              \
+  residual_ln_bwd_kernel<TY, TO, KC><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, seed, \
+                                                           N, D, dx, (TY*)dy, part, sums, counters)
+  switch (cdiv(D, 256)) {
+    case 1: LN_BWD(1); break;
+    case 2: LN_BWD(2); break;
+    case 3: LN_BWD(3); break;
+    default: LN_BWD(4); break;
+  }
+#undef LN_BWD
 }
 
 }  // namespace
 
 extern "C" {
 
-int64_t esgpt_residual_ln_partials(int64_t N) { return cdiv(N, kWaves * kBwdRowsPerWave); }
+int64_t esgpt_residual_ln_partials(int64_t N) {
+  const int64_t nb = cdiv(N, kWaves * kBwdRowsPerWave);
+  return nb + cdiv(nb, kGroupBlocks);
+}
+
+int64_t esgpt_residual_ln_counters(int64_t N) { return cdiv(cdiv(N, kWaves * kBwdRowsPerWave), kGroupBlocks) + 1; }
 
 int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
                           float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
@@ -361,22 +452,22 @@ int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const floa
 int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, const float* h, const float* mean,
                           const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
                           const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
-                          float* sums, void* stream) {
-  ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && sums && D > 0 && D % 4 == 0 && D <= 256 * kMaxChunks);
+                          float* sums, int32_t* counters, void* stream) {
+  ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && sums && counters && D > 0 && D % 4 == 0 &&
+                D <= 256 * kMaxChunks);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
-  if (N == 0) return ESGPT_OK;
+  ESGPT_REQUIRE(esgpt_residual_ln_partials(N) * 3 * D * 4 < (1ll << 31) && ((uintptr_t)sums % 16) == 0);
   hipStream_t st = as_stream(stream);
+  if (N == 0) return zero_async(sums, sizeof(float) * 3 * D, st) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
   const bool yb = y_dtype == ESGPT_BF16, ob = out_dtype == ESGPT_BF16;
   if (!yb && !ob) launch_ln_bwd<float, float>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx,
-                                             dy, part, st);
+                                             dy, part, sums, counters, st);
   else if (!yb && ob) launch_ln_bwd<float, bf16>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D,
-                                                dx, dy, part, st);
+                                                dx, dy, part, sums, counters, st);
   else if (yb && !ob) launch_ln_bwd<bf16, float>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D,
-                                                dx, dy, part, st);
+                                                dx, dy, part, sums, counters, st);
   else launch_ln_bwd<bf16, bf16>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx, dy, part,
-                                 st);
-  const int64_t nb = esgpt_residual_ln_partials(N);
-  colsum_kernel<<<(unsigned)cdiv(3 * D, 64), 1024, 0, st>>>(part, nb, 3 * D, sums);
+                                 sums, counters, st);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

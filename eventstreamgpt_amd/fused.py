@@ -71,7 +71,7 @@ class ResidualLNFn(torch.autograd.Function):
             st = lib.esgpt_residual_ln_bwd(L.ptr(dh_in), dout.data_ptr(), L.dtype_code(out_dtype), h.data_ptr(),
                                            mean.data_ptr(), rstd.data_ptr(), ln_w.data_ptr(), L.ptr(row_mask),
                                            p, L.ptr(seed), N, D, L.ptr(dx), L.ptr(dy), L.dtype_code(y_dtype),
-                                           part.data_ptr(), sums.data_ptr(), L.stream())
+                                           part.data_ptr(), sums.data_ptr(), tickets(dev).data_ptr(), L.stream())
         L.check(st, "residual_ln_bwd")
         return dx, dy, (sums[2] if has_bias else None), sums[0], sums[1], None, None, None, None
 
