@@ -596,11 +596,13 @@ __global__ __launch_bounds__(256) void bag_subject_sum_kernel(esgpt_batch bt, in
   }
 }
 
-// One wave per chunk of kChunk sorted entries. Lanes 0..n-1 load the chunk's entries (coalesced); the wave then
-// walks them in groups of kGroup with the group's gathered gradient rows in flight together (the entry fields are
-// wave-uniform via readlane). Rows fully inside the chunk are stored; a row that continues into a neighbouring
-// chunk (at most the first and the last run) is added with f32 atomics. dtable is zeroed beforehand.
-constexpr int kChunk = 32;
+// One wave per chunk of kChunk sorted entries. Lane l loads entries l and 64 + l of the chunk (coalesced); the wave
+// then walks them in groups of kGroup with the group's gathered gradient rows in flight together (the entry fields
+// are wave-uniform via readlane). Rows fully inside the chunk are stored; a row that continues into a neighbouring
+// chunk (at most the first and the last run) is added with f32 atomics — long chunks keep the number of atomic
+// adds per address low for the very frequent rows (a univariate measurement's row gets ~20k entries per batch).
+// dtable is zeroed beforehand.
+constexpr int kChunk = 128;
 constexpr int kGroup = 8;
 
 __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
@@ -624,13 +626,17 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
   const int64_t n_ent = rowptr[V];
   if (lo >= n_ent) return;
   const int n = (int)min<int64_t>(kChunk, n_ent - lo);
-  int32_t my_v = -1;
-  int64_t my_s = 0;
-  float my_w = 0.f;
-  if (lane < n) {
-    my_v = ent_v[lo + lane];
-    my_s = ent_src[lo + lane];
-    my_w = ent_w[lo + lane];
+  int32_t my_v[2] = {-1, -1};
+  int64_t my_s[2] = {0, 0};
+  float my_w[2] = {0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int p = 64 * u + lane;
+    if (p < n) {
+      my_v[u] = ent_v[lo + p];
+      my_s[u] = ent_src[lo + p];
+      my_w[u] = ent_w[lo + p];
+    }
   }
   // the chunk's first / last run continues into the previous / next chunk when those entries share its row
   const int32_t prev_v = lo > 0 ? ent_v[lo - 1] : -1;
@@ -641,7 +647,7 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
     float acc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-    int32_t cur = __builtin_amdgcn_readlane(my_v, 0);
+    int32_t cur = __builtin_amdgcn_readlane(my_v[0], 0);
     bool head = true;  // the current run starts at the chunk's first entry
     auto flush = [&](bool tail) {
       const bool shared = (head && prev_v == cur) || (tail && next_v == cur);
@@ -656,11 +662,16 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
       }
     };
     for (int p0 = 0; p0 < n; p0 += kGroup) {
+      // the group's entries live in register half u = p0 / 64 (groups never straddle it): uniform selects
+      const bool up = p0 >= 64;
+      const int32_t gv = up ? my_v[1] : my_v[0];
+      const int64_t gs = up ? my_s[1] : my_s[0];
+      const float gw = up ? my_w[1] : my_w[0];
       float x[kGroup][VEC];
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) {
         const int p = min(p0 + j, n - 1);
-        const int64_t s = readlane64(my_s, p);
+        const int64_t s = readlane64(gs, p & 63);
         const float* row = s >= 0 ? dsrc + s * ld : sub + (-1 - s) * D;
         if (VEC == 4) {
           float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -678,13 +689,13 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
       for (int j = 0; j < kGroup; ++j) {
         const int p = p0 + j;
         if (p < n) {
-          const int32_t v = __builtin_amdgcn_readlane(my_v, p);
+          const int32_t v = __builtin_amdgcn_readlane(gv, p & 63);
           if (v != cur) {
             flush(false);
             cur = v;
             head = false;
           }
-          const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), p));
+          const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gw), p & 63));
 #pragma unroll
           for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, x[j][k], acc[k]);
         }

@@ -41,32 +41,10 @@ struct Terms {
   int n;
 };
 
-// Per-event target entries, staged per wave.
-struct EvEntries {
-  int64_t idx[kMaxM];
-  int64_t meas[kMaxM];
-  float val[kMaxM];
-  uint8_t vm[kMaxM];
-};
-
-__device__ __forceinline__ bool term_mask(const esgpt_loss_term& T, const EvEntries& E, int M, bool ev) {
-  if (!ev) return false;
-  switch (T.kind) {
-    case ESGPT_TERM_SINGLE: {
-      for (int m = 0; m < M; ++m)
-        if (E.meas[m] == T.meas_idx) return true;
-      return false;
-    }
-    case ESGPT_TERM_MULTI:
-      return true;
-    case ESGPT_TERM_MVREG:
-    case ESGPT_TERM_UVREG: {
-      for (int m = 0; m < M; ++m)
-        if (E.meas[m] == T.meas_idx && E.vm[m]) return true;
-      return false;
-    }
-  }
-  return false;
+__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)x, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -114,7 +92,6 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
                                                     float* __restrict__ dbias, const int32_t* __restrict__ counts,
                                                     float* __restrict__ contrib, int64_t n_rows,
                                                     int32_t* __restrict__ err) {
-  __shared__ EvEntries s_ev[kWaves];
   __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
@@ -122,14 +99,24 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
   const int64_t B = bt.B, L = bt.L, M = bt.M;
 
   // subjects-with-events per term (the outer safe_weighted_avg of weighted_loss); TTE averages over all B.
-  if (threadIdx.x <= NT) {
-    int n = 0;
-    if (threadIdx.x < NT) {
-      for (int64_t b = 0; b < B; ++b) n += counts[b * (ESGPT_MAX_TERMS + 1) + threadIdx.x] > 0 ? 1 : 0;
-    } else {
-      n = (int)B;
+  // Wave 0: lane = subject, one ballot per term (all terms' count loads in flight together).
+  if (wave == 0) {
+    int nsub[ESGPT_MAX_TERMS];
+#pragma unroll
+    for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] = 0;
+    for (int64_t b0 = 0; b0 < B; b0 += 64) {
+      const int64_t b = b0 + lane;
+      int c[ESGPT_MAX_TERMS];
+#pragma unroll
+      for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
+        c[t] = (t < NT && b < B) ? counts[b * (ESGPT_MAX_TERMS + 1) + t] : 0;
+#pragma unroll
+      for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] += __popcll(__ballot(c[t] > 0));
     }
-    s_nsub_inv[threadIdx.x] = n > 0 ? 1.f / (float)n : 0.f;
+#pragma unroll
+    for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
+      if (lane == t && t < NT) s_nsub_inv[t] = nsub[t] > 0 ? 1.f / (float)nsub[t] : 0.f;
+    if (lane == 0) s_nsub_inv[NT] = B > 0 ? 1.f / (float)B : 0.f;
   }
 
   const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
@@ -141,17 +128,21 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
   const bool has_content = active && p < L;
   const bool ev = has_content && bt.event_mask[b * L + p] != 0;
 
-  EvEntries& E = s_ev[wave];
+  // the event's M entries in registers, lane m = entry m (per-term scans are ballots / readlanes, not LDS loops)
+  int64_t e_idx = 0, e_meas = INT64_MIN;
+  float e_val = 0.f;
+  bool e_vm = false;
   if (has_content && lane < M) {
     const int64_t off = (b * L + p) * M + lane;
-    E.idx[lane] = bt.dyn_idx[off];
-    E.meas[lane] = bt.dyn_meas[off];
-    E.val[lane] = bt.dyn_vals[off];
-    E.vm[lane] = bt.dyn_vmask[off];
+    e_idx = bt.dyn_idx[off];
+    e_meas = bt.dyn_meas[off];
+    e_val = bt.dyn_vals[off];
+    e_vm = bt.dyn_vmask[off] != 0;
   }
-  __syncthreads();
+  __syncthreads();  // s_nsub_inv
 
-  const int32_t* cnt_b = counts + b * (ESGPT_MAX_TERMS + 1);
+  // this subject's per-term counts: lane t holds term t's (one load per lane instead of one per term)
+  const int32_t my_cnt = lane <= NT ? counts[b * (ESGPT_MAX_TERMS + 1) + lane] : 0;
   float* my_contrib = contrib + w;  // contrib[t * n_rows + w]
 
   // ---------------- content terms ----------------
@@ -175,8 +166,11 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
         zrow = zc + row * ldc;
         gT = dzc + row * ldc;
       }
-      const bool mk = term_mask(tm, E, (int)M, ev);
-      const int32_t cnt = cnt_b[t];
+      const bool match = e_meas == tm.meas_idx;             // this lane's entry belongs to the term
+      const uint64_t mm = __ballot(match), mv = __ballot(match && e_vm);
+      const bool mk = ev && (tm.kind == ESGPT_TERM_MULTI ||
+                             (tm.kind == ESGPT_TERM_SINGLE ? mm != 0 : mv != 0));  // term_mask, restated
+      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
       const float scale = (mk && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
       // Gradient columns: with disjoint term columns (checked on the host) every column of a row has exactly one
       // writer, so the zero-filled buffer is stored to without a read; otherwise read-modify-write. The bias row
@@ -190,12 +184,8 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
       if (tm.kind == ESGPT_TERM_SINGLE) {
         const int n = tm.vocab_end - tm.vocab_start;
         int64_t lab = 0;
-        bool has = false;
-        for (int m = 0; m < M; ++m)
-          if (E.meas[m] == tm.meas_idx) {
-            lab += E.idx[m];
-            has = true;
-          }
+        const bool has = mm != 0;
+        for (uint64_t bits = mm; bits; bits &= bits - 1) lab += readlane64(e_idx, __builtin_ctzll(bits));
         lab = has ? lab - tm.vocab_start : 0;
         if (mk && (lab < 0 || lab >= n)) {
           set_err(err, FLAG_BAD_LABEL);
@@ -223,16 +213,36 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
         const int n = tm.vocab_end - tm.vocab_start;
         // lane m < M holds entry m's label within this term (-1: another measurement); labels are broadcast
         // with readlane (wave-uniform m) instead of re-reading the staged entries per column
-        const int my_lab = (lane < M && E.meas[lane] == tm.meas_idx) ? (int)(E.idx[lane] - tm.vocab_start) : -1;
+        const int my_lab = match ? (int)(e_idx - tm.vocab_start) : -1;
         float acc = 0.f;
-        for (int j0 = 0; j0 < n; j0 += 64) {
-          const int j = j0 + lane;
-          bool y = false;
-          for (int m = 0; m < M; ++m) y |= __builtin_amdgcn_readlane(my_lab, m) == j;
-          if (j < n) {
-            const float x = to_f32(zrow[tm.col + j]);
-            acc += bce_logits(x, y ? 1.f : 0.f);
-            if (scale != 0.f) put(tm.col + j, scale / (float)n * (sigmoidf_(x) - (y ? 1.f : 0.f)));
+        // passes of kPass column groups: the pass's logits are loaded before any gradient is stored, so the
+        // loads overlap instead of each waiting behind the previous group's store
+        constexpr int kPass = 16;
+        for (int j1 = 0; j1 < n; j1 += 64 * kPass) {
+          float xs[kPass];
+#pragma unroll
+          for (int it = 0; it < kPass; ++it) {
+            const int j = j1 + 64 * it + lane;
+            xs[it] = j < n ? to_f32(zrow[tm.col + j]) : 0.f;
+          }
+#pragma unroll
+          for (int it = 0; it < kPass; ++it) {
+            const int j = j1 + 64 * it + lane;
+            if (j1 + 64 * it >= n) break;  // wave-uniform
+            bool y = false;
+            for (int m = 0; m < M; ++m) y |= __builtin_amdgcn_readlane(my_lab, m) == j;
+            if (j < n) {
+              // BCE-with-logits and its gradient from ONE exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32):
+              // e = exp(-|x|), loss = max(x, 0) - x·y + log(1 + e), sigmoid(x) = x >= 0 ? 1/(1+e) : e/(1+e)
+              const float x = xs[it], yf = y ? 1.f : 0.f;
+              const float e = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+              const float ope = 1.f + e;
+              acc += fmaxf(x, 0.f) - x * yf + __builtin_amdgcn_logf(ope) * 0.6931471805599453f;
+              if (scale != 0.f) {
+                const float inv = __builtin_amdgcn_rcpf(ope);
+                put(tm.col + j, scale / (float)n * ((x >= 0.f ? inv : e * inv) - yf));
+              }
+            }
           }
         }
         ell = wave_sum(acc) / (float)n;
@@ -242,10 +252,10 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
         bool sel = false;
         int64_t j = 0;
         float nll = 0.f, gmu = 0.f, grho = 0.f;
-        if (lane < M) {
-          sel = E.meas[lane] == tm.meas_idx && E.vm[lane];
+        {
+          sel = match && e_vm;
           if (sel) {
-            j = E.idx[lane] - tm.vocab_start;
+            j = e_idx - tm.vocab_start;
             if (j < 0 || j >= n_targets) {
               set_err(err, FLAG_BAD_LABEL);
               j = 0;
@@ -253,24 +263,26 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
             const float mu = to_f32(zrow[tm.col + 2 * j]);
             const float rho = to_f32(zrow[tm.col + 2 * j + 1]);
             const float sd = elu1(rho);
-            const float x = E.val[lane];
+            const float x = e_val;
             const float zz = (x - mu) / sd;
             nll = 0.5f * zz * zz + logf(sd) + kHalfLog2Pi;
             gmu = -(x - mu) / (sd * sd);
             grho = (1.f / sd - (x - mu) * (x - mu) / (sd * sd * sd)) * delu(rho);
           }
         }
-        const float nsel = wave_sum(sel ? 1.f : 0.f);
+        const float nsel = (float)__popcll(mv);
         ell = nsel > 0.f ? wave_sum(nll) / nsel : 0.f;
         if (scale != 0.f && nsel > 0.f) {
           const float s2 = scale / nsel;
           // combine duplicate targets: the first lane of each target sums its group, then writes once
           float sm = 0.f, sr = 0.f;
           bool first = sel;
-          for (int m = 0; m < M; ++m) {
-            const bool sm_sel = __shfl(sel ? 1 : 0, m, 64) != 0;
-            const int64_t jm = __shfl(j, m, 64);
-            const float gm = __shfl(gmu, m, 64), gr = __shfl(grho, m, 64);
+          for (uint64_t bits = mv; bits; bits &= bits - 1) {  // the selected entries, in lane order
+            const int m = __builtin_ctzll(bits);
+            const bool sm_sel = true;
+            const int64_t jm = readlane64(j, m);
+            const float gm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gmu), m));
+            const float gr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(grho), m));
             if (sel && sm_sel && jm == j) {
               sm += gm;
               sr += gr;
@@ -283,17 +295,10 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
           }
         }
       } else if (tm.kind == ESGPT_TERM_UVREG) {
-        bool has_meas = false, has_val = false;
+        const bool has_meas = mm != 0, has_val = mv != 0;
         float x = 0.f;
-        for (int m = 0; m < M; ++m) {
-          if (E.meas[m] == tm.meas_idx) {
-            has_meas = true;
-            if (E.vm[m]) {
-              has_val = true;
-              x += E.val[m];
-            }
-          }
-        }
+        for (uint64_t bits = mv; bits; bits &= bits - 1)
+          x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e_val), __builtin_ctzll(bits)));
         if (!has_val) x = 0.f;
         const float mu = to_f32(zrow[tm.col]);
         const float rho = to_f32(zrow[tm.col + 1]);
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
     const float x = obs ? bt.time_delta[e] : 1.f;
     const T* z = zt + e * ldt + tte.col;
     T* gz = dzt + e * ldt + tte.col;
-    const int32_t cnt = cnt_b[NT];
+    const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
     const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;  // d(-LL)/d ll
     float ll = 0.f;
     if (tte.kind == ESGPT_TTE_EXP) {
