@@ -2,12 +2,23 @@
 (C2: CI-PPT, 6 layers, d=256, L=256, global attention, synthetic EHR-shaped batches, one MI355X per rank).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-graph] [--no-cpu-baseline]
+                    [--roofline-only]
 
 A step = forward + backward + (RCCL gradient all-reduce) + AdamW + LR-schedule step on one batch of B=32
 subjects per GPU (weak scaling). Inputs are resident in HBM before the timed region. Rank 0 prints ONE JSON line.
-Also reported: the roofline of the dominant hot-path kernels (HIP events around each launch, averaged over an
-instrumented pass of the same steps) and the CPU baseline (the f32 oracle port timed on this host's cores on a
-bounded sample of the same workload).
+
+Also reported (rank 0):
+* ``roofline``: the attention forward kernel on the step's own shapes (MFMA-bound, 4·H·hd·T
+  algorithmic FLOPs per layer launch, T = allowed (query, key) pairs of the batch). Its launch is captured R times
+  into a HIP graph and replayed between HIP events on the capturing stream (back-to-back launches as in the step's
+  own graph); ``traffic`` = HBM bytes per launch from the committed rocprofv3 PMC summary
+  (profiles/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), when present.
+* ``roofline_aux``: the same measurement for the attention backward (8·H·hd·T), the projection GEMMs (c_fc forward
+  with its bias + GELU epilogue: 2·T·D·F; c_fc's grouped backward: 4·T·D·F), the JOINT input layer (HBM bytes,
+  §8d) and the attention forward at a long-sequence shape (the kernel's MFMA efficiency beyond C2's latency-bound
+  size).
+* ``cpu_baseline``: the f32 oracle port timed on this host's cores on a bounded sample of the same workload.
+``--roofline-only`` runs just the roofline launches (the command the PMC passes profile).
 """
 from __future__ import annotations
 
@@ -23,7 +34,6 @@ import torch.distributed as dist
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from eventstreamgpt_amd import kernels as K  # noqa: E402
 from eventstreamgpt_amd.synthetic import CONFIGS  # noqa: E402
 from eventstreamgpt_amd.train import TrainStep, init_distributed  # noqa: E402
 from eventstreamgpt_amd.transformer.config import OptimizationConfig  # noqa: E402
@@ -55,6 +65,146 @@ def embed_fwd_bytes(batch, cfg) -> float:
     S = batch.static_indices.shape[1]
     n_ev = float(em.sum())
     return nnz * D * 4 + B * L * M * 21 + B * L * D * 4 + n_ev * S * D * 4 + B * L * 5
+
+
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+
+
+def graph_time_ms(fn, reps: int = 20, iters: int = 5) -> float:
+    """Average device time of one ``fn()`` launch: ``reps`` launches captured into one HIP graph, the graph replayed
+    ``iters`` times between HIP events on the current (replaying) stream."""
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / (reps * iters)
+
+
+def _attention_launchers(B, Lq, D, H, em, p, dev):
+    """esgpt_attn_fwd / esgpt_attn_bwd launches on preallocated packed-qkv buffers (the step's layout)."""
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.kernels import tickets
+
+    lib = L.load()
+    hd = D // H
+    g = torch.Generator(device=dev).manual_seed(0)
+    bufs = {"qkv": (0.5 * torch.randn(B, Lq, 3 * D, device=dev, generator=g)).bfloat16(),
+            "o": torch.empty(B, Lq, D, device=dev, dtype=torch.bfloat16),
+            "lse": torch.empty(B, H, Lq, device=dev),
+            "do": torch.randn(B, Lq, D, device=dev, generator=g).bfloat16(),
+            "seed": torch.tensor([12345], dtype=torch.int64, device=dev),
+            "em": em.to(torch.bool).contiguous()}
+    bufs["dqkv"] = torch.empty_like(bufs["qkv"])
+    nbytes = lib.esgpt_attn_bwd_workspace(B, H, Lq, Lq, hd)
+    bufs["ws"] = torch.empty(max(1, nbytes), dtype=torch.uint8, device=dev)
+    base, dbase, m, es = bufs["qkv"].data_ptr(), bufs["dqkv"].data_ptr(), bufs["em"].data_ptr(), 2
+    cnt = tickets(torch.device(dev))
+
+    def fwd():
+        L.check(lib.esgpt_attn_fwd(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
+                                   bufs["lse"].data_ptr(), m, m, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
+                                   L.BF16, L.stream()), "attn_fwd")
+
+    def bwd():
+        L.check(lib.esgpt_attn_bwd(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
+                                   bufs["do"].data_ptr(), D, bufs["lse"].data_ptr(), m, m, dbase, dbase + D * es,
+                                   dbase + 2 * D * es, 3 * D, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
+                                   L.BF16, bufs["ws"].data_ptr(), nbytes, L.stream()), "attn_bwd")
+
+    fwd()
+    return fwd, bwd, bufs, cnt
+
+
+def _gemm_launchers(T, D, F, dev):
+    """c_fc on the step's shapes: forward with the bias + GELU epilogue, and its grouped backward."""
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.kernels import tickets
+
+    lib = L.load()
+    g = torch.Generator(device=dev).manual_seed(1)
+    bufs = {"x": torch.randn(T, D, device=dev, generator=g).bfloat16(),
+            "w": (0.05 * torch.randn(F, D, device=dev, generator=g)).bfloat16(),
+            "b": torch.zeros(F, device=dev), "pre": torch.empty(T, F, device=dev, dtype=torch.bfloat16),
+            "y": torch.empty(T, F, device=dev, dtype=torch.bfloat16),
+            "dy": torch.randn(T, F, device=dev, generator=g).bfloat16(),
+            "dx": torch.empty(T, D, device=dev, dtype=torch.bfloat16),
+            "dw": torch.empty(F, D, device=dev), "db": torch.empty(F, device=dev)}
+    nb = lib.esgpt_linear_bwd_workspace(T, D, F, 1)
+    bufs["ws"] = torch.empty(max(1, nb), dtype=torch.uint8, device=dev)
+    cnt = tickets(torch.device(dev))
+    P = {k: v.data_ptr() for k, v in bufs.items()}
+
+    def fwd():
+        L.check(lib.esgpt_linear_fwd(P["x"], D, P["w"], T, D, F, P["b"], 0, P["pre"], P["y"], F, L.stream()),
+                "linear_fwd")
+
+    def bwd():
+        L.check(lib.esgpt_linear_bwd(P["dy"], F, P["x"], D, P["w"], T, D, F, None, -1, None, 0, P["dx"], D, P["dw"],
+                                     P["db"], P["ws"], nb, cnt.data_ptr(), L.stream()), "linear_bwd")
+
+    return fwd, bwd, bufs
+
+
+def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float) -> tuple[dict, list]:
+    """(roofline, roofline_aux): algorithmic work per launch / graph-replayed launch time, per kernel."""
+    traffic = {}
+    if os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            traffic = json.load(f).get("bytes_per_launch", {})
+    B, Lq = batch.event_mask.shape
+    D, H, F = cfg.hidden_size, cfg.num_attention_heads, cfg.intermediate_size
+    hd = D // H
+    T_pairs = attention_flops_fwd(batch, cfg) / (4.0 * H * hd)
+    entries = []
+
+    def add(name, kernel, bound, work, fn, extra=None):
+        ms = graph_time_ms(fn)
+        if bound == "mfma":
+            ach, peak, unit, wk = work / (ms * 1e-3) / 1e12, peak_tf, "TFLOP/s", "algorithmic_flops_per_launch"
+        else:
+            ach, peak, unit, wk = work / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", "algorithmic_bytes_per_launch"
+        e = {"kernel": name, "symbol": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak,
+             "unit": unit, "frac": round(ach / peak, 5), "traffic": traffic.get(kernel), "avg_ms": round(ms, 5),
+             wk: work, "timing": "HIP graph of 20 launches, events on the replaying stream"}
+        e.update(extra or {})
+        entries.append(e)
+
+    drop = "true" if p_attn > 0 else "false"
+    fa, ba, _keep_a, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev)
+    add("attn_fwd", f"attn_fwd_mfma_kernel<{hd}, {drop}>", "mfma", 4.0 * H * hd * T_pairs, fa,
+        {"shape": f"C2 layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"})
+    add("attn_bwd", f"attn_bwd_kernel<{hd}, {drop}>", "mfma", 8.0 * H * hd * T_pairs, ba,
+        {"shape": f"C2 layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"})
+    gf, gb, _keep_g = _gemm_launchers(B * Lq, D, F, dev)
+    add("gemm_fc_fwd", "gemm_kernel<true, true>", "mfma", 2.0 * B * Lq * D * F, gf,
+        {"shape": f"c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"})
+    add("gemm_fc_bwd", "gemm_bwd_pair_kernel", "mfma", 4.0 * B * Lq * D * F, gb,
+        {"shape": f"c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"})
+    emb = model.encoder.input_layer.data_embedding_layer
+    tl = model.encoder.input_layer.time_embedding_layer
+
+    def emb_fwd():
+        with torch.no_grad():
+            emb.embed(batch, time_layer=tl)
+
+    add("embed_joint_fwd", "embed_joint_fwd_kernel<4, 1>", "hbm", embed_fwd_bytes(batch, cfg), emb_fwd)
+    # long-sequence attention: the forward kernel's MFMA efficiency once the grid fills the chip
+    Bl, Ll, Hl = 4, 4096, 8
+    fl, _, _keep_l, _ = _attention_launchers(Bl, Ll, Hl * hd, Hl, torch.ones(Bl, Ll, dtype=torch.bool, device=dev),
+                                             0.0, dev)
+    add("attn_fwd_long", f"attn_fwd_mfma_kernel<{hd}, false>", "mfma", 4.0 * Hl * hd * Bl * Ll * (Ll + 1) / 2, fl,
+        {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"})
+    return entries[0], entries[1:]
 
 
 def cpu_baseline(bc, seconds: float = 12.0) -> dict:
@@ -99,6 +249,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--roofline-only", action="store_true")
     args = ap.parse_args()
 
     rank, world, local = init_distributed()
@@ -121,6 +272,10 @@ def main():
     ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph)
 
     n_batches = 4
+    if args.roofline_only:  # the launches the PMC passes profile (no training steps)
+        roofline, aux = roofline_report(model, cfg, bc.batch(0, device=dev), dev, 0.1, PEAK_BF16_TFLOPS)
+        print(json.dumps({"roofline": roofline, "roofline_aux": aux}))
+        return
     batches = [bc.batch(100 * rank + i, device=dev) for i in range(n_batches)]
     events = [float(b.event_mask.sum()) for b in batches]
 
@@ -149,34 +304,9 @@ def main():
         local_events = float(e.item())
     value = local_events / elapsed
 
-    # ---- instrumented pass: per-launch HIP events around the hot-path kernels (eager) ----
-    K.TIMING["enabled"] = True
-    K.TIMING["events"].clear()
-    ts_eager_graph, ts.use_graph = ts.use_graph, False
-    n_inst = min(args.steps, 5)
-    for i in range(n_inst):
-        ts.step(batches[i % n_batches])
-    summ = K.timing_summary()
-    K.TIMING["enabled"] = False
-    ts.use_graph = ts_eager_graph
-
-    b0 = batches[0]
-    fl = attention_flops_fwd(b0, cfg)
-    attn_ms = summ.get("attn_fwd", (0, float("nan")))[1]
-    attn_tf = fl / (attn_ms * 1e-3) / 1e12
+    # ---- roofline: graph-replayed launches of the hot kernels on the step's shapes ----
     peak_tf = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
-    eb = embed_fwd_bytes(b0, cfg)
-    emb_ms = summ.get("embed_joint_fwd", (0, float("nan")))[1]
-    emb_gbs = eb / (emb_ms * 1e-3) / 1e9
-    roofline = {"kernel": "attn_fwd", "bound": "mfma", "achieved": round(attn_tf, 3), "peak": peak_tf,
-                "unit": "TFLOP/s", "frac": round(attn_tf / peak_tf, 5), "traffic": None,
-                "avg_ms": round(attn_ms, 5), "algorithmic_flops_per_launch": fl}
-    aux = [{"kernel": "embed_joint_fwd", "bound": "hbm", "achieved": round(emb_gbs, 1), "peak": PEAK_HBM_GBS,
-            "unit": "GB/s", "frac": round(emb_gbs / PEAK_HBM_GBS, 4), "avg_ms": round(emb_ms, 5),
-            "algorithmic_bytes_per_launch": eb}]
-    for k in ("attn_bwd", "embed_joint_bwd", "output_loss"):
-        if k in summ:
-            aux.append({"kernel": k, "avg_ms": round(summ[k][1], 5), "launches": summ[k][0]})
+    roofline, aux = roofline_report(model, cfg, batches[0], dev, 0.1, peak_tf) if rank == 0 else ({}, [])
 
     result = {
         "metric": "train events/sec (node)",
