@@ -250,6 +250,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--roofline-only", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true", help="skip the roofline launches (clean step profiles)")
     args = ap.parse_args()
 
     rank, world, local = init_distributed()
@@ -306,7 +307,9 @@ def main():
 
     # ---- roofline: graph-replayed launches of the hot kernels on the step's shapes ----
     peak_tf = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
-    roofline, aux = roofline_report(model, cfg, batches[0], dev, 0.1, peak_tf) if rank == 0 else ({}, [])
+    roofline, aux = ({}, [])
+    if rank == 0 and not args.no_roofline:
+        roofline, aux = roofline_report(model, cfg, batches[0], dev, 0.1, peak_tf)
 
     result = {
         "metric": "train events/sec (node)",
