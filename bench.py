@@ -119,7 +119,7 @@ def _attention_launchers(B, Lq, D, H, em, p, dev):
         L.check(lib.esgpt_attn_bwd(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
                                    bufs["do"].data_ptr(), D, bufs["lse"].data_ptr(), m, m, dbase, dbase + D * es,
                                    dbase + 2 * D * es, 3 * D, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
-                                   L.BF16, bufs["ws"].data_ptr(), nbytes, L.stream()), "attn_bwd")
+                                   L.BF16, bufs["ws"].data_ptr(), nbytes, cnt.data_ptr(), L.stream()), "attn_bwd")
 
     fwd()
     return fwd, bwd, bufs, cnt

@@ -268,8 +268,9 @@ int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
                         int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
                         const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
                         int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
-                        float* dq32, hipStream_t st);
+                        float* dq32, int32_t* counters, hipStream_t st);
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
+int64_t esgpt_attn_bwd_mfma_counters(int64_t B, int64_t H, int64_t Lk);
 bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o);
 
 static int g_force_generic = -1;
@@ -303,8 +304,11 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                                   dropout_p, seed, st);
 }
 
+int64_t esgpt_attn_bwd_counters(int64_t B, int64_t H, int64_t Lk) { return esgpt_attn_bwd_mfma_counters(B, H, Lk); }
+
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
-  // generic kernels: δ = rowsum(dO∘O) [B*H*Lq]; MFMA kernel: f32 dQ accumulator when Lk > 256 (else nothing)
+  // generic kernels: δ = rowsum(dO∘O) [B*H*Lq]; MFMA kernel: f32 dQ accumulator when Lk > 256, + the dK / dV
+  // exchange slabs of the query-split workgroup pairs
   const size_t a = sizeof(float) * (size_t)(B * H * Lq), b = esgpt_attn_bwd_mfma_workspace(B, H, Lq, Lk, hd);
   return a > b ? a : b;
 }
@@ -313,7 +317,7 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
                    const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
                    int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
-                   int dtype, void* workspace, size_t workspace_bytes, void* stream) {
+                   int dtype, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream) {
   ESGPT_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv && hd > 0 && hd <= 128 && Lq <= Lk);
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
@@ -323,7 +327,8 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
   float* delta = (float*)workspace;
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
-                               ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, (float*)workspace, st);
+                               ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, (float*)workspace, counters,
+                               st);
   if (dtype == ESGPT_F32)
     return launch_bwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
                                      ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);

@@ -123,7 +123,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
     __bf16* __restrict__ dq, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d,
-    float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed) {
+    float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed,
+    int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf) {
   constexpr int QT = Cfg<HD>::QT;
   using IQ = Img<HD>;  // Q, dO, K images: [row][HD]
   using IS = Img<QT>;  // dS image: [key][QT]
@@ -140,7 +141,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   const int bh = blockIdx.y, b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
-  const int kb0 = blockIdx.x * KB;
+  const int kblk = blockIdx.x / nsplit, qsplit = blockIdx.x % nsplit;  // key block; query-tile parity
+  const int kb0 = kblk * KB;
   const int kw0 = kb0 + 32 * wave;  // this wave's first key
   const int key = kw0 + r;
   const bool kvalid = key < Lk && (kmask == nullptr || kmask[(int64_t)b * Lk + key] != 0);
@@ -196,12 +198,12 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
       if (sc8 == 0 && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0)) pl = lse[(int64_t)bh * Lq + qi];
     }
   };
-  int q0 = (qlo / QT) * QT;
+  int q0 = (qlo / QT + qsplit) * QT;  // this workgroup's tiles: every nsplit-th one
   if (q0 <= qhi) prefetch(q0);
   STAMP(1);
   int it = 0;
 
-  for (; q0 <= qhi; q0 += QT, ++it) {
+  for (; q0 <= qhi; q0 += nsplit * QT, ++it) {
     __syncthreads();  // the previous tile's reads of sQ / sD / sS are done
     STAMP(2 + 6 * it);
     if (stager) {
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     }
     __syncthreads();
     STAMP(3 + 6 * it);
-    if (q0 + QT <= qhi) prefetch(q0 + QT);  // in flight during this tile's MFMAs
+    if (q0 + nsplit * QT <= qhi) prefetch(q0 + nsplit * QT);  // in flight during this tile's MFMAs
 
     // ---- per wave: S, dP, dV, dK for its 32 keys over the tile's queries ----
 #pragma unroll
@@ -337,6 +339,61 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   }
 
   STAMP(40);
+  // ---- the key block's two query-parity workgroups hold partial dKᵀ / dVᵀ: exchange and add ----
+  // The first to finish publishes its partial (write-through sc1 stores, drained, then an sc1 flag); the second
+  // polls the flag (relaxed sc1 loads + s_sleep), reads the partial with sc1 loads, adds it in registers and stores
+  // the bf16 result. Two-term f32 sums commute, so the result does not depend on which one finishes first.
+  if (nsplit > 1) {
+    const int64_t id = (int64_t)bh * (gridDim.x / nsplit) + kblk;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    constexpr int kSC1 = 16;  // buffer cache policy: sc1 (write-through stores, L1-bypassing loads)
+    // [dk | dv] f32 slab of this pair, [wave][dt][i/4][lane] x 16 B (coalesced per store / load instruction)
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(xbuf + id * (2 * KB * HD), (short)0, 2 * KB * HD * 4, 0x00020000);
+    int* flag = reinterpret_cast<int*>(smem_raw);
+    __syncthreads();  // every wave is done with the LDS images
+    if (tid == 0) *flag = __hip_atomic_fetch_add(xcnt + 2 * id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool first = *flag == 0;
+    if (first) {
+#pragma unroll
+      for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+          const int e = 4 * (((wave * (HD / 32) + dt) * 4 + i / 4) * 64 + lane);  // float index, 16-B granules
+          const u32x4 k4 = {__float_as_uint(dka[dt][i]), __float_as_uint(dka[dt][i + 1]),
+                            __float_as_uint(dka[dt][i + 2]), __float_as_uint(dka[dt][i + 3])};
+          const u32x4 v4 = {__float_as_uint(dva[dt][i]), __float_as_uint(dva[dt][i + 1]),
+                            __float_as_uint(dva[dt][i + 2]), __float_as_uint(dva[dt][i + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(k4, xr, 4 * e, 0, kSC1);
+          __builtin_amdgcn_raw_buffer_store_b128(v4, xr, 4 * (KB * HD + e), 0, kSC1);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(xcnt + 2 * id + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      while (__hip_atomic_load(xcnt + 2 * id + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        __builtin_amdgcn_s_sleep(2);
+      __hip_atomic_store(xcnt + 2 * id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // leave the pair zeroed
+      __hip_atomic_store(xcnt + 2 * id + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; i += 4) {
+        const int e = 4 * (((wave * (HD / 32) + dt) * 4 + i / 4) * 64 + lane);
+        const u32x4 k4 = __builtin_amdgcn_raw_buffer_load_b128(xr, 4 * e, 0, kSC1);
+        const u32x4 v4 = __builtin_amdgcn_raw_buffer_load_b128(xr, 4 * (KB * HD + e), 0, kSC1);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          dka[dt][i + c] += __uint_as_float(k4[c]);
+          dva[dt][i + c] += __uint_as_float(v4[c]);
+        }
+      }
+  }
   // ---- dK, dV (every key belongs to exactly one workgroup): 16-B row stores ----
   if (key < Lk) {
     __bf16* ko = dk + ((int64_t)b * Lk + key) * ld_d + hh * HD;
@@ -372,7 +429,7 @@ template <int HD>
 int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
            const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask, void* dq,
            void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t window,
-           float drop_p, const uint64_t* seed, float* dq32, hipStream_t st) {
+           float drop_p, const uint64_t* seed, float* dq32, int32_t* counters, hipStream_t st) {
   constexpr int lds = Cfg<HD>::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
@@ -385,18 +442,21 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   }
   const int nkb = (int)cdiv(Lk, KB);
   float* acc = nkb > 1 ? dq32 : nullptr;
+  // two workgroups per key block (even / odd query tiles) when there are at least two query tiles
+  const int nsplit = (counters && Lq > Cfg<HD>::QT) ? 2 : 1;
+  float* xbuf = dq32 + (nkb > 1 ? (size_t)(B * H * Lq * HD) : 0);
   if (acc && zero_async(acc, sizeof(float) * (size_t)(B * H * Lq * HD), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  const dim3 grid((unsigned)nkb, (unsigned)(B * H));
+  const dim3 grid((unsigned)(nkb * nsplit), (unsigned)(B * H));
   if (drop_p > 0.f)
     attn_bwd_kernel<HD, true><<<grid, THREADS, lds, st>>>(
         (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
         ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,
-        (int)window, drop_p, seed);
+        (int)window, drop_p, seed, nsplit, counters, xbuf);
   else
     attn_bwd_kernel<HD, false><<<grid, THREADS, lds, st>>>(
         (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
         ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,
-        (int)window, drop_p, seed);
+        (int)window, drop_p, seed, nsplit, counters, xbuf);
   if (acc) {
     const int64_t n4 = B * H * Lq * HD / 4;
     dq_convert_kernel<HD><<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(acc, (__bf16*)dq, ld_d, tq, (int)H, (int)Lq, n4);
@@ -412,21 +472,25 @@ extern "C" int esgpt_debug_stamps(uint64_t* out) {
 }
 #endif
 
+// f32 dQ accumulator (more than one key block) + the dK / dV exchange slabs of the query-split pairs.
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
-  return Lk > KB ? sizeof(float) * (size_t)(B * H * Lq * hd) : 0;
+  const size_t dq = Lk > KB ? sizeof(float) * (size_t)(B * H * Lq * hd) : 0;
+  return dq + sizeof(float) * (size_t)(B * H * cdiv(Lk, KB)) * 2 * KB * hd;
 }
+
+int64_t esgpt_attn_bwd_mfma_counters(int64_t B, int64_t H, int64_t Lk) { return 2 * B * H * cdiv(Lk, KB); }
 
 int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                         int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
                         const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
                         int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
-                        float* dq32, hipStream_t st) {
+                        float* dq32, int32_t* counters, hipStream_t st) {
   if (hd == 32)
     return launch<32>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                      window, drop_p, seed, dq32, st);
+                      window, drop_p, seed, dq32, counters, st);
   if (hd == 64)
     return launch<64>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                      window, drop_p, seed, dq32, st);
+                      window, drop_p, seed, dq32, counters, st);
   return launch<128>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                     window, drop_p, seed, dq32, st);
+                     window, drop_p, seed, dq32, counters, st);
 }

@@ -343,6 +343,12 @@ def end_dropout_step(device: torch.device) -> None:
         bank["next"] = SEED_BANK_SLOTS
 
 
+def _attn_counters(device, B: int, H: int, Lk: int):
+    """Exchange tickets of the attention backward's query-split workgroup pairs (None: unsplit launch)."""
+    t = tickets(device)
+    return t.data_ptr() if L.load().esgpt_attn_bwd_counters(B, H, Lk) <= t.numel() else None
+
+
 class AttentionFn(torch.autograd.Function):
     """Packed-QKV causal/local attention. qkv: [Bs, T, 3D] (q | k | v), returns o: [Bs, T - skf, D]."""
 
@@ -389,7 +395,7 @@ class AttentionFn(torch.autograd.Function):
                                     do.data_ptr(), D, lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask),
                                     dbase + skf * D3 * es, dbase + D * es, dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd,
                                     window, dropout_p, L.ptr(seed), L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes,
-                                    L.stream())
+                                    _attn_counters(qkv.device, Bs, H, Lk), L.stream())
         L.check(st, "attn_bwd")
         return dqkv, None, None, None, None, None, None
 

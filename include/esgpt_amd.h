@@ -123,12 +123,16 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
                    void* stream);
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
+/* Backward exchange tickets: the MFMA backward runs two workgroups per key block (even / odd query tiles) that add
+ * their partial dK / dV through the workspace; `counters` (esgpt_attn_bwd_counters(B, H, Lk) int32, zeroed once
+ * by the caller, left zeroed; stream-ordered use) pairs them. NULL counters: one workgroup per key block. */
+int64_t esgpt_attn_bwd_counters(int64_t B, int64_t H, int64_t Lk);
 int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                    int64_t ld_o,
                    const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
                    const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
                    int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
-                   int dtype, void* workspace, size_t workspace_bytes, void* stream);
+                   int dtype, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream);
 
 /* ---- Output layer losses -----------------------------------------------------------------------------------
  * GenerativeOutputLayerBase.get_{classification,regression,TTE}_outputs (model_output.py:1311-1721) with

@@ -42,8 +42,10 @@ def test_workspace_queries_without_gpu():
     if not os.path.exists(_lib.LIB_PATH):
         pytest.skip("library not built")
     lib = _lib.load(require_device=False)
-    assert lib.esgpt_attn_bwd_workspace(2, 4, 256, 256, 64) == 4 * 2 * 4 * 256
-    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 64) == 4 * 2 * 4 * 512 * 64
+    # MFMA backward: f32 dQ accumulator beyond one 256-key block + the dK/dV exchange slabs of the query-split pairs
+    assert lib.esgpt_attn_bwd_workspace(2, 4, 256, 256, 64) == 4 * (2 * 4 * 1) * 2 * 256 * 64
+    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 64) == 4 * 2 * 4 * 512 * 64 + 4 * (2 * 4 * 2) * 2 * 256 * 64
+    assert lib.esgpt_attn_bwd_counters(2, 4, 512) == 2 * 2 * 4 * 2
     b = _lib.EsgptBatch()
     b.B, b.L, b.M, b.S = 32, 256, 16, 2
     assert lib.esgpt_embed_bag_bwd_workspace(ctypes.byref(b), 1, 1210, 256) > 32 * 256 * 16 * 16
