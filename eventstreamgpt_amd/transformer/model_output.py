@@ -39,6 +39,16 @@ class TransformerOutputWithPast(ModelOutput):
 
 
 @dataclass
+class StreamClassificationModelOutput(ModelOutput):
+    """Output of the stream classification (fine-tuning) model (``model_output.py:1220-1231``): the loss, the
+    predictions (logits) and the labels."""
+
+    loss: torch.FloatTensor
+    preds: torch.FloatTensor = None
+    labels: torch.LongTensor | torch.FloatTensor = None
+
+
+@dataclass
 class GenerativeSequenceModelLosses(ModelOutput):
     classification: dict[str, torch.FloatTensor] | None = None
     regression: dict[str, torch.FloatTensor] | None = None

@@ -493,6 +493,35 @@ def model_losses(p, cfg, batch, pre="") -> dict:
     return {"loss": loss, "classification": cls, "regression": reg, "tte_ll": tte, "encoded": enc}
 
 
+def stream_classification_loss(p, cfg, batch, labels, pooling: str, binary: bool, pre: str = ""):
+    """``ESTForStreamClassification.forward`` (``fine_tuning_model.py:54-91``): encoder (last dep-graph level for
+    NA), pooling over the sequence (``cls`` / ``last`` / masked ``max`` / masked ``mean``, ``utils.py:61-207``),
+    ``logit_layer`` and BCE-with-logits (binary) or cross-entropy. Returns (loss, logits)."""
+    if str(cfg.structured_event_processing_mode) == "conditionally_independent":
+        enc = ci_encoder(p, cfg, batch, pre + "encoder.")
+    else:
+        enc = na_encoder(p, cfg, batch, pre + "encoder.")[:, :, -1, :]
+    x = enc.transpose(1, 2)  # [B, D, L], the reference's layout for the masked reductions
+    em = batch["event_mask"]
+    if pooling == "cls":
+        pooled = x[:, :, 0]
+    elif pooling == "last":
+        pooled = x[:, :, -1]
+    elif pooling == "max":
+        m = torch.where(em.unsqueeze(-2).expand_as(x), x, torch.full_like(x, -float("inf"))).max(-1)[0]
+        pooled = torch.nan_to_num(m, nan=None, posinf=None, neginf=0.0)
+    elif pooling == "mean":
+        pooled = safe_weighted_avg(x, em.unsqueeze(-2).expand_as(x).float())[0]
+    else:
+        raise ValueError(pooling)
+    logits = _lin(p, pre + "logit_layer", pooled).squeeze(-1)
+    if binary:
+        loss = torch.nn.functional.binary_cross_entropy_with_logits(logits, labels)
+    else:
+        loss = torch.nn.functional.cross_entropy(logits, labels)
+    return loss, logits
+
+
 # --------------------------------------------------------------------------------------------------------------
 # Optimiser: generative_modeling.py:460-485 (AdamW + transformers.get_polynomial_decay_schedule_with_warmup)
 # --------------------------------------------------------------------------------------------------------------
