@@ -96,6 +96,9 @@ SIGNATURES = {
                                 _vp, _vp, _sz, _vp, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
+    "esgpt_collate_shape": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "esgpt_collate": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _int,
+                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _int]),
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),
     "esgpt_output_loss": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
                                  _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),

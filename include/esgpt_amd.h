@@ -259,6 +259,25 @@ int64_t esgpt_adamw_chunk(void);
 int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, float lr, float beta1,
                 float beta2, float eps, float weight_decay, int64_t step, void* stream);
 
+/* ---- Batch producer (host) ----------------------------------------------------------------------------------
+ * PytorchDataset.collate (pytorch_dataset.py:527-701) over flat ragged arrays (the DL_reps parquet columns):
+ * subject b = events ev_start[b] .. +ev_count[b]-1 of time_delta (f64; NaN = padded event), event e = elements
+ * el_off[e] .. el_off[e+1]-1 of idx / meas (int64, null = 0) and vals (f64, NaN = missing), static elements
+ * st_start[b] .. +st_count[b]-1 of st_idx / st_meas (st_count NULL: no static data). HOST pointers; outputs are
+ * caller-allocated host buffers (pinned for an async H2D copy) of the shape esgpt_collate_shape returns:
+ * event_mask u8 [B,L], time_delta f32 [B,L], dyn_idx / dyn_meas int64 [B,L,M], dyn_vals f32 [B,L,M], dyn_vmask u8
+ * [B,L,M], st_idx / st_meas int64 [B,S]. padding_left: sequence padding on the left (generation) instead of the
+ * right. esgpt_collate_shape returns ESGPT_ERR_INVALID_ARG when the batch has no dynamic element (the reference's
+ * ValueError). n_threads host threads split the subjects. */
+int esgpt_collate_shape(int64_t B, const int64_t* ev_start, const int64_t* ev_count, const int64_t* el_off,
+                        const int64_t* st_count, int64_t* L, int64_t* M, int64_t* S);
+int esgpt_collate(int64_t B, const int64_t* ev_start, const int64_t* ev_count, const double* time_delta,
+                  const int64_t* el_off, const int64_t* idx, const int64_t* meas, const double* vals,
+                  const int64_t* st_start, const int64_t* st_count, const int64_t* st_idx, const int64_t* st_meas,
+                  int64_t L, int64_t M, int64_t S, int padding_left, uint8_t* event_mask, float* time_delta_out,
+                  int64_t* dyn_idx, int64_t* dyn_meas, float* dyn_vals, uint8_t* dyn_vmask, int64_t* st_idx_out,
+                  int64_t* st_meas_out, int n_threads);
+
 /* ---- Misc ----------------------------------------------------------------------------------------------- */
 const char* esgpt_version(void);
 int esgpt_device_arch_ok(void); /* 1 if device 0 is gfx950 */
