@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import dataclasses
 import enum
+import itertools
 import math
 from typing import Any
 
@@ -382,6 +383,38 @@ class StructuredTransformerConfig(PretrainedConfig):
                 self.mean_log_inter_event_time_min = mean_log_inter_event_time_min
             if std_log_inter_event_time_min is not None:
                 self.std_log_inter_event_time_min = std_log_inter_event_time_min
+
+    def set_to_dataset(self, dataset):
+        """``set_to_dataset`` (``config.py:839-899``) from an ``eventstreamgpt_amd.data.PytorchDataset``."""
+        self.measurement_configs = dataset.measurement_configs
+        if self.structured_event_processing_mode == StructuredEventProcessingMode.NESTED_ATTENTION:
+            in_dep = {x[0] if isinstance(x, (list, tuple)) and len(x) == 2 else x
+                      for x in itertools.chain.from_iterable(self.measurements_per_dep_graph_level)}
+            gen = set(itertools.chain.from_iterable(
+                dataset.vocabulary_config["measurements_per_generative_mode"].values()))
+            if not gen.issubset(in_dep):
+                raise ValueError(f"Config is attempting to generate something outside the dependency graph:\n"
+                                 f"{gen - in_dep}")
+        self.set_to_vocabulary(dataset.vocabulary_config, dataset.max_seq_len,
+                               dataset.mean_log_inter_event_time_min, dataset.std_log_inter_event_time_min)
+        if dataset.has_task:
+            if len(dataset.tasks) == 1:
+                self.finetuning_task = dataset.tasks[0]
+                match dataset.task_types[self.finetuning_task]:
+                    case "binary_classification" | "multi_class_classification":
+                        self.id2label = {i: v for i, v in enumerate(dataset.task_vocabs[self.finetuning_task])}
+                        self.label2id = {v: i for i, v in self.id2label.items()}
+                        self.num_labels = len(self.id2label)
+                        self.problem_type = "single_label_classification"
+                    case "regression":
+                        self.num_labels = 1
+                        self.problem_type = "regression"
+            elif all(t == "binary_classification" for t in dataset.task_types.values()):
+                self.problem_type = "multi_label_classification"
+                self.num_labels = len(dataset.tasks)
+            elif all(t == "regression" for t in dataset.task_types.values()):
+                self.num_labels = len(dataset.tasks)
+                self.problem_type = "regression"
 
     def __eq__(self, other):
         if not isinstance(other, PretrainedConfig):

@@ -302,3 +302,15 @@ def test_dl_reps_random_windows_and_epochs(tmp_path):
         PytorchDatasetConfig(seq_padding_side="middle")
     with pytest.raises(ValueError):
         PytorchDatasetConfig(train_subset_size=1.5)
+
+
+def test_config_set_to_dataset_from_sample_shard():
+    from eventstreamgpt_amd.transformer.config import StructuredTransformerConfig
+
+    pyd = _sample_dataset(max_seq_len=128)
+    cfg = StructuredTransformerConfig(TTE_generation_layer_type="log_normal_mixture",
+                                      TTE_lognormal_generation_num_components=3)
+    cfg.set_to_dataset(pyd)
+    assert cfg.vocab_size == 45 and cfg.max_seq_len == 128  # vocab 45 (sample vocabulary_config)
+    assert cfg.mean_log_inter_event_time_min == pyd.mean_log_inter_event_time_min
+    assert "eye_color" in cfg.measurement_configs
