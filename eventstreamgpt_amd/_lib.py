@@ -77,6 +77,9 @@ SIGNATURES = {
     "esgpt_attn_bwd_counters": (_i64, [_i64, _i64, _i64]),
     "esgpt_attn_bwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                               _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _int, _vp, _sz, _vp, _vp]),
+    "esgpt_kv_append": (_int, [_vp, _i64, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "esgpt_attn_decode": (_int, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
+                                 _int, _vp]),
     "esgpt_residual_ln_partials": (_i64, [_i64]),
     "esgpt_residual_ln_fwd": (_int, [_vp, _vp, _int, _vp, _vp, _f32, _vp, _vp, _vp, _f32, _i64, _i64, _vp, _vp, _int,
                                      _vp, _vp, _vp]),

@@ -155,6 +155,21 @@ class PytorchBatch:
             stream_labels=None if self.stream_labels is None else {k: v[b] for k, v in self.stream_labels.items()},
         )
 
+    def last_sequence_element_unsqueezed(self) -> "PytorchBatch":
+        """The last event of every subject, keeping a length-1 sequence dimension (``data/types.py:314-316``)."""
+        return self[:, -1:]
+
+    def repeat_batch_elements(self, expand_size: int) -> "PytorchBatch":
+        """Each subject repeated ``expand_size`` times consecutively (``data/types.py:318-460``)."""
+        idx = torch.arange(self.batch_size, device=self.device).repeat_interleave(expand_size)
+        kw = {}
+        for k in _TENSOR_FIELDS:
+            v = getattr(self, k)
+            kw[k] = None if v is None else v.index_select(0, idx)
+        sl = self.stream_labels
+        kw["stream_labels"] = None if sl is None else {k: v.index_select(0, idx) for k, v in sl.items()}
+        return PytorchBatch(**kw)
+
     def to(self, device, non_blocking: bool = False) -> "PytorchBatch":
         """Moves every tensor field to ``device``."""
         kw = {}

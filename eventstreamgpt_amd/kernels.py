@@ -401,6 +401,97 @@ class AttentionFn(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------------------------------------------
+# Generation: KV cache (csrc/decode.hip)
+# ----------------------------------------------------------------------------------------------------------------
+class _KVStore:
+    """One layer's preallocated token-major cache, k / v: [B, cap, D]. ``length`` = rows written so far."""
+
+    __slots__ = ("k", "v", "length", "H")
+
+    def __init__(self, B: int, cap: int, D: int, H: int, dtype, device):
+        self.k = torch.empty(B, cap, D, dtype=dtype, device=device)
+        self.v = torch.empty(B, cap, D, dtype=dtype, device=device)
+        self.length = 0
+        self.H = H
+
+
+class LayerKV(tuple):
+    """``present_key_value`` of one layer: the reference's ``(key, value)`` pair, each [B, H, L, hd]
+    (transformer.py:267), as views of a preallocated cache that the next decode step appends into in place
+    (instead of the reference's per-step ``torch.cat``). A plain ``(key, value)`` tuple is accepted as a past too;
+    it is copied into a fresh cache once."""
+
+    def __new__(cls, store: _KVStore, length: int):
+        B, _, D = store.k.shape
+        H = store.H
+        hd = D // H
+        k = store.k[:, :length].view(B, length, H, hd).permute(0, 2, 1, 3)
+        v = store.v[:, :length].view(B, length, H, hd).permute(0, 2, 1, 3)
+        self = super().__new__(cls, (k, v))
+        self.store = store
+        self.length = length
+        return self
+
+
+def _kv_store_for(layer_past, B: int, D: int, H: int, n_new: int, cap_hint: int, dtype, device):
+    """(store, past_len) with room for ``n_new`` more rows. Appends in place when ``layer_past`` is the newest view
+    of its store (the usual decode loop); otherwise (a branched / foreign / full past) copies into a new store."""
+    if isinstance(layer_past, LayerKV):
+        st = layer_past.store
+        P = layer_past.length
+        if (st.length == P and P + n_new <= st.k.shape[1] and st.k.dtype == dtype and st.k.shape[0] == B
+                and st.H == H and st.k.device == device):
+            return st, P
+    P = 0 if layer_past is None else int(layer_past[0].shape[-2])
+    st = _KVStore(B, max(int(cap_hint), P + n_new), D, H, dtype, device)
+    if P:
+        pk, pv = layer_past[0], layer_past[1]
+        if pk.shape[0] != B or pk.shape[1] * pk.shape[3] != D:
+            raise ValueError(f"layer_past of shape {tuple(pk.shape)} does not match batch {B} / hidden size {D}")
+        st.k[:, :P].copy_(pk.permute(0, 2, 1, 3).reshape(B, P, D))
+        st.v[:, :P].copy_(pv.permute(0, 2, 1, 3).reshape(B, P, D))
+    st.length = P
+    return st, P
+
+
+def cached_attention(qkv: torch.Tensor, layer_past, key_mask: torch.Tensor | None, H: int, window: int,
+                     cap_hint: int):
+    """Attention of the Lq new positions of packed ``qkv`` [B, Lq, 3D] over (past + new) keys, appending the new
+    keys / values to the cache. ``key_mask``: bool [B, past + Lq] (the full event mask) or None. Returns
+    (o [B, Lq, D], LayerKV). Inference only (no autograd through the cache)."""
+    if torch.is_grad_enabled() and qkv.requires_grad:
+        raise NotImplementedError("eventstreamgpt_amd: the KV-cache path is for generation (run under torch.no_grad())")
+    lib = L.load()
+    if qkv.device.type != "cuda":
+        raise L.HipExtensionMissing("eventstreamgpt_amd: KV-cache attention needs a HIP device tensor")
+    qkv = qkv.contiguous()
+    B, Lq, D3 = qkv.shape
+    D = D3 // 3
+    hd = D // H
+    st, P = _kv_store_for(layer_past, B, D, H, Lq, cap_hint, qkv.dtype, qkv.device)
+    Lk = P + Lq
+    cap = st.k.shape[1]
+    code = L.dtype_code(qkv.dtype)
+    with _timed("kv_append"):
+        s = lib.esgpt_kv_append(qkv.data_ptr(), D3, st.k.data_ptr(), st.v.data_ptr(), B, Lq, P, cap, D, code,
+                                L.stream())
+    L.check(s, "kv_append")
+    st.length = Lk
+    km = qm = None
+    if key_mask is not None:
+        if tuple(key_mask.shape) != (B, Lk):
+            raise ValueError(f"key mask of shape {tuple(key_mask.shape)} does not cover {Lk} keys of {B} subjects")
+        km = key_mask.to(torch.bool).contiguous()
+        qm = km[:, P:].contiguous()
+    o = torch.empty(B, Lq, D, dtype=qkv.dtype, device=qkv.device)
+    with _timed("attn_decode"):
+        s = lib.esgpt_attn_decode(qkv.data_ptr(), D3, st.k.data_ptr(), st.v.data_ptr(), L.ptr(km), L.ptr(qm),
+                                  o.data_ptr(), D, B, H, Lq, Lk, cap, hd, int(window), code, L.stream())
+    L.check(s, "attn_decode")
+    return o, LayerKV(st, Lk)
+
+
+# ----------------------------------------------------------------------------------------------------------------
 # Output-layer losses
 # ----------------------------------------------------------------------------------------------------------------
 class OutputLossFn(torch.autograd.Function):

@@ -23,6 +23,7 @@ class LogNormalMixtureDistribution(D.TransformedDistribution):
         transforms.append(D.ExpTransform())
         self.mean_log_inter_time = mean_log_inter_time
         self.std_log_inter_time = std_log_inter_time
+        self.params = (locs, log_scales, log_weights)
         super().__init__(gmm, transforms, validate_args=validate_args)
 
     @property

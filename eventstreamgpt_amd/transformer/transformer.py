@@ -6,9 +6,10 @@ Class names, constructor/forward signatures, return types and state_dict keys fo
 ``TemporalPositionEncoding`` :564-619, CI input layer + encoder :622-848, NA input layer + encoder :851-1233).
 
 Compute: the attention core (scores, causal/local band, key padding, softmax, P·V) runs in the gfx950 attention
-kernels over a packed QKV buffer (one GEMM for q/k/v); the input layer runs in the fused embedding kernels. The
-projections, LayerNorm and MLP use PyTorch-ROCm (hipBLASLt GEMMs). Training path only: ``use_cache`` /
-``past`` (generation) and ``output_attentions`` are out of scope for this round and raise.
+kernels over a packed QKV buffer (one GEMM for q/k/v); the input layer runs in the fused embedding kernels. The CI
+training path runs every block through ``fused.ci_encoder_fused`` (own GEMM / LayerNorm kernels). Generation
+(``use_cache`` / ``past``, CI encoder) keeps a preallocated KV cache per layer and attends the new events with the
+decode kernel (``csrc/decode.hip``); the NA model's caches and ``output_attentions`` are not supported and raise.
 """
 from __future__ import annotations
 
@@ -20,7 +21,7 @@ from transformers.modeling_utils import PreTrainedModel
 
 from ..data.data_embedding_layer import DataEmbeddingLayer, MeasIndexGroupOptions
 from ..data.types import PytorchBatch
-from ..kernels import AttentionFn
+from ..kernels import AttentionFn, cached_attention
 from .config import StructuredEventProcessingMode, StructuredTransformerConfig
 from .model_output import TransformerOutputWithPast
 from .structured_attention import StructuredAttention
@@ -80,6 +81,7 @@ class InnerSelfAttention(nn.Module):
                 f"embed_dim must be divisible by num_heads (got `embed_dim`: {self.embed_dim} and "
                 f"`num_heads`: {self.num_heads})."
             )
+        self.max_seq_len = max_seq_len
         self.k_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=False)
         self.v_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=False)
         self.q_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=False)
@@ -88,8 +90,9 @@ class InnerSelfAttention(nn.Module):
     def forward(self, hidden_states, attention_mask=None, layer_past=None, head_mask=None, use_cache=False,
                 output_attentions=False, static_kv_first: bool = False, key_padding_mask=None):
         """``attention_mask`` may be the reference's additive [B,1,1,L] mask; ``key_padding_mask`` (bool [B,L])
-        is the fast path the encoders pass."""
-        _unsupported(layer_past is not None or use_cache, "use_cache/past")
+        is the fast path the encoders pass. With ``layer_past`` / ``use_cache`` (generation) the mask covers past and
+        new keys, [B, past + L]; ``present_key_value`` is a ``LayerKV`` (the reference's ``(key, value)`` pair as views
+        of a preallocated cache, transformer.py:261-268)."""
         _unsupported(output_attentions, "output_attentions")
         if head_mask is not None:
             raise NotImplementedError("eventstreamgpt_amd: head_mask is not supported")
@@ -98,6 +101,11 @@ class InnerSelfAttention(nn.Module):
         w = torch.cat([self.q_proj.weight, self.k_proj.weight, self.v_proj.weight], dim=0)
         qkv = nn.functional.linear(hidden_states, w)
         window = self.window_size if self.attention_type == "local" else 0
+        if layer_past is not None or use_cache:
+            _unsupported(static_kv_first, "use_cache/past with static_kv_first (NA dependency-graph cache)")
+            o, present = cached_attention(qkv, layer_past, key_padding_mask, self.num_heads, window, self.max_seq_len)
+            out = self.resid_dropout(self.out_proj(o))
+            return out, {"present_key_value": present if use_cache else None}
         kpm = None if key_padding_mask is None else key_padding_mask.contiguous()
         # Query padding = key padding for self-attention over events (rows are zeroed downstream).
         qpm = None if (kpm is None or static_kv_first) else kpm
@@ -285,10 +293,13 @@ class ConditionallyIndependentPointProcessTransformer(StructuredTransformerPreTr
                 seq_attention_mask: torch.Tensor | None = None, head_mask=None, use_cache: bool | None = None,
                 output_attentions: bool | None = None, output_hidden_states: bool | None = None,
                 return_dict: bool | None = None):
-        _unsupported(past is not None or bool(use_cache), "use_cache/past")
         _unsupported(bool(output_attentions), "output_attentions")
         from ..fused import ci_encoder_fused, fused_supported
 
+        use_cache = bool(use_cache)
+        if past is not None or use_cache:
+            return self._forward_cached(batch, input_embeds, past, seq_attention_mask, use_cache,
+                                        output_hidden_states, return_dict)
         if (input_embeds is None and batch is not None and batch.event_mask is not None and not output_hidden_states
                 and fused_supported(self)):
             il = self.input_layer
@@ -322,6 +333,46 @@ class ConditionallyIndependentPointProcessTransformer(StructuredTransformerPreTr
         if return_dict is False:
             return tuple(v for v in (hidden, all_hidden) if v is not None)
         return TransformerOutputWithPast(last_hidden_state=hidden, past_key_values=None, hidden_states=all_hidden,
+                                         attentions=None)
+
+
+    def _forward_cached(self, batch, input_embeds, past, seq_attention_mask, use_cache, output_hidden_states,
+                        return_dict):
+        """Generation path (``transformer.py:708-848`` with ``past`` / ``use_cache``): the batch holds only the new
+        events (``prepare_inputs_for_generation`` trims it to the last one once a cache exists) while
+        ``seq_attention_mask`` covers past + new events; each layer attends through its KV cache."""
+        if input_embeds is None:
+            assert batch is not None
+            input_embeds = self.input_layer(batch)
+        else:
+            assert batch is None, "Can't specify both input_embeds and batch."
+        if past is None:
+            past = tuple([None] * len(self.h))
+        if len(past) != len(self.h):
+            raise ValueError(f"past holds {len(past)} layers; the encoder has {len(self.h)}")
+        event_mask = batch.event_mask if batch is not None else None
+        if seq_attention_mask is not None:
+            kpm = seq_attention_mask.reshape(seq_attention_mask.shape[0], -1) == 0
+        else:
+            kpm = event_mask
+        hidden = input_embeds
+        presents = () if use_cache else None
+        all_hidden = () if output_hidden_states else None
+        m3 = None if event_mask is None else event_mask.unsqueeze(-1)
+        for block, layer_past in zip(self.h, past):
+            if output_hidden_states:
+                all_hidden = all_hidden + (hidden,)
+            hidden, extra = block(hidden, layer_past=layer_past, use_cache=use_cache, key_padding_mask=kpm)
+            if m3 is not None:
+                hidden = torch.where(m3, hidden, torch.zeros_like(hidden))
+            if use_cache:
+                presents = presents + (extra["present_key_value"],)
+        hidden = self.ln_f(hidden)
+        if output_hidden_states:
+            all_hidden = all_hidden + (hidden,)
+        if return_dict is False:
+            return tuple(v for v in (hidden, presents, all_hidden) if v is not None)
+        return TransformerOutputWithPast(last_hidden_state=hidden, past_key_values=presents, hidden_states=all_hidden,
                                          attentions=None)
 
 

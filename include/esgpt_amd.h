@@ -134,6 +134,22 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
                    int dtype, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream);
 
+/* ---- Generation: KV-cache decode -------------------------------------------------------------------------
+ * InnerSelfAttention.forward with layer_past / use_cache (transformer.py:261-268 + _attn :171-217), driven by
+ * CIPPTForGenerativeSequenceModeling.prepare_inputs_for_generation (conditionally_independent_model.py:198-248).
+ * The cache of one layer is a preallocated token-major pair k_cache / v_cache [B, cap, D] (D = H*hd), replacing the
+ * reference's per-step torch.cat of [B, H, L, hd] tensors.
+ * esgpt_kv_append: rows [past, past+Lq) of both caches <- the k / v thirds of the packed qkv rows [B, Lq, ld_qkv].
+ * esgpt_attn_decode: o[b, i] = softmax_j(q_i . k_j) v_j over cache rows j < Lk = past + Lq with query i at key
+ *   position Lk - Lq + i (causal; local: position - j < window; key_mask [B, Lk] the full event mask). Rows of
+ *   padded queries (query_mask [B, Lq]) and rows without a visible key are zeros. hd <= 128, hd % 4 == 0 (f32) or
+ *   hd % 8 == 0 (bf16); q / o row strides ld_q / ld_o elements (q may point into a packed qkv buffer). */
+int esgpt_kv_append(const void* qkv, int64_t ld_qkv, void* k_cache, void* v_cache, int64_t B, int64_t Lq,
+                    int64_t past, int64_t cap, int64_t D, int dtype, void* stream);
+int esgpt_attn_decode(const void* q, int64_t ld_q, const void* k_cache, const void* v_cache, const uint8_t* key_mask,
+                      const uint8_t* query_mask, void* o, int64_t ld_o, int64_t B, int64_t H, int64_t Lq, int64_t Lk,
+                      int64_t cap, int64_t hd, int64_t window, int dtype, void* stream);
+
 /* ---- Output layer losses -----------------------------------------------------------------------------------
  * GenerativeOutputLayerBase.get_{classification,regression,TTE}_outputs (model_output.py:1311-1721) with
  * weighted_loss / safe_weighted_avg (utils.py:134-234), fused: one pass computes every per-event loss, the
