@@ -16,7 +16,7 @@ Also reported (rank 0):
 * ``roofline_aux``: the same measurement for the attention backward (8·H·hd·T), the projection GEMMs (c_fc forward
   with its bias + GELU epilogue: 2·T·D·F; c_fc's grouped backward: 4·T·D·F), the JOINT input layer (HBM bytes,
   §8d) and the attention forward at a long-sequence shape (the kernel's MFMA efficiency beyond C2's latency-bound
-  size).
+  size), and the generation decode kernel (HBM bytes: every cached key / value row once per generated event).
 * ``cpu_baseline``: the f32 oracle port timed on this host's cores on a bounded sample of the same workload.
 ``--roofline-only`` runs just the roofline launches (the command the PMC passes profile).
 """
@@ -155,6 +155,26 @@ def _gemm_launchers(T, D, F, dev):
     return fwd, bwd, bufs
 
 
+def _decode_launcher(B, H, hd, Lk, dev):
+    """esgpt_attn_decode for one generated event per subject over a cache of Lk events (f32, the generation dtype):
+    HBM-bound, algorithmic bytes = B·H·Lk·hd·4·2 (every cached key and value row once) + q and o rows."""
+    from eventstreamgpt_amd import _lib as L
+
+    lib = L.load()
+    D = H * hd
+    g = torch.Generator(device=dev).manual_seed(2)
+    bufs = {"qkv": torch.randn(B, 1, 3 * D, device=dev, generator=g),
+            "k": torch.randn(B, Lk, D, device=dev, generator=g), "v": torch.randn(B, Lk, D, device=dev, generator=g),
+            "o": torch.empty(B, 1, D, device=dev)}
+    P = {k: v.data_ptr() for k, v in bufs.items()}
+
+    def fwd():
+        L.check(lib.esgpt_attn_decode(P["qkv"], 3 * D, P["k"], P["v"], None, None, P["o"], D, B, H, 1, Lk, Lk, hd, 0,
+                                      L.F32, L.stream()), "attn_decode")
+
+    return fwd, float(B * H * Lk * hd * 4 * 2 + 2 * B * D * 4), bufs
+
+
 def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float) -> tuple[dict, list]:
     """(roofline, roofline_aux): algorithmic work per launch / graph-replayed launch time, per kernel."""
     traffic = {}
@@ -204,6 +224,11 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float) -> tu
                                              0.0, dev)
     add("attn_fwd_long", f"attn_fwd_mfma_kernel<{hd}, false>", "mfma", 4.0 * Hl * hd * Bl * Ll * (Ll + 1) / 2, fl,
         {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"})
+    # generation: one decode step of the C2 model over a full cache, and a larger batch
+    for Bd in (B, 8 * B):
+        fd, dbytes, _keep_d = _decode_launcher(Bd, H, hd, Lq, dev)
+        add("attn_decode" if Bd == B else "attn_decode_b256", f"attn_decode_kernel<float, {hd}>", "hbm", dbytes, fd,
+            {"shape": f"decode: B={Bd} H={H} hd={hd}, 1 query over a {Lq}-event f32 KV cache"})
     return entries[0], entries[1:]
 
 
