@@ -8,7 +8,8 @@ re-concatenates its cache each step.
 
 Host reads per generated event: one combined NaN / non-finite check over the inputs (the reference issues two
 ``.any()`` reads per input field), the sampler's own reads (data-dependent widths in ``strip_unused_indices``),
-and the stopping criterion. The nested-attention model's generation (dependency-graph caches) is not supported.
+and the stopping criterion. The nested-attention model generates without caches (every graph level re-encodes the
+batch); its ``use_cache=True`` (dependency-graph caches) raises.
 """
 from __future__ import annotations
 
@@ -146,7 +147,7 @@ class StructuredGenerationMixin:
         if mode == StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT:
             sample_fn = self._conditionally_independent_sample_event
         elif mode == StructuredEventProcessingMode.NESTED_ATTENTION:
-            raise NotImplementedError("eventstreamgpt_amd: nested-attention generation is not supported yet")
+            sample_fn = self._nested_attention_sample_event
         else:
             raise ValueError(f"Unsupported structured event processing mode: {mode}")
 
@@ -198,3 +199,28 @@ class StructuredGenerationMixin:
         batch = next_event.append_to_batch(batch, self.config)
         batch = next_event.update_last_event_data(batch, self.config)
         return batch, next_event_preds, outputs.attentions, outputs.hidden_states, model_kwargs
+
+    def _nested_attention_sample_event(self, batch: PytorchBatch, generated_event_index: int, **model_kwargs):
+        """One NA event (``generation_utils.py:340-416``): graph level 0 samples the TTE and appends the event, then
+        each later level is predicted from the batch updated so far and written into the last event."""
+        levels = [{"time"}, *self.config.measurements_per_dep_graph_level[1:]]
+        is_first = generated_event_index == 0
+        scores, attentions, hidden_states = (), (), ()
+        for target, to_fill in enumerate(levels):
+            if is_first and target == 0:
+                target = None
+            _check_finite(batch, generated_event_index)
+            model_inputs = self.prepare_inputs_for_generation(batch, dep_graph_el_generation_target=target,
+                                                              **model_kwargs)
+            outputs = self(**model_inputs, return_dict=True, is_generation=True)
+            model_kwargs = self._update_model_kwargs_for_generation(outputs, model_kwargs)
+            preds = outputs.preds.slice((slice(None), -1))
+            scores += (preds,)
+            attentions += (outputs.attentions,)
+            hidden_states += (outputs.hidden_states,)
+            nxt = preds.sample(batch.event_mask)
+            if to_fill == {"time"}:
+                batch = nxt.append_to_batch(batch, self.config)
+            else:
+                batch = nxt.update_last_event_data(batch, self.config, measurements_to_fill=to_fill)
+        return batch, scores, attentions, hidden_states, model_kwargs

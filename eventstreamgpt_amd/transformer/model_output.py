@@ -544,17 +544,21 @@ class GenerativeOutputLayerBase(torch.nn.Module):
         return L.EsgptTTESpec(L.TTE_LNM, c.TTE_lognormal_generation_num_components, col, 0,
                               float(c.mean_log_inter_event_time_min), float(c.std_log_inter_event_time_min))
 
-    def generation_predictions(self, encoded: torch.Tensor) -> GenerativeSequenceModelPredictions:
-        """Next-event distributions from ``encoded`` [B, L, D] (``get_classification_outputs`` /
-        ``get_regression_outputs`` / ``get_TTE_outputs`` with ``is_generation=True``, ``model_output.py:1311-1721``):
-        single-label (Bernoulli(is-observed), Categorical(vocab slice)); multi-label (None, Bernoulli(slice));
-        multivariate regression (None, Normal over all targets); univariate (Bernoulli(is-observed), Normal); TTE."""
+    def generation_distributions(self, encoded: torch.Tensor, cls_meas=None, reg_meas=None):
+        """(classification, regression) next-event distributions of the given measurements (all when None) from
+        ``encoded`` [B, L, D] (``get_classification_outputs`` / ``get_regression_outputs`` with
+        ``is_generation=True``, ``model_output.py:1374-1721``): single-label (Bernoulli(is-observed),
+        Categorical(vocab slice)); multi-label (None, Bernoulli(slice)); multivariate regression (None, Normal over
+        all targets); univariate (Bernoulli(is-observed), Normal)."""
         c = self.config
         D_ = torch.distributions
         is_obs = self.IsObservedLayer(encoded)
-        scores = self.ClassificationLayer(encoded)
         cls = {}
-        for m, mode in self.classification_mode_per_measurement.items():
+        todo = [(m, mode) for m, mode in self.classification_mode_per_measurement.items()
+                if cls_meas is None or m in cls_meas]
+        if todo:
+            scores = self.ClassificationLayer(encoded)
+        for m, mode in todo:
             vs = c.vocab_offsets_by_measurement[m]
             sc = scores[:, :, vs:self._vocab_end(vs)]
             if mode == DataModality.SINGLE_LABEL_CLASSIFICATION:
@@ -563,9 +567,18 @@ class GenerativeOutputLayerBase(torch.nn.Module):
                 cls[m] = (None, D_.Bernoulli(logits=sc))
         reg = {}
         for m in c.measurements_for(DataModality.MULTIVARIATE_REGRESSION):
-            reg[m] = (None, self.regression_layers[m](X=encoded, idx=None))
+            if reg_meas is None or m in reg_meas:
+                reg[m] = (None, self.regression_layers[m](X=encoded, idx=None))
         for m in c.measurements_for(DataModality.UNIVARIATE_REGRESSION):
-            reg[m] = (D_.Bernoulli(logits=is_obs[:, :, c.measurements_idxmap[m] - 1]), self.regression_layers[m](X=encoded))
+            if reg_meas is None or m in reg_meas:
+                reg[m] = (D_.Bernoulli(logits=is_obs[:, :, c.measurements_idxmap[m] - 1]),
+                          self.regression_layers[m](X=encoded))
+        return cls, reg
+
+    def generation_predictions(self, encoded: torch.Tensor) -> GenerativeSequenceModelPredictions:
+        """Every measurement and the TTE from one encoding (the CI model, ``conditionally_independent_model.py:
+        88-129`` with ``is_generation=True``)."""
+        cls, reg = self.generation_distributions(encoded)
         return GenerativeSequenceModelPredictions(classification=cls, regression=reg, regression_indices={},
                                                   time_to_event=self.TTE_layer(encoded))
 

@@ -1,11 +1,22 @@
-"""Nested attention generative model — drop-in for ``EventStream/transformer/nested_attention_model.py``
-(training path)."""
+"""Nested attention generative model — drop-in for ``EventStream/transformer/nested_attention_model.py``."""
 from __future__ import annotations
 
 import torch
 
+from ..data.types import PytorchBatch
 from .config import StructuredEventProcessingMode, StructuredTransformerConfig
-from .model_output import GenerativeOutputLayerBase, GenerativeSequenceModelOutput, fused_na_losses
+from .generation.generation_utils import StructuredGenerationMixin
+from .model_output import (
+    GenerativeOutputLayerBase,
+    GenerativeSequenceModelLabels,
+    GenerativeSequenceModelLosses,
+    GenerativeSequenceModelOutput,
+    GenerativeSequenceModelPredictions,
+    _level_sets,
+    all_classification_measurements,
+    all_regression_measurements,
+    fused_na_losses,
+)
 from .transformer import NestedAttentionPointProcessTransformer, StructuredTransformerPreTrainedModel
 
 
@@ -20,14 +31,50 @@ class NestedAttentionGenerativeOutputLayer(GenerativeOutputLayerBase):
 
     def forward(self, batch, encoded: torch.FloatTensor, is_generation: bool = False,
                 dep_graph_el_generation_target: int | None = None) -> GenerativeSequenceModelOutput:
-        if is_generation or dep_graph_el_generation_target is not None:
-            raise NotImplementedError("eventstreamgpt_amd: generation is out of scope for this build")
+        if dep_graph_el_generation_target is not None and not is_generation:
+            raise ValueError(
+                f"If dep_graph_el_generation_target ({dep_graph_el_generation_target}) is not None, "
+                f"is_generation ({is_generation}) must be True!"
+            )
+        if is_generation:
+            return self._generation_output(batch, encoded, dep_graph_el_generation_target)
         losses, names = fused_na_losses(self, batch, encoded)
         return self._package(batch, losses, names)
 
+    def _generation_output(self, batch, encoded, target):
+        """``nested_attention_model.py:107-228`` with ``is_generation=True``: target None / 0 -> TTE only (from the
+        whole-event level); target t > 0 -> the measurements of level t from encoded[:, :, t-1] (or from the only
+        level when the encoder saw a single graph element)."""
+        c = self.config
+        G = encoded.shape[2]
+        if target is None or target == 0:
+            loop, do_tte = (), True
+        else:
+            loop, do_tte = ((1,) if G == 1 else (target,)), False
+        cls_all = all_classification_measurements(self)
+        reg_all = all_regression_measurements(c)
+        cls, reg = {}, {}
+        for i in loop:
+            t_idx = target if target is not None else i
+            cat, num = _level_sets(c.measurements_per_dep_graph_level[t_idx])
+            cd, rd = self.generation_distributions(encoded[:, :, i - 1, :], cat & cls_all, num & reg_all)
+            cls.update(cd)
+            reg.update(rd)
+        tte = self.TTE_layer(encoded[:, :, -1, :]) if do_tte else None
+        return GenerativeSequenceModelOutput(
+            loss=None,
+            losses=GenerativeSequenceModelLosses(classification=None, regression=None, time_to_event=None),
+            preds=GenerativeSequenceModelPredictions(classification=cls, regression=reg, regression_indices=None,
+                                                     time_to_event=tte),
+            labels=GenerativeSequenceModelLabels(classification=None, regression=None, regression_indices=None,
+                                                 time_to_event=None),
+            event_mask=batch["event_mask"],
+            dynamic_values_mask=batch["dynamic_values_mask"],
+        )
 
-class NAPPTForGenerativeSequenceModeling(StructuredTransformerPreTrainedModel):
-    """``NAPPTForGenerativeSequenceModeling`` (``:231-366``)."""
+
+class NAPPTForGenerativeSequenceModeling(StructuredGenerationMixin, StructuredTransformerPreTrainedModel):
+    """``NAPPTForGenerativeSequenceModeling`` (``:231-366``), with ``generate`` (uncached)."""
 
     def __init__(self, config: StructuredTransformerConfig):
         super().__init__(config)
@@ -37,9 +84,20 @@ class NAPPTForGenerativeSequenceModeling(StructuredTransformerPreTrainedModel):
         self.output_layer = NestedAttentionGenerativeOutputLayer(config)
         self.post_init()
 
+    def prepare_inputs_for_generation(self, batch: PytorchBatch, past=None, **kwargs) -> dict:
+        """``nested_attention_model.py:265-324``. The dependency-graph KV caches (``use_cache=True``) are not
+        supported: generation re-encodes the batch for every graph level."""
+        if not kwargs.get("use_cache", False):
+            return {**kwargs, "batch": batch}
+        raise NotImplementedError("eventstreamgpt_amd: nested-attention generation with use_cache=True (sequence + "
+                                  "dependency-graph KV caches) is not supported; use use_cache=False")
+
     def forward(self, batch, is_generation: bool = False, **kwargs) -> GenerativeSequenceModelOutput:
         encoded = self.encoder(batch, **kwargs)
-        out = self.output_layer(batch, encoded.last_hidden_state, is_generation=is_generation)
+        out = self.output_layer(batch, encoded.last_hidden_state, is_generation=is_generation,
+                                dep_graph_el_generation_target=kwargs.get("dep_graph_el_generation_target", None))
+        if kwargs.get("use_cache", False):
+            out["past_key_values"] = encoded.past_key_values
         if kwargs.get("output_hidden_states", False):
             out["hidden_states"] = encoded.hidden_states
         return out

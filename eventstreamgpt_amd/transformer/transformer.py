@@ -399,8 +399,11 @@ class NestedAttentionPointProcessInputLayer(torch.nn.Module):
         self.embedding_dropout = torch.nn.Dropout(p=config.input_dropout)
 
     def forward(self, batch: PytorchBatch, dep_graph_el_generation_target: int | None = None) -> torch.Tensor:
-        _unsupported(dep_graph_el_generation_target is not None, "dep_graph_el_generation_target")
         embed = self.data_embedding_layer.embed(batch, time_layer=self.time_embedding_layer, cumsum=True)
+        if dep_graph_el_generation_target is not None:
+            # generation: only the graph element preceding the target (transformer.py:926-929; target 0 -> the
+            # whole event); the embedding is already masked, so slicing after the mask is the same.
+            embed = embed[:, :, dep_graph_el_generation_target - 1].unsqueeze(2)
         return self.embedding_dropout(embed)
 
 
@@ -423,7 +426,9 @@ class NestedAttentionPointProcessTransformer(StructuredTransformerPreTrainedMode
                 seq_attention_mask: torch.Tensor | None = None, head_mask=None, use_cache: bool | None = None,
                 output_attentions: bool | None = None, output_hidden_states: bool | None = None,
                 return_dict: bool | None = None, dep_graph_past=None, dep_graph_el_generation_target=None):
-        _unsupported(past is not None or dep_graph_past is not None or bool(use_cache), "use_cache/past")
+        use_cache = use_cache if use_cache is not None else self.config.use_cache  # as the reference (:1029)
+        _unsupported(past is not None or dep_graph_past is not None or bool(use_cache),
+                     "use_cache/past in the nested-attention encoder (pass use_cache=False)")
         _unsupported(bool(output_attentions), "output_attentions")
         if input_embeds is None:
             assert batch is not None

@@ -61,6 +61,54 @@ def batch_dict(b):
     return {k: v.clone() for k, v in b.items() if isinstance(v, torch.Tensor)}
 
 
+def dist_params(d):
+    """Distribution -> its defining tensors (what our heads must reproduce)."""
+    D = torch.distributions
+    if d is None:
+        return None
+    if isinstance(d, tuple):
+        return [dist_params(x) for x in d]
+    if isinstance(d, D.Bernoulli):
+        return {"bernoulli_logits": d.logits.detach()}
+    if isinstance(d, D.Categorical):
+        return {"categorical_probs": d.probs.detach()}
+    if isinstance(d, D.Normal):
+        return {"normal_loc": d.loc.detach(), "normal_scale": d.scale.detach()}
+    if isinstance(d, D.Exponential):
+        return {"exponential_rate": d.rate.detach()}
+    raise TypeError(type(d))
+
+
+def predictions():
+    """Reference forward(batch, is_generation=True[, dep_graph_el_generation_target=t]) on the ci_small / na_small
+    golden models and batches: every next-event distribution's parameters (nested_attention_model.py:47-228,
+    conditionally_independent_model.py:45-161)."""
+    import json
+
+    from EventStream.data.types import PytorchBatch as RefBatch
+    from EventStream.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+    from EventStream.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    res = {}
+    for name, cls, targets in (("ci_small", CIPPTForGenerativeSequenceModeling, [None]),
+                               ("na_small", NAPPTForGenerativeSequenceModeling, [None, 0, 1, 2, 3])):
+        fx = torch.load(os.path.join(HERE, f"{name}.pt"), weights_only=True)
+        model = cls(RefConfig(**json.loads(fx["config_kwargs"])))
+        model.load_state_dict(fx["state_dict"])
+        model.eval()
+        per_t = {}
+        for t in targets:
+            kw = {"use_cache": False} if t is None else {"dep_graph_el_generation_target": t, "use_cache": False}
+            with torch.no_grad():
+                o = model(RefBatch(**fx["batch"]), is_generation=True, **kw)
+            p = o.preds
+            per_t[str(t)] = {"classification": {k: dist_params(v) for k, v in (p.classification or {}).items()},
+                             "regression": {k: dist_params(v) for k, v in (p.regression or {}).items()},
+                             "time_to_event": dist_params(p.time_to_event)}
+        res[name] = per_t
+    return res
+
+
 def main():
     from EventStream.data.types import PytorchBatch as RefBatch
 
@@ -94,6 +142,7 @@ def main():
     idx[2] = 0
     vals = torch.randn(6, 9, generator=g)
     out["strip"] = dict(idx=idx, vals=vals, want=ref_strip(idx, vals))
+    out["predictions"] = predictions()
     torch.save(out, os.path.join(HERE, "generation_ref.pt"))
     print("wrote generation_ref.pt")
 
