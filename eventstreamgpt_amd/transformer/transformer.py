@@ -426,7 +426,8 @@ class NestedAttentionPointProcessTransformer(StructuredTransformerPreTrainedMode
                 seq_attention_mask: torch.Tensor | None = None, head_mask=None, use_cache: bool | None = None,
                 output_attentions: bool | None = None, output_hidden_states: bool | None = None,
                 return_dict: bool | None = None, dep_graph_past=None, dep_graph_el_generation_target=None):
-        use_cache = use_cache if use_cache is not None else self.config.use_cache  # as the reference (:1029)
+        # The reference resolves use_cache=None to config.use_cache (True by default) and then builds caches nobody
+        # reads outside generation; here None means no cache, and an explicit cache request raises.
         _unsupported(past is not None or dep_graph_past is not None or bool(use_cache),
                      "use_cache/past in the nested-attention encoder (pass use_cache=False)")
         _unsupported(bool(output_attentions), "output_attentions")
