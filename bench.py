@@ -302,7 +302,8 @@ def main():
         roofline, aux = roofline_report(model, cfg, bc.batch(0, device=dev), dev, 0.1, PEAK_BF16_TFLOPS)
         print(json.dumps({"roofline": roofline, "roofline_aux": aux}))
         return
-    batches = [bc.batch(100 * rank + i, device=dev) for i in range(n_batches)]
+    # packed like the native collate's output (one buffer per batch): staging into the graph's inputs is one copy
+    batches = [bc.batch(100 * rank + i, device=dev).packed() for i in range(n_batches)]
     events = [float(b.event_mask.sum()) for b in batches]
 
     for i in range(args.warmup):

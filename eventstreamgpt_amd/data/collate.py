@@ -153,16 +153,14 @@ def collate_ragged(r: RaggedEvents, padding_side: str = "right", do_produce_stat
     _lib.check(status, "esgpt_collate_shape")
     L, M, S = int(L[0]), int(M[0]), int(S[0])
 
-    def new(shape, dt):
-        return torch.empty(shape, dtype=dt, pin_memory=pin_memory and torch.cuda.is_available())
-
-    out = PytorchBatch(
-        event_mask=new((B, L), torch.bool), time_delta=new((B, L), torch.float32),
-        dynamic_indices=new((B, L, M), torch.int64), dynamic_measurement_indices=new((B, L, M), torch.int64),
-        dynamic_values=new((B, L, M), torch.float32), dynamic_values_mask=new((B, L, M), torch.bool))
+    # every field a view into ONE (optionally pinned) buffer: the batch then moves to the device in one copy
+    spec = {"event_mask": ((B, L), torch.bool), "time_delta": ((B, L), torch.float32),
+            "dynamic_indices": ((B, L, M), torch.int64), "dynamic_measurement_indices": ((B, L, M), torch.int64),
+            "dynamic_values": ((B, L, M), torch.float32), "dynamic_values_mask": ((B, L, M), torch.bool)}
     if do_produce_static_data:
-        out.static_indices = new((B, S), torch.int64)
-        out.static_measurement_indices = new((B, S), torch.int64)
+        spec["static_indices"] = ((B, S), torch.int64)
+        spec["static_measurement_indices"] = ((B, S), torch.int64)
+    out = PytorchBatch.empty_packed(spec, pin_memory=pin_memory)
     p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     st_args = ((_vp(r.st_start), _vp(st_count), _vp(r.st_idx), _vp(r.st_meas)) if do_produce_static_data and
                r.st_count is not None else (None, None, None, None))

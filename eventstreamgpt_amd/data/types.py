@@ -37,6 +37,8 @@ class TemporalityType(StrEnum):
     FUNCTIONAL_TIME_DEPENDENT = enum.auto()
 
 
+_FLAT_ALIGN = 256
+
 _TENSOR_FIELDS = (
     "event_mask",
     "time_delta",
@@ -170,8 +172,83 @@ class PytorchBatch:
         kw["stream_labels"] = None if sl is None else {k: v.index_select(0, idx) for k, v in sl.items()}
         return PytorchBatch(**kw)
 
+    # ---- one-buffer layout: every tensor field a view into one flat byte buffer ----
+    def flat_buffer(self) -> torch.Tensor | None:
+        """The flat uint8 buffer every tensor field of this batch views, if it was built packed (``packed``,
+        ``empty_packed`` or the native collate), else None. Staging such a batch is ONE copy (H2D or D2D)."""
+        flat = getattr(self, "_flat", None)
+        if flat is None:
+            return None
+        sig = getattr(self, "_flat_sig", ())
+        for name, off, shape, dt in sig:  # still the views it was built with (fields may be reassigned)
+            v = getattr(self, name)
+            if (v is None or v.dtype != dt or tuple(v.shape) != shape or not v.is_contiguous()
+                    or v.data_ptr() != flat.data_ptr() + off):
+                return None
+        return flat
+
+    @staticmethod
+    def empty_packed(spec: dict, device=None, pin_memory: bool = False) -> "PytorchBatch":
+        """A batch whose fields ``spec`` = {name: (shape, dtype)} are views into one flat buffer (256-B aligned)."""
+        sig, off = [], 0
+        for name in _TENSOR_FIELDS:
+            if name not in spec:
+                continue
+            shape, dt = tuple(spec[name][0]), spec[name][1]
+            n = dt.itemsize
+            for d in shape:
+                n *= d
+            sig.append((name, off, shape, dt))
+            off += (n + _FLAT_ALIGN - 1) // _FLAT_ALIGN * _FLAT_ALIGN
+        flat = torch.empty(max(off, 1), dtype=torch.uint8, device=device,
+                           pin_memory=pin_memory and device in (None, "cpu") and torch.cuda.is_available())
+        return PytorchBatch._from_flat(flat, tuple(sig))
+
+    @staticmethod
+    def _from_flat(flat: torch.Tensor, sig) -> "PytorchBatch":
+        kw = {}
+        for name, off, shape, dt in sig:
+            n = dt.itemsize
+            for d in shape:
+                n *= d
+            kw[name] = flat[off:off + n].view(dt).view(shape)
+        out = PytorchBatch(**kw)
+        out._flat, out._flat_sig = flat, sig
+        return out
+
+    def packed(self) -> "PytorchBatch":
+        """A copy of this batch with every tensor field in one flat buffer on the same device."""
+        spec = {k: (tuple(v.shape), v.dtype) for k, v in self.as_dict().items()}
+        out = PytorchBatch.empty_packed(spec, device=self.device)
+        for k, v in self.as_dict().items():
+            getattr(out, k).copy_(v)
+        out.stream_labels = None if self.stream_labels is None else dict(self.stream_labels)
+        return out
+
+    def copy_(self, src: "PytorchBatch", non_blocking: bool = False) -> "PytorchBatch":
+        """In-place copy of ``src``'s fields (same shapes): one buffer copy when both share a packed layout."""
+        a, b = self.flat_buffer(), src.flat_buffer()
+        done = set()
+        if a is not None and b is not None and self._flat_sig == src._flat_sig:
+            a.copy_(b, non_blocking=non_blocking)
+            done = {name for name, *_ in self._flat_sig}
+        for k, v in src.as_dict().items():
+            if k not in done:
+                getattr(self, k).copy_(v, non_blocking=non_blocking)
+        return self
+
     def to(self, device, non_blocking: bool = False) -> "PytorchBatch":
-        """Moves every tensor field to ``device``."""
+        """Moves every tensor field to ``device`` (a packed batch moves as one buffer and stays packed)."""
+        flat = self.flat_buffer()
+        if flat is not None:
+            out = PytorchBatch._from_flat(flat.to(device, non_blocking=non_blocking), self._flat_sig)
+            packed = {name for name, *_ in self._flat_sig}
+            for k, v in self.as_dict().items():  # fields set after packing travel on their own
+                if k not in packed:
+                    setattr(out, k, v.to(device, non_blocking=non_blocking))
+            sl = self.stream_labels
+            out.stream_labels = None if sl is None else {k: v.to(device) for k, v in sl.items()}
+            return out
         kw = {}
         for k in _TENSOR_FIELDS:
             v = getattr(self, k)

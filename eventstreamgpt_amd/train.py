@@ -168,8 +168,8 @@ class TrainStep:
             torch._foreach_copy_(grads, torch._utils._unflatten_dense_tensors(flat, grads))
 
     def _copy_into_static(self, batch: PytorchBatch):
-        for k, v in batch.as_dict().items():
-            getattr(self.static_batch, k).copy_(v, non_blocking=True)
+        # one D2D copy when the batch is packed (native collate / .packed()), else one per field
+        self.static_batch.copy_(batch, non_blocking=True)
 
     def step(self, batch: PytorchBatch) -> torch.Tensor:
         if not self.use_graph:
@@ -191,7 +191,7 @@ class TrainStep:
         return loss
 
     def _capture(self, batch: PytorchBatch):
-        self.static_batch = PytorchBatch(**{k: v.clone() for k, v in batch.as_dict().items()})
+        self.static_batch = batch.packed()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

@@ -314,3 +314,26 @@ def test_config_set_to_dataset_from_sample_shard():
     assert cfg.vocab_size == 45 and cfg.max_seq_len == 128  # vocab 45 (sample vocabulary_config)
     assert cfg.mean_log_inter_event_time_min == pyd.mean_log_inter_event_time_min
     assert "eye_color" in cfg.measurement_configs
+
+
+def test_packed_batch_one_buffer_roundtrip():
+    """A packed batch keeps every field in one buffer; copy_ / to() preserve values and the layout, and fields
+    set after packing still travel."""
+    from eventstreamgpt_amd.synthetic import CONFIGS
+
+    b = CONFIGS["C1"].batch(0, batch_size=3)
+    p = b.packed()
+    flat = p.flat_buffer()
+    assert flat is not None and flat.dtype == torch.uint8
+    for k, v in b.as_dict().items():
+        assert torch.equal(getattr(p, k), v), k
+    q = CONFIGS["C1"].batch(1, batch_size=3).packed()
+    q.start_time = torch.arange(3.0)
+    p.start_time = torch.zeros(3)
+    p.copy_(q)
+    for k, v in q.as_dict().items():
+        assert torch.equal(getattr(p, k), v), k
+    moved = q.to("cpu")
+    assert moved.flat_buffer() is not None and torch.equal(moved.start_time, q.start_time)
+    p.event_mask = p.event_mask.clone()  # a reassigned field breaks the packed view -> per-field path
+    assert p.flat_buffer() is None
