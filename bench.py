@@ -8,15 +8,15 @@ A step = forward + backward + (RCCL gradient all-reduce) + AdamW + LR-schedule s
 subjects per GPU (weak scaling). Inputs are resident in HBM before the timed region. Rank 0 prints ONE JSON line.
 
 Also reported (rank 0):
-* ``roofline``: the attention forward kernel on the step's own shapes (MFMA-bound, 4·H·hd·T
-  algorithmic FLOPs per layer launch, T = allowed (query, key) pairs of the batch). Its launch is captured R times
+* ``roofline``: the step's dominant kernel by device time, the grouped projection backward (dX + dW + db of one
+  Linear in one launch, MFMA-bound, 4·T·D·F algorithmic FLOPs) on c_fc's shape. Its launch is captured R times
   into a HIP graph and replayed between HIP events on the capturing stream (back-to-back launches as in the step's
   own graph); ``traffic`` = HBM bytes per launch from the committed rocprofv3 PMC summary
   (profiles/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), when present.
-* ``roofline_aux``: the same measurement for the attention backward (8·H·hd·T), the projection GEMMs (c_fc forward
-  with its bias + GELU epilogue: 2·T·D·F; c_fc's grouped backward: 4·T·D·F), the JOINT input layer (HBM bytes,
-  §8d) and the attention forward at a long-sequence shape (the kernel's MFMA efficiency beyond C2's latency-bound
-  size), and the generation decode kernel (HBM bytes: every cached key / value row once per generated event).
+* ``roofline_aux``: the same measurement for the attention forward / backward on the step's shapes (SURVEY.md §8d:
+  4·H·hd·T / 8·H·hd·T, T = allowed (query, key) pairs of the batch), the c_fc forward with its bias + GELU epilogue
+  (2·T·D·F), the JOINT input layer (HBM bytes, §8d) and the attention forward at a long-sequence shape (the
+  kernel's MFMA efficiency beyond C2's latency-bound size), and the generation decode kernel (HBM bytes: every cached key / value row once per generated event).
 * ``cpu_baseline``: the f32 oracle port timed on this host's cores on a bounded sample of the same workload.
 ``--roofline-only`` runs just the roofline launches (the command the PMC passes profile).
 """
@@ -229,7 +229,11 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float) -> tu
         fd, dbytes, _keep_d = _decode_launcher(Bd, H, hd, Lq, dev)
         add("attn_decode" if Bd == B else "attn_decode_b256", f"attn_decode_kernel<float, {hd}>", "hbm", dbytes, fd,
             {"shape": f"decode: B={Bd} H={H} hd={hd}, 1 query over a {Lq}-event f32 KV cache"})
-    return entries[0], entries[1:]
+    # `roofline` = the step's dominant kernel by device time: the grouped projection backward (gemm_bwd_pair_kernel,
+    # ~35 % of the C2 step in profiles/r01_c2_step_kernel_stats.csv), measured on c_fc's shape (its largest launch)
+    dom = next(i for i, e in enumerate(entries) if e["kernel"] == "gemm_fc_bwd")
+    entries[dom]["dominant"] = "largest share of the step's device time (grouped projection backward)"
+    return entries[dom], entries[:dom] + entries[dom + 1:]
 
 
 def cpu_baseline(bc, seconds: float = 12.0) -> dict:
