@@ -16,7 +16,8 @@
 // Decode is HBM-bound: every visible cached row is read once per (query, head) -> 2*hd*s bytes per visible pair.
 // One workgroup (4 waves) per (b, h, query); the waves take interleaved 64-key blocks, each lane scores one key
 // (q broadcast from LDS, the key row read as 16-B vectors), P.V runs lane-per-dimension over the block with the
-// probabilities broadcast from LDS (coalesced value rows), and the four partial softmax states merge through LDS.
+// probabilities broadcast from LDS (coalesced value rows, a whole 64-key block in flight, issued with the key rows),
+// and the four partial softmax states merge through LDS.
 #include "common.h"
 
 using namespace esgpt;
@@ -24,6 +25,7 @@ using namespace esgpt;
 namespace {
 
 constexpr int DEC_WAVES = 4;
+constexpr int PV_ROWS = 64;  // value elements per lane in flight per P.V step (64 rows for hd <= 64)
 
 template <typename T>
 __global__ __launch_bounds__(256) void kv_append_kernel(const T* __restrict__ qkv, int64_t ld_qkv, T* __restrict__ kc,
@@ -115,10 +117,23 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const T* __restrict__ 
 #pragma unroll
   for (int u = 0; u < DPL; ++u) acc[u] = 0.f;
 
+  constexpr int PVU = PV_ROWS / DPL;  // value rows per P.V step (registers: PVU * DPL)
   for (int64_t blk = w; blk < nblk; blk += DEC_WAVES) {
     const int64_t j0 = jlo + blk * 64;
     const int64_t j = j0 + lane;
     const int64_t nb = min((int64_t)64, pos + 1 - j0);
+    // The first P.V step's value rows are loaded together with the key rows (one memory round trip per block for
+    // hd <= 64); rows past the block clamp to its last row and get p = 0.
+    float vv[PVU][DPL];
+#pragma unroll
+    for (int x = 0; x < PVU; ++x) {
+      const T* vp = vbase + (j0 + min(x, (int)nb - 1)) * D;
+#pragma unroll
+      for (int u = 0; u < DPL; ++u) {
+        const int d = lane + 64 * u;
+        vv[x][u] = (d < hd) ? to_f32(vp[d]) : 0.f;
+      }
+    }
     float s = -INFINITY;
     if (lane < nb && (!km || km[j])) s = dot_row<T, HDP>(qs, kbase + j * D, hd);
     const float mb = wave_max(s);
@@ -134,14 +149,24 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const T* __restrict__ 
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int u = 0; u < DPL; ++u) acc[u] *= c;
-    for (int t = 0; t < nb; ++t) {
-      const float pt = ps[w][t];
-      if (pt == 0.f) continue;
-      const T* vp = vbase + (j0 + t) * D;
+    // P.V: PVU value rows in flight per step, so the row loads overlap instead of forming one chain per key.
+    for (int t0 = 0; t0 < nb; t0 += PVU) {
+      if (t0 > 0) {
 #pragma unroll
-      for (int u = 0; u < DPL; ++u) {
-        const int d = lane + 64 * u;
-        if (d < hd) acc[u] = fmaf(pt, to_f32(vp[d]), acc[u]);
+        for (int x = 0; x < PVU; ++x) {
+          const T* vp = vbase + (j0 + min(t0 + x, (int)nb - 1)) * D;
+#pragma unroll
+          for (int u = 0; u < DPL; ++u) {
+            const int d = lane + 64 * u;
+            vv[x][u] = (d < hd) ? to_f32(vp[d]) : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < PVU; ++x) {
+        const float pt = (t0 + x < nb) ? ps[w][t0 + x] : 0.f;
+#pragma unroll
+        for (int u = 0; u < DPL; ++u) acc[u] = fmaf(pt, vv[x][u], acc[u]);
       }
     }
     __builtin_amdgcn_wave_barrier();

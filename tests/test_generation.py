@@ -366,3 +366,33 @@ def test_nested_attention_generate():
     assert bool(torch.isfinite(out.time_delta).all())
     with pytest.raises(NotImplementedError):
         model.generate(b, max_new_events=1, use_cache=True)
+
+
+@pytest.mark.gpu
+def test_kv_cache_branching_and_foreign_past():
+    """A past reused after the cache advanced (branching) is copied, not overwritten; a plain reference-format
+    (key, value) tuple is accepted as a past; both give the same outputs as a fresh run."""
+    from eventstreamgpt_amd.kernels import LayerKV, cached_attention
+
+    torch.manual_seed(0)
+    B, H, hd, P = 2, 4, 16, 20
+    D = H * hd
+    qkv = (torch.randn(B, P + 2, 3 * D) * 0.5).cuda()
+    mask = torch.ones(B, P + 2, dtype=torch.bool, device="cuda")
+    with torch.no_grad():
+        _, past = cached_attention(qkv[:, :P], None, mask[:, :P], H, 0, cap_hint=32)
+        o_a, past_a = cached_attention(qkv[:, P:P + 1], past, mask[:, :P + 1], H, 0, cap_hint=32)
+        # branch: a different next event from the same past
+        o_b, past_b = cached_attention(qkv[:, P + 1:P + 2], past, mask[:, :P + 1], H, 0, cap_hint=32)
+        assert past_b.store is not past_a.store  # copy-on-write
+        # the first branch's cache is intact: continuing it equals a fresh run over [0..P] + event P+1
+        o_a2, _ = cached_attention(qkv[:, P + 1:P + 2], past_a, mask[:, :P + 2], H, 0, cap_hint=32)
+        _, fresh = cached_attention(qkv[:, :P + 1], None, mask[:, :P + 1], H, 0, cap_hint=32)
+        o_f, _ = cached_attention(qkv[:, P + 1:P + 2], fresh, mask[:, :P + 2], H, 0, cap_hint=32)
+        torch.testing.assert_close(o_a2, o_f, rtol=1e-6, atol=1e-6)
+        # reference-format past: plain [B, H, L, hd] tensors
+        foreign = (past[0].clone(), past[1].clone())
+        assert not isinstance(foreign, LayerKV)
+        o_c, past_c = cached_attention(qkv[:, P:P + 1], foreign, mask[:, :P + 1], H, 0, cap_hint=32)
+        torch.testing.assert_close(o_c, o_a, rtol=1e-6, atol=1e-6)
+        assert past_c[0].shape == (B, H, P + 1, hd)
