@@ -193,8 +193,9 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float) -> tu
             ach, peak, unit, wk = work / (ms * 1e-3) / 1e12, peak_tf, "TFLOP/s", "algorithmic_flops_per_launch"
         else:
             ach, peak, unit, wk = work / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", "algorithmic_bytes_per_launch"
+        tkey = (extra or {}).pop("traffic_key", kernel)
         e = {"kernel": name, "symbol": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak,
-             "unit": unit, "frac": round(ach / peak, 5), "traffic": traffic.get(kernel), "avg_ms": round(ms, 5),
+             "unit": unit, "frac": round(ach / peak, 5), "traffic": traffic.get(tkey), "avg_ms": round(ms, 5),
              wk: work, "timing": "HIP graph of 20 launches, events on the replaying stream"}
         e.update(extra or {})
         entries.append(e)
@@ -228,7 +229,8 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float) -> tu
     for Bd in (B, 8 * B):
         fd, dbytes, _keep_d = _decode_launcher(Bd, H, hd, Lq, dev)
         add("attn_decode" if Bd == B else "attn_decode_b256", f"attn_decode_kernel<float, {hd}>", "hbm", dbytes, fd,
-            {"shape": f"decode: B={Bd} H={H} hd={hd}, 1 query over a {Lq}-event f32 KV cache"})
+            {"shape": f"decode: B={Bd} H={H} hd={hd}, 1 query over a {Lq}-event f32 KV cache",
+             "traffic_key": f"attn_decode_kernel<float, {hd}>@grid{Bd * H * 256}"})
     # `roofline` = the step's dominant kernel by device time: the grouped projection backward (gemm_bwd_pair_kernel,
     # ~35 % of the C2 step in profiles/r01_c2_step_kernel_stats.csv), measured on c_fc's shape (its largest launch)
     dom = next(i for i, e in enumerate(entries) if e["kernel"] == "gemm_fc_bwd")

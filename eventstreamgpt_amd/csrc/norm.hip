@@ -20,7 +20,18 @@ namespace {
 
 constexpr int kWaves = 4;
 constexpr int kMaxChunks = 4;       // 4-column chunks per lane: D <= 1024
-constexpr int kBwdRowsPerWave = 4;  // backward: rows per wave, every load issued before the row reductions
+constexpr int kBwdRowsPerWave = 8;  // backward default: rows per wave, every load issued before the row reductions
+
+// Backward rows per wave (2, 4 or 8; ESGPT_LN_BWD_ROWS tuning hook, read once).
+int bwd_rows() {
+  static int r = 0;
+  if (r == 0) {
+    const char* e = getenv("ESGPT_LN_BWD_ROWS");
+    const int v = e ? atoi(e) : kBwdRowsPerWave;
+    r = (v == 2 || v == 4 || v == 8) ? v : kBwdRowsPerWave;
+  }
+  return r;
+}
 constexpr int kGroupBlocks = 32;    // backward column sums: blocks per first-level group
 
 struct V4 {
@@ -141,14 +152,13 @@ __device__ __forceinline__ u32x4 ordered_sum4(__amdgpu_buffer_rsrc_t rs, int bas
 // reductions. Column partials (dgamma, dbeta, dbias) of the block's rows go to part[blockIdx.x][3][D]; the last
 // block to finish in each group of kGroupBlocks sums its group's partials into part[nb + group], and the last group
 // sums those into sums[3][D]: fixed order (deterministic), no second launch, counters left at zero.
-template <typename TY, typename TO, int KC>
+template <typename TY, typename TO, int KC, int R>
 __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     const float* __restrict__ dh_in, const TO* __restrict__ dout, const float* __restrict__ h,
     const float* __restrict__ mean_i, const float* __restrict__ rstd_i, const float* __restrict__ w,
     const uint8_t* __restrict__ rmask, float drop_p, const uint64_t* __restrict__ seed, int64_t N, int64_t D,
     float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part, float* __restrict__ sums,
     int32_t* __restrict__ counters) {
-  constexpr int R = kBwdRowsPerWave;
   __shared__ float s_part[kWaves][3][4 * 64];
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(part, (short)0, 0x7fffffff, 0x00020000);
@@ -404,16 +414,24 @@ template <typename TY, typename TO>
 void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const float* mean, const float* rstd,
                    const float* w, const uint8_t* rmask, float p, const uint64_t* seed, int64_t N, int64_t D, float* dx,
                    void* dy, float* part, float* sums, int32_t* counters, hipStream_t st) {
-  const unsigned grid = (unsigned)cdiv(N, kWaves * kBwdRowsPerWave);
-#define LN_BWD(KC)                                                                                              \
-  residual_ln_bwd_kernel<TY, TO, KC><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, seed, \
-                                                           N, D, dx, (TY*)dy, part, sums, counters)
+  const int R = bwd_rows();
+  const unsigned grid = (unsigned)cdiv(N, kWaves * R);
+#define LN_BWD(KC, RR)                                                                                             \
+  residual_ln_bwd_kernel<TY, TO, KC, RR><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, \
+                                                               seed, N, D, dx, (TY*)dy, part, sums, counters)
+#define LN_BWD_R(KC)              \
+  do {                            \
+    if (R == 2) LN_BWD(KC, 2);    \
+    else if (R == 8) LN_BWD(KC, 8); \
+    else LN_BWD(KC, 4);           \
+  } while (0)
   switch (cdiv(D, 256)) {
-    case 1: LN_BWD(1); break;
-    case 2: LN_BWD(2); break;
-    case 3: LN_BWD(3); break;
-    default: LN_BWD(4); break;
+    case 1: LN_BWD_R(1); break;
+    case 2: LN_BWD_R(2); break;
+    case 3: LN_BWD_R(3); break;
+    default: LN_BWD_R(4); break;
   }
+#undef LN_BWD_R
 #undef LN_BWD
 }
 
@@ -422,11 +440,11 @@ void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const f
 extern "C" {
 
 int64_t esgpt_residual_ln_partials(int64_t N) {
-  const int64_t nb = cdiv(N, kWaves * kBwdRowsPerWave);
+  const int64_t nb = cdiv(N, kWaves * bwd_rows());
   return nb + cdiv(nb, kGroupBlocks);
 }
 
-int64_t esgpt_residual_ln_counters(int64_t N) { return cdiv(cdiv(N, kWaves * kBwdRowsPerWave), kGroupBlocks) + 1; }
+int64_t esgpt_residual_ln_counters(int64_t N) { return cdiv(cdiv(N, kWaves * bwd_rows()), kGroupBlocks) + 1; }
 
 int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
                           float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,

@@ -15,7 +15,10 @@ import sys
 from collections import defaultdict
 
 SYMBOLS = ["attn_fwd_mfma_kernel<64, true>", "attn_fwd_mfma_kernel<64, false>", "attn_bwd_kernel<64, true>",
-           "gemm_kernel<true, true>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>"]
+           "gemm_kernel<true, true>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>",
+           "attn_decode_kernel<float, 64>"]
+# kernels launched at several shapes by bench.py: keyed "<symbol>@grid<work-items>"
+BY_GRID = {"attn_decode_kernel<float, 64>"}
 
 
 def averages(d: str, counter: str) -> dict:
@@ -26,7 +29,8 @@ def averages(d: str, counter: str) -> dict:
                 continue
             for s in SYMBOLS:
                 if s in r["Kernel_Name"]:
-                    acc[s].append(float(r["Counter_Value"]))
+                    key = f"{s}@grid{r.get('Grid_Size', '?')}" if s in BY_GRID else s
+                    acc[key].append(float(r["Counter_Value"]))
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
@@ -36,7 +40,7 @@ def main():
                      "`python bench.py --roofline-only`; bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per dispatch "
                      "(gfx950 FETCH_SIZE calibration)",
            "bytes_per_launch": {}, "raw_kib": {}}
-    for s in SYMBOLS:
+    for s in sorted(set(fetch) | set(write)):
         if s in fetch and s in write:
             out["bytes_per_launch"][s] = round((2 * fetch[s][0] + write[s][0]) * 1024)
             out["raw_kib"][s] = {"FETCH_SIZE": fetch[s][0], "WRITE_SIZE": write[s][0], "dispatches": fetch[s][1]}
