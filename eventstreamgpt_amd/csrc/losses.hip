@@ -225,12 +225,18 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
             const int j = j1 + 64 * it + lane;
             xs[it] = j < n ? to_f32(zrow[tm.col + j]) : 0.f;
           }
+          // multi-hot labels of this pass group: each of the M entries marks the (column group, lane) holding its
+          // label — M readlanes per group of 64·kPass columns instead of M per column
+          uint32_t ymask = 0;
+          for (int m = 0; m < M; ++m) {
+            const int rel = __builtin_amdgcn_readlane(my_lab, m) - j1;  // my_lab = -1: not this term's entry
+            if (rel >= 0 && rel < 64 * kPass && (rel & 63) == lane) ymask |= 1u << (rel >> 6);
+          }
 #pragma unroll
           for (int it = 0; it < kPass; ++it) {
             const int j = j1 + 64 * it + lane;
             if (j1 + 64 * it >= n) break;  // wave-uniform
-            bool y = false;
-            for (int m = 0; m < M; ++m) y |= __builtin_amdgcn_readlane(my_lab, m) == j;
+            const bool y = (ymask >> it) & 1u;
             if (j < n) {
               // BCE-with-logits and its gradient from ONE exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32):
               // e = exp(-|x|), loss = max(x, 0) - x·y + log(1 + e), sigmoid(x) = x >= 0 ? 1/(1+e) : e/(1+e)
