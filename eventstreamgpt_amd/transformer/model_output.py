@@ -71,25 +71,26 @@ def _slice_value(val, idx):
         return LogNormalMixtureDistribution(locs[idx], log_scales[idx], log_weights[idx], val.mean_log_inter_time,
                                             val.std_log_inter_time)
     if isinstance(val, D.Bernoulli):
-        return D.Bernoulli(logits=val.logits[idx])
+        return D.Bernoulli(logits=val.logits[idx], validate_args=False)
     if isinstance(val, D.Categorical):
-        return D.Categorical(logits=val.logits[idx])
+        return D.Categorical(logits=val.logits[idx], validate_args=False)
     if isinstance(val, D.Normal):
-        return D.Normal(loc=val.loc[idx], scale=val.scale[idx])
+        return D.Normal(loc=val.loc[idx], scale=val.scale[idx], validate_args=False)
     if isinstance(val, D.Exponential):
-        return D.Exponential(rate=val.rate[idx])
+        return D.Exponential(rate=val.rate[idx], validate_args=False)
     if isinstance(val, D.Distribution):
         raise IndexError(f"eventstreamgpt_amd: cannot slice distribution {type(val).__name__}")
     return val[idx]
 
 
-def strip_unused_indices(dynamic_indices, *other_tensors):
+def strip_unused_indices(dynamic_indices, *other_tensors, width: int | None = None):
     """Moves the non-zero entries of ``dynamic_indices`` to the front of the last dim (stable) and trims it to the
     largest per-row count; ``other_tensors`` follow the same permutation, zero-filled (``model_output.py:108-169``).
-    The output width is data-dependent (one host read, as in the reference)."""
+    The output width is data-dependent: one host read unless the caller passes it (``width``)."""
     present = dynamic_indices != 0
     n = present.sum(-1)
-    width = int(n.max()) if n.numel() else 0
+    if width is None:
+        width = int(n.max()) if n.numel() else 0
     order = torch.argsort((~present).to(torch.int8), dim=-1, stable=True)[..., :width]
     keep = torch.arange(width, device=dynamic_indices.device) < n.unsqueeze(-1)
 
@@ -165,12 +166,25 @@ class GenerativeSequenceModelSamples(ModelOutput):
             # along dim 0 only, so both come out as [B, 0].
             z = torch.zeros(batch.batch_size, 0, dtype=torch.long, device=batch.device)
             cat = [z, torch.zeros_like(z), torch.zeros_like(z).float(), torch.zeros_like(z).bool()]
+        if not di:  # nothing to compact: skip the width read
+            return (self.time_to_event, event_mask, *cat)
         return (self.time_to_event, event_mask, *strip_unused_indices(*cat))
 
     def format_updates_to_last_batch_event(self, batch: PytorchBatch, config, measurements_to_build=None):
         """Sampled contents of ``measurements_to_build`` as (indices, meas, values, values_mask) [B, n]
         (``:392-616``)."""
+        raw, bad = self._format_updates_raw(batch, config, measurements_to_build)
+        if bad is not None and bool(bad.any()):
+            raise ValueError("For {measurement}, need preds < vocab_size!")
+        return strip_unused_indices(*raw)
+
+    def _format_updates_raw(self, batch: PytorchBatch, config, measurements_to_build):
+        """The updates before the final compaction, plus a device flag of out-of-range single-label samples (the
+        reference raises on them; the caller reads the flag with its other host reads). The reference compacts
+        each multi-label block on the way too; the final stable compaction gives the same result without those
+        host reads."""
         di, dm, dv, dvm = [], [], [], []
+        bad = []
 
         def zeros_like_last():
             dv.append((0 * di[-1]).float())
@@ -188,8 +202,7 @@ class GenerativeSequenceModelSamples(ModelOutput):
             preds = self.classification[m]
             if len(preds.shape) != 1:
                 raise ValueError(f"For {m}, expect 1D preds, got {preds.shape}!")
-            if (preds >= size).any():
-                raise ValueError("For {measurement}, need preds < vocab_size!")
+            bad.append((preds >= size).any())
             idx = off + preds
             di.append(idx.unsqueeze(-1))
             dm.append((config.measurements_idxmap[m] * torch.ones_like(idx)).unsqueeze(-1))
@@ -209,7 +222,7 @@ class GenerativeSequenceModelSamples(ModelOutput):
             if preds.shape[-1] != size:
                 raise ValueError(f"For {m}, expect preds.shape[-1] == vocab_size, got {preds.shape[-1]}!")
             idx = (torch.arange(size, device=preds.device).long() + off).unsqueeze(0).expand_as(preds)
-            idx = strip_unused_indices(torch.where(preds == 1, idx, 0))
+            idx = torch.where(preds == 1, idx, 0)
             di.append(idx)
             dm.append(config.measurements_idxmap[m] * (idx != 0).long())
             return True
@@ -271,13 +284,14 @@ class GenerativeSequenceModelSamples(ModelOutput):
             elif modality == DataModality.MULTIVARIATE_REGRESSION and group_mode == MeasIndexGroupOptions.NUMERICAL_ONLY:
                 mi = config.measurements_idxmap[m]
                 existing = batch.dynamic_measurement_indices[:, -1] == mi
-                idx = strip_unused_indices(torch.where(existing, batch.dynamic_indices[:, -1], 0))
+                idx = torch.where(existing, batch.dynamic_indices[:, -1], 0)
                 di.append(idx)
                 dm.append(mi * torch.ones_like(idx))
                 add_multivariate(m, indices=idx)
             else:
                 raise ValueError(f"{modality}, {group_mode} invalid!")
-        return strip_unused_indices(torch.cat(di, 1), torch.cat(dm, 1), torch.cat(dv, 1), torch.cat(dvm, 1))
+        raw = (torch.cat(di, 1), torch.cat(dm, 1), torch.cat(dv, 1), torch.cat(dvm, 1))
+        return raw, (torch.stack(bad) if bad else None)
 
     @staticmethod
     def pad_data_elements(batch: PytorchBatch, new_di, new_dm, new_dv, new_dvm):
@@ -333,13 +347,22 @@ class GenerativeSequenceModelSamples(ModelOutput):
             raise ValueError("You shouldn't ever be trying to fill the 'time' aspect of a batch!")
         prev = (batch.dynamic_indices[:, -1], batch.dynamic_measurement_indices[:, -1], batch.dynamic_values[:, -1],
                 batch.dynamic_values_mask[:, -1])
-        new = self.format_updates_to_last_batch_event(batch, config, measurements_to_build=measurements_to_fill)
+        raw, bad = self._format_updates_raw(batch, config, measurements_to_fill)
         drop = torch.zeros_like(prev[0], dtype=torch.bool)
         for m in measurements_to_fill:
             if type(m) is not tuple or m[1] != MeasIndexGroupOptions.NUMERICAL_ONLY:
                 continue
             drop |= prev[1] == config.measurements_idxmap[m[0]]
-        prev = strip_unused_indices(*[torch.where(drop, 0, t) for t in prev])
+        prev = [torch.where(drop, 0, t) for t in prev]
+        # ONE host read: both compacted widths and the out-of-range flag
+        flags = [(prev[0] != 0).sum(-1).max(), (raw[0] != 0).sum(-1).max()]
+        if bad is not None:
+            flags.append(bad.any().long())
+        read = torch.stack([f.long() for f in flags]).tolist()
+        if bad is not None and read[2]:
+            raise ValueError("For {measurement}, need preds < vocab_size!")
+        prev = strip_unused_indices(*prev, width=read[0])
+        new = strip_unused_indices(*raw, width=read[1])
         new = [torch.cat((p, n), 1) for p, n in zip(prev, new)]
         (di, dm, dv, dvm), (ndi, ndm, ndv, ndvm) = self.pad_data_elements(batch, *new)
         di, dm, dv, dvm = di.clone(), dm.clone(), dv.clone(), dvm.clone()
@@ -562,16 +585,17 @@ class GenerativeOutputLayerBase(torch.nn.Module):
             vs = c.vocab_offsets_by_measurement[m]
             sc = scores[:, :, vs:self._vocab_end(vs)]
             if mode == DataModality.SINGLE_LABEL_CLASSIFICATION:
-                cls[m] = (D_.Bernoulli(logits=is_obs[:, :, c.measurements_idxmap[m] - 1]), D_.Categorical(logits=sc))
+                cls[m] = (D_.Bernoulli(logits=is_obs[:, :, c.measurements_idxmap[m] - 1], validate_args=False),
+                          D_.Categorical(logits=sc, validate_args=False))
             else:
-                cls[m] = (None, D_.Bernoulli(logits=sc))
+                cls[m] = (None, D_.Bernoulli(logits=sc, validate_args=False))
         reg = {}
         for m in c.measurements_for(DataModality.MULTIVARIATE_REGRESSION):
             if reg_meas is None or m in reg_meas:
                 reg[m] = (None, self.regression_layers[m](X=encoded, idx=None))
         for m in c.measurements_for(DataModality.UNIVARIATE_REGRESSION):
             if reg_meas is None or m in reg_meas:
-                reg[m] = (D_.Bernoulli(logits=is_obs[:, :, c.measurements_idxmap[m] - 1]),
+                reg[m] = (D_.Bernoulli(logits=is_obs[:, :, c.measurements_idxmap[m] - 1], validate_args=False),
                           self.regression_layers[m](X=encoded))
         return cls, reg
 
