@@ -358,7 +358,7 @@ def main():
         "data": "synthetic (EHR-shaped batches, random-init weights)",
         "config": {"workload": f"{args.config}: {bc.name}", "model": "CIPPT" if "CI" in bc.name else "NAPPT",
                    "global_batch": bc.batch_size * world, "seq_len": bc.seq_len, "parallelism": f"dp{world}",
-                   "events_per_step_per_gpu": round(sum(events) / n_batches, 1), "hip_graph": use_graph,
+                   "events_per_step_per_gpu": round(sum(events) / n_batches, 1), "hip_graph": ts.use_graph,
                    "dropout": {"input": 0.1, "resid": 0.1, "attention": 0.1}},
         "roofline": roofline,
         "roofline_aux": aux,

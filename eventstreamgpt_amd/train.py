@@ -102,6 +102,20 @@ class FusedAdamW:
                                   "weight_decay": self.weight_decay}]}
 
 
+def graph_safe(model) -> bool:
+    """True when the model's training step runs entirely through the fused CI path (capturable)."""
+    from .fused import fused_supported
+    from .transformer.config import StructuredEventProcessingMode
+
+    enc = getattr(model, "encoder", None)
+    cfg = getattr(model, "config", None)
+    if enc is None or cfg is None:
+        return False
+    if cfg.structured_event_processing_mode != StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT:
+        return False
+    return fused_supported(enc)
+
+
 class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False):
@@ -134,7 +148,10 @@ class TrainStep:
         else:
             self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
             self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, self.lr_lambda)
-        self.use_graph = use_graph
+        # HIP-graph capture only for the fully fused CI step (every kernel ours). The module-by-module paths (NA
+        # blocks, unsupported CI shapes) run PyTorch-ROCm GEMMs whose bias-gradient results were garbage on graph
+        # replay (tools/na_graph_check.py: c_fc.bias gradients ~1e38 from the second replay on); they run eagerly.
+        self.use_graph = use_graph and graph_safe(model)
         self.graph = None
         self.static_batch = None
         self.static_loss = None
