@@ -1,13 +1,15 @@
 // Causal / local-window attention for gfx950 (InnerSelfAttention._attn, transformer.py:171-217).
 //
-// Two implementations behind one entry point:
+// Three implementations behind one entry point:
 //   * attn_*_generic  — one lane per query (forward, dQ) or per key (dK/dV), f32 arithmetic, any head dim up to
 //     128, f32 or bf16 I/O. Lanes of a wave hold consecutive queries of one (batch, head), so every K/V (or Q/dO)
-//     row load in the key loop is wave-uniform (a broadcast). Used for the f32 parity mode and for the short
-//     dependency-graph sequences of the NA model (Lk = G + 1 <= 9), where a flash tile would be mostly padding.
+//     row load in the key loop is wave-uniform (a broadcast). Used for the f32 parity mode and for sequences
+//     longer than 16 without an MFMA path.
+//   * attn_*_small — Lk <= 16 (the NA model's dependency-graph sequences, Lk = G + 1): one wave per (sequence,
+//     head), lane = head dimension, K / V in registers, one fused backward pass.
 //   * attn_*_mfma (attention_mfma.hip) — bf16 v_mfma_f32_32x32x16_bf16 flash kernels for hd in {32, 64, 128}.
 //
-// Semantics (both): s_ij = q_i . k_j in f32 with NO 1/sqrt(hd) scaling; key j is visible to query i (at key
+// Semantics (all): s_ij = q_i . k_j in f32 with NO 1/sqrt(hd) scaling; key j is visible to query i (at key
 // position p_i = i + Lk - Lq) iff j <= p_i, (local) p_i - j < window, and key_mask[j]; softmax in f32; the
 // attention-probability dropout of the reference (transformer.py:208, nn.Dropout on attn_weights) multiplies
 // p_ij by keep_ij / (1 - p) with keep regenerated from a counter hash of (seed, (bh*Lq + i)*Lk + j);
@@ -214,6 +216,201 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(
   }
 }
 
+// ---- short sequences (Lk <= 16: the NA dependency graph, G + 1 tokens) ----------------------------------------
+// One wave per (sequence, head), lane = head dimension (DPL dims per lane): every row load is one coalesced wave
+// load, the whole sequence's K / V (and dK / dV) stay in registers, scores and dP are wave reductions, and the
+// backward is ONE pass (dQ, dK, dV without the generic kernels' per-lane row walks or a second launch). Same
+// visibility, masking, dropout-hash and zero-row semantics as the generic kernels above.
+constexpr int kSmallLk = 16;
+
+template <typename T, int DPL, int LKM>
+__global__ __launch_bounds__(256) void attn_fwd_small(const T* __restrict__ q, const T* __restrict__ k,
+                                                      const T* __restrict__ v, int64_t ld_in, int64_t tq,
+                                                      T* __restrict__ o, int64_t ld_o, float* __restrict__ lse,
+                                                      const uint8_t* __restrict__ kmask,
+                                                      const uint8_t* __restrict__ qmask, int64_t B, int64_t H,
+                                                      int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
+                                                      const uint64_t* __restrict__ seed) {
+  const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;  // wave-uniform
+  const int lane = lane_id();
+  const int64_t h = bh % H, b = bh / H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
+  float kr[LKM][DPL], vr[LKM][DPL];
+  bool kv[LKM];
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    kv[j] = j < Lk && (!kmask || kmask[b * Lk + j] != 0);
+    const T* kp = k + (b * Lk + min((int64_t)j, Lk - 1)) * ld_in + h * hd;
+    const T* vp = v + (b * Lk + min((int64_t)j, Lk - 1)) * ld_in + h * hd;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) {
+      const int d = lane + 64 * u;
+      kr[j][u] = (j < Lk && d < hd) ? to_f32(kp[d]) : 0.f;
+      vr[j][u] = (j < Lk && d < hd) ? to_f32(vp[d]) : 0.f;
+    }
+  }
+  for (int64_t i = 0; i < Lq; ++i) {
+    const int64_t pos = i + (Lk - Lq);
+    const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+    const bool qvalid = qmask ? (qmask[b * Lq + i] != 0) : true;
+    const T* qp = q + (b * tq + i) * ld_in + h * hd;
+    float qr[DPL];
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) qr[u] = (lane + 64 * u < hd) ? to_f32(qp[lane + 64 * u]) : 0.f;
+    float s[LKM];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < LKM; ++j) {
+      s[j] = -INFINITY;
+      if (qvalid && kv[j] && j >= jlo && j <= pos) {  // wave-uniform
+        float t = 0.f;
+#pragma unroll
+        for (int u = 0; u < DPL; ++u) t = fmaf(qr[u], kr[j][u], t);
+        s[j] = wave_sum(t);
+        m = fmaxf(m, s[j]);
+      }
+    }
+    float l = 0.f, acc[DPL];
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) acc[u] = 0.f;
+#pragma unroll
+    for (int j = 0; j < LKM; ++j) {
+      if (s[j] == -INFINITY) continue;
+      const float p = expf(s[j] - m);
+      l += p;  // normaliser over undropped probabilities
+      const float pd = dr.p > 0.f ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, i, j)) : p;
+#pragma unroll
+      for (int u = 0; u < DPL; ++u) acc[u] = fmaf(pd, vr[j][u], acc[u]);
+    }
+    const bool ok = qvalid && l > 0.f;
+    const float inv = ok ? 1.f / l : 0.f;
+    T* op = o + (b * Lq + i) * ld_o + h * hd;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u)
+      if (lane + 64 * u < hd) op[lane + 64 * u] = from_f32<T>(acc[u] * inv);
+    if (lane == 0) lse[bh * Lq + i] = ok ? m + logf(l) : 0.f;
+  }
+}
+
+template <typename T, int DPL, int LKM>
+__global__ __launch_bounds__(256) void attn_bwd_small(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
+    const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
+    const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, T* __restrict__ dk,
+    T* __restrict__ dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window,
+    float drop_p, const uint64_t* __restrict__ seed) {
+  const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;  // wave-uniform
+  const int lane = lane_id();
+  const int64_t h = bh % H, b = bh / H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
+  float kr[LKM][DPL], vr[LKM][DPL], dka[LKM][DPL], dva[LKM][DPL];
+  bool kv[LKM];
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    kv[j] = j < Lk && (!kmask || kmask[b * Lk + j] != 0);
+    const T* kp = k + (b * Lk + min((int64_t)j, Lk - 1)) * ld_in + h * hd;
+    const T* vp = v + (b * Lk + min((int64_t)j, Lk - 1)) * ld_in + h * hd;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) {
+      const int d = lane + 64 * u;
+      kr[j][u] = (j < Lk && d < hd) ? to_f32(kp[d]) : 0.f;
+      vr[j][u] = (j < Lk && d < hd) ? to_f32(vp[d]) : 0.f;
+      dka[j][u] = dva[j][u] = 0.f;
+    }
+  }
+  for (int64_t i = 0; i < Lq; ++i) {
+    const int64_t pos = i + (Lk - Lq);
+    const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+    const bool qvalid = qmask ? (qmask[b * Lq + i] != 0) : true;
+    const T* qp = q + (b * tq + i) * ld_in + h * hd;
+    const T* dop = dout + (b * Lq + i) * ld_do + h * hd;
+    const T* opp = o + (b * Lq + i) * ld_o + h * hd;
+    float qr[DPL], dor[DPL], dqa[DPL];
+    float dl = 0.f;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) {
+      const int d = lane + 64 * u;
+      qr[u] = d < hd ? to_f32(qp[d]) : 0.f;
+      dor[u] = d < hd ? to_f32(dop[d]) : 0.f;
+      dl = fmaf(dor[u], d < hd ? to_f32(opp[d]) : 0.f, dl);
+      dqa[u] = 0.f;
+    }
+    dl = qvalid ? wave_sum(dl) : 0.f;  // delta = rowsum(dO o O)
+    const float ls = lse[bh * Lq + i];
+#pragma unroll
+    for (int j = 0; j < LKM; ++j) {
+      if (!(qvalid && kv[j] && j >= jlo && j <= pos)) continue;  // wave-uniform
+      float s = 0.f, dpv = 0.f;
+#pragma unroll
+      for (int u = 0; u < DPL; ++u) {
+        s = fmaf(qr[u], kr[j][u], s);
+        dpv = fmaf(dor[u], vr[j][u], dpv);
+      }
+      s = wave_sum(s);
+      dpv = wave_sum(dpv);
+      const float keep = dr.p > 0.f ? dropout_mult(dr, elem_index(bh, Lq, Lk, i, j)) : 1.f;
+      const float p = expf(s - ls);
+      const float ds = p * (dpv * keep - dl);
+      const float pd = p * keep;
+#pragma unroll
+      for (int u = 0; u < DPL; ++u) {
+        dqa[u] = fmaf(ds, kr[j][u], dqa[u]);
+        dka[j][u] = fmaf(ds, qr[u], dka[j][u]);
+        dva[j][u] = fmaf(pd, dor[u], dva[j][u]);
+      }
+    }
+    T* dqp = dq + (b * tq + i) * ld_d + h * hd;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u)
+      if (lane + 64 * u < hd) dqp[lane + 64 * u] = from_f32<T>(dqa[u]);
+  }
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    if (j >= Lk) break;
+    T* dkp = dk + (b * Lk + j) * ld_d + h * hd;
+    T* dvp = dv + (b * Lk + j) * ld_d + h * hd;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u) {
+      const int d = lane + 64 * u;
+      if (d < hd) {
+        dkp[d] = from_f32<T>(dka[j][u]);
+        dvp[d] = from_f32<T>(dva[j][u]);
+      }
+    }
+  }
+}
+
+template <typename T>
+int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                 int64_t ld_o, float* lse_w, const float* lse_r, const void* dout, int64_t ld_do,
+                 const uint8_t* kmask, const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B,
+                 int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                 hipStream_t st) {
+  const dim3 grid((unsigned)cdiv(B * H, 4)), block(256);
+#define SMALL(DPL, LKM)                                                                                             \
+  do {                                                                                                              \
+    if (fwd)                                                                                                        \
+      attn_fwd_small<T, DPL, LKM><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (T*)o, \
+                                                          ld_o, lse_w, kmask, qmask, B, H, Lq, Lk, (int)hd, window,  \
+                                                          drop_p, seed);                                           \
+    else                                                                                                            \
+      attn_bwd_small<T, DPL, LKM><<<grid, block, 0, st>>>(                                                          \
+          (const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o, ld_o, (const T*)dout, ld_do, lse_r, kmask, \
+          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed);                        \
+  } while (0)
+  if (hd <= 64) {
+    if (Lk <= 8) SMALL(1, 8);
+    else SMALL(1, 16);
+  } else {
+    if (Lk <= 8) SMALL(2, 8);
+    else SMALL(2, 16);
+  }
+#undef SMALL
+  return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+}
+
 template <typename T>
 int launch_fwd_generic(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
                        float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
@@ -297,6 +494,13 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return esgpt_attn_fwd_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
                                dropout_p, seed, st);
+  if (Lk <= kSmallLk && !force_generic()) {
+    if (dtype == ESGPT_F32)
+      return launch_small<float>(true, q, k, v, ld_in, tq, o, ld_o, lse, nullptr, nullptr, 0, key_mask, query_mask,
+                                 nullptr, nullptr, nullptr, 0, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+    return launch_small<bf16>(true, q, k, v, ld_in, tq, o, ld_o, lse, nullptr, nullptr, 0, key_mask, query_mask,
+                              nullptr, nullptr, nullptr, 0, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+  }
   if (dtype == ESGPT_F32)
     return launch_fwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
                                      dropout_p, seed, st);
@@ -329,6 +533,13 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
     return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
                                ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, (float*)workspace, counters,
                                st);
+  if (Lk <= kSmallLk && !force_generic()) {
+    if (dtype == ESGPT_F32)
+      return launch_small<float>(false, q, k, v, ld_in, tq, o, ld_o, nullptr, lse, dout, ld_do, key_mask, query_mask,
+                                 dq, dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+    return launch_small<bf16>(false, q, k, v, ld_in, tq, o, ld_o, nullptr, lse, dout, ld_do, key_mask, query_mask,
+                              dq, dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+  }
   if (dtype == ESGPT_F32)
     return launch_bwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
                                      ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);
