@@ -461,3 +461,49 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
             nxt = blocks[i + 1].attn.layer_norm if i + 1 < len(blocks) else encoder.ln_f
             h, ln = ResidualLNFn.apply(h1, y2, blk.mlp.c_proj.bias, nxt.weight, nxt.bias, rows, p_res, eps, dt)
     return ln.view(B, Lq, D)
+
+
+def block_fused_supported(blk, hidden: torch.Tensor) -> bool:
+    """An ``InnerBlock`` can run through the HIP kernels (bf16 autocast on a HIP tensor, GEMM-friendly shapes)."""
+    if not (hidden.is_cuda and compute_dtype() == torch.bfloat16 and ENABLED):
+        return False
+    cfg_act = getattr(blk.mlp, "act_name", None)
+    D = hidden.shape[-1]
+    F_ = blk.mlp.c_fc.out_features
+    n_tok = hidden.numel() // D
+    return (cfg_act in _ACTS and D % 8 == 0 and F_ % 8 == 0 and n_tok % 8 == 0 and D <= 1024
+            and blk.attn.attention.head_dim <= 128)
+
+
+def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_first: bool) -> torch.Tensor:
+    """``InnerBlock.forward`` (``transformer.py:409-461``, pre-LN attention + MLP with residuals) through the HIP
+    kernels: LayerNorm, one packed-QKV GEMM, attention, out_proj with its bias + residual dropout + the second
+    LayerNorm fused, the MLP GEMMs (bias + activation epilogue) — the same pieces as the fused CI encoder, for a
+    stand-alone block (the NA sequence and dependency-graph modules). ``hidden`` [Bs, T, D] f32; returns
+    [Bs, T - skf, D] f32."""
+    att = blk.attn.attention
+    Bs, T, D = hidden.shape
+    skf = 1 if static_kv_first else 0
+    eps = float(blk.layer_norm.eps)
+    train = blk.training
+    p_res = float(att.resid_dropout.p) if train else 0.0
+    p_att = att.attn_dropout_p if train else 0.0
+    dt = torch.bfloat16
+    wqkv, wo, wfc, wpj = weight_shadow([blk], dt)[0]
+    ln1 = blk.attn.layer_norm
+    x2 = hidden.reshape(Bs * T, D).float().contiguous()
+    kpm = None if key_padding_mask is None else key_padding_mask.contiguous()
+    qpm = None if (kpm is None or static_kv_first) else kpm
+    window = att.window_size if att.attention_type == "local" else 0
+    with torch.autocast("cuda", enabled=False):
+        _, ln = ResidualLNFn.apply(None, x2, None, ln1.weight, ln1.bias, None, 0.0, eps, dt)
+        qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight)).view(Bs, T, 3 * D)
+        o = AttentionFn.apply(qkv, kpm, qpm, att.num_heads, window, static_kv_first, p_att)
+        Tq = T - skf
+        y = proj(o.reshape(Bs * Tq, D), wo, None, (att.out_proj.weight,))
+        res = hidden[:, skf:, :].reshape(Bs * Tq, D).float().contiguous()
+        h1, ln2 = ResidualLNFn.apply(res, y, att.out_proj.bias, blk.layer_norm.weight, blk.layer_norm.bias, None,
+                                     p_res, eps, dt)
+        y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name])
+        out = h1 + F.dropout(y2.float() + blk.mlp.c_proj.bias, p=p_res, training=train)
+    return out.view(Bs, Tq, D)

@@ -107,6 +107,10 @@ def graph_safe(model) -> bool:
     from .fused import fused_supported
     from .transformer.config import StructuredEventProcessingMode
 
+    import os
+
+    if os.environ.get("ESGPT_FORCE_GRAPH") == "1":  # diagnostics (tools/na_graph_check.py)
+        return True
     enc = getattr(model, "encoder", None)
     cfg = getattr(model, "config", None)
     if enc is None or cfg is None:

@@ -164,6 +164,7 @@ class InnerMLP(nn.Module):
         self.c_fc = nn.Linear(embed_dim, inner_dim)
         self.c_proj = nn.Linear(inner_dim, embed_dim)
         self.act = _act(config.activation_function)
+        self.act_name = config.activation_function
         self.dropout = nn.Dropout(float(config.resid_dropout))
 
     def forward(self, hidden_states):
@@ -181,6 +182,14 @@ class InnerBlock(nn.Module):
 
     def forward(self, hidden_states, attention_mask=None, layer_past=None, head_mask=None, use_cache=False,
                 output_attentions=False, static_kv_first: bool = False, key_padding_mask=None):
+        from ..fused import block_fused_supported, inner_block_fused
+
+        if (layer_past is None and not use_cache and not output_attentions and head_mask is None
+                and block_fused_supported(self, hidden_states)):
+            kpm = key_padding_mask
+            if kpm is None and attention_mask is not None:
+                kpm = attention_mask.reshape(attention_mask.shape[0], -1) == 0
+            return inner_block_fused(self, hidden_states, kpm, static_kv_first), {}
         residual = hidden_states if not static_kv_first else hidden_states[:, 1:, :]
         attn_output, outputs = self.attn(hidden_states, attention_mask=attention_mask, layer_past=layer_past,
                                          head_mask=head_mask, use_cache=use_cache,

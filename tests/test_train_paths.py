@@ -37,3 +37,40 @@ def test_nested_attention_train_steps_finite():
         ts.check()
         assert all(torch.isfinite(p).all() for p in m.parameters())
     assert all(abs(a - b) < 1e-4 * max(1.0, abs(a)) for a, b in zip(losses[False], losses[True]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["na_small", "na_joint_attn"])
+def test_nested_attention_bf16_fused_blocks_match_module_path(name):
+    """bf16: the NA blocks through the HIP kernels (fused.inner_block_fused) against the PyTorch module path, and the
+    loss against the reference's f32 golden value (bf16 tolerance)."""
+    from helpers import load_case
+
+    from eventstreamgpt_amd import fused
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    fx, cfg, batch = load_case(name)
+    b = batch.to("cuda")
+    res = {}
+    for enabled in (True, False):
+        fused.ENABLED = enabled
+        try:
+            m = NAPPTForGenerativeSequenceModeling(cfg)
+            m.load_state_dict(fx["state_dict"])
+            m = m.cuda().train()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = m(b)
+            out.loss.backward()
+            res[enabled] = (float(out.loss), {k: p.grad.detach().float().clone() for k, p in m.named_parameters()
+                                              if p.grad is not None})
+        finally:
+            fused.ENABLED = True
+    (lf, gf), (lm, gm) = res[True], res[False]
+    want = float(fx["loss"])
+    assert abs(lf - want) <= 2e-2 * abs(want), (lf, want)
+    assert abs(lf - lm) <= 2e-2 * abs(lm), (lf, lm)
+    assert set(gf) == set(gm)
+    for k in gm:
+        scale = gm[k].abs().max().clamp_min(1e-6)
+        assert torch.isfinite(gf[k]).all(), k
+        assert ((gf[k] - gm[k]).abs().max() / scale).item() < 0.1, k

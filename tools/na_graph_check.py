@@ -49,5 +49,5 @@ def run(graph: bool):
 
 
 eager = run(False)
-graph = run(True)
+graph = run(os.environ.get("EAGER2") != "1")  # EAGER2=1: eager twice (run-to-run determinism)
 print("eager vs graph:", [f"{a - b:.2e}" for a, b in zip(eager, graph)], flush=True)
