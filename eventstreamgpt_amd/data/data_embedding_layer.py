@@ -175,7 +175,16 @@ class DataEmbeddingLayer(torch.nn.Module):
                               cat_scale, num_scale, static_scale)
         w = torch.cat([self.cat_proj.weight, self.num_proj.weight], dim=1)
         bias = (cat_scale + static_scale) * self.cat_proj.bias + num_scale * self.num_proj.bias
-        y = torch.nn.functional.linear(x, w, bias).float()
+        from ..fused import ProjFn, compute_dtype, gemm_supported
+
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.is_cuda and compute_dtype() == torch.bfloat16 and gemm_supported(x2.shape[0], w.shape[1], w.shape[0]):
+            # bf16: the HIP GEMM (bias in the epilogue; dW, db in one grouped backward launch)
+            with torch.autocast("cuda", enabled=False):
+                y = ProjFn.apply(x2.to(torch.bfloat16).contiguous(), w.detach().to(torch.bfloat16),
+                                 bias.float().contiguous(), w).float().view(*x.shape[:-1], w.shape[0])
+        else:
+            y = torch.nn.functional.linear(x, w, bias).float()
         return EmbedEpilogueFn.apply(y, bv, G, post, sin_div, cos_div)
 
     def forward(self, batch: PytorchBatch) -> torch.Tensor:

@@ -88,17 +88,9 @@ class InnerSelfAttention(nn.Module):
         self.out_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=True)
 
     def _packed_qkv_weight(self):
-        """[q; k; v] weights as one [3D, D] matrix (one GEMM for the three projections). Outside autograd (e.g. the
-        generation loop) the packed copy is cached until a weight changes (tensor version counters)."""
-        ws = (self.q_proj.weight, self.k_proj.weight, self.v_proj.weight)
-        if torch.is_grad_enabled() and any(w.requires_grad for w in ws):
-            return torch.cat(ws, dim=0)
-        key = tuple((w.data_ptr(), w._version, w.dtype, w.device) for w in ws)
-        cached = getattr(self, "_qkv_cache", None)
-        if cached is None or cached[0] != key:
-            cached = (key, torch.cat([w.detach() for w in ws], dim=0))
-            self._qkv_cache = cached
-        return cached[1]
+        """[q; k; v] weights as one [3D, D] matrix (one GEMM for the three projections). Not cached: the fused AdamW
+        updates weights in place through raw pointers, which version counters do not see."""
+        return torch.cat([self.q_proj.weight, self.k_proj.weight, self.v_proj.weight], dim=0)
 
     def forward(self, hidden_states, attention_mask=None, layer_past=None, head_mask=None, use_cache=False,
                 output_attentions=False, static_kv_first: bool = False, key_padding_mask=None):
