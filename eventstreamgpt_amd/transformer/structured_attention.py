@@ -36,15 +36,15 @@ class StructuredAttention(torch.nn.Module):
         per_event = hidden_states[:, :, -1, :]
         if event_mask is not None:
             m3 = event_mask.unsqueeze(-1)
-            per_event = torch.where(m3, per_event, torch.zeros_like(per_event))
+            per_event = torch.where(m3, per_event, 0.0)
         ctx = self.seq_module(per_event, key_padding_mask=kpm, **seq_module_kwargs)
         seq_ret = None
         if isinstance(ctx, tuple):
             ctx, seq_ret = ctx
         if event_mask is not None:
-            ctx = torch.where(m3, ctx, torch.zeros_like(ctx))
+            ctx = torch.where(m3, ctx, 0.0)
 
-        history = torch.cat((torch.zeros_like(ctx[:, :1, :]), ctx[:, :-1, :]), dim=1)
+        history = torch.nn.functional.pad(ctx[:, :-1, :], (0, 0, 1, 0))  # [0, ctx_0 .. ctx_{L-2}]
         # [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i]: the last graph element is replaced by the contextualised
         # event (structured_attention.py:125-149).
         dep_graph_seq = torch.cat((history.unsqueeze(2), hidden_states[:, :, :-1, :], ctx.unsqueeze(2)), dim=2)
@@ -56,5 +56,5 @@ class StructuredAttention(torch.nn.Module):
             out, dep_ret = out
         out = out.reshape(bsz, seq_len, dep_graph_len, hidden_size)
         if event_mask is not None:
-            out = torch.where(event_mask[:, :, None, None], out, torch.zeros_like(out))
+            out = torch.where(event_mask[:, :, None, None], out, 0.0)
         return out, {"seq_module": seq_ret, "dep_graph_module": dep_ret}

@@ -340,7 +340,7 @@ class ConditionallyIndependentPointProcessTransformer(StructuredTransformerPreTr
                 all_hidden = all_hidden + (hidden,)
             hidden, _ = block(hidden, key_padding_mask=kpm)
             if m3 is not None:
-                hidden = torch.where(m3, hidden, torch.zeros_like(hidden))
+                hidden = torch.where(m3, hidden, 0.0)
         hidden = self.ln_f(hidden)
         if output_hidden_states:
             all_hidden = all_hidden + (hidden,)
@@ -378,7 +378,7 @@ class ConditionallyIndependentPointProcessTransformer(StructuredTransformerPreTr
                 all_hidden = all_hidden + (hidden,)
             hidden, extra = block(hidden, layer_past=layer_past, use_cache=use_cache, key_padding_mask=kpm)
             if m3 is not None:
-                hidden = torch.where(m3, hidden, torch.zeros_like(hidden))
+                hidden = torch.where(m3, hidden, 0.0)
             if use_cache:
                 presents = presents + (extra["present_key_value"],)
         hidden = self.ln_f(hidden)
