@@ -20,17 +20,21 @@ def grads(graph: bool):
     cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
     torch.manual_seed(0)
     m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
-    ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=10**9, max_training_steps=10**10),
+    ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=int(os.environ.get("WARM", 10**9)),
+                                                max_training_steps=10**10),
                    torch.bfloat16, use_graph=graph)
     out = []
     for b in batches:
         loss = float(ts.step(b))
         torch.cuda.synchronize()
-        out.append((loss, {n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None}))
+        out.append((loss, {n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None},
+                    {n: p.detach().float().clone() for n, p in m.named_parameters()}))
     return out
 
 
 e, g = grads(False), grads(True)
-for step, ((le, ge), (lg, gg)) in enumerate(zip(e, g)):
+for step, ((le, ge, pe), (lg, gg, pg)) in enumerate(zip(e, g)):
     diffs = sorted((((ge[k] - gg[k]).abs().max() / ge[k].abs().max().clamp_min(1e-12)).item(), k) for k in ge)[::-1]
-    print(f"step {step}: loss {le:.6f} vs {lg:.6f}; largest relative grad differences: {diffs[:5]}", flush=True)
+    pdiffs = sorted((((pe[k] - pg[k]).abs().max()).item(), k) for k in pe)[::-1]
+    print(f"step {step}: loss {le:.6f} vs {lg:.6f}; grad diffs {diffs[:3]}; param diffs after update {pdiffs[:3]}",
+          flush=True)
