@@ -62,7 +62,7 @@ _PK = ctypes.POINTER(EsgptBuckets)
 SIGNATURES = {
     "esgpt_version": (ctypes.c_char_p, []),
     "esgpt_adamw_chunk": (_i64, []),
-    "esgpt_adamw": (_int, [_vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i64, _vp]),
+    "esgpt_adamw": (_int, [_vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i64, _vp, _vp, _vp]),
     "esgpt_device_arch_ok": (_int, []),
     "esgpt_embed_joint_fwd": (_int, [_PB, _PK, _vp, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_embed_split_bags_fwd": (_int, [_PB, _PK, _vp, _i64, _vp, _i64, _i64, _int, _f32, _f32, _f32, _vp, _vp,

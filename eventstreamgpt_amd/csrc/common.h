@@ -85,6 +85,15 @@ __device__ __forceinline__ void set_err(int32_t* err, int code) {
   if (err) atomicOr(err, code);
 }
 
+// Out-of-range embedding index: the flag plus the largest offending index in the error block's int64 slot
+// (bytes 8..15), so the host can raise the reference's "Invalid embedding! {max} >= {V}".
+__device__ __forceinline__ void set_bad_index(int32_t* err, int64_t idx) {
+  if (err) {
+    atomicOr(err, ESGPT_FLAG_BAD_INDEX);
+    atomicMax(reinterpret_cast<long long*>(err + 2), (long long)idx);
+  }
+}
+
 // Dropout (attention probabilities, residual / input): a counter-based hash of (seed, element index), so the
 // forward and backward regenerate the same keep-mask without storing it. 32-bit arithmetic only (no 64-bit
 // multiplies in the hot loops): key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)) once per kernel, then per

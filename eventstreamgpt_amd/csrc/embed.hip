@@ -55,7 +55,7 @@ __device__ __forceinline__ Entry load_entry(const esgpt_batch& bt, int64_t e, in
     en.val = bt.dyn_vals[off];
     en.vmask = bt.dyn_vmask[off] != 0;
     if (en.idx < 0 || en.idx >= V) {
-      set_err(err, ESGPT_FLAG_BAD_INDEX);
+      set_bad_index(err, en.idx);
       en.idx = 0;
     }
   }
@@ -101,7 +101,7 @@ __device__ __forceinline__ void load_static(const esgpt_batch& bt, int64_t b, in
     sidx = bt.st_idx[b * S + lane];
     meas = bt.st_meas[b * S + lane];
     if (sidx < 0 || sidx >= V) {
-      set_err(err, ESGPT_FLAG_BAD_INDEX);
+      set_bad_index(err, sidx);
       sidx = 0;
     }
   }

@@ -21,7 +21,7 @@ namespace {
 constexpr int kWaves = 4;
 constexpr int kMaxM = 64;
 constexpr int kMaxK = 64;  // LNM components
-#define FLAG_BAD_LABEL 8
+
 
 constexpr float kHalfLog2Pi = 0.91893853320467274178f;
 constexpr float kTiny = 1.17549435e-38f;  // torch.finfo(torch.float32).tiny
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
         for (uint64_t bits = mm; bits; bits &= bits - 1) lab += readlane64(e_idx, __builtin_ctzll(bits));
         lab = has ? lab - tm.vocab_start : 0;
         if (mk && (lab < 0 || lab >= n)) {
-          set_err(err, FLAG_BAD_LABEL);
+          set_err(err, ESGPT_FLAG_BAD_LABEL);
           lab = 0;
         }
         float mx = -INFINITY;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
           if (sel) {
             j = e_idx - tm.vocab_start;
             if (j < 0 || j >= n_targets) {
-              set_err(err, FLAG_BAD_LABEL);
+              set_err(err, ESGPT_FLAG_BAD_LABEL);
               j = 0;
             }
             const float mu = to_f32(zrow[tm.col + 2 * j]);

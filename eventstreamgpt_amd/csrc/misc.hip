@@ -23,10 +23,18 @@ constexpr int kAdamChunk = 4096;
 
 __global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __restrict__ table,
                                                     const int64_t* __restrict__ blocks, float lr, float beta1,
-                                                    float beta2, float eps, float wd, float step_size,
-                                                    float bc2_sqrt) {
+                                                    float beta2, float eps, float wd, float step_size_all,
+                                                    float bc2_sqrt_all, const float* __restrict__ per_tensor,
+                                                    const int32_t* __restrict__ err) {
+  // A data-dependent error raised by this step's forward (bad embedding index, NaN TTE log-likelihood, subject
+  // without an observed TTE) leaves the parameters untouched: the reference raises before its optimizer step.
+  if (err != nullptr && err[0] != 0) return;
   const int64_t e = blocks[blockIdx.x];
-  const esgpt_adam_tensor t = table[e >> 40];
+  const int64_t ti = e >> 40;
+  const esgpt_adam_tensor t = table[ti];
+  // per-parameter step counts (torch keeps one `step` per parameter): (lr / bc1, sqrt(bc2)) per tensor
+  const float step_size = per_tensor ? per_tensor[2 * ti] : step_size_all;
+  const float bc2_sqrt = per_tensor ? per_tensor[2 * ti + 1] : bc2_sqrt_all;
   const int64_t start = e & ((1ll << 40) - 1);
   const int64_t end = start + kAdamChunk < t.n ? start + kAdamChunk : t.n;
   const float decay = 1.f - lr * wd;
@@ -82,13 +90,15 @@ const char* esgpt_version(void) { return "eventstreamgpt_amd 0.1.0 (gfx950)"; }
 int64_t esgpt_adamw_chunk(void) { return esgpt::kAdamChunk; }
 
 int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, float lr, float beta1,
-                float beta2, float eps, float weight_decay, int64_t step, void* stream) {
-  ESGPT_REQUIRE(table && blocks && n_blocks >= 0 && step >= 1);
+                float beta2, float eps, float weight_decay, int64_t step, const float* per_tensor,
+                const int32_t* err, void* stream) {
+  ESGPT_REQUIRE(table && blocks && n_blocks >= 0 && (step >= 1 || per_tensor != nullptr));
   if (n_blocks == 0) return ESGPT_OK;
-  const double bc1 = 1.0 - pow((double)beta1, (double)step), bc2 = 1.0 - pow((double)beta2, (double)step);
+  const double s = step >= 1 ? (double)step : 1.0;
+  const double bc1 = 1.0 - pow((double)beta1, s), bc2 = 1.0 - pow((double)beta2, s);
   esgpt::adamw_kernel<<<(unsigned)n_blocks, 256, 0, esgpt::as_stream(stream)>>>(table, blocks, lr, beta1, beta2, eps,
                                                                    weight_decay, (float)(lr / bc1),
-                                                                   (float)sqrt(bc2));
+                                                                   (float)sqrt(bc2), per_tensor, err);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

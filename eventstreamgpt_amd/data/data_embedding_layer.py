@@ -112,13 +112,17 @@ class DataEmbeddingLayer(torch.nn.Module):
             )
             self.num_proj = torch.nn.Linear(numerical_embedding_dim, out_dim)
         self._buckets = None
+        self._group_error = None
         if split_by_measurement_indices:
+            # The reference raises this in forward (_split_batch_into_measurement_index_buckets, :529-535), not at
+            # construction; the message is kept and raised on the first embedding call.
             for i, g in enumerate(split_by_measurement_indices):
                 if len(g) == 0 and i > 0:
-                    raise ValueError(
+                    self._group_error = (
                         f"Empty measurement index group: {g} at index {i}! Only the first (i=0) group can be empty "
                         "(in cases where there are no FUNCTIONAL_TIME_DEPENDENT measurements)."
                     )
+                    break
             from ..kernels import buckets_struct
 
             self._buckets = buckets_struct(split_by_measurement_indices)
@@ -149,6 +153,8 @@ class DataEmbeddingLayer(torch.nn.Module):
         masked by ``event_mask``. Returns f32 [B, L, G, D]."""
         from ..kernels import EmbedEpilogueFn, EmbedSpec, JointEmbedFn, SplitBagsFn, batch_view
 
+        if self._group_error is not None:
+            raise ValueError(self._group_error)
         bv = batch_view(batch)
         flags = self._flags()
         sin_div = cos_div = None

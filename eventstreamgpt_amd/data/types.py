@@ -217,16 +217,29 @@ class PytorchBatch:
         return out
 
     def packed(self) -> "PytorchBatch":
-        """A copy of this batch with every tensor field in one flat buffer on the same device."""
+        """A copy of this batch with every tensor field in one flat buffer on the same device (stream labels are
+        copied into tensors of their own, so the copy never aliases this batch's labels)."""
         spec = {k: (tuple(v.shape), v.dtype) for k, v in self.as_dict().items()}
         out = PytorchBatch.empty_packed(spec, device=self.device)
         for k, v in self.as_dict().items():
             getattr(out, k).copy_(v)
-        out.stream_labels = None if self.stream_labels is None else dict(self.stream_labels)
+        out.stream_labels = None if self.stream_labels is None else {k: v.clone() for k, v in self.stream_labels.items()}
         return out
 
+    def shape_signature(self) -> tuple:
+        """Names, shapes and dtypes of every tensor field and stream label: two batches with equal signatures can be
+        staged into each other's buffers (``copy_``); a captured HIP graph replays only batches of its signature."""
+        sig = tuple((k, tuple(v.shape), v.dtype) for k, v in self.as_dict().items())
+        sl = self.stream_labels
+        lab = () if sl is None else tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(sl.items()))
+        return sig, lab
+
     def copy_(self, src: "PytorchBatch", non_blocking: bool = False) -> "PytorchBatch":
-        """In-place copy of ``src``'s fields (same shapes): one buffer copy when both share a packed layout."""
+        """In-place copy of ``src``'s fields and stream labels: one buffer copy when both share a packed layout.
+        Shapes must match exactly (no broadcasting: a size-1 dimension would silently duplicate entries)."""
+        if self.shape_signature() != src.shape_signature():
+            raise ValueError(f"PytorchBatch.copy_: shape signature mismatch\n  dst {self.shape_signature()}\n"
+                             f"  src {src.shape_signature()}")
         a, b = self.flat_buffer(), src.flat_buffer()
         done = set()
         if a is not None and b is not None and self._flat_sig == src._flat_sig:
@@ -235,6 +248,9 @@ class PytorchBatch:
         for k, v in src.as_dict().items():
             if k not in done:
                 getattr(self, k).copy_(v, non_blocking=non_blocking)
+        if src.stream_labels is not None:
+            for k, v in src.stream_labels.items():
+                self.stream_labels[k].copy_(v, non_blocking=non_blocking)
         return self
 
     def to(self, device, non_blocking: bool = False) -> "PytorchBatch":

@@ -186,12 +186,18 @@ def linear_fwd_act(x, w, bias, act: int):
     return pre, y
 
 
+# Launch-shape recorder (bench.py: the in-step roofline of the grouped projection backward over every launch shape)
+SHAPES = {"enabled": False, "linear_bwd": []}
+
+
 def linear_bwd(dy, x, w, alpha=None, act: int = -1, pre=None, need_dx: bool = True, need_db: bool = False):
     """One launch for the backward of y = x · wᵀ: dx = alpha·dy·w [· act'(pre)] (bf16), dw = alpha·dyᵀ·x (f32) and
     db = alpha·Σ_rows dy (f32). ``alpha``: optional device scalar. Returns (dx | None, dw, db | None)."""
     lib = L.load()
     T, dout = dy.shape
     din = x.shape[1]
+    if SHAPES["enabled"]:
+        SHAPES["linear_bwd"].append((T, din, dout, bool(need_dx), int(act), bool(need_db)))
     dev = dy.device
     dw = torch.empty(dout, din, dtype=torch.float32, device=dev)
     dx = torch.empty(T, din, dtype=dy.dtype, device=dev) if need_dx else None

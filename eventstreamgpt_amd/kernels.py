@@ -94,15 +94,61 @@ def batch_view(batch: PytorchBatch) -> BatchView:
 
 
 _ERR: dict[int, torch.Tensor] = {}
+_LAST_V: dict[int, int] = {}
+
+
+def _dev_index(device: torch.device) -> int:
+    return device.index if device.index is not None else torch.cuda.current_device()
 
 
 def err_word(device: torch.device) -> torch.Tensor:
-    idx = device.index if device.index is not None else torch.cuda.current_device()
+    """The device error block of the C ABI (16 bytes: int32 ESGPT_FLAG_* bits, pad, int64 max bad index), viewed as
+    int64 [2]. Kernels OR flags into it; esgpt_adamw is a no-op while the flags are set."""
+    idx = _dev_index(device)
     w = _ERR.get(idx)
     if w is None:
-        w = torch.zeros(1, dtype=torch.int32, device=device)
+        w = torch.zeros(2, dtype=torch.int64, device=torch.device("cuda", idx))
         _ERR[idx] = w
     return w
+
+
+def note_vocab(device: torch.device, V: int) -> None:
+    """Remembers the table size of the latest embedding launch (the ``n_total_embeddings`` of its message)."""
+    _LAST_V[_dev_index(device)] = int(V)
+
+
+def raise_for_error(code: int, max_index: int, n_total_embeddings: int | None = None, batch=None) -> None:
+    """The reference's exception for an error block's flags, in the reference's check order:
+    ``torch._assert(indices.max() < V, f"Invalid embedding! {indices.max()} >= {V}")``
+    (data_embedding_layer.py:485-488), then the TTE checks of get_TTE_outputs (model_output.py:1360-1367):
+    ``ValueError(f"NaNs in TTE_LL: {batch}")`` before ``ValueError(f"No observed time-to-event for >= 1 patient in
+    batch: {batch}")``."""
+    code &= 0xFFFFFFFF
+    if not code:
+        return
+    tail = "" if batch is None else f": {batch}"
+    if code & L.FLAG_BAD_INDEX:
+        raise AssertionError(f"Invalid embedding! {torch.tensor(max_index)} >= {n_total_embeddings}")
+    if code & L.FLAG_TTE_NAN:
+        raise ValueError(f"NaNs in TTE_LL{tail}")
+    if code & L.FLAG_TTE_NO_OBS:
+        raise ValueError(f"No observed time-to-event for >= 1 patient in batch{tail}")
+    if code & L.FLAG_BAD_LABEL:
+        raise IndexError("Target out of bounds in classification / regression labels")
+    raise RuntimeError(f"eventstreamgpt_amd: unknown device error flags {code:#x}")
+
+
+def check_errors(device: torch.device | None = None, n_total_embeddings: int | None = None, batch=None):
+    """Reads (one host sync) and clears the device error block; raises the reference's exception for it.
+    ``n_total_embeddings`` defaults to the table size of the latest embedding launch on the device."""
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    w = err_word(device)
+    code, mx = (int(x) for x in w.tolist())
+    if code:
+        w.zero_()
+        if n_total_embeddings is None:
+            n_total_embeddings = _LAST_V.get(_dev_index(device))
+        raise_for_error(code, mx, n_total_embeddings, batch)
 
 
 _TICKETS: dict[int, torch.Tensor] = {}
@@ -211,6 +257,7 @@ class JointEmbedFn(torch.autograd.Function):
         V, D = table.shape
         table = table.contiguous().float()
         out = torch.empty(bv.B, bv.L, spec.G, D, dtype=torch.float32, device=table.device)
+        note_vocab(table.device, V)
         with _timed("embed_joint_fwd"):
             st = lib.esgpt_embed_joint_fwd(bv.ref, _bref(spec.groups), table.data_ptr(), V, D, L.ptr(sin_div),
                                            L.ptr(cos_div), spec.flags, spec.static_w, spec.dynamic_w,
@@ -246,6 +293,7 @@ class SplitBagsFn(torch.autograd.Function):
         cat_table = cat_table.contiguous().float()
         num_table = num_table.contiguous().float()
         x = torch.empty(bv.B * bv.L * spec.G, Dc + Dn, dtype=torch.float32, device=cat_table.device)
+        note_vocab(cat_table.device, V)
         L.check(lib.esgpt_embed_split_bags_fwd(bv.ref, _bref(spec.groups), cat_table.data_ptr(), Dc,
                                                num_table.data_ptr(), Dn, V, spec.flags, cat_scale, num_scale,
                                                static_scale, x.data_ptr(), err_word(x.device).data_ptr(),

@@ -1,27 +1,41 @@
 """Minimal Lightning-free training step (``generative_modeling.py:434-485``) for one GPU or DDP over RCCL.
 
 * loss = model(batch).loss (per-rank weighted_loss normalisation, exactly like the reference under DDP);
-* AdamW(lr=init_lr, weight_decay) + transformers' polynomial-decay-with-warmup schedule, stepped every step;
+* AdamW(lr=init_lr, weight_decay) + transformers' polynomial-decay-with-warmup schedule, stepped every step
+  (``configure_optimizers``, ``generative_modeling.py:460-485``); one step count per parameter, as torch keeps;
 * gradients are reset to ``None`` before each backward (Lightning's ``zero_grad(set_to_none=True)``), so autograd
   hands each parameter its gradient without an accumulate-add; parameters without a gradient are skipped by
   AdamW exactly as in the reference;
-* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Gradients are packed
-  into size-capped flat buckets, all-reduced and divided by world size (the DDP gradient-averaging semantics of
-  the reference's Lightning trainer); a parameter without a gradient contributes zeros.
-* optional HIP-graph capture of forward+backward (static shapes; batches are copied into static buffers).
+* data-dependent errors (bad embedding index, NaN TTE log-likelihood, subject without an observed TTE) are raised
+  with the reference's exception type and message. The kernels flag them in a device error block; the AdamW kernel
+  skips its update while a flag is set (the reference raises before its optimizer step, so the parameters stay at
+  their pre-error values), and ``step`` raises the error of step k at the latest when step k + 2 is submitted (the
+  host never waits for the step it just queued), ``check()`` at once;
+* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Every ``param.grad`` ends
+  the step as a view into one flat f32 buffer laid out last-layer-first and cut into ~25 MB buckets; a bucket is
+  all-reduced (average) in place as soon as backward has produced all of its gradients (post-accumulate-grad hooks),
+  so the exchange overlaps the rest of backward;
+* optional HIP-graph capture of forward+backward, one graph per batch shape signature (static shapes; batches are
+  copied into the graph's static buffers). A batch whose signature matches no captured graph is captured (up to
+  ``max_graphs``) or run eagerly — never broadcast into the wrong buffers.
 """
 from __future__ import annotations
+
+from collections import deque
 
 import torch
 import torch.distributed as dist
 
 from .data.types import PytorchBatch
-from .kernels import begin_dropout_step, check_errors, end_dropout_step
+from .kernels import begin_dropout_step, check_errors, end_dropout_step, err_word, raise_for_error
 from .transformer.config import OptimizationConfig
 
 
 def poly_decay_lambda(warmup: int, total: int, power: float, init_lr: float, end_lr: float):
-    """``transformers.get_polynomial_decay_schedule_with_warmup`` as a multiplier of ``init_lr``."""
+    """``transformers.get_polynomial_decay_schedule_with_warmup`` (its ``lr_lambda``) as a multiplier of
+    ``init_lr``; raises the same ValueError when ``end_lr`` is not below ``init_lr``."""
+    if not (init_lr > end_lr):
+        raise ValueError(f"lr_end ({end_lr}) must be smaller than initial lr ({init_lr})")
 
     def f(step: int) -> float:
         if step < warmup:
@@ -37,9 +51,11 @@ def poly_decay_lambda(warmup: int, total: int, power: float, init_lr: float, end
 class FusedAdamW:
     """``torch.optim.AdamW`` (default betas / eps, decoupled weight decay; ``generative_modeling.py:460-466``) as ONE
     gfx950 kernel launch per step over every parameter (csrc/misc.hip ``esgpt_adamw``), instead of torch's
-    multi-tensor launches. Parameters whose ``.grad`` is None are skipped, like torch. The tensor table (device
-    pointers of p / grad / exp_avg / exp_avg_sq) is rebuilt only when a gradient's storage changes (never under
-    HIP-graph replay, where gradients live in the graph's pool)."""
+    multi-tensor launches. Parameters whose ``.grad`` is None are skipped and keep their step count, like torch;
+    when the active parameters' step counts differ, their bias corrections go to the kernel as a per-tensor table.
+    The tensor table (device pointers of p / grad / exp_avg / exp_avg_sq) is rebuilt only when a gradient's storage
+    changes (never under HIP-graph replay, where gradients live in the graph's pool). The launch is a no-op while
+    the device error block holds a flag (``err``)."""
 
     def __init__(self, params, lr: float, weight_decay: float = 0.01, betas=(0.9, 0.999), eps: float = 1e-8):
         from . import _lib as L
@@ -54,6 +70,8 @@ class FusedAdamW:
         self._key = None
         self._table = self._blocks = None
         self._active = []
+        self._per_dev = None
+        self._per_host = None
 
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:
@@ -78,6 +96,7 @@ class FusedAdamW:
         dev = self.params[0].device
         self._table = torch.tensor(rows, dtype=torch.int64).to(dev)
         self._blocks = torch.tensor(blocks, dtype=torch.int64).to(dev)
+        self._per_dev = torch.empty(2 * max(1, len(items)), dtype=torch.float32, device=dev)
         self._key = key
         self._active = items
 
@@ -86,14 +105,23 @@ class FusedAdamW:
         self._plan()
         if not self._active:
             return
-        # torch keeps one step counter per parameter; they advance together for parameters updated every step
-        step = self.steps[self._active[0]] + 1
+        lr = float(self.lr if lr is None else lr)
+        b1, b2 = self.betas
         for i in self._active:
             self.steps[i] += 1
-        b1, b2 = self.betas
-        self.L.check(self.lib.esgpt_adamw(self._table.data_ptr(), self._blocks.data_ptr(), self._blocks.numel(),
-                                          float(self.lr if lr is None else lr), b1, b2, self.eps,
-                                          self.weight_decay, step, self.L.stream()), "adamw")
+        steps = [self.steps[i] for i in self._active]
+        per = None
+        if any(s != steps[0] for s in steps):  # torch's per-parameter `step`: own bias corrections per tensor
+            vals = []
+            for s in steps:
+                vals += [lr / (1.0 - b1**s), (1.0 - b2**s) ** 0.5]
+            self._per_host = torch.tensor(vals, dtype=torch.float32).pin_memory()  # kept alive until the next step
+            self._per_dev[: len(vals)].copy_(self._per_host, non_blocking=True)
+            per = self._per_dev.data_ptr()
+        dev = self.params[0].device
+        self.L.check(self.lib.esgpt_adamw(self._table.data_ptr(), self._blocks.data_ptr(), self._blocks.numel(), lr,
+                                          b1, b2, self.eps, self.weight_decay, steps[0], per,
+                                          err_word(dev).data_ptr(), self.L.stream()), "adamw")
 
     def state_dict(self):
         return {"state": {i: {"step": self.steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}
@@ -107,10 +135,6 @@ def graph_safe(model) -> bool:
     from .fused import fused_supported
     from .transformer.config import StructuredEventProcessingMode
 
-    import os
-
-    if os.environ.get("ESGPT_FORCE_GRAPH") == "1":  # diagnostics (tools/na_graph_check.py)
-        return True
     enc = getattr(model, "encoder", None)
     cfg = getattr(model, "config", None)
     if enc is None or cfg is None:
@@ -120,9 +144,93 @@ def graph_safe(model) -> bool:
     return fused_supported(enc)
 
 
+class GradBuckets:
+    """DDP gradient exchange: one flat f32 buffer holding every trainable parameter's gradient, laid out in reverse
+    registration order (the last layers' gradients are produced first in backward) and cut into buckets of
+    ~``bucket_mb``. A post-accumulate-grad hook counts each bucket's gradients; when the last one arrives the
+    bucket's gradients that are not already views of the buffer are copied in (one multi-tensor copy), ``p.grad`` is
+    re-pointed at its view, and the bucket is all-reduced in place (average) asynchronously, overlapping the rest
+    of backward. ``finish()`` zero-fills and reduces buckets whose parameters got no gradient, waits for every
+    exchange on the current stream, and leaves every ``param.grad`` a view of the buffer (what FusedAdamW reads)."""
+
+    def __init__(self, params: list, world: int, bucket_mb: float = 25.0):
+        self.params = params
+        self.world = world
+        dev = params[0].device
+        self.avg = dist.get_backend() == "nccl"  # RCCL has ncclAvg; gloo sums (divided afterwards)
+        order = list(reversed(range(len(params))))
+        total = sum(params[i].numel() for i in order)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.views, self.bucket_of, self.buckets = {}, {}, []
+        lim = int(bucket_mb * 2**20 / 4)
+        off, start, cur = 0, 0, []
+        for i in order:
+            n = params[i].numel()
+            self.views[i] = self.flat[off: off + n].view_as(params[i])
+            cur.append(i)
+            off += n
+            if off - start >= lim:
+                self.buckets.append((cur, start, off))
+                cur, start = [], off
+        if cur:
+            self.buckets.append((cur, start, off))
+        for b, (idx, _, _) in enumerate(self.buckets):
+            for i in idx:
+                self.bucket_of[i] = b
+        self._ready = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+        self._hooks = [params[i].register_post_accumulate_grad_hook(self._make_hook(i)) for i in range(len(params))]
+
+    def _make_hook(self, i: int):
+        def hook(p):
+            b = self.bucket_of[i]
+            self._ready[b] += 1
+            if self._ready[b] == len(self.buckets[b][0]):
+                self._launch(b)
+
+        return hook
+
+    def reset(self):
+        self._ready = [0] * len(self.buckets)
+        self._launched = [False] * len(self.buckets)
+        self._works = []
+
+    def _launch(self, b: int):
+        idx, s, e = self.buckets[b]
+        src, dst = [], []
+        with torch.no_grad():
+            for i in idx:
+                p, v = self.params[i], self.views[i]
+                if p.grad is None:
+                    v.zero_()
+                elif p.grad.data_ptr() != v.data_ptr():
+                    src.append(p.grad)
+                    dst.append(v)
+            if src:
+                torch._foreach_copy_(dst, src)
+            for i in idx:
+                self.params[i].grad = self.views[i]
+            seg = self.flat[s:e]
+            op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+            self._works.append((dist.all_reduce(seg, op=op, async_op=True), seg))
+        self._launched[b] = True
+
+    def finish(self):
+        for b in range(len(self.buckets)):
+            if not self._launched[b]:
+                self._launch(b)
+        for w, seg in self._works:
+            w.wait()
+            if not self.avg:
+                seg.div_(self.world)
+        self.reset()
+
+
 class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
-                 bucket_mb: float = 25.0, use_graph: bool = False):
+                 bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
+                 max_graphs: int = 4, _force_graph: bool = False):
         self.model = model
         self.cfg = opt_cfg
         self.dtype = compute_dtype
@@ -131,17 +239,7 @@ class TrainStep:
         params = [p for p in model.parameters() if p.requires_grad]
         self.params = params
         dev = params[0].device
-        # buckets of parameter indices in reverse order (the last layers' gradients are final first)
-        self.buckets, cur, size = [], [], 0
-        lim = int(bucket_mb * 2**20 / 4)
-        for i in reversed(range(len(params))):
-            cur.append(i)
-            size += params[i].numel()
-            if size >= lim:
-                self.buckets.append(cur)
-                cur, size = [], 0
-        if cur:
-            self.buckets.append(cur)
+        self.device = dev
         total = opt_cfg.max_training_steps or 1_000_000
         warm = opt_cfg.lr_num_warmup_steps or 0
         self.lr_lambda = poly_decay_lambda(warm, total, opt_cfg.lr_decay_power, opt_cfg.init_lr, opt_cfg.end_lr)
@@ -152,84 +250,162 @@ class TrainStep:
         else:
             self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
             self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, self.lr_lambda)
-        # HIP-graph capture only for the fully fused CI step (every kernel ours). The module-by-module paths (NA
-        # blocks, unsupported CI shapes) run PyTorch-ROCm GEMMs whose bias-gradient results were garbage on graph
-        # replay (tools/na_graph_check.py: c_fc.bias gradients ~1e38 from the second replay on); they run eagerly.
-        self.use_graph = use_graph and graph_safe(model)
-        self.graph = None
-        self.static_batch = None
-        self.static_loss = None
+        self.grad_buckets = GradBuckets(params, self.world, bucket_mb) if self.distributed else None
+        # HIP-graph capture only for the fully fused CI step (every kernel ours). `_force_graph` is for diagnostics
+        # of the module-by-module paths (tools/na_graph_*.py).
+        self.use_graph = use_graph and (_force_graph or graph_safe(model))
+        self.max_graphs = max_graphs
+        self.graphs: dict = {}  # shape signature -> (graph, static batch, static loss)
+        self.check_errors = check_errors and dev.type == "cuda"
+        self._pending: deque = deque()  # (event, pinned error block copy, batch) of submitted steps
+        self._vocab = getattr(getattr(model, "config", None), "vocab_size", None)
+        self._copy_stream = None
+        self._staging: dict = {}
+        self._prefetched = None
+        self._release = None
 
     # --------------------------------------------------------------------------------------------------------
-    def _fwd_bwd(self, batch: PytorchBatch):
-        # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
-        dev = self.params[0].device
+    def _fwd_bwd(self, batch: PytorchBatch, autocast_cache: bool = True):
+        dev = self.device
         if dev.type == "cuda":
             begin_dropout_step(dev)
-        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32,
-                            cache_enabled=not self.use_graph):
+        # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
+        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32, cache_enabled=autocast_cache):
             out = self.model(batch)
         out.loss.backward()
         if dev.type == "cuda":
             end_dropout_step(dev)
         return out.loss.detach()
 
-    def _allreduce(self):
-        if not self.distributed:
-            return
-        for idx in self.buckets:
-            ps = [self.params[i] for i in idx]
-            for p in ps:
-                if p.grad is None:
-                    p.grad = torch.zeros_like(p)
-            grads = [p.grad for p in ps]
-            flat = torch._utils._flatten_dense_tensors(grads)
-            dist.all_reduce(flat)
-            flat.div_(self.world)
-            torch._foreach_copy_(grads, torch._utils._unflatten_dense_tensors(flat, grads))
+    def _capture(self, batch: PytorchBatch):
+        static = batch.packed()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up allocator / lazy init outside the graph
+                self.opt.zero_grad(set_to_none=True)
+                self._fwd_bwd(static, autocast_cache=False)
+                if self.grad_buckets is not None:
+                    self.grad_buckets.finish()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        check_errors(self.device, self._vocab)  # a warm-up error is this batch's error: raise it now
+        # gradients are (re)allocated inside the capture from the graph's pool and stay static across replays
+        self.opt.zero_grad(set_to_none=True)
+        hooks = None
+        if self.grad_buckets is not None:  # the exchange is not captured: it runs after each replay
+            hooks = self.grad_buckets._hooks
+            for h in hooks:
+                h.remove()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self._fwd_bwd(static, autocast_cache=False)
+        torch.cuda.synchronize()
+        if hooks is not None:
+            gb = self.grad_buckets
+            gb._hooks = [p.register_post_accumulate_grad_hook(gb._make_hook(i)) for i, p in enumerate(self.params)]
+        grads = [p.grad for p in self.params]
+        self.graphs[batch.shape_signature()] = (g, static, loss, grads)
 
-    def _copy_into_static(self, batch: PytorchBatch):
-        # one D2D copy when the batch is packed (native collate / .packed()), else one per field
-        self.static_batch.copy_(batch, non_blocking=True)
+    def _raise_pending(self, keep: int):
+        """Raises the first device error among submitted steps, waiting only for steps older than the newest
+        ``keep`` (``keep = 0``: all of them)."""
+        while len(self._pending) > keep or (self._pending and self._pending[0][0].query()):
+            ev, host, batch = self._pending.popleft()
+            ev.synchronize()
+            code, mx = int(host[0]), int(host[1])
+            if code & 0xFFFFFFFF:
+                self._pending.clear()
+                err_word(self.device).zero_()
+                raise_for_error(code, mx, self._vocab, batch)
+
+    def prefetch(self, batch: PytorchBatch) -> None:
+        """Starts the host -> device copy of a (pinned, packed) host batch on a side stream, so it overlaps the step
+        in flight; the next ``step(batch)`` with the same object waits for that copy instead of issuing its own.
+        Two staging buffers per shape signature alternate, so a copy never overwrites a batch still being read."""
+        if batch.device.type != "cpu" or self.device.type != "cuda":
+            return
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.device)
+        sig = batch.shape_signature()
+        ring = self._staging.setdefault(sig, [None, None, 0])
+        k = ring[2]
+        ring[2] ^= 1
+        slot = ring[k]
+        if slot is None:
+            dst = batch.packed().to(self.device)
+            slot = ring[k] = [dst, torch.cuda.Event()]
+            slot[1].record()  # no reader yet
+        dst, free_ev = slot
+        cs = self._copy_stream
+        cs.wait_event(free_ev)  # the previous reader of this buffer is done
+        with torch.cuda.stream(cs):
+            dst.copy_(batch, non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record(cs)
+        self._prefetched = (batch, dst, ready, free_ev)
+
+    def _to_device(self, batch: PytorchBatch) -> PytorchBatch:
+        if batch.device.type == self.device.type or self.device.type != "cuda":
+            return batch
+        pf = self._prefetched
+        if pf is not None and pf[0] is batch:
+            self._prefetched = None
+            _, dst, ready, free_ev = pf
+            torch.cuda.current_stream().wait_event(ready)
+            self._release = free_ev
+            return dst
+        return batch.to(self.device, non_blocking=True)
 
     def step(self, batch: PytorchBatch) -> torch.Tensor:
-        if not self.use_graph:
+        """One optimizer step on ``batch`` (device-resident, or a pinned host batch: the H2D copy is part of the
+        step, overlapped when ``prefetch(batch)`` was called during the previous step)."""
+        if self.check_errors:
+            self._raise_pending(keep=1)
+        batch = self._to_device(batch)
+        entry = None
+        if self.use_graph:
+            sig = batch.shape_signature()
+            entry = self.graphs.get(sig)
+            if entry is None and len(self.graphs) < self.max_graphs:
+                self._capture(batch)
+                entry = self.graphs[sig]
+        if entry is None:
             self.opt.zero_grad(set_to_none=True)
             loss = self._fwd_bwd(batch)
         else:
-            if self.graph is None:
-                self._capture(batch)
-            self._copy_into_static(batch)
-            self.graph.replay()
-            loss = self.static_loss
-        self._allreduce()
+            g, static, sloss, grads = entry
+            static.copy_(batch, non_blocking=True)
+            for p, gr in zip(self.params, grads):  # the graph writes its gradients into its own pool
+                p.grad = gr
+            g.replay()
+            loss = sloss.clone()  # the next replay overwrites the static loss
+        if self.grad_buckets is not None:
+            if entry is not None:  # graph: hooks did not run during replay; exchange every bucket now
+                self.grad_buckets.reset()
+            self.grad_buckets.finish()
         if self.sched is None:
             self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step))
         else:
             self.opt.step()
             self.sched.step()
         self.sched_step += 1
+        if self._release is not None:  # the staging buffer may be refilled once this step has consumed it
+            self._release.record()
+            self._release = None
+        if self.check_errors:
+            host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+            host.copy_(err_word(self.device), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending.append((ev, host, batch))
         return loss
 
-    def _capture(self, batch: PytorchBatch):
-        self.static_batch = batch.packed()
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):  # warm up allocator / lazy init outside the graph
-                self.opt.zero_grad(set_to_none=True)
-                self._fwd_bwd(self.static_batch)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        # gradients are (re)allocated inside the capture from the graph's pool and stay static across replays
-        self.opt.zero_grad(set_to_none=True)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.static_loss = self._fwd_bwd(self.static_batch)
-        torch.cuda.synchronize()
-
     def check(self):
-        check_errors()
+        """Waits for every submitted step and raises the first device error (the reference's exception)."""
+        if self.check_errors:
+            self._raise_pending(keep=0)
+        check_errors(self.device if self.device.type == "cuda" else None, self._vocab)
 
 
 def init_distributed():
@@ -256,4 +432,3 @@ def n_params(model) -> int:
 
 def grad_bytes(model) -> int:
     return 4 * n_params(model)
-

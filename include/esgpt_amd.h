@@ -12,8 +12,10 @@
  *     synchronises with the host, allocates, or frees. Callers own all outputs and workspaces.
  *   - Return value: ESGPT_OK or an ESGPT_ERR_* code for invalid arguments / launch failures. Data-dependent
  *     errors (out-of-range embedding index, NaN TTE log-likelihood, subject without observed TTE) are OR-ed
- *     into the caller-provided device word `err` (ESGPT_FLAG_*); the Python wrapper reads it once per step and
- *     raises the reference's exception type and message.
+ *     into the caller-provided device error block `err` (16 bytes, 8-B aligned, zeroed by the caller: int32
+ *     ESGPT_FLAG_* bits at byte 0, and at bytes 8..15 the int64 maximum of every out-of-range embedding index).
+ *     esgpt_adamw skips its update while the flags are non-zero (the reference raises before its optimizer step);
+ *     the Python wrapper reads the block once per step and raises the reference's exception type and message.
  *   - dtype codes: ESGPT_F32 (float) or ESGPT_BF16 (bfloat16) for activation tensors; masters are f32.
  */
 #ifndef ESGPT_AMD_H_
@@ -37,6 +39,7 @@ extern "C" {
 #define ESGPT_FLAG_BAD_INDEX 1    /* "Invalid embedding! {max} >= {V}"  (data_embedding_layer.py:485-488) */
 #define ESGPT_FLAG_TTE_NAN 2      /* "NaNs in TTE_LL"                    (model_output.py:1362-1363)     */
 #define ESGPT_FLAG_TTE_NO_OBS 4   /* "No observed time-to-event ..."     (model_output.py:1366-1367)     */
+#define ESGPT_FLAG_BAD_LABEL 8    /* classification / regression target outside its vocabulary slice      */
 
 /* embedding flags */
 #define ESGPT_EMB_NORMALIZE 1     /* do_normalize_by_measurement_index                                     */
@@ -263,7 +266,10 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
  * Fused AdamW step (torch.optim.AdamW semantics: decoupled weight decay, bias-corrected moments;
  * generative_modeling.py:460-485 configure_optimizers) over many parameter tensors in ONE launch.
  * table: device array of esgpt_adam_tensor; blocks: device array of (tensor index << 40 | first element), one
- * entry per esgpt_adamw_chunk() elements of each tensor. step = the 1-based optimizer step (bias corrections). */
+ * entry per esgpt_adamw_chunk() elements of each tensor. step = the 1-based optimizer step (bias corrections) shared
+ * by every tensor, or per_tensor (device f32 [n_tensors][2] = (lr / (1 - beta1^step_t), sqrt(1 - beta2^step_t)) with
+ * tensor t's own step count, as torch keeps one `step` per parameter; NULL = use `step`). err: the error block of
+ * the step's forward (NULL = none); a non-zero flag word makes the launch a no-op. */
 typedef struct esgpt_adam_tensor {
   float* p;
   const float* g;
@@ -273,7 +279,8 @@ typedef struct esgpt_adam_tensor {
 } esgpt_adam_tensor;
 int64_t esgpt_adamw_chunk(void);
 int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, float lr, float beta1,
-                float beta2, float eps, float weight_decay, int64_t step, void* stream);
+                float beta2, float eps, float weight_decay, int64_t step, const float* per_tensor,
+                const int32_t* err, void* stream);
 
 /* ---- Batch producer (host) ----------------------------------------------------------------------------------
  * PytorchDataset.collate (pytorch_dataset.py:527-701) over flat ragged arrays (the DL_reps parquet columns):

@@ -52,8 +52,23 @@ def _worker(rank, world, port, q):
     m = Toy()
     ts = TrainStep(m, OptimizationConfig(init_lr=0.1, lr_num_warmup_steps=0, max_training_steps=10),
                    compute_dtype=torch.float32, bucket_mb=2e-5)  # tiny buckets: exercise several all-reduces
-    assert ts.distributed and len(ts.buckets) > 1
+    gb = ts.grad_buckets
+    assert ts.distributed and len(gb.buckets) > 1
+    launched_in_backward = []
+    orig = gb._launch
+
+    def spy(b):  # buckets launched by the post-accumulate-grad hooks, i.e. while backward is still running
+        launched_in_backward.append((b, torch._C._current_graph_task_id() != -1))
+        orig(b)
+
+    gb._launch = spy
     ts.step(_data(rank))
+    assert launched_in_backward and all(in_bwd for _, in_bwd in launched_in_backward)
+    assert len(launched_in_backward) == len(gb.buckets)
+    # every gradient is a view into the one flat exchange buffer
+    base = gb.flat.data_ptr()
+    for p in ts.params:
+        assert base <= p.grad.data_ptr() < base + 4 * gb.flat.numel()
     q.put((rank, {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}))  # by value, not shm
     dist.destroy_process_group()
 

@@ -1,0 +1,106 @@
+"""World-size-2 data parallelism of the real training step on the GPU: both ranks on cuda:0 with the
+gloo backend (the box has one GPU; RCCL refuses two ranks on one device), the CI model through TrainStep with
+FusedAdamW and the HIP graph, each rank on its own subjects. Compared with one process that computes each rank's
+gradients (per-rank weighted_loss normalisation), averages them and takes the same optimizer steps
+(generative_modeling.py:434-485 under Lightning DDP)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+STEPS = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup():
+    from eventstreamgpt_amd.synthetic import CONFIGS
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+    from eventstreamgpt_amd.transformer.config import OptimizationConfig
+
+    bc = CONFIGS["C1"]
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+    torch.manual_seed(0)
+    m = CIPPTForGenerativeSequenceModeling(cfg).to("cuda:0").train()
+    opt = OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=100)
+    return bc, m, opt
+
+
+def _batches(bc, rank):
+    return [bc.batch(10 * rank + s, batch_size=8, device="cuda:0").packed() for s in range(STEPS)]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from eventstreamgpt_amd.train import TrainStep
+
+        bc, m, opt = _setup()
+        ts = TrainStep(m, opt, torch.bfloat16, use_graph=True, bucket_mb=0.05)  # several buckets
+        assert ts.use_graph and ts.distributed and len(ts.grad_buckets.buckets) > 1
+        losses = [float(ts.step(b)) for b in _batches(bc, rank)]
+        ts.check()
+        base = ts.grad_buckets.flat.data_ptr()
+        in_flat = all(base <= p.grad.data_ptr() < base + 4 * ts.grad_buckets.flat.numel() for p in ts.params)
+        q.put((rank, losses, in_flat, {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_on_one_gpu_match_averaged_gradients():
+    from eventstreamgpt_amd.train import FusedAdamW, poly_decay_lambda
+
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, losses, in_flat, sd = q.get(timeout=240)
+        res[r] = (losses, in_flat, sd)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    # single process: per-rank losses / gradients on each rank's batch, averaged, then the same AdamW steps
+    bc, m, opt_cfg = _setup()
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = FusedAdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
+    lam = poly_decay_lambda(opt_cfg.lr_num_warmup_steps, opt_cfg.max_training_steps, opt_cfg.lr_decay_power,
+                            opt_cfg.init_lr, opt_cfg.end_lr)
+    batches = {r: _batches(bc, r) for r in range(world)}
+    for s in range(STEPS):
+        acc = [torch.zeros_like(p) for p in params]
+        for r in range(world):
+            for p in params:
+                p.grad = None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(batches[r][s]).loss
+            loss.backward()
+            assert abs(float(loss) - res[r][0][s]) <= 1e-3 * abs(float(loss)), (r, s)
+            for a, p in zip(acc, params):
+                a += p.grad
+        for a, p in zip(acc, params):
+            p.grad = a / world
+        opt.step(opt_cfg.init_lr * lam(s))
+    want = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    for r in range(world):
+        assert res[r][1], "param.grad must be views into the flat exchange buffer"
+        for k, v in want.items():
+            got = torch.from_numpy(res[r][2][k])
+            assert (got.float() - v.float()).abs().max().item() < 1e-4, (r, k)

@@ -27,7 +27,7 @@ def run(graph: bool):
     torch.manual_seed(0)
     m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
     ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=100),
-                   torch.bfloat16, use_graph=graph)
+                   torch.bfloat16, use_graph=graph, _force_graph=True)
     out = []
     for i, b in enumerate(batches):
         loss = ts.step(b)

@@ -4,7 +4,6 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["ESGPT_FORCE_GRAPH"] = "1"
 import torch
 
 from eventstreamgpt_amd.synthetic import CONFIGS
@@ -22,7 +21,7 @@ def grads(graph: bool):
     m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
     ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=int(os.environ.get("WARM", 10**9)),
                                                 max_training_steps=10**10),
-                   torch.bfloat16, use_graph=graph)
+                   torch.bfloat16, use_graph=graph, _force_graph=True)
     out = []
     for b in batches:
         loss = float(ts.step(b))
