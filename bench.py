@@ -196,20 +196,20 @@ def embed_bwd_bytes(batch, cfg) -> float:
 def _embed_bwd_launcher(model, batch):
     """The JOINT input layer's table gradient (esgpt_embed_bag_bwd: every kernel of the CSR-transpose backward)."""
     from eventstreamgpt_amd import _lib as L
-    from eventstreamgpt_amd.kernels import _bag_bwd, batch_view
+    from eventstreamgpt_amd.kernels import bag_bwd
 
     emb = model.encoder.input_layer.data_embedding_layer
-    bv = batch_view(batch)
+    B, Lq = batch.event_mask.shape
     D, V = emb.embed_layer.weight.shape[1], emb.embed_layer.weight.shape[0]
     g = torch.Generator(device=batch.device).manual_seed(3)
-    dsrc = torch.randn(bv.B * bv.L, D, device=batch.device, generator=g)
+    dsrc = torch.randn(B * Lq, D, device=batch.device, generator=g)
     flags = emb._flags()
-    static = bool(flags & L.EMB_STATIC) and bv.S > 0
+    static = bool(flags & L.EMB_STATIC) and batch.static_indices is not None and batch.static_indices.shape[1] > 0
     keep = {"dsrc": dsrc}
 
     def bwd():
-        keep["out"] = _bag_bwd(bv, emb._buckets, L.BAG_JOINT, flags, emb.dynamic_weight if static else 1.0,
-                               emb.static_weight, dsrc, D, D, V, 1)
+        keep["out"] = bag_bwd(batch, emb._buckets, L.BAG_JOINT, flags, emb.dynamic_weight if static else 1.0,
+                              emb.static_weight, dsrc, D, D, V, 1)
 
     return bwd, keep
 

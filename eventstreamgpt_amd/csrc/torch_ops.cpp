@@ -1,0 +1,594 @@
+// PyTorch-ROCm custom operators (TORCH_LIBRARY(esgpt)) over the C ABI of libesgpt_amd.so.
+//
+// The reference (Jwoo5/EventStreamGPT) swaps ATen ops inside its module methods; the drop-in modules of this package
+// call these operators instead (torch.ops.esgpt.*): the input layer (data_embedding_layer.py:351-708,
+// transformer.py:594-672, 903-936), attention (transformer.py:171-217), the block elementwise stages and projections
+// (transformer.py:350-461), the generative heads + losses (model_output.py:1253-1721) and AdamW
+// (generative_modeling.py:460-485). Each operator allocates its outputs and workspaces with torch's caching
+// allocator on the inputs' device and launches on torch's current HIP stream; no host synchronisation.
+//
+// Data-dependent errors go to a caller-owned device error block and split-K / cross-workgroup tickets to a
+// caller-owned counter array (eventstreamgpt_amd/kernels.py: err_word / tickets). Both are side channels: the
+// tickets are left as found, the error block only accumulates flags that the Python layer turns into the
+// reference's exceptions. The schemas therefore list them as plain inputs, keeping every differentiable operator
+// functional (torch.library.register_autograd requires that). Fake (meta) kernels and autograd formulas are
+// registered from Python (eventstreamgpt_amd/ops.py).
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <vector>
+
+#include "../../include/esgpt_amd.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+void* stream_of(const Tensor& t) {
+  return reinterpret_cast<void*>(c10::hip::getCurrentHIPStream(t.device().index()).stream());
+}
+
+void check(int status, const char* what) {
+  TORCH_CHECK(status == ESGPT_OK, "eventstreamgpt_amd: ", what, " failed (status ", status,
+              status == ESGPT_ERR_INVALID_ARG ? ": invalid argument" :
+              status == ESGPT_ERR_LAUNCH ? ": launch failure" :
+              status == ESGPT_ERR_UNSUPPORTED ? ": unsupported configuration" : "", ")");
+}
+
+template <typename T>
+T* ptr(const Tensor& t) { return t.defined() ? reinterpret_cast<T*>(t.data_ptr()) : nullptr; }
+template <typename T>
+T* optr(const optional<Tensor>& t) { return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
+
+int dtype_code(at::ScalarType s) {
+  if (s == at::kFloat) return ESGPT_F32;
+  if (s == at::kBFloat16) return ESGPT_BF16;
+  TORCH_CHECK(false, "eventstreamgpt_amd: unsupported activation dtype ", s);
+}
+
+void require_hip(const Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda(), "eventstreamgpt_amd: ", what, " must be a HIP device tensor (there is no CPU path)");
+}
+
+// ---- batch descriptor: PytorchBatch fields in the ABI's dtypes (contiguous copies only when needed) ----------
+struct Batch {
+  Tensor em, td, tm, di, dm, dv, dvm, si, sm;
+  esgpt_batch b;
+};
+
+Tensor as(const Tensor& t, at::ScalarType s) { return t.to(s).contiguous(); }
+Tensor as_opt(const optional<Tensor>& t, at::ScalarType s) {
+  return (t.has_value() && t->defined()) ? as(*t, s) : Tensor();
+}
+
+Batch make_batch(const Tensor& event_mask, const Tensor& time_delta, const optional<Tensor>& time,
+                 const Tensor& dyn_idx, const Tensor& dyn_meas, const Tensor& dyn_vals, const Tensor& dyn_vmask,
+                 const optional<Tensor>& st_idx, const optional<Tensor>& st_meas) {
+  require_hip(event_mask, "the batch");
+  Batch x;
+  x.em = as(event_mask, at::kBool);
+  x.td = as(time_delta, at::kFloat);
+  x.tm = as_opt(time, at::kFloat);
+  x.di = as(dyn_idx, at::kLong);
+  x.dm = as(dyn_meas, at::kLong);
+  x.dv = as(dyn_vals, at::kFloat);
+  x.dvm = as(dyn_vmask, at::kBool);
+  x.si = as_opt(st_idx, at::kLong);
+  x.sm = as_opt(st_meas, at::kLong);
+  TORCH_CHECK(x.di.dim() == 3, "dynamic_indices must be [B, L, M]");
+  x.b.dyn_idx = ptr<const int64_t>(x.di);
+  x.b.dyn_meas = ptr<const int64_t>(x.dm);
+  x.b.dyn_vals = ptr<const float>(x.dv);
+  x.b.dyn_vmask = ptr<const uint8_t>(x.dvm);
+  x.b.event_mask = ptr<const uint8_t>(x.em);
+  x.b.time_delta = ptr<const float>(x.td);
+  x.b.time_abs = x.tm.defined() ? ptr<const float>(x.tm) : nullptr;
+  x.b.st_idx = x.si.defined() ? ptr<const int64_t>(x.si) : nullptr;
+  x.b.st_meas = x.sm.defined() ? ptr<const int64_t>(x.sm) : nullptr;
+  x.b.B = x.di.size(0);
+  x.b.L = x.di.size(1);
+  x.b.M = x.di.size(2);
+  x.b.S = x.si.defined() ? x.si.size(1) : 0;
+  return x;
+}
+
+// buckets: [] (un-bucketed) or [G, cat_bits[8], num_bits[8]] (bit patterns as int64)
+bool make_buckets(at::IntArrayRef v, esgpt_buckets& k) {
+  if (v.empty()) return false;
+  TORCH_CHECK(v.size() == 17, "buckets must be [G, cat_bits x8, num_bits x8]");
+  k.G = v[0];
+  for (int g = 0; g < 8; ++g) {
+    k.cat_bits[g] = static_cast<uint64_t>(v[1 + g]);
+    k.num_bits[g] = static_cast<uint64_t>(v[9 + g]);
+  }
+  return true;
+}
+
+#define BATCH_ARGS                                                                                         \
+  const Tensor &event_mask, const Tensor &time_delta, const optional<Tensor> &time, const Tensor &dyn_idx,  \
+      const Tensor &dyn_meas, const Tensor &dyn_vals, const Tensor &dyn_vmask, const optional<Tensor> &st_idx, \
+      const optional<Tensor> &st_meas
+#define BATCH_PASS event_mask, time_delta, time, dyn_idx, dyn_meas, dyn_vals, dyn_vmask, st_idx, st_meas
+#define BATCH_SCHEMA                                                                                    \
+  "Tensor event_mask, Tensor time_delta, Tensor? time, Tensor dyn_idx, Tensor dyn_meas, Tensor dyn_vals, " \
+  "Tensor dyn_vmask, Tensor? st_idx, Tensor? st_meas"
+
+// ---- input layer ---------------------------------------------------------------------------------------------
+Tensor embed_joint(const Tensor& table, BATCH_ARGS, at::IntArrayRef buckets, const optional<Tensor>& sin_div,
+                   const optional<Tensor>& cos_div, int64_t flags, double static_w, double dynamic_w, int64_t G,
+                   const Tensor& err) {
+  const c10::DeviceGuard guard(table.device());
+  Batch bt = make_batch(BATCH_PASS);
+  esgpt_buckets bk;
+  const bool has_bk = make_buckets(buckets, bk);
+  Tensor tab = as(table, at::kFloat);
+  const int64_t V = tab.size(0), D = tab.size(1);
+  Tensor out = at::empty({bt.b.B, bt.b.L, G, D}, tab.options());
+  check(esgpt_embed_joint_fwd(&bt.b, has_bk ? &bk : nullptr, ptr<const float>(tab), V, D, optr<const float>(sin_div),
+                              optr<const float>(cos_div), (int)flags, (float)static_w, (float)dynamic_w,
+                              ptr<float>(out), ptr<int32_t>(err), stream_of(tab)),
+        "embed_joint");
+  return out;
+}
+
+Tensor embed_split_bags(const Tensor& cat_table, const Tensor& num_table, BATCH_ARGS, at::IntArrayRef buckets,
+                        int64_t flags, double cat_scale, double num_scale, double static_scale, int64_t G,
+                        const Tensor& err) {
+  const c10::DeviceGuard guard(cat_table.device());
+  Batch bt = make_batch(BATCH_PASS);
+  esgpt_buckets bk;
+  const bool has_bk = make_buckets(buckets, bk);
+  Tensor ct = as(cat_table, at::kFloat), nt = as(num_table, at::kFloat);
+  const int64_t V = ct.size(0), Dc = ct.size(1), Dn = nt.size(1);
+  Tensor x = at::empty({bt.b.B * bt.b.L * G, Dc + Dn}, ct.options());
+  check(esgpt_embed_split_bags_fwd(&bt.b, has_bk ? &bk : nullptr, ptr<const float>(ct), Dc, ptr<const float>(nt), Dn,
+                                   V, (int)flags, (float)cat_scale, (float)num_scale, (float)static_scale,
+                                   ptr<float>(x), ptr<int32_t>(err), stream_of(ct)),
+        "embed_split_bags");
+  return x;
+}
+
+Tensor embed_epilogue(const Tensor& y, BATCH_ARGS, int64_t G, int64_t flags, const optional<Tensor>& sin_div,
+                      const optional<Tensor>& cos_div) {
+  const c10::DeviceGuard guard(y.device());
+  Batch bt = make_batch(BATCH_PASS);
+  Tensor yc = as(y, at::kFloat);
+  const int64_t D = yc.size(-1);
+  Tensor out = at::empty({bt.b.B, bt.b.L, G, D}, yc.options());
+  check(esgpt_embed_epilogue_fwd(&bt.b, G, D, ptr<const float>(yc), optr<const float>(sin_div),
+                                 optr<const float>(cos_div), (int)flags, ptr<float>(out), stream_of(yc)),
+        "embed_epilogue");
+  return out;
+}
+
+Tensor embed_epilogue_bwd(const Tensor& dout, BATCH_ARGS, int64_t G, int64_t flags) {
+  const c10::DeviceGuard guard(dout.device());
+  Batch bt = make_batch(BATCH_PASS);
+  Tensor d = as(dout, at::kFloat);
+  const int64_t D = d.size(-1);
+  Tensor dy = at::empty({bt.b.B * bt.b.L * G, D}, d.options());
+  check(esgpt_embed_epilogue_bwd(&bt.b, G, D, ptr<const float>(d), (int)flags, ptr<float>(dy), stream_of(d)),
+        "embed_epilogue_bwd");
+  return dy;
+}
+
+// dsrc: rows of leading dimension ld (elements), D columns used (may be a column slice of a wider matrix)
+Tensor embed_bag_bwd(const Tensor& dsrc, BATCH_ARGS, at::IntArrayRef buckets, int64_t selector, int64_t flags,
+                     double dyn_scale, double static_scale, int64_t ld, int64_t D, int64_t V, int64_t G) {
+  const c10::DeviceGuard guard(dsrc.device());
+  TORCH_CHECK(dsrc.scalar_type() == at::kFloat && dsrc.stride(-1) == 1, "embed_bag_bwd: f32 rows expected");
+  Batch bt = make_batch(BATCH_PASS);
+  esgpt_buckets bk;
+  const bool has_bk = make_buckets(buckets, bk);
+  Tensor dtable = at::empty({V, D}, dsrc.options());
+  const size_t nb = esgpt_embed_bag_bwd_workspace(&bt.b, G, V, D);
+  Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, dsrc.options().dtype(at::kByte));
+  check(esgpt_embed_bag_bwd(&bt.b, has_bk ? &bk : nullptr, (int)selector, (int)flags, (float)dyn_scale,
+                            (float)static_scale, ptr<const float>(dsrc), ld, D, V, ptr<float>(dtable), ws.data_ptr(),
+                            nb, stream_of(dsrc)),
+        "embed_bag_bwd");
+  return dtable;
+}
+
+// ---- attention (packed qkv [Bs, T, 3D]) ------------------------------------------------------------------------
+std::tuple<Tensor, Tensor> attention(const Tensor& qkv_, const optional<Tensor>& key_mask,
+                                     const optional<Tensor>& query_mask, int64_t H, int64_t window,
+                                     bool static_kv_first, double dropout_p, const optional<Tensor>& seed) {
+  const c10::DeviceGuard guard(qkv_.device());
+  require_hip(qkv_, "qkv");
+  Tensor qkv = qkv_.contiguous();
+  const int64_t Bs = qkv.size(0), T = qkv.size(1), D3 = qkv.size(2), D = D3 / 3, hd = D / H;
+  const int64_t skf = static_kv_first ? 1 : 0, Lk = T, Lq = T - skf;
+  const int64_t es = qkv.element_size();
+  char* base = reinterpret_cast<char*>(qkv.data_ptr());
+  Tensor km = as_opt(key_mask, at::kBool), qm = as_opt(query_mask, at::kBool);
+  Tensor o = at::empty({Bs, Lq, D}, qkv.options());
+  Tensor lse = at::empty({Bs, H, Lq}, qkv.options().dtype(at::kFloat));
+  check(esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                       ptr<float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
+                       qm.defined() ? ptr<const uint8_t>(qm) : nullptr, Bs, H, Lq, Lk, hd, window, (float)dropout_p,
+                       optr<const uint64_t>(seed), dtype_code(qkv.scalar_type()), stream_of(qkv)),
+        "attention");
+  return {o, lse};
+}
+
+Tensor attention_bwd(const Tensor& qkv_, const Tensor& o, const Tensor& dout_, const Tensor& lse,
+                     const optional<Tensor>& key_mask, const optional<Tensor>& query_mask, int64_t H, int64_t window,
+                     bool static_kv_first, double dropout_p, const optional<Tensor>& seed, const Tensor& tickets) {
+  const c10::DeviceGuard guard(qkv_.device());
+  Tensor qkv = qkv_.contiguous();
+  Tensor dout = dout_.to(qkv.scalar_type()).contiguous();
+  const int64_t Bs = qkv.size(0), T = qkv.size(1), D3 = qkv.size(2), D = D3 / 3, hd = D / H;
+  const int64_t skf = static_kv_first ? 1 : 0, Lk = T, Lq = T - skf;
+  const int64_t es = qkv.element_size();
+  Tensor dqkv = skf ? at::zeros_like(qkv) : at::empty_like(qkv);
+  const size_t nb = esgpt_attn_bwd_workspace(Bs, H, Lq, Lk, hd);
+  Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, qkv.options().dtype(at::kByte));
+  int32_t* counters = esgpt_attn_bwd_counters(Bs, H, Lk) <= tickets.numel() ? ptr<int32_t>(tickets) : nullptr;
+  Tensor km = as_opt(key_mask, at::kBool), qm = as_opt(query_mask, at::kBool);
+  char* base = reinterpret_cast<char*>(qkv.data_ptr());
+  char* dbase = reinterpret_cast<char*>(dqkv.data_ptr());
+  check(esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D, dout.data_ptr(),
+                       D, ptr<const float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
+                       qm.defined() ? ptr<const uint8_t>(qm) : nullptr, dbase + skf * D3 * es, dbase + D * es,
+                       dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd, window, (float)dropout_p, optr<const uint64_t>(seed),
+                       dtype_code(qkv.scalar_type()), ws.data_ptr(), nb, counters, stream_of(qkv)),
+        "attention_bwd");
+  return dqkv;
+}
+
+// ---- generation: KV cache ----------------------------------------------------------------------------------------
+void kv_append(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_cache, int64_t past) {
+  const c10::DeviceGuard guard(qkv.device());
+  TORCH_CHECK(qkv.is_contiguous() && k_cache.is_contiguous() && v_cache.is_contiguous(), "kv_append: contiguous");
+  const int64_t B = qkv.size(0), Lq = qkv.size(1), D3 = qkv.size(2), cap = k_cache.size(1), D = k_cache.size(2);
+  check(esgpt_kv_append(qkv.data_ptr(), D3, k_cache.data_ptr(), v_cache.data_ptr(), B, Lq, past, cap, D,
+                        dtype_code(qkv.scalar_type()), stream_of(qkv)),
+        "kv_append");
+}
+
+Tensor attn_decode(const Tensor& qkv, const Tensor& k_cache, const Tensor& v_cache, const optional<Tensor>& key_mask,
+                   const optional<Tensor>& query_mask, int64_t H, int64_t Lk, int64_t window) {
+  const c10::DeviceGuard guard(qkv.device());
+  const int64_t B = qkv.size(0), Lq = qkv.size(1), D3 = qkv.size(2), D = D3 / 3, cap = k_cache.size(1);
+  Tensor km = as_opt(key_mask, at::kBool), qm = as_opt(query_mask, at::kBool);
+  Tensor o = at::empty({B, Lq, D}, qkv.options());
+  check(esgpt_attn_decode(qkv.data_ptr(), D3, k_cache.data_ptr(), v_cache.data_ptr(),
+                          km.defined() ? ptr<const uint8_t>(km) : nullptr,
+                          qm.defined() ? ptr<const uint8_t>(qm) : nullptr, o.data_ptr(), D, B, H, Lq, Lk, cap, D / H,
+                          window, dtype_code(qkv.scalar_type()), stream_of(qkv)),
+        "attn_decode");
+  return o;
+}
+
+// ---- output-layer losses -------------------------------------------------------------------------------------------
+std::vector<esgpt_loss_term> make_terms(at::IntArrayRef t) {
+  TORCH_CHECK(t.size() % 8 == 0, "terms: 8 ints per term");
+  std::vector<esgpt_loss_term> out(std::max<size_t>(1, t.size() / 8));
+  for (size_t i = 0; i < t.size() / 8; ++i) {
+    out[i] = esgpt_loss_term{(int32_t)t[8 * i], (int32_t)t[8 * i + 1], (int32_t)t[8 * i + 2], (int32_t)t[8 * i + 3],
+                             (int32_t)t[8 * i + 4], (int32_t)t[8 * i + 5], (int32_t)t[8 * i + 6], 0};
+  }
+  return out;
+}
+
+// losses f32 [n_terms + 2] (per term, -TTE_LL, total) and d(total)/d(zc), d(total)/d(zt), the position-0 bias rows
+std::tuple<Tensor, Tensor, Tensor, Tensor> output_loss(const Tensor& zc_, const optional<Tensor>& zt_,
+                                                       const optional<Tensor>& zc_bias, BATCH_ARGS, int64_t n_levels,
+                                                       int64_t shift, at::IntArrayRef terms, at::IntArrayRef tte_i,
+                                                       at::ArrayRef<double> tte_f, const Tensor& err) {
+  const c10::DeviceGuard guard(zc_.device());
+  Batch bt = make_batch(BATCH_PASS);
+  Tensor zc = zc_.contiguous();
+  const bool same = !(zt_.has_value() && zt_->defined());
+  Tensor zt = same ? zc : zt_->contiguous();
+  Tensor bias = (zc_bias.has_value() && zc_bias->defined()) ? zc_bias->to(zc.scalar_type()).contiguous() : Tensor();
+  auto tv = make_terms(terms);
+  const int n_terms = (int)(terms.size() / 8);
+  TORCH_CHECK(tte_i.size() == 3 && tte_f.size() == 2, "tte spec: [kind, K, col], [mean_log, std_log]");
+  esgpt_tte_spec tte{(int32_t)tte_i[0], (int32_t)tte_i[1], (int32_t)tte_i[2], 0, (float)tte_f[0], (float)tte_f[1]};
+  Tensor dzc = at::empty_like(zc);
+  Tensor dzt = same ? at::empty({0}, zc.options()) : at::empty_like(zt);
+  const int64_t ldc = zc.size(-1);
+  Tensor dbias = shift ? at::empty({bt.b.B, ldc}, zc.options().dtype(at::kFloat)) : at::empty({0}, zc.options().dtype(at::kFloat));
+  Tensor losses = at::empty({n_terms + 2}, zc.options().dtype(at::kFloat));
+  const size_t nb = esgpt_output_loss_workspace(bt.b.B, bt.b.L, n_terms);
+  Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, zc.options().dtype(at::kByte));
+  check(esgpt_output_loss(&bt.b, zc.data_ptr(), ldc, n_levels, (int)shift, bias.defined() ? bias.data_ptr() : nullptr,
+                          zt.data_ptr(), zt.size(-1), dtype_code(zc.scalar_type()), tv.data(), n_terms, &tte,
+                          dzc.data_ptr(), same ? dzc.data_ptr() : dzt.data_ptr(), shift ? ptr<float>(dbias) : nullptr,
+                          ptr<float>(losses), ws.data_ptr(), nb, ptr<int32_t>(err), stream_of(zc)),
+        "output_loss");
+  return {losses, dzc, dzt, dbias};
+}
+
+// ---- block elementwise stages -----------------------------------------------------------------------------------
+std::tuple<Tensor, Tensor, Tensor, Tensor> residual_ln(const optional<Tensor>& x, const optional<Tensor>& y,
+                                                       const optional<Tensor>& bias, const Tensor& ln_w,
+                                                       const Tensor& ln_b, const optional<Tensor>& row_mask,
+                                                       double p, const optional<Tensor>& seed, double eps,
+                                                       at::ScalarType out_dtype) {
+  const c10::DeviceGuard guard(ln_w.device());
+  Tensor xc = (x.has_value() && x->defined()) ? x->to(at::kFloat).contiguous() : Tensor();
+  Tensor yc = (y.has_value() && y->defined()) ? y->contiguous() : Tensor();
+  Tensor bc = (bias.has_value() && bias->defined()) ? bias->to(at::kFloat).contiguous() : Tensor();
+  TORCH_CHECK(xc.defined() || yc.defined(), "residual_ln: x or y required");
+  const Tensor& ref = xc.defined() ? xc : yc;
+  const int64_t N = ref.size(0), D = ref.size(1);
+  const at::ScalarType y_dtype = yc.defined() ? yc.scalar_type() : at::kFloat;
+  auto f32 = ln_w.options().dtype(at::kFloat);
+  Tensor h = at::empty({N, D}, f32), out = at::empty({N, D}, f32.dtype(out_dtype));
+  Tensor mean = at::empty({N}, f32), rstd = at::empty({N}, f32);
+  Tensor rm = as_opt(row_mask, at::kBool);
+  check(esgpt_residual_ln_fwd(xc.defined() ? ptr<const float>(xc) : nullptr, yc.defined() ? yc.data_ptr() : nullptr,
+                              dtype_code(y_dtype), bc.defined() ? ptr<const float>(bc) : nullptr,
+                              rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p, optr<const uint64_t>(seed),
+                              ptr<const float>(ln_w), ptr<const float>(ln_b), (float)eps, N, D, ptr<float>(h),
+                              out.data_ptr(), dtype_code(out_dtype), ptr<float>(mean), ptr<float>(rstd),
+                              stream_of(ln_w)),
+        "residual_ln");
+  return {h, out, mean, rstd};
+}
+
+// (dx f32 [N, D] | empty, dy y_dtype [N, D] | empty, sums f32 [3, D] = (d ln_w, d ln_b, d bias))
+std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd(const optional<Tensor>& dh, const Tensor& dout_, const Tensor& h,
+                                                   const Tensor& mean, const Tensor& rstd, const Tensor& ln_w,
+                                                   const optional<Tensor>& row_mask, double p,
+                                                   const optional<Tensor>& seed, bool need_dx, bool need_dy,
+                                                   at::ScalarType y_dtype, at::ScalarType out_dtype,
+                                                   const Tensor& tickets) {
+  const c10::DeviceGuard guard(h.device());
+  const int64_t N = h.size(0), D = h.size(1);
+  Tensor dout = dout_.to(out_dtype).contiguous();
+  Tensor dhc = (dh.has_value() && dh->defined()) ? dh->to(at::kFloat).contiguous() : Tensor();
+  auto f32 = h.options().dtype(at::kFloat);
+  Tensor dx = need_dx ? at::empty({N, D}, f32) : at::empty({0}, f32);
+  Tensor dy = need_dy ? at::empty({N, D}, f32.dtype(y_dtype)) : at::empty({0}, f32.dtype(y_dtype));
+  Tensor part = at::empty({esgpt_residual_ln_partials(N) * 3 * D}, f32);
+  Tensor sums = at::empty({3, D}, f32);
+  Tensor rm = as_opt(row_mask, at::kBool);
+  check(esgpt_residual_ln_bwd(dhc.defined() ? ptr<const float>(dhc) : nullptr, dout.data_ptr(), dtype_code(out_dtype),
+                              ptr<const float>(h), ptr<const float>(mean), ptr<const float>(rstd),
+                              ptr<const float>(ln_w), rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p,
+                              optr<const uint64_t>(seed), N, D, need_dx ? ptr<float>(dx) : nullptr,
+                              need_dy ? dy.data_ptr() : nullptr, dtype_code(y_dtype), ptr<float>(part),
+                              ptr<float>(sums), ptr<int32_t>(tickets), stream_of(h)),
+        "residual_ln_bwd");
+  return {dx, dy, sums};
+}
+
+Tensor bias_act(const Tensor& f_, const Tensor& bias, int64_t act) {
+  const c10::DeviceGuard guard(f_.device());
+  Tensor f = f_.contiguous();
+  Tensor g = at::empty_like(f);
+  check(esgpt_bias_act_fwd(f.data_ptr(), ptr<const float>(bias), (int)act, f.size(0), f.size(1), g.data_ptr(),
+                           dtype_code(f.scalar_type()), stream_of(f)),
+        "bias_act");
+  return g;
+}
+
+std::tuple<Tensor, Tensor> bias_act_bwd(const Tensor& dg_, const Tensor& f, const Tensor& bias, int64_t act) {
+  const c10::DeviceGuard guard(f.device());
+  Tensor dg = dg_.to(f.scalar_type()).contiguous();
+  const int64_t N = f.size(0), F = f.size(1);
+  Tensor dz = at::empty_like(f);
+  Tensor part = at::empty({esgpt_bias_act_partials(N) * F}, f.options().dtype(at::kFloat));
+  Tensor dbias = at::empty({F}, f.options().dtype(at::kFloat));
+  check(esgpt_bias_act_bwd(dg.data_ptr(), f.data_ptr(), ptr<const float>(bias), (int)act, N, F, dz.data_ptr(),
+                           ptr<float>(part), ptr<float>(dbias), dtype_code(f.scalar_type()), stream_of(f)),
+        "bias_act_bwd");
+  return {dz, dbias};
+}
+
+Tensor column_sum(const Tensor& x_) {
+  const c10::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous();
+  const int64_t N = x.size(0), F = x.size(1);
+  Tensor part = at::empty({esgpt_column_sum_partials(N) * F}, x.options().dtype(at::kFloat));
+  Tensor out = at::empty({F}, x.options().dtype(at::kFloat));
+  check(esgpt_column_sum(x.data_ptr(), dtype_code(x.scalar_type()), N, F, ptr<float>(part), ptr<float>(out),
+                         stream_of(x)),
+        "column_sum");
+  return out;
+}
+
+// ---- projections ---------------------------------------------------------------------------------------------------
+void gemm_into(int64_t a_layout, const Tensor& a, int64_t lda, int64_t b_layout, const Tensor& b, int64_t ldb,
+               int64_t M, int64_t N, int64_t K, const optional<Tensor>& bias, const optional<Tensor>& alpha,
+               const Tensor& c, bool accumulate, const Tensor& tickets) {
+  const size_t nb = esgpt_gemm_workspace(M, N, K);
+  Tensor ws = nb ? at::empty({(int64_t)nb}, a.options().dtype(at::kByte)) : Tensor();
+  TORCH_CHECK(!nb || esgpt_gemm_counters(M, N) <= tickets.numel(), "GEMM tile grid exceeds the ticket array");
+  check(esgpt_gemm_bf16((int)a_layout, a.data_ptr(), lda, (int)b_layout, b.data_ptr(), ldb, M, N, K,
+                        optr<const float>(bias), optr<const float>(alpha), c.data_ptr(), c.stride(0),
+                        dtype_code(c.scalar_type()), accumulate ? 1 : 0, ws.defined() ? ws.data_ptr() : nullptr, nb,
+                        ptr<int32_t>(tickets), stream_of(a)),
+        "gemm");
+}
+
+// C[M, N] = alpha·A·B (+ bias) in a fresh tensor of out_dtype (layouts: include/esgpt_amd.h)
+Tensor gemm(int64_t a_layout, const Tensor& a, int64_t lda, int64_t b_layout, const Tensor& b, int64_t ldb, int64_t M,
+            int64_t N, int64_t K, const optional<Tensor>& bias, const optional<Tensor>& alpha, at::ScalarType out_dtype,
+            const Tensor& tickets) {
+  const c10::DeviceGuard guard(a.device());
+  Tensor c = at::empty({M, N}, a.options().dtype(out_dtype));
+  gemm_into(a_layout, a, lda, b_layout, b, ldb, M, N, K, bias, alpha, c, false, tickets);
+  return c;
+}
+
+// in-place form (accumulate into / overwrite an existing f32 or bf16 matrix)
+void gemm_(const Tensor& c, int64_t a_layout, const Tensor& a, int64_t lda, int64_t b_layout, const Tensor& b,
+           int64_t ldb, int64_t M, int64_t N, int64_t K, const optional<Tensor>& bias, const optional<Tensor>& alpha,
+           bool accumulate, const Tensor& tickets) {
+  const c10::DeviceGuard guard(a.device());
+  gemm_into(a_layout, a, lda, b_layout, b, ldb, M, N, K, bias, alpha, c, accumulate, tickets);
+}
+
+// y = x·wᵀ (+ bias) (bf16); act >= 0: pre = x·wᵀ + bias and y = act(pre) (pre empty when act < 0)
+std::tuple<Tensor, Tensor> linear_act(const Tensor& x, const Tensor& w, const optional<Tensor>& bias, int64_t act) {
+  const c10::DeviceGuard guard(x.device());
+  TORCH_CHECK(x.stride(-1) == 1 && w.is_contiguous(), "linear: row-major x and w expected");
+  const int64_t T = x.size(0), din = x.size(1), dout = w.size(0);
+  Tensor y = at::empty({T, dout}, x.options());
+  Tensor pre = act >= 0 ? at::empty({T, dout}, x.options()) : at::empty({0}, x.options());
+  check(esgpt_linear_fwd(x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout, optr<const float>(bias), (int)act,
+                         act >= 0 ? pre.data_ptr() : nullptr, y.data_ptr(), dout, stream_of(x)),
+        "linear_fwd");
+  return {pre, y};
+}
+
+// (dx bf16 [T, in] | empty, dw f32 [out, in], db f32 [out] | empty) of y = x·wᵀ (one grouped launch)
+std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x, const Tensor& w,
+                                              const optional<Tensor>& alpha, int64_t act, const optional<Tensor>& pre,
+                                              bool need_dx, bool need_db, const Tensor& tickets) {
+  const c10::DeviceGuard guard(x.device());
+  Tensor dy = dy_.contiguous();
+  const int64_t T = dy.size(0), dout = dy.size(1), din = x.size(1);
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor dw = at::empty({dout, din}, f32);
+  Tensor dx = need_dx ? at::empty({T, din}, dy.options()) : at::empty({0}, dy.options());
+  Tensor db = need_db ? at::empty({dout}, f32) : at::empty({0}, f32);
+  const size_t nb = esgpt_linear_bwd_workspace(T, din, dout, need_dx ? 1 : 0);
+  Tensor ws = nb ? at::empty({(int64_t)nb}, x.options().dtype(at::kByte)) : Tensor();
+  TORCH_CHECK(!nb || esgpt_gemm_counters(dout, din) <= tickets.numel(), "GEMM tile grid exceeds the ticket array");
+  const bool has_pre = pre.has_value() && pre->defined();
+  check(esgpt_linear_bwd(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
+                         optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
+                         has_pre ? pre->stride(0) : 0, need_dx ? dx.data_ptr() : nullptr, need_dx ? din : 0,
+                         ptr<float>(dw), need_db ? ptr<float>(db) : nullptr, ws.defined() ? ws.data_ptr() : nullptr, nb,
+                         ptr<int32_t>(tickets), stream_of(x)),
+        "linear_bwd");
+  return {dx, dw, db};
+}
+
+// y = x·wᵀ (+ bias) with the bf16 weight shadow w; `masters` are the f32 parameters (row blocks of w) that receive
+// the weight gradient in the registered backward — unused here (ProjFn of the drop-in modules).
+Tensor linear(const Tensor& x_, const Tensor& w, const optional<Tensor>& bias, at::TensorList masters,
+              const Tensor& tickets) {
+  const c10::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous();
+  const int64_t T = x.size(0), din = x.size(1), dout = w.size(0);
+  Tensor y = at::empty({T, dout}, x.options());
+  gemm_into(ESGPT_GEMM_K_CONTIG, x, din, ESGPT_GEMM_K_CONTIG, w, din, T, dout, din, bias, c10::nullopt, y, false,
+            tickets);
+  return y;
+}
+
+// InnerMLP up to c_proj's bias (transformer.py:378-391): pre = x·W_fcᵀ + b_fc, g = act(pre), y = g·W_projᵀ.
+// Returns (y, pre, g); pre and g are kept for the backward.
+std::tuple<Tensor, Tensor, Tensor> mlp(const Tensor& x_, const Tensor& w_fc, const Tensor& w_pj, const Tensor& b_fc,
+                                       int64_t act, const Tensor& p_fc, const Tensor& p_pj, const Tensor& tickets) {
+  const c10::DeviceGuard guard(x_.device());
+  Tensor x = x_.contiguous();
+  auto pg = linear_act(x, w_fc, b_fc, act);
+  Tensor g = std::get<1>(pg);
+  const int64_t T = g.size(0), F = g.size(1), D = w_pj.size(0);
+  Tensor y = at::empty({T, D}, x.options());
+  gemm_into(ESGPT_GEMM_K_CONTIG, g, F, ESGPT_GEMM_K_CONTIG, w_pj, F, T, D, F, c10::nullopt, c10::nullopt, y, false,
+            tickets);
+  return {y, std::get<0>(pg), g};
+}
+
+// Generative heads + fused losses (model_output.py:1253-1721): zc = xc·wcᵀ + bc (bf16 GEMM; wc / bc padded to a
+// multiple of 8 rows), zt likewise for a separate TTE head (NA), then output_loss. Returns (losses, dzc, dzt, dbias)
+// — the unscaled loss gradients w.r.t. the logits, consumed by the registered backward (scaled there by the incoming
+// d(total) read from device memory). cw/cb/tw/tb: the f32 parameters receiving the head gradients (unused here).
+std::tuple<Tensor, Tensor, Tensor, Tensor> head_loss(const Tensor& xc, const optional<Tensor>& xt, BATCH_ARGS,
+                                                     at::IntArrayRef terms, at::IntArrayRef tte_i,
+                                                     at::ArrayRef<double> tte_f, int64_t shift, int64_t n_levels,
+                                                     const Tensor& wc, const Tensor& bc, const optional<Tensor>& wt,
+                                                     const optional<Tensor>& bt, at::TensorList cw, at::TensorList cb,
+                                                     at::TensorList tw, at::TensorList tb, const Tensor& err,
+                                                     const Tensor& tickets) {
+  const c10::DeviceGuard guard(xc.device());
+  Tensor zc = linear(xc, wc, bc, {}, tickets);
+  optional<Tensor> zt;
+  if (wt.has_value() && wt->defined()) zt = linear(*xt, *wt, bt, {}, tickets);
+  optional<Tensor> zb;
+  if (shift) zb = bc.to(at::kBFloat16);
+  return output_loss(zc, zt, zb, BATCH_PASS, n_levels, shift, terms, tte_i, tte_f, err);
+}
+
+// ---- optimizer -------------------------------------------------------------------------------------------------------
+void adamw(const Tensor& table, const Tensor& blocks, double lr, double beta1, double beta2, double eps, double wd,
+           int64_t step, const optional<Tensor>& per_tensor, const Tensor& err) {
+  const c10::DeviceGuard guard(table.device());
+  check(esgpt_adamw(reinterpret_cast<const esgpt_adam_tensor*>(table.data_ptr()), ptr<const int64_t>(blocks),
+                    blocks.numel(), (float)lr, (float)beta1, (float)beta2, (float)eps, (float)wd, step,
+                    optr<const float>(per_tensor), ptr<const int32_t>(err), stream_of(table)),
+        "adamw");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(esgpt, m) {
+  m.def("embed_joint(Tensor table, " BATCH_SCHEMA ", int[] buckets, Tensor? sin_div, Tensor? cos_div, int flags, "
+        "float static_w, float dynamic_w, int G, Tensor err) -> Tensor");
+  m.def("embed_split_bags(Tensor cat_table, Tensor num_table, " BATCH_SCHEMA ", int[] buckets, int flags, "
+        "float cat_scale, float num_scale, float static_scale, int G, Tensor err) -> Tensor");
+  m.def("embed_epilogue(Tensor y, " BATCH_SCHEMA ", int G, int flags, Tensor? sin_div, Tensor? cos_div) -> Tensor");
+  m.def("embed_epilogue_bwd(Tensor dout, " BATCH_SCHEMA ", int G, int flags) -> Tensor");
+  m.def("embed_bag_bwd(Tensor dsrc, " BATCH_SCHEMA ", int[] buckets, int selector, int flags, float dyn_scale, "
+        "float static_scale, int ld, int D, int V, int G) -> Tensor");
+  m.def("attention(Tensor qkv, Tensor? key_mask, Tensor? query_mask, int H, int window, bool static_kv_first, "
+        "float dropout_p, Tensor? seed) -> (Tensor, Tensor)");
+  m.def("attention_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor? key_mask, Tensor? query_mask, int H, "
+        "int window, bool static_kv_first, float dropout_p, Tensor? seed, Tensor tickets) -> Tensor");
+  m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, int past) -> ()");
+  m.def("attn_decode(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor? key_mask, Tensor? query_mask, int H, "
+        "int Lk, int window) -> Tensor");
+  m.def("output_loss(Tensor zc, Tensor? zt, Tensor? zc_bias, " BATCH_SCHEMA ", int n_levels, int shift, int[] terms, "
+        "int[] tte_i, float[] tte_f, Tensor err) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("residual_ln(Tensor? x, Tensor? y, Tensor? bias, Tensor ln_w, Tensor ln_b, Tensor? row_mask, float p, "
+        "Tensor? seed, float eps, ScalarType out_dtype) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("residual_ln_bwd(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, Tensor? row_mask, "
+        "float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, ScalarType out_dtype, "
+        "Tensor tickets) -> (Tensor, Tensor, Tensor)");
+  m.def("bias_act(Tensor f, Tensor bias, int act) -> Tensor");
+  m.def("bias_act_bwd(Tensor dg, Tensor f, Tensor bias, int act) -> (Tensor, Tensor)");
+  m.def("column_sum(Tensor x) -> Tensor");
+  m.def("gemm(int a_layout, Tensor a, int lda, int b_layout, Tensor b, int ldb, int M, int N, int K, Tensor? bias, "
+        "Tensor? alpha, ScalarType out_dtype, Tensor tickets) -> Tensor");
+  m.def("gemm_(Tensor(a!) c, int a_layout, Tensor a, int lda, int b_layout, Tensor b, int ldb, int M, int N, int K, "
+        "Tensor? bias, Tensor? alpha, bool accumulate, Tensor tickets) -> ()");
+  m.def("linear_act(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
+  m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
+        "Tensor tickets) -> (Tensor, Tensor, Tensor)");
+  m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
+  m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, int act, Tensor p_fc, Tensor p_pj, Tensor tickets) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("head_loss(Tensor xc, Tensor? xt, " BATCH_SCHEMA ", int[] terms, int[] tte_i, float[] tte_f, int shift, "
+        "int n_levels, Tensor wc, Tensor bc, Tensor? wt, Tensor? bt, Tensor[] cw, Tensor[] cb, Tensor[] tw, "
+        "Tensor[] tb, Tensor err, Tensor tickets) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("adamw(Tensor table, Tensor blocks, float lr, float beta1, float beta2, float eps, float weight_decay, "
+        "int step, Tensor? per_tensor, Tensor err) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
+  m.impl("embed_joint", &embed_joint);
+  m.impl("embed_split_bags", &embed_split_bags);
+  m.impl("embed_epilogue", &embed_epilogue);
+  m.impl("embed_epilogue_bwd", &embed_epilogue_bwd);
+  m.impl("embed_bag_bwd", &embed_bag_bwd);
+  m.impl("attention", &attention);
+  m.impl("attention_bwd", &attention_bwd);
+  m.impl("kv_append", &kv_append);
+  m.impl("attn_decode", &attn_decode);
+  m.impl("output_loss", &output_loss);
+  m.impl("residual_ln", &residual_ln);
+  m.impl("residual_ln_bwd", &residual_ln_bwd);
+  m.impl("bias_act", &bias_act);
+  m.impl("bias_act_bwd", &bias_act_bwd);
+  m.impl("column_sum", &column_sum);
+  m.impl("gemm", &gemm);
+  m.impl("gemm_", &gemm_);
+  m.impl("linear_act", &linear_act);
+  m.impl("linear_bwd", &linear_bwd);
+  m.impl("linear", &linear);
+  m.impl("mlp", &mlp);
+  m.impl("head_loss", &head_loss);
+  m.impl("adamw", &adamw);
+}

@@ -111,7 +111,7 @@ class DataEmbeddingLayer(torch.nn.Module):
                 n_total_embeddings, numerical_embedding_dim, mode="sum", padding_idx=0
             )
             self.num_proj = torch.nn.Linear(numerical_embedding_dim, out_dim)
-        self._buckets = None
+        self._buckets = []  # the operators' int[] buckets ([] = un-bucketed)
         self._group_error = None
         if split_by_measurement_indices:
             # The reference raises this in forward (_split_batch_into_measurement_index_buckets, :529-535), not at
@@ -123,9 +123,9 @@ class DataEmbeddingLayer(torch.nn.Module):
                         "(in cases where there are no FUNCTIONAL_TIME_DEPENDENT measurements)."
                     )
                     break
-            from ..kernels import buckets_struct
+            from ..kernels import buckets_list, buckets_struct
 
-            self._buckets = buckets_struct(split_by_measurement_indices)
+            self._buckets = buckets_list(buckets_struct(split_by_measurement_indices))
 
     @staticmethod
     def get_measurement_index_normalziation(measurement_indices: torch.Tensor) -> torch.Tensor:
@@ -151,11 +151,10 @@ class DataEmbeddingLayer(torch.nn.Module):
     def embed(self, batch: PytorchBatch, time_layer=None, cumsum: bool = False) -> torch.Tensor:
         """Fused input-layer embedding: data embedding (+ temporal encoding at level 0, + cumsum over levels),
         masked by ``event_mask``. Returns f32 [B, L, G, D]."""
-        from ..kernels import EmbedEpilogueFn, EmbedSpec, JointEmbedFn, SplitBagsFn, batch_view
+        from ..kernels import EmbedSpec, embed_epilogue, joint_embed, split_bags
 
         if self._group_error is not None:
             raise ValueError(self._group_error)
-        bv = batch_view(batch)
         flags = self._flags()
         sin_div = cos_div = None
         post = 0
@@ -170,28 +169,28 @@ class DataEmbeddingLayer(torch.nn.Module):
         static = bool(flags & L.EMB_STATIC)
         if self.embedding_mode == EmbeddingMode.JOINT:
             spec = EmbedSpec(flags | post, self.static_weight, self.dynamic_weight, self._buckets, G)
-            return JointEmbedFn.apply(self.embed_layer.weight, bv, spec, sin_div, cos_div)
+            return joint_embed(self.embed_layer.weight, batch, spec, sin_div, cos_div)
         # SPLIT: bags -> one GEMM with [cat_proj | num_proj] -> epilogue (time / cumsum / mask).
         dw = self.dynamic_weight if static else 1.0
         cat_scale = dw * self.categorical_weight
         num_scale = dw * self.numerical_weight
         static_scale = self.static_weight if static else 0.0
         spec = EmbedSpec(flags, self.static_weight, self.dynamic_weight, self._buckets, G)
-        x = SplitBagsFn.apply(self.categorical_embed_layer.weight, self.numerical_embed_layer.weight, bv, spec,
-                              cat_scale, num_scale, static_scale)
+        x = split_bags(self.categorical_embed_layer.weight, self.numerical_embed_layer.weight, batch, spec,
+                       cat_scale, num_scale, static_scale)
         w = torch.cat([self.cat_proj.weight, self.num_proj.weight], dim=1)
         bias = (cat_scale + static_scale) * self.cat_proj.bias + num_scale * self.num_proj.bias
-        from ..fused import ProjFn, compute_dtype, gemm_supported
+        from ..fused import compute_dtype, gemm_supported, linear_op
 
         x2 = x.reshape(-1, x.shape[-1])
         if x2.is_cuda and compute_dtype() == torch.bfloat16 and gemm_supported(x2.shape[0], w.shape[1], w.shape[0]):
             # bf16: the HIP GEMM (bias in the epilogue; dW, db in one grouped backward launch)
             with torch.autocast("cuda", enabled=False):
-                y = ProjFn.apply(x2.to(torch.bfloat16).contiguous(), w.detach().to(torch.bfloat16),
-                                 bias.float().contiguous(), w).float().view(*x.shape[:-1], w.shape[0])
+                y = linear_op(x2.to(torch.bfloat16).contiguous(), w.detach().to(torch.bfloat16),
+                              bias.float().contiguous(), [w]).float().view(*x.shape[:-1], w.shape[0])
         else:
             y = torch.nn.functional.linear(x, w, bias).float()
-        return EmbedEpilogueFn.apply(y, bv, G, post, sin_div, cos_div)
+        return embed_epilogue(y, batch, G, post, sin_div, cos_div)
 
     def forward(self, batch: PytorchBatch) -> torch.Tensor:
         """``DataEmbeddingLayer.forward`` (``:609-708``): [B, L, D] or [B, L, G, D] (no temporal encoding)."""

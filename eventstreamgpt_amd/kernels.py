@@ -1,8 +1,11 @@
-"""Autograd wrappers around the C ABI (the PyTorch-ROCm custom-op layer).
+"""Python face of the custom operators (``torch.ops.esgpt``, defined in csrc/torch_ops.cpp; fake kernels and
+autograd formulas in ``ops.py``) plus the per-device state they share: the device error block, the split-K /
+cross-workgroup ticket array and the dropout seed bank.
 
-Each ``torch.autograd.Function`` launches the gfx950 kernels on torch's current HIP stream with raw device
-pointers; outputs and workspaces are allocated by torch (the library allocates nothing). Nothing here falls back
-to a CPU / ATen implementation: a missing library or a non-CUDA tensor raises.
+Every function here launches through ``torch.ops.esgpt.*`` on torch's current HIP stream; outputs and workspaces
+are allocated by torch (the library allocates nothing). Nothing here falls back to a CPU / ATen implementation: a
+missing library or a non-HIP tensor raises ``HipExtensionMissing``. ``BatchView`` (the ``esgpt_batch`` ctypes
+descriptor) remains for the raw C-ABI binding used by the ABI tests and the benchmark's isolated launches.
 """
 from __future__ import annotations
 
@@ -104,6 +107,8 @@ def _dev_index(device: torch.device) -> int:
 def err_word(device: torch.device) -> torch.Tensor:
     """The device error block of the C ABI (16 bytes: int32 ESGPT_FLAG_* bits, pad, int64 max bad index), viewed as
     int64 [2]. Kernels OR flags into it; esgpt_adamw is a no-op while the flags are set."""
+    if device.type != "cuda":  # fake / meta tracing of the operators
+        return torch.empty(2, dtype=torch.int64, device=device)
     idx = _dev_index(device)
     w = _ERR.get(idx)
     if w is None:
@@ -128,7 +133,7 @@ def raise_for_error(code: int, max_index: int, n_total_embeddings: int | None = 
         return
     tail = "" if batch is None else f": {batch}"
     if code & L.FLAG_BAD_INDEX:
-        raise AssertionError(f"Invalid embedding! {torch.tensor(max_index)} >= {n_total_embeddings}")
+        raise AssertionError(f"Invalid embedding! {torch.tensor(max_index)} >= {n_total_embeddings}")  # 0-dim: prints the value
     if code & L.FLAG_TTE_NAN:
         raise ValueError(f"NaNs in TTE_LL{tail}")
     if code & L.FLAG_TTE_NO_OBS:
@@ -159,29 +164,14 @@ def tickets(device: torch.device) -> torch.Tensor:
     """Per-device int32 counters of the kernels' in-launch last-arriver reductions (split-K GEMM tiles, column
     sums). Zeroed once here; every launch leaves the counters it used at zero. The launches that use them are
     stream-ordered (one stream per device in the training step)."""
+    if device.type != "cuda":  # fake / meta tracing of the operators
+        return torch.empty(TICKETS_LEN, dtype=torch.int32, device=device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     t = _TICKETS.get(idx)
     if t is None:
         t = torch.zeros(TICKETS_LEN, dtype=torch.int32, device=torch.device("cuda", idx))
         _TICKETS[idx] = t
     return t
-
-
-def check_errors(device: torch.device | None = None, n_total_embeddings: int | None = None):
-    """Reads (one host sync) and clears the device error word; raises the reference's exception for it."""
-    device = device or torch.device("cuda", torch.cuda.current_device())
-    w = err_word(device)
-    code = int(w.item())
-    if code:
-        w.zero_()
-        if code & L.FLAG_BAD_INDEX:
-            raise AssertionError(f"Invalid embedding! index >= {n_total_embeddings}")
-        if code & L.FLAG_TTE_NO_OBS:
-            raise ValueError("No observed time-to-event for >= 1 patient in batch")
-        if code & L.FLAG_TTE_NAN:
-            raise ValueError("NaNs in TTE_LL")
-        if code & L.FLAG_BAD_LABEL:
-            raise IndexError("Target out of bounds in classification / regression labels")
 
 
 def buckets_struct(groups: list[list] | None):
@@ -213,8 +203,33 @@ def buckets_struct(groups: list[list] | None):
     return s
 
 
+def _s64(u: int) -> int:
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def buckets_list(bk) -> list[int]:
+    """``esgpt_buckets`` → the operators' ``int[] buckets`` ([] = un-bucketed; else G, cat_bits x8, num_bits x8)."""
+    if bk is None:
+        return []
+    return [int(bk.G)] + [_s64(int(b)) for b in bk.cat_bits] + [_s64(int(b)) for b in bk.num_bits]
+
+
 def _bref(bk):
     return None if bk is None else ctypes.byref(bk)
+
+
+def _ops():
+    from . import ops
+
+    return ops.load()
+
+
+def batch_args(batch: PytorchBatch) -> tuple:
+    """The nine batch tensors of every input-layer / loss operator, in schema order."""
+    if batch.event_mask.device.type != "cuda":
+        raise L.HipExtensionMissing("eventstreamgpt_amd kernels need the batch on a HIP device (no CPU path).")
+    return (batch.event_mask, batch.time_delta, batch.time, batch.dynamic_indices, batch.dynamic_measurement_indices,
+            batch.dynamic_values, batch.dynamic_values_mask, batch.static_indices, batch.static_measurement_indices)
 
 
 # ----------------------------------------------------------------------------------------------------------------
@@ -225,114 +240,39 @@ class EmbedSpec:
     flags: int
     static_w: float
     dynamic_w: float
-    groups: object  # EsgptBuckets or None
+    groups: list  # buckets_list(...) ([] = un-bucketed)
     G: int
 
 
-def _bag_bwd(bv, spec_groups, selector, flags, dyn_scale, static_scale, dsrc, ld, D, V, G):
-    lib = L.load()
-    dtable = torch.empty(V, D, dtype=torch.float32, device=dsrc.device)
-    nbytes = lib.esgpt_embed_bag_bwd_workspace(bv.ref, G, V, D)
-    ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=dsrc.device)
-    L.check(lib.esgpt_embed_bag_bwd(bv.ref, _bref(spec_groups), selector, flags, dyn_scale, static_scale,
-                                    dsrc.data_ptr(), ld, D, V, dtable.data_ptr(), ws.data_ptr(), nbytes, L.stream()),
-            "embed_bag_bwd")
-    return dtable
+def joint_embed(table, batch: PytorchBatch, spec: EmbedSpec, sin_div, cos_div):
+    """``esgpt::embed_joint``: the JOINT DataEmbeddingLayer (+ time encoding / NA cumsum / mask) → f32 [B, L, G, D];
+    differentiable in ``table``."""
+    args = batch_args(batch)
+    note_vocab(table.device, table.shape[0])
+    with _timed("embed_joint_fwd"):
+        return _ops().embed_joint(table, *args, spec.groups, sin_div, cos_div, spec.flags, float(spec.static_w),
+                                  float(spec.dynamic_w), spec.G, err_word(table.device))
 
 
-def _epilogue_bwd(bv, G, D, dout, flags):
-    lib = L.load()
-    dy = torch.empty_like(dout)
-    L.check(lib.esgpt_embed_epilogue_bwd(bv.ref, G, D, dout.data_ptr(), flags, dy.data_ptr(), L.stream()),
-            "embed_epilogue_bwd")
-    return dy
+def split_bags(cat_table, num_table, batch: PytorchBatch, spec: EmbedSpec, cat_scale, num_scale, static_scale):
+    """``esgpt::embed_split_bags``: SPLIT mode pre-projection bags X [B*L*G, Dc+Dn] =
+    [cat_scale*bag_c + static_scale*static_c, num_scale*bag_n]; differentiable in both tables."""
+    args = batch_args(batch)
+    note_vocab(cat_table.device, cat_table.shape[0])
+    return _ops().embed_split_bags(cat_table, num_table, *args, spec.groups, spec.flags, float(cat_scale),
+                                   float(num_scale), float(static_scale), spec.G, err_word(cat_table.device))
 
 
-class JointEmbedFn(torch.autograd.Function):
-    """JOINT DataEmbeddingLayer (+ optional time encoding / NA cumsum) → f32 [B, L, G, D]."""
-
-    @staticmethod
-    def forward(ctx, table, bv: BatchView, spec: EmbedSpec, sin_div, cos_div):
-        lib = L.load()
-        V, D = table.shape
-        table = table.contiguous().float()
-        out = torch.empty(bv.B, bv.L, spec.G, D, dtype=torch.float32, device=table.device)
-        note_vocab(table.device, V)
-        with _timed("embed_joint_fwd"):
-            st = lib.esgpt_embed_joint_fwd(bv.ref, _bref(spec.groups), table.data_ptr(), V, D, L.ptr(sin_div),
-                                           L.ptr(cos_div), spec.flags, spec.static_w, spec.dynamic_w,
-                                           out.data_ptr(), err_word(table.device).data_ptr(), L.stream())
-        L.check(st, "embed_joint_fwd")
-        ctx.bv, ctx.spec, ctx.V, ctx.D = bv, spec, V, D
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        bv, spec, V, D = ctx.bv, ctx.spec, ctx.V, ctx.D
-        dout = dout.contiguous().float()
-        if spec.flags & L.EMB_CUMSUM:
-            dsrc = _epilogue_bwd(bv, spec.G, D, dout, spec.flags)
-        else:
-            dsrc = dout
-        static = bool(spec.flags & L.EMB_STATIC) and bv.S > 0
-        dyn_scale = spec.dynamic_w if static else 1.0
-        with _timed("embed_joint_bwd"):
-            dtable = _bag_bwd(bv, spec.groups, L.BAG_JOINT, spec.flags, dyn_scale, spec.static_w, dsrc, D, D, V,
-                              spec.G)
-        return dtable, None, None, None, None
+def embed_epilogue(y, batch: PytorchBatch, G: int, flags: int, sin_div, cos_div):
+    """``esgpt::embed_epilogue``: out[e,g] = mask_e * cumsum_g(y + time@g0) (flags select time / cumsum)."""
+    return _ops().embed_epilogue(y, *batch_args(batch), G, flags, sin_div, cos_div)
 
 
-class SplitBagsFn(torch.autograd.Function):
-    """SPLIT mode pre-projection bags: X [B*L*G, Dc+Dn] = [cat_scale*bag_c + static_scale*static_c, num_scale*bag_n]."""
-
-    @staticmethod
-    def forward(ctx, cat_table, num_table, bv: BatchView, spec: EmbedSpec, cat_scale, num_scale, static_scale):
-        lib = L.load()
-        V, Dc = cat_table.shape
-        Dn = num_table.shape[1]
-        cat_table = cat_table.contiguous().float()
-        num_table = num_table.contiguous().float()
-        x = torch.empty(bv.B * bv.L * spec.G, Dc + Dn, dtype=torch.float32, device=cat_table.device)
-        note_vocab(cat_table.device, V)
-        L.check(lib.esgpt_embed_split_bags_fwd(bv.ref, _bref(spec.groups), cat_table.data_ptr(), Dc,
-                                               num_table.data_ptr(), Dn, V, spec.flags, cat_scale, num_scale,
-                                               static_scale, x.data_ptr(), err_word(x.device).data_ptr(),
-                                               L.stream()), "embed_split_bags_fwd")
-        ctx.bv, ctx.spec, ctx.V, ctx.Dc, ctx.Dn = bv, spec, V, Dc, Dn
-        ctx.scales = (cat_scale, num_scale, static_scale)
-        return x
-
-    @staticmethod
-    def backward(ctx, dx):
-        bv, spec, V, Dc, Dn = ctx.bv, ctx.spec, ctx.V, ctx.Dc, ctx.Dn
-        cat_scale, num_scale, static_scale = ctx.scales
-        dx = dx.contiguous().float()
-        flags = spec.flags
-        if static_scale == 0.0:
-            flags &= ~L.EMB_STATIC
-        dcat = _bag_bwd(bv, spec.groups, L.BAG_CAT, flags, cat_scale, static_scale, dx, Dc + Dn, Dc, V, spec.G)
-        dnum = _bag_bwd(bv, spec.groups, L.BAG_NUM, flags, num_scale, 0.0, dx[:, Dc:], Dc + Dn, Dn, V, spec.G)
-        return dcat, dnum, None, None, None, None, None
-
-
-class EmbedEpilogueFn(torch.autograd.Function):
-    """out[e,g] = mask_e * cumsum_g(y + time@g0) (flags select time / cumsum)."""
-
-    @staticmethod
-    def forward(ctx, y, bv: BatchView, G, flags, sin_div, cos_div):
-        lib = L.load()
-        D = y.shape[-1]
-        y = y.contiguous().float()
-        out = torch.empty(bv.B, bv.L, G, D, dtype=torch.float32, device=y.device)
-        L.check(lib.esgpt_embed_epilogue_fwd(bv.ref, G, D, y.data_ptr(), L.ptr(sin_div), L.ptr(cos_div), flags,
-                                             out.data_ptr(), L.stream()), "embed_epilogue_fwd")
-        ctx.bv, ctx.G, ctx.D, ctx.flags = bv, G, D, flags
-        return out
-
-    @staticmethod
-    def backward(ctx, dout):
-        dy = _epilogue_bwd(ctx.bv, ctx.G, ctx.D, dout.contiguous().float(), ctx.flags)
-        return dy.view(-1, ctx.D), None, None, None, None, None
+def bag_bwd(batch: PytorchBatch, groups: list, selector: int, flags: int, dyn_scale: float, static_scale: float,
+            dsrc, ld: int, D: int, V: int, G: int):
+    """``esgpt::embed_bag_bwd``: the table gradient of the bag sums (dsrc rows of leading dimension ``ld``)."""
+    return _ops().embed_bag_bwd(dsrc, *batch_args(batch), groups, selector, flags, float(dyn_scale),
+                                float(static_scale), ld, D, V, G)
 
 
 # ----------------------------------------------------------------------------------------------------------------
@@ -397,55 +337,22 @@ def _attn_counters(device, B: int, H: int, Lk: int):
     return t.data_ptr() if L.load().esgpt_attn_bwd_counters(B, H, Lk) <= t.numel() else None
 
 
-class AttentionFn(torch.autograd.Function):
-    """Packed-QKV causal/local attention. qkv: [Bs, T, 3D] (q | k | v), returns o: [Bs, T - skf, D]."""
+def attention(qkv, key_mask, query_mask, H: int, window: int, static_kv_first: bool, dropout_p: float = 0.0):
+    """``esgpt::attention``: packed-QKV causal / local attention. qkv: [Bs, T, 3D] (q | k | v), returns
+    o: [Bs, T - skf, D]; differentiable in ``qkv`` (one fused MFMA backward)."""
+    if qkv.device.type != "cuda":
+        raise L.HipExtensionMissing("eventstreamgpt_amd: attention needs a HIP device tensor (no CPU path)")
+    seed = next_dropout_seed(qkv.device) if dropout_p > 0 else None
+    with _timed("attn_fwd"):
+        o, _lse = _ops().attention(qkv, key_mask, query_mask, H, window, bool(static_kv_first), float(dropout_p),
+                                   seed)
+    return o
 
-    @staticmethod
-    def forward(ctx, qkv, key_mask, query_mask, H: int, window: int, static_kv_first: bool, dropout_p: float = 0.0):
-        lib = L.load()
-        qkv = qkv.contiguous()
-        Bs, T, D3 = qkv.shape
-        D = D3 // 3
-        hd = D // H
-        skf = 1 if static_kv_first else 0
-        Lk, Lq = T, T - skf
-        es = qkv.element_size()
-        base = qkv.data_ptr()
-        o = torch.empty(Bs, Lq, D, dtype=qkv.dtype, device=qkv.device)
-        lse = torch.empty(Bs, H, Lq, dtype=torch.float32, device=qkv.device)
-        seed = next_dropout_seed(qkv.device) if dropout_p > 0 else None
-        with _timed("attn_fwd"):
-            st = lib.esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
-                                    lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask), Bs, H, Lq, Lk, hd, window,
-                                    float(dropout_p), L.ptr(seed), L.dtype_code(qkv.dtype), L.stream())
-        L.check(st, "attn_fwd")
-        ctx.save_for_backward(qkv, o, lse, key_mask, query_mask, seed)
-        ctx.cfg = (H, window, skf, float(dropout_p))
-        return o
 
-    @staticmethod
-    def backward(ctx, do):
-        lib = L.load()
-        qkv, o, lse, key_mask, query_mask, seed = ctx.saved_tensors
-        H, window, skf, dropout_p = ctx.cfg
-        do = do.contiguous().to(qkv.dtype)
-        Bs, T, D3 = qkv.shape
-        D = D3 // 3
-        hd = D // H
-        Lk, Lq = T, T - skf
-        es = qkv.element_size()
-        dqkv = (torch.zeros if skf else torch.empty)(Bs, T, D3, dtype=qkv.dtype, device=qkv.device)
-        nbytes = lib.esgpt_attn_bwd_workspace(Bs, H, Lq, Lk, hd)
-        ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=qkv.device)
-        base, dbase = qkv.data_ptr(), dqkv.data_ptr()
-        with _timed("attn_bwd"):
-            st = lib.esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
-                                    do.data_ptr(), D, lse.data_ptr(), L.ptr(key_mask), L.ptr(query_mask),
-                                    dbase + skf * D3 * es, dbase + D * es, dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd,
-                                    window, dropout_p, L.ptr(seed), L.dtype_code(qkv.dtype), ws.data_ptr(), nbytes,
-                                    _attn_counters(qkv.device, Bs, H, Lk), L.stream())
-        L.check(st, "attn_bwd")
-        return dqkv, None, None, None, None, None, None
+class AttentionFn:
+    """Call-compatible name of ``attention`` (``AttentionFn.apply(qkv, key_mask, query_mask, H, window, skf, p)``)."""
+
+    apply = staticmethod(attention)
 
 
 # ----------------------------------------------------------------------------------------------------------------
@@ -509,9 +416,9 @@ def cached_attention(qkv: torch.Tensor, layer_past, key_mask: torch.Tensor | Non
     (o [B, Lq, D], LayerKV). Inference only (no autograd through the cache)."""
     if torch.is_grad_enabled() and qkv.requires_grad:
         raise NotImplementedError("eventstreamgpt_amd: the KV-cache path is for generation (run under torch.no_grad())")
-    lib = L.load()
     if qkv.device.type != "cuda":
         raise L.HipExtensionMissing("eventstreamgpt_amd: KV-cache attention needs a HIP device tensor")
+    ops = _ops()
     qkv = qkv.contiguous()
     B, Lq, D3 = qkv.shape
     D = D3 // 3
@@ -519,11 +426,8 @@ def cached_attention(qkv: torch.Tensor, layer_past, key_mask: torch.Tensor | Non
     st, P = _kv_store_for(layer_past, B, D, H, Lq, cap_hint, qkv.dtype, qkv.device)
     Lk = P + Lq
     cap = st.k.shape[1]
-    code = L.dtype_code(qkv.dtype)
     with _timed("kv_append"):
-        s = lib.esgpt_kv_append(qkv.data_ptr(), D3, st.k.data_ptr(), st.v.data_ptr(), B, Lq, P, cap, D, code,
-                                L.stream())
-    L.check(s, "kv_append")
+        ops.kv_append(qkv, st.k, st.v, P)
     st.length = Lk
     km = qm = None
     if key_mask is not None:
@@ -531,58 +435,32 @@ def cached_attention(qkv: torch.Tensor, layer_past, key_mask: torch.Tensor | Non
             raise ValueError(f"key mask of shape {tuple(key_mask.shape)} does not cover {Lk} keys of {B} subjects")
         km = key_mask.to(torch.bool).contiguous()
         qm = km[:, P:].contiguous()
-    o = torch.empty(B, Lq, D, dtype=qkv.dtype, device=qkv.device)
     with _timed("attn_decode"):
-        s = lib.esgpt_attn_decode(qkv.data_ptr(), D3, st.k.data_ptr(), st.v.data_ptr(), L.ptr(km), L.ptr(qm),
-                                  o.data_ptr(), D, B, H, Lq, Lk, cap, hd, int(window), code, L.stream())
-    L.check(s, "attn_decode")
+        o = ops.attn_decode(qkv, st.k, st.v, km, qm, H, Lk, int(window))
     return o, LayerKV(st, Lk)
 
 
 # ----------------------------------------------------------------------------------------------------------------
 # Output-layer losses
 # ----------------------------------------------------------------------------------------------------------------
-class OutputLossFn(torch.autograd.Function):
-    """Fused generative losses. Returns f32 [n_terms + 2] = per-term losses, -TTE_LL, total.
+def terms_list(terms) -> list[int]:
+    """``esgpt_loss_term`` structs → the operators' flat ``int[] terms`` (8 ints per term)."""
+    out = []
+    for t in terms:
+        out += [t.kind, t.meas_idx, t.vocab_start, t.vocab_end, t.col, t.obs_col, t.level, 0]
+    return out
 
-    Only the total (last element) carries gradient; the per-term entries are for logging.
-    ``zt=None`` means the TTE parameters live in ``zc`` (CI: one fused head GEMM).
-    """
 
-    @staticmethod
-    def forward(ctx, zc, zt, zc_bias, bv: BatchView, terms, tte, shift: int, n_levels: int):
-        lib = L.load()
-        zc = zc.contiguous()
-        ldc = zc.shape[-1]
-        same = zt is None
-        zt_ = zc if same else zt.contiguous()
-        ldt = zt_.shape[-1]
-        if zc_bias is not None:
-            zc_bias = zc_bias.to(zc.dtype).contiguous()
-        n_terms = len(terms)
-        arr = (L.EsgptLossTerm * max(1, n_terms))(*terms)
-        dzc = torch.empty_like(zc)
-        dzt = dzc if same else torch.empty_like(zt_)
-        dbias = torch.empty(bv.B, ldc, dtype=torch.float32, device=zc.device) if shift else None
-        losses = torch.empty(n_terms + 2, dtype=torch.float32, device=zc.device)
-        nbytes = lib.esgpt_output_loss_workspace(bv.B, bv.L, n_terms)
-        ws = torch.empty(max(1, nbytes), dtype=torch.uint8, device=zc.device)
-        with _timed("output_loss"):
-            st = lib.esgpt_output_loss(bv.ref, zc.data_ptr(), ldc, n_levels, shift, L.ptr(zc_bias), zt_.data_ptr(),
-                                       ldt, L.dtype_code(zc.dtype), arr, n_terms, ctypes.byref(tte), dzc.data_ptr(),
-                                       dzt.data_ptr(), L.ptr(dbias), losses.data_ptr(), ws.data_ptr(), nbytes,
-                                       err_word(zc.device).data_ptr(), L.stream())
-        L.check(st, "output_loss")
-        ctx.same = same
-        ctx.has_bias = zc_bias is not None
-        ctx.save_for_backward(dzc, None if same else dzt, dbias)
-        return losses
+def tte_lists(tte) -> tuple[list[int], list[float]]:
+    return [int(tte.kind), int(tte.K), int(tte.col)], [float(tte.mean_log), float(tte.std_log)]
 
-    @staticmethod
-    def backward(ctx, g):
-        dzc, dzt, dbias = ctx.saved_tensors
-        gt = g[-1].to(dzc.dtype)
-        d_zc = dzc * gt
-        d_zt = None if ctx.same else dzt * gt
-        d_bias = (dbias.sum(0) * g[-1]) if (ctx.has_bias and dbias is not None) else None
-        return d_zc, d_zt, d_bias, None, None, None, None, None
+
+def output_loss(zc, zt, zc_bias, batch: PytorchBatch, terms, tte, shift: int, n_levels: int):
+    """``esgpt::output_loss``: fused generative losses. Returns f32 [n_terms + 2] = per-term losses, -TTE_LL,
+    total. Only the total (last element) carries gradient; the per-term entries are for logging. ``zt=None`` means
+    the TTE parameters live in ``zc`` (CI: one fused head GEMM)."""
+    ti, tf = tte_lists(tte)
+    with _timed("output_loss"):
+        losses, _, _, _ = _ops().output_loss(zc, zt, zc_bias, *batch_args(batch), n_levels, shift,
+                                             terms_list(terms), ti, tf, err_word(zc.device))
+    return losses

@@ -1,0 +1,393 @@
+"""``torch.ops.esgpt``: the PyTorch-ROCm custom operators of this package.
+
+The operators are defined and implemented in C++ (``csrc/torch_ops.cpp`` → ``libesgpt_torch.so``:
+``TORCH_LIBRARY(esgpt, m)`` with HIP implementations that call the C ABI of ``libesgpt_amd.so``). This module loads
+that library and registers, per operator, a fake (meta) kernel — output shapes / dtypes without running anything,
+for fake tensors, ``torch.compile`` and export — and, for the differentiable ones, the autograd formula
+(``torch.library.register_autograd``) whose backward calls the matching ``*_bwd`` operator.
+
+Differentiable operators and the reference code they replace:
+
+====================  =====================================================================================
+``embed_joint``       DataEmbeddingLayer JOINT (+ static SUM_ALL, temporal encoding, NA level cumsum, mask):
+                      data_embedding_layer.py:351-388, 609-708; transformer.py:594-672, 903-936
+``embed_split_bags``  the two EmbeddingBag gathers of ``_split_embed`` (data_embedding_layer.py:390-450)
+``embed_epilogue``    temporal encoding / level cumsum / mask after the SPLIT projection
+``attention``         InnerSelfAttention._attn (transformer.py:171-217) on a packed q|k|v buffer
+``residual_ln``       residual + resid dropout + event mask + LayerNorm (transformer.py:350-461, 810-831)
+``bias_act``          c_fc bias + activation (transformer.py:378-391)
+``linear``            a bias-optional projection on the bf16 weight shadow, gradients to the f32 parameters
+``mlp``               InnerMLP up to c_proj's bias (transformer.py:378-391)
+``output_loss``       get_{classification,regression,TTE}_outputs + weighted_loss (model_output.py:1311-1721)
+``head_loss``         the generative heads' GEMM + ``output_loss`` (model_output.py:1253-1721)
+====================  =====================================================================================
+
+Non-differentiable: ``embed_bag_bwd``, ``embed_epilogue_bwd``, ``attention_bwd``, ``residual_ln_bwd``,
+``bias_act_bwd``, ``linear_act``, ``linear_bwd``, ``gemm`` / ``gemm_``, ``column_sum``, ``kv_append``,
+``attn_decode`` (generation) and ``adamw`` (generative_modeling.py:460-485).
+
+There is no CPU kernel: calling an operator on CPU tensors raises (no fallback).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _lib as L
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+TORCH_LIB_PATH = os.environ.get("ESGPT_AMD_TORCH_LIB", os.path.join(_HERE, "libesgpt_torch.so"))
+_state = {"loaded": False}
+
+OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
+       "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
+       "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
+       "adamw")
+
+
+def load():
+    """Loads ``libesgpt_torch.so`` (once) and registers the fake kernels and autograd formulas; returns
+    ``torch.ops.esgpt``. Raises ``HipExtensionMissing`` when the library has not been built."""
+    if not _state["loaded"]:
+        L.load(require_device=False)  # the kernel library first (libesgpt_torch.so links it by $ORIGIN)
+        if not os.path.exists(TORCH_LIB_PATH):
+            raise L.HipExtensionMissing(
+                f"eventstreamgpt_amd: custom-op library not found at {TORCH_LIB_PATH}. Build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C eventstreamgpt_amd/csrc`).")
+        torch.ops.load_library(TORCH_LIB_PATH)
+        _register()
+        _state["loaded"] = True
+    return torch.ops.esgpt
+
+
+def _tickets(device):
+    from .kernels import tickets
+
+    return tickets(device)
+
+
+def _batch_d(args, start):
+    """(B, L, M) from the 9 batch tensors starting at args[start]."""
+    di = args[start + 3]
+    return di.shape[0], di.shape[1], di.shape[2]
+
+
+def _register():
+    lib = "esgpt::"
+    fake = torch.library.register_fake
+    E = torch.empty
+
+    # ---------------------------------------------------------------- fake (meta) kernels
+    @fake(lib + "embed_joint")
+    def _(table, em, td, tm, di, dm, dv, dvm, si, sm, buckets, sin_div, cos_div, flags, static_w, dynamic_w, G, err):
+        return table.new_empty(di.shape[0], di.shape[1], G, table.shape[1], dtype=torch.float32)
+
+    @fake(lib + "embed_split_bags")
+    def _(ct, nt, em, td, tm, di, dm, dv, dvm, si, sm, buckets, flags, cs, ns, ss, G, err):
+        return ct.new_empty(di.shape[0] * di.shape[1] * G, ct.shape[1] + nt.shape[1], dtype=torch.float32)
+
+    @fake(lib + "embed_epilogue")
+    def _(y, em, td, tm, di, dm, dv, dvm, si, sm, G, flags, sin_div, cos_div):
+        return y.new_empty(di.shape[0], di.shape[1], G, y.shape[-1], dtype=torch.float32)
+
+    @fake(lib + "embed_epilogue_bwd")
+    def _(dout, em, td, tm, di, dm, dv, dvm, si, sm, G, flags):
+        return dout.new_empty(di.shape[0] * di.shape[1] * G, dout.shape[-1], dtype=torch.float32)
+
+    @fake(lib + "embed_bag_bwd")
+    def _(dsrc, em, td, tm, di, dm, dv, dvm, si, sm, buckets, selector, flags, dyn_scale, static_scale, ld, D, V, G):
+        return dsrc.new_empty(V, D, dtype=torch.float32)
+
+    @fake(lib + "attention")
+    def _(qkv, key_mask, query_mask, H, window, skf, p, seed):
+        Bs, T, D3 = qkv.shape
+        Lq = T - (1 if skf else 0)
+        return qkv.new_empty(Bs, Lq, D3 // 3), qkv.new_empty(Bs, H, Lq, dtype=torch.float32)
+
+    @fake(lib + "attention_bwd")
+    def _(qkv, o, dout, lse, key_mask, query_mask, H, window, skf, p, seed, tickets):
+        return torch.empty_like(qkv)
+
+    @fake(lib + "kv_append")
+    def _(qkv, k_cache, v_cache, past):
+        return None
+
+    @fake(lib + "attn_decode")
+    def _(qkv, k_cache, v_cache, key_mask, query_mask, H, Lk, window):
+        return qkv.new_empty(qkv.shape[0], qkv.shape[1], qkv.shape[2] // 3)
+
+    def _loss_fake(zc, zt, shift, n_terms, B):
+        f32 = torch.float32
+        dzt = zc.new_empty(0) if zt is None else torch.empty_like(zt)
+        dbias = zc.new_empty(B, zc.shape[-1], dtype=f32) if shift else zc.new_empty(0, dtype=f32)
+        return zc.new_empty(n_terms + 2, dtype=f32), torch.empty_like(zc), dzt, dbias
+
+    @fake(lib + "output_loss")
+    def _(zc, zt, zc_bias, em, td, tm, di, dm, dv, dvm, si, sm, n_levels, shift, terms, tte_i, tte_f, err):
+        return _loss_fake(zc, zt, shift, len(terms) // 8, di.shape[0])
+
+    @fake(lib + "head_loss")
+    def _(xc, xt, em, td, tm, di, dm, dv, dvm, si, sm, terms, tte_i, tte_f, shift, n_levels, wc, bc, wt, bt, cw, cb,
+          tw, tb, err, tickets):
+        zc = xc.new_empty(xc.shape[0], wc.shape[0])
+        zt = None if wt is None else xt.new_empty(xt.shape[0], wt.shape[0])
+        return _loss_fake(zc, zt, shift, len(terms) // 8, di.shape[0])
+
+    @fake(lib + "residual_ln")
+    def _(x, y, bias, ln_w, ln_b, row_mask, p, seed, eps, out_dtype):
+        ref = x if x is not None else y
+        N, D = ref.shape
+        f = ln_w.new_empty
+        return f(N, D, dtype=torch.float32), f(N, D, dtype=out_dtype), f(N, dtype=torch.float32), \
+            f(N, dtype=torch.float32)
+
+    @fake(lib + "residual_ln_bwd")
+    def _(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype, out_dtype, tickets):
+        N, D = h.shape
+        f = h.new_empty
+        return (f(N, D, dtype=torch.float32) if need_dx else f(0, dtype=torch.float32),
+                f(N, D, dtype=y_dtype) if need_dy else f(0, dtype=y_dtype), f(3, D, dtype=torch.float32))
+
+    @fake(lib + "bias_act")
+    def _(f, bias, act):
+        return torch.empty_like(f)
+
+    @fake(lib + "bias_act_bwd")
+    def _(dg, f, bias, act):
+        return torch.empty_like(f), f.new_empty(f.shape[1], dtype=torch.float32)
+
+    @fake(lib + "column_sum")
+    def _(x):
+        return x.new_empty(x.shape[1], dtype=torch.float32)
+
+    @fake(lib + "gemm")
+    def _(a_layout, a, lda, b_layout, b, ldb, M, N, K, bias, alpha, out_dtype, tickets):
+        return a.new_empty(M, N, dtype=out_dtype)
+
+    @fake(lib + "gemm_")
+    def _(c, a_layout, a, lda, b_layout, b, ldb, M, N, K, bias, alpha, accumulate, tickets):
+        return None
+
+    @fake(lib + "linear_act")
+    def _(x, w, bias, act):
+        y = x.new_empty(x.shape[0], w.shape[0])
+        return (x.new_empty(x.shape[0], w.shape[0]) if act >= 0 else x.new_empty(0)), y
+
+    @fake(lib + "linear_bwd")
+    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets):
+        f32 = torch.float32
+        return (x.new_empty(dy.shape[0], x.shape[1], dtype=dy.dtype) if need_dx else x.new_empty(0, dtype=dy.dtype),
+                x.new_empty(dy.shape[1], x.shape[1], dtype=f32),
+                x.new_empty(dy.shape[1], dtype=f32) if need_db else x.new_empty(0, dtype=f32))
+
+    @fake(lib + "linear")
+    def _(x, w, bias, masters, tickets):
+        return x.new_empty(x.shape[0], w.shape[0])
+
+    @fake(lib + "mlp")
+    def _(x, w_fc, w_pj, b_fc, act, p_fc, p_pj, tickets):
+        T = x.shape[0]
+        return x.new_empty(T, w_pj.shape[0]), x.new_empty(T, w_fc.shape[0]), x.new_empty(T, w_fc.shape[0])
+
+    @fake(lib + "adamw")
+    def _(table, blocks, lr, beta1, beta2, eps, wd, step, per_tensor, err):
+        return None
+
+    # ---------------------------------------------------------------- autograd formulas
+    reg = torch.library.register_autograd
+    ops = torch.ops.esgpt
+
+    # embed_joint: d table (the EmbeddingBag backward, atomic-free CSR form; NA cumsum undone first)
+    def _ej_setup(ctx, inputs, output):
+        table, *batch = inputs[:10]
+        buckets, sin_div, cos_div, flags, static_w, dynamic_w, G, err = inputs[10:]
+        ctx.save_for_backward(*batch)
+        ctx.meta = (tuple(buckets), flags, static_w, dynamic_w, G, table.shape[0], table.shape[1])
+
+    def _ej_bwd(ctx, dout):
+        batch = ctx.saved_tensors
+        buckets, flags, static_w, dynamic_w, G, V, D = ctx.meta
+        dout = dout.contiguous().float()
+        if flags & L.EMB_CUMSUM:
+            dsrc = ops.embed_epilogue_bwd(dout, *batch, G, flags)
+        else:
+            dsrc = dout.view(-1, D)
+        S = 0 if batch[7] is None else batch[7].shape[1]
+        static = bool(flags & L.EMB_STATIC) and S > 0
+        dtable = ops.embed_bag_bwd(dsrc, *batch, list(buckets), L.BAG_JOINT, flags,
+                                   dynamic_w if static else 1.0, static_w, D, D, V, G)
+        return (dtable,) + (None,) * 17
+
+    reg(lib + "embed_joint", _ej_bwd, setup_context=_ej_setup)
+
+    # embed_split_bags: d cat_table, d num_table (the two bag backwards over column blocks of dx)
+    def _es_setup(ctx, inputs, output):
+        ct, nt, *rest = inputs
+        batch = rest[:9]
+        buckets, flags, cat_scale, num_scale, static_scale, G, err = rest[9:]
+        ctx.save_for_backward(*batch)
+        ctx.meta = (tuple(buckets), flags, cat_scale, num_scale, static_scale, G, ct.shape[0], ct.shape[1],
+                    nt.shape[1])
+
+    def _es_bwd(ctx, dx):
+        batch = ctx.saved_tensors
+        buckets, flags, cat_scale, num_scale, static_scale, G, V, Dc, Dn = ctx.meta
+        dx = dx.contiguous().float()
+        if static_scale == 0.0:
+            flags &= ~L.EMB_STATIC
+        dcat = ops.embed_bag_bwd(dx, *batch, list(buckets), L.BAG_CAT, flags, cat_scale, static_scale, Dc + Dn, Dc,
+                                 V, G)
+        dnum = ops.embed_bag_bwd(dx[:, Dc:], *batch, list(buckets), L.BAG_NUM, flags, num_scale, 0.0, Dc + Dn, Dn,
+                                 V, G)
+        return (dcat, dnum) + (None,) * 16
+
+    reg(lib + "embed_split_bags", _es_bwd, setup_context=_es_setup)
+
+    # embed_epilogue: d y
+    def _ee_setup(ctx, inputs, output):
+        y, *rest = inputs
+        ctx.save_for_backward(*rest[:9])
+        ctx.meta = (rest[9], rest[10], tuple(y.shape))
+
+    def _ee_bwd(ctx, dout):
+        G, flags, yshape = ctx.meta
+        dy = ops.embed_epilogue_bwd(dout.contiguous().float(), *ctx.saved_tensors, G, flags)
+        return (dy.view(yshape),) + (None,) * 13
+
+    reg(lib + "embed_epilogue", _ee_bwd, setup_context=_ee_setup)
+
+    # attention: d qkv (one fused MFMA backward; the dropout keep-mask is regenerated from the same seed)
+    def _at_setup(ctx, inputs, output):
+        qkv, km, qm, H, window, skf, p, seed = inputs
+        o, lse = output
+        ctx.mark_non_differentiable(lse)
+        ctx.save_for_backward(qkv, o, lse, km, qm, seed)
+        ctx.meta = (H, window, skf, p)
+
+    def _at_bwd(ctx, do, _dlse):
+        qkv, o, lse, km, qm, seed = ctx.saved_tensors
+        H, window, skf, p = ctx.meta
+        dqkv = ops.attention_bwd(qkv, o, do, lse, km, qm, H, window, skf, p, seed, _tickets(qkv.device))
+        return dqkv, None, None, None, None, None, None, None
+
+    reg(lib + "attention", _at_bwd, setup_context=_at_setup)
+
+    # residual_ln: d x, d y, d bias, d ln_w, d ln_b (column sums in the same launch)
+    def _rl_setup(ctx, inputs, output):
+        x, y, bias, ln_w, ln_b, row_mask, p, seed, eps, out_dtype = inputs
+        h, out, mean, rstd = output
+        ctx.mark_non_differentiable(mean, rstd)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(h, mean, rstd, ln_w, row_mask, seed)
+        ctx.meta = (x is not None, y is not None, bias is not None, y.dtype if y is not None else torch.float32,
+                    out_dtype, p)
+
+    def _rl_bwd(ctx, dh, dout, _dm, _dr):
+        h, mean, rstd, ln_w, row_mask, seed = ctx.saved_tensors
+        has_x, has_y, has_bias, y_dtype, out_dtype, p = ctx.meta
+        if dout is None:
+            dout = torch.zeros(h.shape, dtype=out_dtype, device=h.device)
+        dx, dy, sums = ops.residual_ln_bwd(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x, has_y, y_dtype,
+                                           out_dtype, _tickets(h.device))
+        return (dx if has_x else None, dy if has_y else None, sums[2] if has_bias else None, sums[0], sums[1],
+                None, None, None, None, None)
+
+    reg(lib + "residual_ln", _rl_bwd, setup_context=_rl_setup)
+
+    # bias_act: d f, d bias
+    def _ba_setup(ctx, inputs, output):
+        f, bias, act = inputs
+        ctx.save_for_backward(f, bias)
+        ctx.act = act
+
+    def _ba_bwd(ctx, dg):
+        f, bias = ctx.saved_tensors
+        dz, dbias = ops.bias_act_bwd(dg, f, bias, ctx.act)
+        return dz, dbias, None
+
+    reg(lib + "bias_act", _ba_bwd, setup_context=_ba_setup)
+
+    # linear: d x, d bias, and the f32 weight gradient split over the master parameters (one grouped launch)
+    def _li_setup(ctx, inputs, output):
+        x, w, bias, masters, tickets = inputs
+        ctx.save_for_backward(x, w)
+        ctx.rows = [m.shape[0] for m in masters]
+        ctx.has_bias = bias is not None
+
+    def _li_bwd(ctx, dy):
+        x, w = ctx.saved_tensors
+        need_db = ctx.has_bias and ctx.needs_input_grad[2]
+        dx, dw, db = ops.linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db, _tickets(x.device))
+        return (dx if ctx.needs_input_grad[0] else None, None, db if need_db else None,
+                list(torch.split(dw, ctx.rows, 0)), None)
+
+    reg(lib + "linear", _li_bwd, setup_context=_li_setup)
+
+    # mlp: d x, d b_fc, d W_fc, d W_proj (activation gradient in c_proj's dX epilogue)
+    def _ml_setup(ctx, inputs, output):
+        x, w_fc, w_pj, b_fc, act, p_fc, p_pj, tickets = inputs
+        y, pre, g = output
+        ctx.mark_non_differentiable(pre, g)
+        ctx.save_for_backward(x, w_fc, w_pj, pre, g)
+        ctx.act = act
+
+    def _ml_bwd(ctx, dy, _dpre, _dg):
+        x, w_fc, w_pj, pre, g = ctx.saved_tensors
+        t = _tickets(x.device)
+        dz, dw_pj, _ = ops.linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, False, t)
+        need_dx = ctx.needs_input_grad[0]
+        dx, dw_fc, db_fc = ops.linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True, t)
+        return (dx if need_dx else None, None, None, db_fc, None, dw_fc, dw_pj, None)
+
+    reg(lib + "mlp", _ml_bwd, setup_context=_ml_setup)
+
+    # output_loss: d zc, d zt, d zc_bias (per-term entries of the losses output are for logging only)
+    def _ol_setup(ctx, inputs, output):
+        zc, zt, zc_bias = inputs[:3]
+        losses, dzc, dzt, dbias = output
+        ctx.mark_non_differentiable(dzc, dzt, dbias)
+        ctx.save_for_backward(dzc, dzt, dbias)
+        ctx.meta = (zt is not None, zc_bias is not None)
+
+    def _ol_bwd(ctx, g, *_):
+        dzc, dzt, dbias = ctx.saved_tensors
+        has_zt, has_bias = ctx.meta
+        gt = g[-1]
+        d_bias = (dbias.sum(0) * gt).to(dzc.dtype) if (has_bias and dbias.numel()) else None
+        return ((dzc * gt.to(dzc.dtype)), (dzt * gt.to(dzt.dtype)) if has_zt else None, d_bias) + (None,) * 15
+
+    reg(lib + "output_loss", _ol_bwd, setup_context=_ol_setup)
+
+    # head_loss: head GEMM backward scaled by d(total) read from device memory (the GEMM's alpha pointer)
+    def _hl_setup(ctx, inputs, output):
+        xc, xt = inputs[0], inputs[1]
+        wc, bc, wt, bt, cw, cb, tw, tb = inputs[16:24]
+        losses, dzc, dzt, dbias = output
+        ctx.mark_non_differentiable(dzc, dzt, dbias)
+        ctx.save_for_backward(xc, xt, wc, wt, dzc, dzt, dbias)
+        ctx.rows = ([w.shape[0] for w in cw], [w.shape[0] for w in tw])
+        ctx.n = (len(cw), len(tw))
+
+    def _hl_bwd(ctx, g, *_):
+        xc, xt, wc, wt, dzc, dzt, dbias = ctx.saved_tensors
+        n_cw, n_tw = ctx.n
+        rows_c, rows_t = ctx.rows
+        alpha = g.contiguous()[-1:]
+        t = _tickets(xc.device)
+        dxc, dwc, dbc = ops.linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, t)
+        if dbias.numel():
+            dbc = dbc + dbias.sum(0) * alpha
+        nc = sum(rows_c)
+        gw_c = list(torch.split(dwc[:nc], rows_c, 0))
+        gb_c = list(torch.split(dbc[:nc], rows_c, 0))
+        dxt, gw_t, gb_t = None, [], []
+        if n_tw:
+            dxt, dwt, dbt = ops.linear_bwd(dzt, xt, wt, alpha, -1, None, True, True, t)
+            nt = sum(rows_t)
+            gw_t = list(torch.split(dwt[:nt], rows_t, 0))
+            gb_t = list(torch.split(dbt[:nt], rows_t, 0))
+        return (dxc, dxt) + (None,) * 14 + (None, None, None, None, gw_c, gb_c, gw_t, gb_t,
+                                             None, None)
+
+    reg(lib + "head_loss", _hl_bwd, setup_context=_hl_setup)

@@ -50,8 +50,8 @@ def poly_decay_lambda(warmup: int, total: int, power: float, init_lr: float, end
 
 class FusedAdamW:
     """``torch.optim.AdamW`` (default betas / eps, decoupled weight decay; ``generative_modeling.py:460-466``) as ONE
-    gfx950 kernel launch per step over every parameter (csrc/misc.hip ``esgpt_adamw``), instead of torch's
-    multi-tensor launches. Parameters whose ``.grad`` is None are skipped and keep their step count, like torch;
+    gfx950 kernel launch per step over every parameter (``torch.ops.esgpt.adamw`` → csrc/misc.hip ``esgpt_adamw``),
+    instead of torch's multi-tensor launches. Parameters whose ``.grad`` is None are skipped and keep their step count, like torch;
     when the active parameters' step counts differ, their bias corrections go to the kernel as a per-tensor table.
     The tensor table (device pointers of p / grad / exp_avg / exp_avg_sq) is rebuilt only when a gradient's storage
     changes (never under HIP-graph replay, where gradients live in the graph's pool). The launch is a no-op while
@@ -59,9 +59,11 @@ class FusedAdamW:
 
     def __init__(self, params, lr: float, weight_decay: float = 0.01, betas=(0.9, 0.999), eps: float = 1e-8):
         from . import _lib as L
+        from . import ops
 
         self.L = L
         self.lib = L.load()
+        self.ops = ops.load()
         self.params = list(params)
         self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, betas, eps
         self.exp_avg = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
@@ -117,11 +119,10 @@ class FusedAdamW:
                 vals += [lr / (1.0 - b1**s), (1.0 - b2**s) ** 0.5]
             self._per_host = torch.tensor(vals, dtype=torch.float32).pin_memory()  # kept alive until the next step
             self._per_dev[: len(vals)].copy_(self._per_host, non_blocking=True)
-            per = self._per_dev.data_ptr()
+            per = self._per_dev
         dev = self.params[0].device
-        self.L.check(self.lib.esgpt_adamw(self._table.data_ptr(), self._blocks.data_ptr(), self._blocks.numel(), lr,
-                                          b1, b2, self.eps, self.weight_decay, steps[0], per,
-                                          err_word(dev).data_ptr(), self.L.stream()), "adamw")
+        self.ops.adamw(self._table, self._blocks, lr, b1, b2, self.eps, self.weight_decay, steps[0], per,
+                       err_word(dev))
 
     def state_dict(self):
         return {"state": {i: {"step": self.steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}

@@ -4,7 +4,7 @@
 ``IsObservedLayer``, ``ClassificationLayer``, ``regression_layers``; ``:1253-1309``). Training losses follow
 ``get_TTE_outputs`` / ``get_classification_outputs`` / ``get_regression_outputs`` (``:1311-1721``) but are
 computed by ONE head GEMM (all heads' weights concatenated along the output dimension) plus the fused loss kernel
-(``kernels.OutputLossFn``), which also produces d(loss)/d(logits).
+(``kernels.output_loss``: ``torch.ops.esgpt.output_loss``), which also produces d(loss)/d(logits).
 
 Head column layout of the fused GEMM: [ClassificationLayer (V) | IsObservedLayer (n_meas) |
 regression_layers[m].proj (in measurements_per_generative_mode order) || TTE_layer.proj].
@@ -20,7 +20,7 @@ from .. import _lib as L
 from ..data.data_embedding_enums import MeasIndexGroupOptions
 from ..data.types import DataModality, PytorchBatch, TemporalityType
 from ..fused import head_losses, linear_bias
-from ..kernels import OutputLossFn, batch_view
+from ..kernels import output_loss
 from .config import TimeToEventGenerationHeadType
 from .generative_layers import (
     ExponentialTTELayer,
@@ -644,14 +644,13 @@ def fused_ci_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
                                     all_regression_measurements(layer.config), 0)
     mods = layer._content_modules() + [layer.TTE_layer.proj]
     B, Lq, D = encoded.shape
-    bv = batch_view(batch)
     tte = layer._tte_spec(layer._layout["n_content"])
-    fused = head_losses(encoded.reshape(B * Lq, D), None, bv, terms, tte, 1, 1, mods, [])
+    fused = head_losses(encoded.reshape(B * Lq, D), None, batch, terms, tte, 1, 1, mods, [])
     if fused is not None:
         return fused, names
     z = linear_bias(encoded.reshape(B * Lq, D), [m.weight for m in mods], [m.bias for m in mods])
     b = torch.cat([m.bias for m in mods], 0)
-    losses = OutputLossFn.apply(z, None, b, bv, terms, tte, 1, 1)
+    losses = output_loss(z, None, b, batch, terms, tte, 1, 1)
     return losses, names
 
 
@@ -678,10 +677,9 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
             terms.append(tt)
             names.append(nn_)
     mods = layer._content_modules()
-    bv = batch_view(batch)
     if terms:
         fused = head_losses(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D),
-                            encoded[:, :, G - 1, :].reshape(B * Lq, D), bv, terms, layer._tte_spec(0), 0,
+                            encoded[:, :, G - 1, :].reshape(B * Lq, D), batch, terms, layer._tte_spec(0), 0,
                             max(1, G - 1), mods, [layer.TTE_layer.proj])
         if fused is not None:
             return fused, names
@@ -692,5 +690,5 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
         zc = torch.zeros(1, 1, device=encoded.device, dtype=encoded.dtype)
     zt = linear_bias(encoded[:, :, G - 1, :].reshape(B * Lq, D), [layer.TTE_layer.proj.weight],
                      [layer.TTE_layer.proj.bias])
-    losses = OutputLossFn.apply(zc, zt, None, bv, terms, layer._tte_spec(0), 0, max(1, G - 1))
+    losses = output_loss(zc, zt, None, batch, terms, layer._tte_spec(0), 0, max(1, G - 1))
     return losses, names

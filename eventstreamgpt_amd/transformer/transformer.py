@@ -21,7 +21,7 @@ from transformers.modeling_utils import PreTrainedModel
 
 from ..data.data_embedding_layer import DataEmbeddingLayer, MeasIndexGroupOptions
 from ..data.types import PytorchBatch
-from ..kernels import AttentionFn, cached_attention
+from ..kernels import attention, cached_attention
 from .config import StructuredEventProcessingMode, StructuredTransformerConfig
 from .model_output import TransformerOutputWithPast
 from .structured_attention import StructuredAttention
@@ -115,7 +115,7 @@ class InnerSelfAttention(nn.Module):
         # Query padding = key padding for self-attention over events (rows are zeroed downstream).
         qpm = None if (kpm is None or static_kv_first) else kpm
         p = self.attn_dropout_p if self.training else 0.0
-        o = AttentionFn.apply(qkv, kpm, qpm, self.num_heads, window, static_kv_first, p)
+        o = attention(qkv, kpm, qpm, self.num_heads, window, static_kv_first, p)
         out = self.resid_dropout(self.out_proj(o))
         return out, {"present_key_value": None}
 

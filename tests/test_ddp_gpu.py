@@ -41,25 +41,36 @@ def _batches(bc, rank):
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    import traceback
+
     try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
         from eventstreamgpt_amd.train import TrainStep
 
         bc, m, opt = _setup()
         ts = TrainStep(m, opt, torch.bfloat16, use_graph=True, bucket_mb=0.05)  # several buckets
         assert ts.use_graph and ts.distributed and len(ts.grad_buckets.buckets) > 1
-        losses = [float(ts.step(b)) for b in _batches(bc, rank)]
+        losses = []
+        for i, b in enumerate(_batches(bc, rank)):
+            losses.append(float(ts.step(b)))
+            q.put(("progress", rank, f"step {i} loss {losses[-1]:.6f}"))
         ts.check()
         base = ts.grad_buckets.flat.data_ptr()
         in_flat = all(base <= p.grad.data_ptr() < base + 4 * ts.grad_buckets.flat.numel() for p in ts.params)
-        q.put((rank, losses, in_flat, {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()}))
-    finally:
+        q.put(("done", rank, (losses, in_flat, {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()})))
         dist.destroy_process_group()
+    except BaseException:
+        q.put(("error", rank, traceback.format_exc()))
+        raise
 
 
 def test_two_ranks_on_one_gpu_match_averaged_gradients():
+    import queue
+    import time
+
     from eventstreamgpt_amd.train import FusedAdamW, poly_decay_lambda
 
     world = 2
@@ -70,11 +81,27 @@ def test_two_ranks_on_one_gpu_match_averaged_gradients():
     for p in procs:
         p.start()
     res = {}
-    for _ in range(world):
-        r, losses, in_flat, sd = q.get(timeout=240)
-        res[r] = (losses, in_flat, sd)
+    deadline = time.time() + 150
+    try:
+        while len(res) < world:
+            try:
+                kind, r, payload = q.get(timeout=5)
+            except queue.Empty:
+                assert time.time() < deadline, "ranks did not finish in 150 s"
+                assert all(p.is_alive() or p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+                continue
+            if kind == "error":
+                raise AssertionError(f"rank {r} failed:\n{payload}")
+            if kind == "progress":
+                print(f"rank {r}: {payload}", flush=True)
+                continue
+            res[r] = payload
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
     for p in procs:
-        p.join(timeout=60)
         assert p.exitcode == 0
 
     # single process: per-rank losses / gradients on each rank's batch, averaged, then the same AdamW steps

@@ -1,0 +1,160 @@
+"""The custom operators (torch.ops.esgpt) against the raw C ABI (ctypes, exactly the reference-side binding of
+INTEGRATION.md) on the same inputs: identical results (bit-exact; the embedding-bag backward's atomic adds of rows
+straddling a chunk make its sums order-dependent at the last bit)."""
+import ctypes
+
+import pytest
+import torch
+
+from eventstreamgpt_amd import _lib as L
+from eventstreamgpt_amd.kernels import BatchView, batch_args, err_word, tickets
+from eventstreamgpt_amd.synthetic import CONFIGS
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def env():
+    from eventstreamgpt_amd import ops
+
+    return ops.load(), L.load()
+
+
+def _g(seed):
+    return torch.Generator(device=DEV).manual_seed(seed)
+
+
+def test_attention_fwd_bwd_equal_c_abi(env):
+    esgpt, lib = env
+    B, T, H, hd = 3, 200, 4, 64
+    D = H * hd
+    qkv = (0.5 * torch.randn(B, T, 3 * D, device=DEV, generator=_g(0))).bfloat16()
+    km = torch.rand(B, T, device=DEV, generator=_g(1)) > 0.1
+    o, lse = esgpt.attention(qkv, km, km, H, 0, False, 0.0, None)
+    o2 = torch.empty_like(o)
+    lse2 = torch.empty_like(lse)
+    base, es = qkv.data_ptr(), 2
+    L.check(lib.esgpt_attn_fwd(base, base + D * es, base + 2 * D * es, 3 * D, T, o2.data_ptr(), D, lse2.data_ptr(),
+                               km.data_ptr(), km.data_ptr(), B, H, T, T, hd, 0, 0.0, None, L.BF16, L.stream()), "fwd")
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    do = torch.randn(B, T, D, device=DEV, generator=_g(2)).bfloat16()
+    t = tickets(torch.device(DEV))
+    dqkv = esgpt.attention_bwd(qkv, o, do, lse, km, km, H, 0, False, 0.0, None, t)
+    d2 = torch.empty_like(qkv)
+    nb = lib.esgpt_attn_bwd_workspace(B, H, T, T, hd)
+    ws = torch.empty(max(1, nb), dtype=torch.uint8, device=DEV)
+    db = d2.data_ptr()
+    cnt = t.data_ptr() if lib.esgpt_attn_bwd_counters(B, H, T) <= t.numel() else None
+    L.check(lib.esgpt_attn_bwd(base, base + D * es, base + 2 * D * es, 3 * D, T, o.data_ptr(), D, do.data_ptr(), D,
+                               lse.data_ptr(), km.data_ptr(), km.data_ptr(), db, db + D * es, db + 2 * D * es, 3 * D,
+                               B, H, T, T, hd, 0, 0.0, None, L.BF16, ws.data_ptr(), nb, cnt, L.stream()), "bwd")
+    assert torch.equal(dqkv, d2)
+
+
+def test_embed_joint_and_bag_bwd_equal_c_abi(env):
+    esgpt, lib = env
+    bc = CONFIGS["C2"]
+    b = bc.batch(0, batch_size=8, device=DEV)
+    V, Dm = 1210, 256
+    table = torch.randn(V, Dm, device=DEV, generator=_g(3))
+    err = err_word(torch.device(DEV))
+    out = esgpt.embed_joint(table, *batch_args(b), [], None, None, L.EMB_STATIC, 0.5, 0.5, 1, err)
+    bv = BatchView(b)
+    out2 = torch.empty_like(out)
+    L.check(lib.esgpt_embed_joint_fwd(bv.ref, None, table.data_ptr(), V, Dm, None, None, L.EMB_STATIC, 0.5, 0.5,
+                                      out2.data_ptr(), err.data_ptr(), L.stream()), "embed")
+    assert torch.equal(out, out2)
+    dsrc = torch.randn(8 * bc.seq_len, Dm, device=DEV, generator=_g(4))
+    dt = esgpt.embed_bag_bwd(dsrc, *batch_args(b), [], L.BAG_JOINT, L.EMB_STATIC, 0.5, 0.5, Dm, Dm, V, 1)
+    dt2 = torch.empty_like(dt)
+    nb = lib.esgpt_embed_bag_bwd_workspace(bv.ref, 1, V, Dm)
+    ws = torch.empty(max(1, nb), dtype=torch.uint8, device=DEV)
+    L.check(lib.esgpt_embed_bag_bwd(bv.ref, None, L.BAG_JOINT, L.EMB_STATIC, 0.5, 0.5, dsrc.data_ptr(), Dm, Dm, V,
+                                    dt2.data_ptr(), ws.data_ptr(), nb, L.stream()), "bag_bwd")
+    torch.testing.assert_close(dt, dt2, rtol=1e-6, atol=1e-6)
+
+
+def test_output_loss_equal_c_abi(env):
+    esgpt, lib = env
+    from eventstreamgpt_amd.kernels import terms_list, tte_lists
+    from eventstreamgpt_amd.transformer import model_output as MO
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C2"]
+    m = CIPPTForGenerativeSequenceModeling(bc.model_config())
+    layer = m.output_layer
+    layer._layout = layer._build_layout()
+    terms, _ = layer._terms_for(MO.all_classification_measurements(layer), MO.all_regression_measurements(m.config), 0)
+    tte = layer._tte_spec(layer._layout["n_content"])
+    b = bc.batch(1, batch_size=8, device=DEV)
+    C = 1624
+    zc = torch.randn(8 * bc.seq_len, C, device=DEV, generator=_g(5)).bfloat16()
+    bias = torch.randn(C, device=DEV, generator=_g(6)).bfloat16()
+    err = err_word(torch.device(DEV))
+    ti, tf = tte_lists(tte)
+    losses, dzc, _, dbias = esgpt.output_loss(zc, None, bias, *batch_args(b), 1, 1, terms_list(terms), ti, tf, err)
+    bv = BatchView(b)
+    arr = (L.EsgptLossTerm * len(terms))(*terms)
+    l2, d2, db2 = torch.empty_like(losses), torch.empty_like(dzc), torch.empty_like(dbias)
+    nb = lib.esgpt_output_loss_workspace(8, bc.seq_len, len(terms))
+    ws = torch.empty(max(1, nb), dtype=torch.uint8, device=DEV)
+    L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), C, 1, 1, bias.data_ptr(), zc.data_ptr(), C, L.BF16, arr,
+                                  len(terms), ctypes.byref(tte), d2.data_ptr(), d2.data_ptr(), db2.data_ptr(),
+                                  l2.data_ptr(), ws.data_ptr(), nb, err.data_ptr(), L.stream()), "loss")
+    assert torch.equal(losses, l2) and torch.equal(dzc, d2) and torch.equal(dbias, db2)
+
+
+def test_linear_and_residual_ln_equal_c_abi(env):
+    esgpt, lib = env
+    T, din, dout = 1024, 256, 1024
+    x = torch.randn(T, din, device=DEV, generator=_g(7)).bfloat16()
+    w = (0.05 * torch.randn(dout, din, device=DEV, generator=_g(8))).bfloat16()
+    b = torch.randn(dout, device=DEV, generator=_g(9))
+    pre, y = esgpt.linear_act(x, w, b, 0)
+    pre2, y2 = torch.empty_like(pre), torch.empty_like(y)
+    L.check(lib.esgpt_linear_fwd(x.data_ptr(), din, w.data_ptr(), T, din, dout, b.data_ptr(), 0, pre2.data_ptr(),
+                                 y2.data_ptr(), dout, L.stream()), "linear_fwd")
+    assert torch.equal(pre, pre2) and torch.equal(y, y2)
+    dy = torch.randn(T, dout, device=DEV, generator=_g(10)).bfloat16()
+    t = tickets(torch.device(DEV))
+    dx, dw, db = esgpt.linear_bwd(dy, x, w, None, -1, None, True, True, t)
+    dx2, dw2, db2 = torch.empty_like(dx), torch.empty_like(dw), torch.empty_like(db)
+    nb = lib.esgpt_linear_bwd_workspace(T, din, dout, 1)
+    ws = torch.empty(max(1, nb), dtype=torch.uint8, device=DEV)
+    L.check(lib.esgpt_linear_bwd(dy.data_ptr(), dout, x.data_ptr(), din, w.data_ptr(), T, din, dout, None, -1, None,
+                                 0, dx2.data_ptr(), din, dw2.data_ptr(), db2.data_ptr(), ws.data_ptr(), nb,
+                                 t.data_ptr(), L.stream()), "linear_bwd")
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2) and torch.equal(db, db2)
+    N, D = 600, 256
+    h0 = torch.randn(N, D, device=DEV, generator=_g(11))
+    yy = torch.randn(N, D, device=DEV, generator=_g(12)).bfloat16()
+    lw, lb, bb = (torch.randn(D, device=DEV, generator=_g(13 + i)) for i in range(3))
+    h, out, mean, rstd = esgpt.residual_ln(h0, yy, bb, lw, lb, None, 0.0, None, 1e-5, torch.bfloat16)
+    h2, out2, m2, r2 = torch.empty_like(h), torch.empty_like(out), torch.empty_like(mean), torch.empty_like(rstd)
+    L.check(lib.esgpt_residual_ln_fwd(h0.data_ptr(), yy.data_ptr(), L.BF16, bb.data_ptr(), None, 0.0, None,
+                                      lw.data_ptr(), lb.data_ptr(), 1e-5, N, D, h2.data_ptr(), out2.data_ptr(), L.BF16,
+                                      m2.data_ptr(), r2.data_ptr(), L.stream()), "ln_fwd")
+    assert torch.equal(h, h2) and torch.equal(out, out2) and torch.equal(mean, m2) and torch.equal(rstd, r2)
+
+
+def test_adamw_op_equals_c_abi(env):
+    esgpt, lib = env
+    from eventstreamgpt_amd.train import FusedAdamW
+
+    g = torch.Generator().manual_seed(0)
+    base = [torch.randn(s, generator=g) for s in [(300, 64), (7,), (4099,)]]
+    grads = [torch.randn(b.shape, generator=g).to(DEV) for b in base]
+    pa = [b.clone().to(DEV).requires_grad_(True) for b in base]
+    pb = [b.clone().to(DEV).requires_grad_(True) for b in base]
+    oa, ob = FusedAdamW(pa, lr=1e-2), FusedAdamW(pb, lr=1e-2)
+    for p, gr in zip(pa, grads):
+        p.grad = gr.clone()
+    for p, gr in zip(pb, grads):
+        p.grad = gr.clone()
+    oa.step()  # torch.ops.esgpt.adamw
+    ob._plan()
+    L.check(lib.esgpt_adamw(ob._table.data_ptr(), ob._blocks.data_ptr(), ob._blocks.numel(), 1e-2, 0.9, 0.999, 1e-8,
+                            0.01, 1, None, None, L.stream()), "adamw")
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
