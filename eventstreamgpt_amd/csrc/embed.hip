@@ -1,5 +1,5 @@
 // Input layer kernels for gfx950: the ragged measurement embedding-bag (JOINT / SPLIT, bucketed for NA),
-// static merge, temporal position encoding and the atomic-free CSR backward.
+// static merge, temporal position encoding and the deterministic, atomic-free sorted-CSR backward.
 //
 // Reference semantics: EventStream/data/data_embedding_layer.py (DataEmbeddingLayer, :200-708) and
 // EventStream/transformer/transformer.py (time_from_deltas :539-561, TemporalPositionEncoding :564-619,
@@ -483,49 +483,103 @@ __device__ __forceinline__ bool bag_slot(const BagBwdArgs& a, int64_t slot, int6
   return true;
 }
 
-// Slot ranges: block i owns the contiguous slots [i*per, (i+1)*per) in both the count and the fill pass.
-constexpr int kBagBlocks = 256;
-constexpr int kLdsBins = 16384;  // vocabularies up to this size are histogrammed in LDS (2 x 64 KiB)
+// ------------------------------------------------------------------------------------------------------------
+// Deterministic, atomic-free bag backward: a stable counting sort of the slots by vocabulary row, then a segmented
+// reduction in slot order (every sum runs in a fixed order: table gradients are bitwise repeatable).
+//   K0 bag_subject_sum  (static SUM_ALL) subject sums of dsrc over valid events and levels, in event order
+//   K1 bag_block_sort   per block of kSortCh slots: (row << 32 | slot) keys bitonic-sorted in LDS (a total order, so
+//                       slot order within a row), the block's per-row counts (counts[blk][V]) and every valid
+//                       slot's (row, rank within the block's run) in block-sorted order
+//   K2 bag_col_prefix   per row: exclusive prefix of counts over blocks (in place) and the row total
+//      bag_row_scan     exclusive scan of the row totals -> rowptr[0..V]
+//   K3 bag_scatter      (row, block, rank) -> CSR position rowptr[row] + prefix[blk][row] + rank: (row, src, w)
+//   K4 bag_reduce       one wave per kChunk CSR entries: rows complete in the chunk are stored; a row continuing
+//                       into the previous / next chunk is stored as that chunk's head / tail partial
+//   K5 bag_combine      rows spanning chunks: tail(c0) + head(c0+1) + ... + head(c1), in chunk order; empty rows 0
+// ------------------------------------------------------------------------------------------------------------
+constexpr int kSortCh = 4096;       // slots per sort block (LDS: 32 KiB of 64-bit keys)
+constexpr int kSortThreads = 1024;
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 
-// Per-block LDS histogram, then one global add per non-empty bin (hot rows such as event types would otherwise
-// serialise thousands of same-address atomics).
-template <bool LDS>
-__global__ __launch_bounds__(256) void bag_count_kernel(BagBwdArgs a, int64_t n_slots, int64_t per,
-                                                        int32_t* __restrict__ count) {
-  extern __shared__ int32_t s_hist[];
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n_slots, lo + per);
-  if (LDS) {
-    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x) s_hist[i] = 0;
-    __syncthreads();
+__device__ __forceinline__ int key_lower_bound(const uint64_t* k, int n, uint32_t row) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((uint32_t)(k[mid] >> 32) < row) lo = mid + 1; else hi = mid;
   }
-  for (int64_t slot = lo + threadIdx.x; slot < hi; slot += blockDim.x) {
-    int64_t v, src;
-    float w;
-    if (bag_slot(a, slot, v, w, src)) {
-      if (LDS) atomicAdd(s_hist + v, 1);
-      else atomicAdd(count + v, 1);
-    }
-  }
-  if (LDS) {
-    __syncthreads();
-    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x)
-      if (s_hist[i]) atomicAdd(count + i, s_hist[i]);
-  }
+  return lo;
 }
 
-// Exclusive scan of count[0..V) into rowptr[0..V]; single workgroup of 1024 threads. Also zeroes cursor.
-__global__ __launch_bounds__(1024) void bag_scan_kernel(const int32_t* __restrict__ count, int64_t V,
-                                                        int32_t* __restrict__ rowptr, int32_t* __restrict__ cursor) {
+__global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs a, int64_t n_slots,
+                                                                      int32_t* __restrict__ counts,
+                                                                      int2* __restrict__ sorted,
+                                                                      int32_t* __restrict__ n_valid) {
+  __shared__ uint64_t s_key[kSortCh];
+  __shared__ int s_nv;
+  const int64_t base = (int64_t)blockIdx.x * kSortCh;
+  for (int i = threadIdx.x; i < kSortCh; i += kSortThreads) {
+    int64_t v = 0, src = 0;
+    float w = 0.f;
+    uint32_t row = kNoRow;
+    if (base + i < n_slots && bag_slot(a, base + i, v, w, src)) row = (uint32_t)v;
+    s_key[i] = ((uint64_t)row << 32) | (uint32_t)i;
+  }
+  __syncthreads();
+  for (int k = 2; k <= kSortCh; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < kSortCh / 2; t += kSortThreads) {
+        const int lo = 2 * t - (t & (j - 1)), hi = lo + j;
+        const uint64_t x = s_key[lo], y = s_key[hi];
+        if ((x > y) == ((lo & k) == 0)) {
+          s_key[lo] = y;
+          s_key[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (threadIdx.x == 0) s_nv = key_lower_bound(s_key, kSortCh, kNoRow);
+  __syncthreads();
+  const int nv = s_nv;
+  int2* out = sorted + base;
+  for (int i = threadIdx.x; i < nv; i += kSortThreads) {
+    const uint32_t row = (uint32_t)(s_key[i] >> 32);
+    const int slot = (int)(uint32_t)s_key[i];
+    out[i] = make_int2((int)row, (i - key_lower_bound(s_key, nv, row)) | (slot << 12));  // rank < 4096, slot < 4096
+  }
+  int32_t* col = counts + (int64_t)blockIdx.x * a.V;
+  for (int64_t v = threadIdx.x; v < a.V; v += kSortThreads)
+    col[v] = key_lower_bound(s_key, nv, (uint32_t)v + 1) - key_lower_bound(s_key, nv, (uint32_t)v);
+  if (threadIdx.x == 0) n_valid[blockIdx.x] = nv;
+}
+
+// counts[blk][v] -> exclusive prefix over blocks (in place); total[v]
+__global__ __launch_bounds__(256) void bag_col_prefix_kernel(int32_t* __restrict__ counts, int nblk, int64_t V,
+                                                             int32_t* __restrict__ total) {
+  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= V) return;
+  int32_t run = 0;
+  for (int b = 0; b < nblk; ++b) {
+    const int32_t c = counts[(int64_t)b * V + v];
+    counts[(int64_t)b * V + v] = run;
+    run += c;
+  }
+  total[v] = run;
+}
+
+// rowptr[0..V] = exclusive scan of total[0..V) (one workgroup; per-thread contiguous segments, fixed order)
+__global__ __launch_bounds__(1024) void bag_row_scan_kernel(const int32_t* __restrict__ total, int64_t V,
+                                                            int32_t* __restrict__ rowptr) {
   __shared__ int32_t s_part[1024];
   const int tid = threadIdx.x;
   const int64_t per = (V + 1023) / 1024;
   const int64_t lo = tid * per, hi = min(V, lo + per);
   int32_t sum = 0;
-  for (int64_t i = lo; i < hi; ++i) sum += count[i];
+  for (int64_t i = lo; i < hi; ++i) sum += total[i];
   s_part[tid] = sum;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
-    int32_t add = (tid >= o) ? s_part[tid - o] : 0;
+    const int32_t add = (tid >= o) ? s_part[tid - o] : 0;
     __syncthreads();
     s_part[tid] += add;
     __syncthreads();
@@ -533,92 +587,58 @@ __global__ __launch_bounds__(1024) void bag_scan_kernel(const int32_t* __restric
   int32_t run = s_part[tid] - sum;
   for (int64_t i = lo; i < hi; ++i) {
     rowptr[i] = run;
-    cursor[i] = 0;
-    run += count[i];
+    run += total[i];
   }
   if (tid == 1023) rowptr[V] = s_part[1023];
 }
 
-// Scatter into CSR order. LDS variant: block-local counts, one global cursor reservation per (block, bin), then
-// in-block ranks from LDS atomics.
-template <bool LDS>
-__global__ __launch_bounds__(256) void bag_fill_kernel(BagBwdArgs a, int64_t n_slots, int64_t per,
-                                                       const int32_t* __restrict__ rowptr,
-                                                       int32_t* __restrict__ cursor, int64_t* __restrict__ ent_src,
-                                                       float* __restrict__ ent_w, int32_t* __restrict__ ent_v) {
-  extern __shared__ int32_t s_mem[];
-  int32_t* s_cnt = s_mem;
-  int32_t* s_base = s_mem + a.V;
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(n_slots, lo + per);
-  if (LDS) {
-    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x) s_cnt[i] = 0;
-    __syncthreads();
-    for (int64_t slot = lo + threadIdx.x; slot < hi; slot += blockDim.x) {
-      int64_t v, src;
-      float w;
-      if (bag_slot(a, slot, v, w, src)) atomicAdd(s_cnt + v, 1);
-    }
-    __syncthreads();
-    for (int64_t i = threadIdx.x; i < a.V; i += blockDim.x) {
-      const int32_t c = s_cnt[i];
-      s_base[i] = c ? rowptr[i] + atomicAdd(cursor + i, c) : 0;
-      s_cnt[i] = 0;
-    }
-    __syncthreads();
-  }
-  for (int64_t slot = lo + threadIdx.x; slot < hi; slot += blockDim.x) {
+// CSR entry: (row, src, weight bits, 0); src < 0 = subject-sum row (-1 - b)
+__global__ __launch_bounds__(256) void bag_scatter_kernel(BagBwdArgs a, const int2* __restrict__ sorted,
+                                                          const int32_t* __restrict__ n_valid,
+                                                          const int32_t* __restrict__ prefix,
+                                                          const int32_t* __restrict__ rowptr, int4* __restrict__ ent) {
+  const int blk = blockIdx.y;
+  const int nv = n_valid[blk];
+  const int64_t base = (int64_t)blk * kSortCh;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
+    const int2 e = sorted[base + i];
+    const int row = e.x, rank = e.y & 4095, slot = e.y >> 12;
     int64_t v, src;
     float w;
-    if (!bag_slot(a, slot, v, w, src)) continue;
-    const int32_t pos = LDS ? s_base[v] + atomicAdd(s_cnt + v, 1) : rowptr[v] + atomicAdd(cursor + v, 1);
-    ent_src[pos] = src;
-    ent_w[pos] = w;
-    ent_v[pos] = (int32_t)v;
+    bag_slot(a, base + slot, v, w, src);  // valid by construction: recompute its weight and source row
+    const int64_t pos = (int64_t)rowptr[row] + prefix[(int64_t)blk * a.V + row] + rank;
+    ent[pos] = make_int4(row, (int)src, __float_as_int(w), 0);
   }
 }
 
-// Subject sums of dsrc over valid events and all levels: sub[b, d] (zeroed beforehand). Block (b, c) sums the
-// event chunk c of subject b for every column and adds it in.
-constexpr int kSubChunks = 8;
+// Subject sums of dsrc over valid events and all levels, in event order: sub[b, d]. Block (b, column chunk).
 __global__ __launch_bounds__(256) void bag_subject_sum_kernel(esgpt_batch bt, int64_t G, const float* __restrict__ dsrc,
                                                               int64_t ld, int64_t D, float* __restrict__ sub) {
   const int64_t b = blockIdx.x;
-  const int64_t per = (bt.L + kSubChunks - 1) / kSubChunks;
-  const int64_t l0 = blockIdx.y * per, l1 = min(bt.L, l0 + per);
-  for (int64_t d = threadIdx.x; d < D; d += blockDim.x) {
-    float acc = 0.f;
-    for (int64_t l = l0; l < l1; ++l) {
-      const int64_t e = b * bt.L + l;
-      if (!bt.event_mask[e]) continue;
-      for (int64_t g = 0; g < G; ++g) acc += dsrc[(e * G + g) * ld + d];
-    }
-    if (l1 > l0) atomicAdd(sub + b * D + d, acc);
+  const int64_t d = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  float acc = 0.f;
+  for (int64_t l = 0; l < bt.L; ++l) {
+    const int64_t e = b * bt.L + l;
+    if (!bt.event_mask[e]) continue;
+    for (int64_t g = 0; g < G; ++g) acc += dsrc[(e * G + g) * ld + d];
   }
+  sub[b * D + d] = acc;
 }
 
-// One wave per chunk of kChunk sorted entries. Lane l loads entries l and 64 + l of the chunk (coalesced); the wave
-// then walks them in groups of kGroup with the group's gathered gradient rows in flight together (the entry fields
-// are wave-uniform via readlane). Rows fully inside the chunk are stored; a row that continues into a neighbouring
-// chunk (at most the first and the last run) is added with f32 atomics — long chunks keep the number of atomic
-// adds per address low for the very frequent rows (a univariate measurement's row gets ~20k entries per batch).
-// dtable is zeroed beforehand.
+// One wave per chunk of kChunk CSR entries. Lane l holds entries l and 64 + l of the chunk; the wave walks them in
+// groups of kGroup with the group's gathered gradient rows in flight together (entry fields wave-uniform via
+// readlane). A run (the entries of one row) that starts before / continues after the chunk is written to the
+// chunk's head / tail partial instead of the table (a run shared with both sides: the head partial).
 constexpr int kChunk = 128;
 constexpr int kGroup = 8;
 
-__device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(uint64_t)x, l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), l);
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
 template <int VEC>
-__global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_t* __restrict__ rowptr,
-                                                         const int64_t* __restrict__ ent_src,
-                                                         const float* __restrict__ ent_w,
-                                                         const int32_t* __restrict__ ent_v,
-                                                         const float* __restrict__ dsrc, int64_t ld,
-                                                         const float* __restrict__ sub, int64_t D,
-                                                         float* __restrict__ dtable) {
+__global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restrict__ rowptr, int64_t V,
+                                                         const int4* __restrict__ ent, const float* __restrict__ dsrc,
+                                                         int64_t ld, const float* __restrict__ sub, int64_t D,
+                                                         float* __restrict__ dtable, float* __restrict__ part_head,
+                                                         float* __restrict__ part_tail) {
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int64_t chunk = (int64_t)blockIdx.x * kWavesPerBlock + wave;
@@ -626,21 +646,20 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
   const int64_t n_ent = rowptr[V];
   if (lo >= n_ent) return;
   const int n = (int)min<int64_t>(kChunk, n_ent - lo);
-  int32_t my_v[2] = {-1, -1};
-  int64_t my_s[2] = {0, 0};
+  int32_t my_v[2] = {-1, -1}, my_s[2] = {0, 0};
   float my_w[2] = {0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int p = 64 * u + lane;
     if (p < n) {
-      my_v[u] = ent_v[lo + p];
-      my_s[u] = ent_src[lo + p];
-      my_w[u] = ent_w[lo + p];
+      const int4 x = ent[lo + p];
+      my_v[u] = x.x;
+      my_s[u] = x.y;
+      my_w[u] = __int_as_float(x.z);
     }
   }
-  // the chunk's first / last run continues into the previous / next chunk when those entries share its row
-  const int32_t prev_v = lo > 0 ? ent_v[lo - 1] : -1;
-  const int32_t next_v = lo + n < n_ent ? ent_v[lo + n] : -1;
+  const int32_t prev_v = lo > 0 ? ent[lo - 1].x : -1;
+  const int32_t next_v = lo + n < n_ent ? ent[lo + n].x : -1;
   for (int64_t base = 0; base < D; base += 64 * VEC) {
     const int64_t d0 = base + (int64_t)lane * VEC;
     const bool dok = d0 < D;  // VEC == 4 only when D % 4 == 0
@@ -650,29 +669,31 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
     int32_t cur = __builtin_amdgcn_readlane(my_v[0], 0);
     bool head = true;  // the current run starts at the chunk's first entry
     auto flush = [&](bool tail) {
-      const bool shared = (head && prev_v == cur) || (tail && next_v == cur);
-      float* dst = dtable + (int64_t)cur * D + d0;
+      float* dst;
+      if (head && prev_v == cur) dst = part_head + chunk * D;
+      else if (tail && next_v == cur) dst = part_tail + chunk * D;
+      else dst = dtable + (int64_t)cur * D;
+      if (VEC == 4) {
+        if (dok) *reinterpret_cast<float4*>(dst + d0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      } else {
 #pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        if (dok && (VEC == 4 || d0 + k < D)) {
-          if (shared) atomicAdd(dst + k, acc[k]);
-          else dst[k] = acc[k];
-        }
-        acc[k] = 0.f;
+        for (int k = 0; k < VEC; ++k)
+          if (d0 + k < D) dst[d0 + k] = acc[k];
       }
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
     };
     for (int p0 = 0; p0 < n; p0 += kGroup) {
-      // the group's entries live in register half u = p0 / 64 (groups never straddle it): uniform selects
-      const bool up = p0 >= 64;
+      const bool up = p0 >= 64;  // groups never straddle the two register halves
       const int32_t gv = up ? my_v[1] : my_v[0];
-      const int64_t gs = up ? my_s[1] : my_s[0];
+      const int32_t gs = up ? my_s[1] : my_s[0];
       const float gw = up ? my_w[1] : my_w[0];
       float x[kGroup][VEC];
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) {
         const int p = min(p0 + j, n - 1);
-        const int64_t s = readlane64(gs, p & 63);
-        const float* row = s >= 0 ? dsrc + s * ld : sub + (-1 - s) * D;
+        const int32_t s = __builtin_amdgcn_readlane(gs, p & 63);
+        const float* row = s >= 0 ? dsrc + (int64_t)s * ld : sub + (int64_t)(-1 - s) * D;
         if (VEC == 4) {
           float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
           if (dok) t = *reinterpret_cast<const float4*>(row + d0);
@@ -705,15 +726,42 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(int64_t V, const int32_
   }
 }
 
+// Rows spanning several chunks, and empty rows. One wave per (row, 256-column block).
+__global__ __launch_bounds__(256) void bag_combine_kernel(const int32_t* __restrict__ rowptr, int64_t V, int64_t D,
+                                                          const float* __restrict__ part_head,
+                                                          const float* __restrict__ part_tail,
+                                                          float* __restrict__ dtable) {
+  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int64_t dblocks = (D + 255) / 256;
+  const int64_t v = w / dblocks;
+  if (v >= V) return;
+  const int64_t d0 = (w % dblocks) * 256 + lane_id() * 4;
+  const int64_t s = rowptr[v], e = rowptr[v + 1];
+  float* dst = dtable + v * D;
+  if (s == e) {
+    for (int64_t d = d0; d < min(D, d0 + 4); ++d) dst[d] = 0.f;
+    return;
+  }
+  const int64_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
+  if (c0 == c1) return;  // written by bag_reduce
+  for (int64_t d = d0; d < min(D, d0 + 4); ++d) {
+    float acc = part_tail[c0 * D + d];
+    for (int64_t c = c0 + 1; c <= c1; ++c) acc += part_head[c * D + d];
+    dst[d] = acc;
+  }
+}
+
 struct BagWs {
-  int32_t* count;
-  int32_t* rowptr;
-  int32_t* cursor;
-  int32_t* n_ent_dummy;
-  int64_t* ent_src;
-  float* ent_w;
-  int32_t* ent_v;
-  float* sub;
+  int32_t* counts;   // [nblk][V]: block counts, then in-place prefixes over blocks
+  int32_t* total;    // [V]
+  int32_t* rowptr;   // [V + 1]
+  int32_t* n_valid;  // [nblk]
+  int2* sorted;      // [nblk * kSortCh]
+  int4* ent;         // [n_slots]
+  float* part_head;  // [n_chunks][D]
+  float* part_tail;  // [n_chunks][D]
+  float* sub;        // [B][D]
+  int64_t nblk, n_slots, n_chunks;
   size_t bytes;
 };
 
@@ -721,7 +769,9 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static BagWs carve(void* base, const esgpt_batch* bt, int64_t G, int64_t V, int64_t D) {
   BagWs w{};
-  const int64_t n_slots = bt->B * bt->L * G * bt->M + bt->B * bt->S;
+  w.n_slots = bt->B * bt->L * G * bt->M + bt->B * bt->S;
+  w.nblk = std::max<int64_t>(1, cdiv(w.n_slots, kSortCh));
+  w.n_chunks = std::max<int64_t>(1, cdiv(w.n_slots, kChunk));
   char* p = (char*)base;
   size_t off = 0;
   auto take = [&](size_t n) {
@@ -729,12 +779,14 @@ static BagWs carve(void* base, const esgpt_batch* bt, int64_t G, int64_t V, int6
     off += align_up(n);
     return r;
   };
-  w.count = (int32_t*)take(sizeof(int32_t) * (V + 1));
+  w.counts = (int32_t*)take(sizeof(int32_t) * w.nblk * V);
+  w.total = (int32_t*)take(sizeof(int32_t) * V);
   w.rowptr = (int32_t*)take(sizeof(int32_t) * (V + 1));
-  w.cursor = (int32_t*)take(sizeof(int32_t) * (V + 1));
-  w.ent_src = (int64_t*)take(sizeof(int64_t) * n_slots);
-  w.ent_w = (float*)take(sizeof(float) * n_slots);
-  w.ent_v = (int32_t*)take(sizeof(int32_t) * n_slots);
+  w.n_valid = (int32_t*)take(sizeof(int32_t) * w.nblk);
+  w.sorted = (int2*)take(sizeof(int2) * w.nblk * kSortCh);
+  w.ent = (int4*)take(sizeof(int4) * w.n_slots);
+  w.part_head = (float*)take(sizeof(float) * w.n_chunks * D);
+  w.part_tail = (float*)take(sizeof(float) * w.n_chunks * D);
   w.sub = (float*)take(sizeof(float) * bt->B * D);
   w.bytes = off;
   return w;
@@ -827,50 +879,32 @@ size_t esgpt_embed_bag_bwd_workspace(const esgpt_batch* batch, int64_t G, int64_
 int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, int selector, int flags,
                         float dyn_scale, float static_scale, const float* dsrc, int64_t ld, int64_t D, int64_t V,
                         float* dtable, void* workspace, size_t workspace_bytes, void* stream) {
-  ESGPT_REQUIRE(batch && dsrc && dtable && D > 0 && V > 0 && V < (1ll << 31));
+  ESGPT_REQUIRE(batch && dsrc && dtable && D > 0 && V > 0 && V < (1ll << 31) - 1);
   const Buckets bk = make_buckets(buckets);
   ESGPT_REQUIRE(bk.G >= 1 && bk.G <= kMaxG);
   BagWs w = carve(workspace, batch, bk.G, V, D);
   ESGPT_REQUIRE(workspace && workspace_bytes >= w.bytes);
+  ESGPT_REQUIRE(w.n_slots < (1ll << 31) && batch->B * batch->L * bk.G < (1ll << 31));  // int32 CSR fields
   hipStream_t st = as_stream(stream);
   BagBwdArgs a{*batch, bk, selector, flags, dyn_scale, static_scale, V};
-  const int64_t n_slots = batch->B * batch->L * bk.G * batch->M + batch->B * batch->S;
-  if (zero_async(dtable, sizeof(float) * V * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if (zero_async(w.count, sizeof(int32_t) * (V + 1), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if (n_slots == 0) return ESGPT_OK;
-  const int64_t nblk = std::min<int64_t>(kBagBlocks, cdiv(n_slots, 256));
-  const int64_t per = cdiv(n_slots, nblk);
-  // Dynamic LDS stays within the 64 KiB default: count needs 4 B/bin, fill 8 B/bin.
-  const bool lds = V <= kLdsBins;
-  const bool lds_fill = V <= kLdsBins / 2;
-  if (lds) {
-    bag_count_kernel<true><<<(unsigned)nblk, 256, sizeof(int32_t) * V, st>>>(a, n_slots, per, w.count);
-  } else {
-    bag_count_kernel<false><<<(unsigned)nblk, 256, 0, st>>>(a, n_slots, per, w.count);
-  }
-  bag_scan_kernel<<<1, 1024, 0, st>>>(w.count, V, w.rowptr, w.cursor);
-  if (lds_fill) {
-    bag_fill_kernel<true><<<(unsigned)nblk, 256, 2 * sizeof(int32_t) * V, st>>>(a, n_slots, per, w.rowptr, w.cursor,
-                                                                               w.ent_src, w.ent_w, w.ent_v);
-  } else {
-    bag_fill_kernel<false><<<(unsigned)nblk, 256, 0, st>>>(a, n_slots, per, w.rowptr, w.cursor, w.ent_src, w.ent_w,
-                                                          w.ent_v);
-  }
-  if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM) {
-    if (zero_async(w.sub, sizeof(float) * batch->B * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-    bag_subject_sum_kernel<<<dim3((unsigned)batch->B, kSubChunks), 256, 0, st>>>(*batch, bk.G, dsrc, ld, D, w.sub);
-  }
-  ESGPT_LAUNCH_CHECK();
+  if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM)
+    bag_subject_sum_kernel<<<dim3((unsigned)batch->B, (unsigned)cdiv(D, 256)), 256, 0, st>>>(*batch, bk.G, dsrc, ld,
+                                                                                          D, w.sub);
+  bag_block_sort_kernel<<<(unsigned)w.nblk, kSortThreads, 0, st>>>(a, w.n_slots, w.counts, w.sorted, w.n_valid);
+  bag_col_prefix_kernel<<<(unsigned)cdiv(V, 256), 256, 0, st>>>(w.counts, (int)w.nblk, V, w.total);
+  bag_row_scan_kernel<<<1, 1024, 0, st>>>(w.total, V, w.rowptr);
+  bag_scatter_kernel<<<dim3(4, (unsigned)w.nblk), 256, 0, st>>>(a, w.sorted, w.n_valid, w.counts, w.rowptr, w.ent);
   // The number of entries is data-dependent (not known on the host without a sync): launch for the upper bound;
   // chunks past rowptr[V] exit immediately.
-  const int64_t n_chunks = cdiv(n_slots, kChunk);
-  const unsigned g_red = (unsigned)cdiv(n_chunks, kWavesPerBlock);
-  if (D % 4 == 0 && D >= 256 && ld % 4 == 0 && ((uintptr_t)dsrc % 16) == 0)
-    bag_reduce_kernel<4><<<g_red, 256, 0, st>>>(V, w.rowptr, w.ent_src, w.ent_w, w.ent_v, dsrc, ld, w.sub, D,
-                                                dtable);
+  const unsigned g_red = (unsigned)cdiv(w.n_chunks, kWavesPerBlock);
+  if (D % 4 == 0 && D >= 256 && ld % 4 == 0 && ((uintptr_t)dsrc % 16) == 0 && ((uintptr_t)dtable % 16) == 0)
+    bag_reduce_kernel<4><<<g_red, 256, 0, st>>>(w.rowptr, V, w.ent, dsrc, ld, w.sub, D, dtable, w.part_head,
+                                                w.part_tail);
   else
-    bag_reduce_kernel<1><<<g_red, 256, 0, st>>>(V, w.rowptr, w.ent_src, w.ent_w, w.ent_v, dsrc, ld, w.sub, D,
-                                                dtable);
+    bag_reduce_kernel<1><<<g_red, 256, 0, st>>>(w.rowptr, V, w.ent, dsrc, ld, w.sub, D, dtable, w.part_head,
+                                                w.part_tail);
+  bag_combine_kernel<<<(unsigned)cdiv(V * cdiv(D, 256), kWavesPerBlock), 256, 0, st>>>(w.rowptr, V, D, w.part_head,
+                                                                                      w.part_tail, dtable);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -67,6 +67,16 @@ def _tickets(device):
     return tickets(device)
 
 
+def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db):
+    """``esgpt::linear_bwd`` from a registered backward (records the launch shape for bench.py when asked)."""
+    from . import fused
+
+    if fused.SHAPES["enabled"]:
+        fused.SHAPES["linear_bwd"].append((dy.shape[0], x.shape[1], dy.shape[1], bool(need_dx), int(act),
+                                           bool(need_db)))
+    return torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device))
+
+
 def _batch_d(args, start):
     """(B, L, M) from the 9 batch tensors starting at args[start]."""
     di = args[start + 3]
@@ -318,7 +328,7 @@ def _register():
     def _li_bwd(ctx, dy):
         x, w = ctx.saved_tensors
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
-        dx, dw, db = ops.linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db, _tickets(x.device))
+        dx, dw, db = _linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db)
         return (dx if ctx.needs_input_grad[0] else None, None, db if need_db else None,
                 list(torch.split(dw, ctx.rows, 0)), None)
 
@@ -334,10 +344,9 @@ def _register():
 
     def _ml_bwd(ctx, dy, _dpre, _dg):
         x, w_fc, w_pj, pre, g = ctx.saved_tensors
-        t = _tickets(x.device)
-        dz, dw_pj, _ = ops.linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, False, t)
+        dz, dw_pj, _ = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, False)
         need_dx = ctx.needs_input_grad[0]
-        dx, dw_fc, db_fc = ops.linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True, t)
+        dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True)
         return (dx if need_dx else None, None, None, db_fc, None, dw_fc, dw_pj, None)
 
     reg(lib + "mlp", _ml_bwd, setup_context=_ml_setup)
@@ -374,8 +383,7 @@ def _register():
         n_cw, n_tw = ctx.n
         rows_c, rows_t = ctx.rows
         alpha = g.contiguous()[-1:]
-        t = _tickets(xc.device)
-        dxc, dwc, dbc = ops.linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, t)
+        dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True)
         if dbias.numel():
             dbc = dbc + dbias.sum(0) * alpha
         nc = sum(rows_c)
@@ -383,7 +391,7 @@ def _register():
         gb_c = list(torch.split(dbc[:nc], rows_c, 0))
         dxt, gw_t, gb_t = None, [], []
         if n_tw:
-            dxt, dwt, dbt = ops.linear_bwd(dzt, xt, wt, alpha, -1, None, True, True, t)
+            dxt, dwt, dbt = _linear_bwd(dzt, xt, wt, alpha, -1, None, True, True)
             nt = sum(rows_t)
             gw_t = list(torch.split(dwt[:nt], rows_t, 0))
             gb_t = list(torch.split(dbt[:nt], rows_t, 0))

@@ -1,8 +1,10 @@
 """GPU parity: the HIP path (through the C ABI) against the reference's golden vectors and the CPU oracle.
 
-Tolerances (BASELINE.json north_star): f32 forward/backward <= 1e-5 relative on losses and encodings; gradients
-are compared with a max-abs-normalised error (<= 1e-4: different but valid f32 summation orders); bf16 losses
-<= 1e-2 relative.
+Tolerances (BASELINE.json north_star): f32 forward AND backward <= 1e-5 relative — losses, encodings and every
+parameter gradient (max-abs-normalised per tensor; measured worst 3.1e-6, tools/parity_report.py); bf16 losses
+<= 1e-2 relative (measured <= 3e-4). bf16 gradients have no north_star bound; they are held per tensor to a
+max-abs-normalised error <= 3e-2 and a cosine >= 0.9995 against the f32 oracle (measured worst 1.4e-2 / 0.99993 at
+the C4 width: bf16 operands carry 8 mantissa bits through 6-12 layers).
 """
 import pytest
 import torch
@@ -65,7 +67,7 @@ def test_model_matches_reference_f32(name, fused_mode):
     for k, g in fx["grads"].items():
         got = named[k].grad
         assert got is not None, k
-        assert rel_err(got.cpu(), g) < 1e-4, (k, rel_err(got.cpu(), g))
+        assert rel_err(got.cpu(), g) < 1e-5, (k, rel_err(got.cpu(), g))
 
 
 def _rand_qkv(B, T, H, hd, dtype, seed):
@@ -123,8 +125,8 @@ def test_attention_kernel(shape, dtype):
         go = torch.where(km[..., None], go, torch.zeros_like(go))
     o.backward(go.to(dtype))
     ref.backward(go)
-    gtol = 1e-4 if dtype == torch.float32 else 3e-2
-    assert rel_err(x.grad.float(), ref_in.grad) < gtol
+    gtol = 1e-5 if dtype == torch.float32 else 3e-2
+    assert rel_err(x.grad.float(), ref_in.grad) < gtol, rel_err(x.grad.float(), ref_in.grad)
 
 
 def test_embedding_c2_joint_matches_oracle():
@@ -151,23 +153,59 @@ def test_embedding_c2_joint_matches_oracle():
                    p["e.data_embedding_layer.embed_layer.weight"].grad) < 1e-5
 
 
-@pytest.mark.parametrize("cfg_name", ["C2", "C5"])
-def test_full_step_bf16_matches_oracle(cfg_name):
-    """Full CI model at the config's real width on a reduced batch, bf16 autocast vs the f32 oracle:
-    loss within 1e-2 relative."""
+def _grad_check(m, cfg, batch, loss, loss_tol, grad_tol, cos_min):
+    """Model loss / every parameter gradient vs the f32 oracle on the same weights and batch."""
+    trainable = {k for k, p in m.named_parameters() if p.requires_grad}
+    p = {k: v.detach().cpu().clone().requires_grad_(k in trainable) for k, v in m.state_dict().items()}
+    ref = O.model_losses(p, cfg, batch)
+    assert abs(loss.item() - ref["loss"].item()) <= loss_tol * abs(ref["loss"].item()), (loss.item(), ref["loss"])
+    loss.backward()
+    ref["loss"].backward()
+    named = dict(m.named_parameters())
+    checked = 0
+    for k, v in p.items():
+        if v.grad is None:
+            continue
+        got = named[k].grad
+        assert got is not None, k
+        g, w = got.double().cpu().flatten(), v.grad.double().flatten()
+        assert rel_err(g, w) <= grad_tol, (k, rel_err(g, w))
+        if w.abs().max() > 0:
+            assert torch.nn.functional.cosine_similarity(g, w, dim=0).item() >= cos_min, k
+        checked += 1
+    assert checked == len([1 for k in trainable if p[k].grad is not None]) and checked > 10
+
+
+@pytest.mark.parametrize("cfg_name,B", [("C2", 4), ("C3", 2), ("C4", 2), ("C5", 2)])
+def test_width_bf16_matches_oracle(cfg_name, B):
+    """Every model of SURVEY §8's config table at its real width (C3: 12 layers, d=512, L=512, H=8, alternating
+    global / local-32; C4: NA, SPLIT, 4 dependency-graph levels; C5: L=1024, LNM K=8, 10k vocabulary) on a reduced
+    batch, bf16 autocast vs the f32 oracle: the loss within 1e-2 (north_star) and every parameter gradient."""
     from eventstreamgpt_amd.synthetic import CONFIGS
 
     bc = CONFIGS[cfg_name]
     cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
     torch.manual_seed(0)
-    m = _model(cfg).to(DEV)
-    batch = bc.batch(0, batch_size=4)
+    m = _model(cfg).to(DEV).train()
+    batch = bc.batch(0, batch_size=B)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         out = m(batch.to(DEV))
-    p = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-    ref = O.model_losses(p, cfg, batch)
-    assert out.loss.item() == pytest.approx(ref["loss"].item(), rel=1e-2)
-    out.loss.backward()
+    _grad_check(m, cfg, batch, out.loss, 1e-2, 3e-2, 0.9995)
+
+
+@pytest.mark.parametrize("cfg_name,B", [("C2", 2), ("C3", 1)])
+def test_width_f32_matches_oracle(cfg_name, B):
+    """f32 at the C2 / C3 widths (C3's 12 layers of global / local-32 attention at L=512): loss and every gradient
+    within 1e-5 of the oracle."""
+    from eventstreamgpt_amd.synthetic import CONFIGS
+
+    bc = CONFIGS[cfg_name]
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+    torch.manual_seed(0)
+    m = _model(cfg).to(DEV).train()
+    batch = bc.batch(0, batch_size=B)
+    out = m(batch.to(DEV))
+    _grad_check(m, cfg, batch, out.loss, 1e-5, 1e-5, 0.0)
 
 
 def _np_mix32(x):
@@ -245,7 +283,7 @@ def test_attention_dropout(shape, dtype):
         go = torch.where(km[..., None], go, torch.zeros_like(go))
     o.backward(go.to(dtype))
     ref.backward(go)
-    assert rel_err(x.grad.float(), ref_in.grad) < (1e-4 if dtype == torch.float32 else 3e-2)
+    assert rel_err(x.grad.float(), ref_in.grad) < (1e-5 if dtype == torch.float32 else 3e-2)
 
 
 @pytest.mark.parametrize("D", [64, 256, 1024])

@@ -68,3 +68,37 @@ def test_tte_reference_known_answers():
     p = {"TTE_layer.proj.weight": w, "TTE_layer.proj.bias": torch.zeros(1)}
     ll = O.tte_log_likelihood(p, "", C, batch, enc)
     assert ll.item() == pytest.approx(-3.6534264097200273, abs=1e-5)
+
+
+def _ka_tensor(x):
+    return torch.tensor(x["data"], dtype=getattr(torch, x["dtype"]))
+
+
+def test_oracle_embedding_known_answers():
+    """The oracle's DataEmbeddingLayer restatement reproduces the reference's own known answers
+    (tests/data/test_data_embedding_layer.py:255-346, 348-576, 732-913; fixture transcribed by
+    tests/golden/make_embedding_known_answers.py)."""
+    import json
+
+    fx = json.load(open(os.path.join(GOLDEN, "embedding_known_answers.json")))
+    assert len(fx["cases"]) == 9
+    for c in fx["cases"]:
+        prm = c["params"]
+        ew = dict(mode="split" if prm.get("categorical_embedding_dim") else "joint",
+                  do_normalize_by_measurement_index=prm.get("do_normalize_by_measurement_index", False),
+                  static_embedding_mode=prm["static_embedding_mode"], static_weight=prm.get("static_weight", 0.5),
+                  dynamic_weight=prm.get("dynamic_weight", 0.5), categorical_weight=prm.get("categorical_weight", 0.5),
+                  numerical_weight=prm.get("numerical_weight", 0.5))
+        p = {"e.embed_layer.weight": torch.eye(4), "e.categorical_embed_layer.weight": torch.eye(4),
+             "e.cat_proj.weight": 0.5 * torch.eye(4), "e.cat_proj.bias": torch.zeros(4),
+             "e.numerical_embed_layer.weight": 2 * torch.eye(4), "e.num_proj.weight": -torch.eye(4),
+             "e.num_proj.bias": torch.zeros(4)}
+        want = _ka_tensor(c["want"])
+        if c["kind"] == "forward":
+            batch = {k: _ka_tensor(v) for k, v in c["batch"]["PytorchBatch"].items()}
+            got = O.data_embedding(p, "e.", ew, batch)
+        else:
+            got = O.embed_bags(p, "e.", ew, _ka_tensor(c["indices"]), _ka_tensor(c["measurement_indices"]),
+                               _ka_tensor(c["values"]), _ka_tensor(c["values_mask"]),
+                               _ka_tensor(c["cat_mask"]) if "cat_mask" in c else None)
+        torch.testing.assert_close(got, want, msg=c["msg"])

@@ -153,3 +153,38 @@ def test_nested_attention_bf16_fused_blocks_match_module_path(name):
         scale = gm[k].abs().max().clamp_min(1e-6)
         assert torch.isfinite(gf[k]).all(), k
         assert ((gf[k] - gm[k]).abs().max() / scale).item() < 0.1, k
+
+
+@pytest.mark.gpu
+def test_nested_attention_graph_replay_matches_eager_with_allocations_between_replays():
+    """The NA training step captured as a HIP graph (forced: graph_safe() keeps NA eager by default) replays with
+    fresh batches while the host allocates and frees device memory between replays (so a buffer the graph uses but
+    does not own would be reused and corrupted), and matches eager steps: losses every step, parameters after."""
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C4"]
+    batches = [bc.batch(i, batch_size=4, device="cuda").packed() for i in range(5)]
+
+    def run(graph):
+        cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+        torch.manual_seed(0)
+        m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
+        ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=100),
+                       torch.bfloat16, use_graph=graph, _force_graph=True)
+        losses, junk = [], []
+        for i, b in enumerate(batches):
+            losses.append(float(ts.step(b)))
+            # host-side allocations between replays: reuse any freed block a captured kernel still points at
+            junk = [torch.full((1 << (16 + (i + j) % 6),), float(j + 1), device="cuda") for j in range(24)]
+            torch.cuda.synchronize()
+            del junk
+        ts.check()
+        return losses, {k: v.detach().float().clone() for k, v in m.state_dict().items()}, ts.use_graph
+
+    le, se, _ = run(False)
+    lg, sg, used = run(True)
+    assert used
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-3 * abs(a), (le, lg)
+    for k in se:
+        assert (sg[k] - se[k]).abs().max().item() < 1e-4, k
