@@ -12,6 +12,9 @@
 // algorithmic bytes per event = nnz_e * D * 4 (rows, per occurrence) + M * 18 (index/meas/value/mask) + G*D*4.
 #include <algorithm>
 
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
+
 #include "common.h"
 
 using namespace esgpt;
@@ -486,95 +489,128 @@ __device__ __forceinline__ bool bag_slot(const BagBwdArgs& a, int64_t slot, int6
 // ------------------------------------------------------------------------------------------------------------
 // Deterministic, atomic-free bag backward: a stable counting sort of the slots by vocabulary row, then a segmented
 // reduction in slot order (every sum runs in a fixed order: table gradients are bitwise repeatable).
-//   K0 bag_subject_sum  (static SUM_ALL) subject sums of dsrc over valid events and levels, in event order
-//   K1 bag_block_sort   per block of kSortCh slots: (row << 32 | slot) keys bitonic-sorted in LDS (a total order, so
-//                       slot order within a row), the block's per-row counts (counts[blk][V]) and every valid
-//                       slot's (row, rank within the block's run) in block-sorted order
+//   K0 bag_subject_*    (static SUM_ALL) subject sums of dsrc over valid events and levels (16-event chunks, then
+//                       the chunks in order)
+//   K1 bag_block_sort   per block of kSortCh slots: a stable radix sort of the slots by row (slot order within a
+//                       row), the block's per-row counts (counts[blk][V]) and every valid slot's (row, rank within
+//                       the block's run) in block-sorted order
 //   K2 bag_col_prefix   per row: exclusive prefix of counts over blocks (in place) and the row total
 //      bag_row_scan     exclusive scan of the row totals -> rowptr[0..V]
 //   K3 bag_scatter      (row, block, rank) -> CSR position rowptr[row] + prefix[blk][row] + rank: (row, src, w)
 //   K4 bag_reduce       one wave per kChunk CSR entries: rows complete in the chunk are stored; a row continuing
 //                       into the previous / next chunk is stored as that chunk's head / tail partial
-//   K5 bag_combine      rows spanning chunks: tail(c0) + head(c0+1) + ... + head(c1), in chunk order; empty rows 0
+//   K5 bag_combine      rows spanning chunks (a compact list): tail(c0) + the heads of c0+1 .. c1 (a fixed
+//                       16-wave interleave and a fixed combine order); rows without entries stay zero-filled
 // ------------------------------------------------------------------------------------------------------------
-constexpr int kSortCh = 4096;       // slots per sort block (LDS: 32 KiB of 64-bit keys)
-constexpr int kSortThreads = 1024;
-constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 4;
+constexpr int kSortCh = kSortThreads * kSortItems;  // slots per sort block
 
-__device__ __forceinline__ int key_lower_bound(const uint64_t* k, int n, uint32_t row) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if ((uint32_t)(k[mid] >> 32) < row) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-__global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs a, int64_t n_slots,
+// K1: a stable LSD radix sort of the block's (row, local slot) pairs (rocPRIM block_radix_sort: bit-stable, no
+// atomics; invalid slots carry the sentinel row V and sort last), run starts by a block max-scan of the positions
+// where the row changes, then per valid slot (row, rank within the block's run | local slot << 12) in sorted order
+// and, at every run end, the run length into counts[blk][row] (zeroed beforehand).
+__global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs a, int64_t n_slots, int end_bit,
                                                                       int32_t* __restrict__ counts,
                                                                       int2* __restrict__ sorted,
                                                                       int32_t* __restrict__ n_valid) {
-  __shared__ uint64_t s_key[kSortCh];
+  using Sort = rocprim::block_radix_sort<uint32_t, kSortThreads, kSortItems, uint32_t>;
+  using Scan = rocprim::block_scan<int, kSortThreads>;
+  __shared__ union {
+    typename Sort::storage_type sort;
+    typename Scan::storage_type scan;
+  } tmp;
+  __shared__ uint32_t s_row[kSortCh];
   __shared__ int s_nv;
+  const int t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * kSortCh;
-  for (int i = threadIdx.x; i < kSortCh; i += kSortThreads) {
+  const uint32_t sentinel = (uint32_t)a.V;
+  uint32_t key[kSortItems], val[kSortItems];
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const int pos = t * kSortItems + i;  // blocked arrangement: the input order is slot order (stable sort)
     int64_t v = 0, src = 0;
     float w = 0.f;
-    uint32_t row = kNoRow;
-    if (base + i < n_slots && bag_slot(a, base + i, v, w, src)) row = (uint32_t)v;
-    s_key[i] = ((uint64_t)row << 32) | (uint32_t)i;
+    key[i] = (base + pos < n_slots && bag_slot(a, base + pos, v, w, src)) ? (uint32_t)v : sentinel;
+    val[i] = (uint32_t)pos;
+  }
+  if (t == 0) s_nv = 0;
+  Sort().sort(key, val, tmp.sort, 0, end_bit);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) s_row[t * kSortItems + i] = key[i];
+  __syncthreads();
+  int start[kSortItems];
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const int pos = t * kSortItems + i;
+    start[i] = (pos == 0 || s_row[pos - 1] != key[i]) ? pos : 0;
+  }
+  Scan().inclusive_scan(start, start, tmp.scan, rocprim::maximum<int>());
+  int2* out = sorted + base;
+  int32_t* col = counts + (int64_t)blockIdx.x * a.V;
+#pragma unroll
+  for (int i = 0; i < kSortItems; ++i) {
+    const int pos = t * kSortItems + i;
+    if (key[i] >= sentinel) continue;
+    const int rank = pos - start[i];
+    out[pos] = make_int2((int)key[i], rank | ((int)val[i] << 12));
+    const bool run_end = pos + 1 == kSortCh || s_row[pos + 1] != key[i];
+    if (run_end) col[key[i]] = rank + 1;
+    if (pos + 1 == kSortCh || s_row[pos + 1] >= sentinel) s_nv = pos + 1;
   }
   __syncthreads();
-  for (int k = 2; k <= kSortCh; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < kSortCh / 2; t += kSortThreads) {
-        const int lo = 2 * t - (t & (j - 1)), hi = lo + j;
-        const uint64_t x = s_key[lo], y = s_key[hi];
-        if ((x > y) == ((lo & k) == 0)) {
-          s_key[lo] = y;
-          s_key[hi] = x;
-        }
-      }
-      __syncthreads();
+  if (t == 0) n_valid[blockIdx.x] = s_nv;
+}
+
+// counts[blk][v] -> exclusive prefix over blocks (in place); total[v]. Workgroup = 64 rows (lanes) x 16 waves; wave
+// w owns the contiguous block segment [w*S, (w+1)*S): segment sums, their exclusive prefix over waves (LDS), then
+// the segment rewritten as running prefixes. Loads of a segment are issued 16 at a time.
+constexpr int kPrefWaves = 16;
+__global__ __launch_bounds__(1024) void bag_col_prefix_kernel(int32_t* __restrict__ counts, int nblk, int64_t V,
+                                                              int32_t* __restrict__ total) {
+  __shared__ int32_t s_seg[kPrefWaves][64];
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int64_t v = (int64_t)blockIdx.x * 64 + lane;
+  const bool ok = v < V;
+  const int S = (nblk + kPrefWaves - 1) / kPrefWaves;
+  const int b0 = wave * S, b1 = min(nblk, b0 + S);
+  int32_t sum = 0;
+  for (int bb = b0; bb < b1; bb += 16) {
+    int32_t c[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) c[u] = (ok && bb + u < b1) ? counts[(int64_t)(bb + u) * V + v] : 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sum += c[u];
+  }
+  s_seg[wave][lane] = sum;
+  __syncthreads();
+  int32_t run = 0;
+  for (int w = 0; w < wave; ++w) run += s_seg[w][lane];
+  if (wave == kPrefWaves - 1 && ok) total[v] = run + sum;
+  for (int bb = b0; bb < b1; bb += 16) {
+    int32_t c[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) c[u] = (ok && bb + u < b1) ? counts[(int64_t)(bb + u) * V + v] : 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (ok && bb + u < b1) counts[(int64_t)(bb + u) * V + v] = run;
+      run += c[u];
     }
   }
-  if (threadIdx.x == 0) s_nv = key_lower_bound(s_key, kSortCh, kNoRow);
-  __syncthreads();
-  const int nv = s_nv;
-  int2* out = sorted + base;
-  for (int i = threadIdx.x; i < nv; i += kSortThreads) {
-    const uint32_t row = (uint32_t)(s_key[i] >> 32);
-    const int slot = (int)(uint32_t)s_key[i];
-    out[i] = make_int2((int)row, (i - key_lower_bound(s_key, nv, row)) | (slot << 12));  // rank < 4096, slot < 4096
-  }
-  int32_t* col = counts + (int64_t)blockIdx.x * a.V;
-  for (int64_t v = threadIdx.x; v < a.V; v += kSortThreads)
-    col[v] = key_lower_bound(s_key, nv, (uint32_t)v + 1) - key_lower_bound(s_key, nv, (uint32_t)v);
-  if (threadIdx.x == 0) n_valid[blockIdx.x] = nv;
 }
 
-// counts[blk][v] -> exclusive prefix over blocks (in place); total[v]
-__global__ __launch_bounds__(256) void bag_col_prefix_kernel(int32_t* __restrict__ counts, int nblk, int64_t V,
-                                                             int32_t* __restrict__ total) {
-  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
-  int32_t run = 0;
-  for (int b = 0; b < nblk; ++b) {
-    const int32_t c = counts[(int64_t)b * V + v];
-    counts[(int64_t)b * V + v] = run;
-    run += c;
-  }
-  total[v] = run;
-}
-
-// rowptr[0..V] = exclusive scan of total[0..V) (one workgroup; per-thread contiguous segments, fixed order)
+// rowptr[0..V] = exclusive scan of total[0..V) (one workgroup; per-thread contiguous segments, fixed order), and
+// the compact list of rows whose entries span more than one reduce chunk (multi[1 + j], count in multi[0]).
 __global__ __launch_bounds__(1024) void bag_row_scan_kernel(const int32_t* __restrict__ total, int64_t V,
-                                                            int32_t* __restrict__ rowptr) {
+                                                            int32_t* __restrict__ rowptr, int32_t* __restrict__ multi,
+                                                            int chunk) {
   __shared__ int32_t s_part[1024];
+  __shared__ int32_t s_cnt[1024];
   const int tid = threadIdx.x;
   const int64_t per = (V + 1023) / 1024;
   const int64_t lo = tid * per, hi = min(V, lo + per);
-  int32_t sum = 0;
+  int32_t sum = 0, nm = 0;
   for (int64_t i = lo; i < hi; ++i) sum += total[i];
   s_part[tid] = sum;
   __syncthreads();
@@ -587,9 +623,27 @@ __global__ __launch_bounds__(1024) void bag_row_scan_kernel(const int32_t* __res
   int32_t run = s_part[tid] - sum;
   for (int64_t i = lo; i < hi; ++i) {
     rowptr[i] = run;
-    run += total[i];
+    const int32_t e = run + total[i];
+    if (e > run && run / chunk != (e - 1) / chunk) ++nm;
+    run = e;
   }
   if (tid == 1023) rowptr[V] = s_part[1023];
+  s_cnt[tid] = nm;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int32_t add = (tid >= o) ? s_cnt[tid - o] : 0;
+    __syncthreads();
+    s_cnt[tid] += add;
+    __syncthreads();
+  }
+  int32_t j = s_cnt[tid] - nm;
+  run = s_part[tid] - sum;
+  for (int64_t i = lo; i < hi; ++i) {
+    const int32_t e = run + total[i];
+    if (e > run && run / chunk != (e - 1) / chunk) multi[1 + j++] = (int32_t)i;
+    run = e;
+  }
+  if (tid == 1023) multi[0] = s_cnt[1023];
 }
 
 // CSR entry: (row, src, weight bits, 0); src < 0 = subject-sum row (-1 - b)
@@ -611,27 +665,54 @@ __global__ __launch_bounds__(256) void bag_scatter_kernel(BagBwdArgs a, const in
   }
 }
 
-// Subject sums of dsrc over valid events and all levels, in event order: sub[b, d]. Block (b, column chunk).
-__global__ __launch_bounds__(256) void bag_subject_sum_kernel(esgpt_batch bt, int64_t G, const float* __restrict__ dsrc,
-                                                              int64_t ld, int64_t D, float* __restrict__ sub) {
+// Subject sums of dsrc over valid events and all levels, deterministic in two levels: block (b, event chunk c,
+// column block) sums kSubEv events (16 loads in flight per thread) into sub_part[b][c][D]; then sub[b] = the chunk
+// partials in chunk order.
+constexpr int kSubEv = 16;
+__global__ __launch_bounds__(256) void bag_subject_part_kernel(esgpt_batch bt, int64_t G, const float* __restrict__ dsrc,
+                                                               int64_t ld, int64_t D, float* __restrict__ sub_part) {
+  const int64_t b = blockIdx.x, c = blockIdx.y;
+  const int64_t nch = gridDim.y;
+  const int64_t d = (int64_t)blockIdx.z * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  const int64_t l0 = c * kSubEv;
+  float acc = 0.f;
+  for (int64_t g = 0; g < G; ++g) {
+    float x[kSubEv];
+#pragma unroll
+    for (int u = 0; u < kSubEv; ++u) {
+      const int64_t l = l0 + u;
+      const int64_t e = b * bt.L + l;
+      x[u] = (l < bt.L && bt.event_mask[e]) ? dsrc[(e * G + g) * ld + d] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kSubEv; ++u) acc += x[u];
+  }
+  sub_part[(b * nch + c) * D + d] = acc;
+}
+
+__global__ __launch_bounds__(256) void bag_subject_sum_kernel(const float* __restrict__ sub_part, int64_t nch,
+                                                              int64_t D, float* __restrict__ sub) {
   const int64_t b = blockIdx.x;
   const int64_t d = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
   if (d >= D) return;
   float acc = 0.f;
-  for (int64_t l = 0; l < bt.L; ++l) {
-    const int64_t e = b * bt.L + l;
-    if (!bt.event_mask[e]) continue;
-    for (int64_t g = 0; g < G; ++g) acc += dsrc[(e * G + g) * ld + d];
+  for (int64_t c0 = 0; c0 < nch; c0 += 16) {
+    float x[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) x[u] = c0 + u < nch ? sub_part[(b * nch + c0 + u) * D + d] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc += x[u];
   }
   sub[b * D + d] = acc;
 }
 
-// One wave per chunk of kChunk CSR entries. Lane l holds entries l and 64 + l of the chunk; the wave walks them in
-// groups of kGroup with the group's gathered gradient rows in flight together (entry fields wave-uniform via
-// readlane). A run (the entries of one row) that starts before / continues after the chunk is written to the
-// chunk's head / tail partial instead of the table (a run shared with both sides: the head partial).
-constexpr int kChunk = 128;
-constexpr int kGroup = 8;
+// One wave per chunk of kChunk = 64 CSR entries (lane l holds entry l); the wave walks them in groups of kGroup with
+// the group's gathered gradient rows in flight together (entry fields wave-uniform via readlane). A run (the entries
+// of one row) that starts before / continues after the chunk is written to the chunk's head / tail partial instead
+// of the table (a run shared with both sides: the head partial).
+constexpr int kChunk = 64;
+constexpr int kGroup = 16;
 
 template <int VEC>
 __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restrict__ rowptr, int64_t V,
@@ -646,17 +727,13 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
   const int64_t n_ent = rowptr[V];
   if (lo >= n_ent) return;
   const int n = (int)min<int64_t>(kChunk, n_ent - lo);
-  int32_t my_v[2] = {-1, -1}, my_s[2] = {0, 0};
-  float my_w[2] = {0.f, 0.f};
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int p = 64 * u + lane;
-    if (p < n) {
-      const int4 x = ent[lo + p];
-      my_v[u] = x.x;
-      my_s[u] = x.y;
-      my_w[u] = __int_as_float(x.z);
-    }
+  int32_t my_v = -1, my_s = 0;
+  float my_w = 0.f;
+  if (lane < n) {
+    const int4 x = ent[lo + lane];
+    my_v = x.x;
+    my_s = x.y;
+    my_w = __int_as_float(x.z);
   }
   const int32_t prev_v = lo > 0 ? ent[lo - 1].x : -1;
   const int32_t next_v = lo + n < n_ent ? ent[lo + n].x : -1;
@@ -666,7 +743,7 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
     float acc[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-    int32_t cur = __builtin_amdgcn_readlane(my_v[0], 0);
+    int32_t cur = __builtin_amdgcn_readlane(my_v, 0);
     bool head = true;  // the current run starts at the chunk's first entry
     auto flush = [&](bool tail) {
       float* dst;
@@ -684,15 +761,11 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
       for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
     };
     for (int p0 = 0; p0 < n; p0 += kGroup) {
-      const bool up = p0 >= 64;  // groups never straddle the two register halves
-      const int32_t gv = up ? my_v[1] : my_v[0];
-      const int32_t gs = up ? my_s[1] : my_s[0];
-      const float gw = up ? my_w[1] : my_w[0];
       float x[kGroup][VEC];
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) {
         const int p = min(p0 + j, n - 1);
-        const int32_t s = __builtin_amdgcn_readlane(gs, p & 63);
+        const int32_t s = __builtin_amdgcn_readlane(my_s, p);
         const float* row = s >= 0 ? dsrc + (int64_t)s * ld : sub + (int64_t)(-1 - s) * D;
         if (VEC == 4) {
           float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -710,13 +783,13 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
       for (int j = 0; j < kGroup; ++j) {
         const int p = p0 + j;
         if (p < n) {
-          const int32_t v = __builtin_amdgcn_readlane(gv, p & 63);
+          const int32_t v = __builtin_amdgcn_readlane(my_v, p);
           if (v != cur) {
             flush(false);
             cur = v;
             head = false;
           }
-          const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gw), p & 63));
+          const float w = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_w), p));
 #pragma unroll
           for (int k = 0; k < VEC; ++k) acc[k] = fmaf(w, x[j][k], acc[k]);
         }
@@ -726,28 +799,78 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
   }
 }
 
-// Rows spanning several chunks, and empty rows. One wave per (row, 256-column block).
-__global__ __launch_bounds__(256) void bag_combine_kernel(const int32_t* __restrict__ rowptr, int64_t V, int64_t D,
+// Rows spanning several chunks (the compact list of bag_row_scan). Persistent 1024-thread workgroups; per (row,
+// 256-column block): wave w sums the row's head partials of chunks c0 + 1 + w, c0 + 17 + w, ... (8 independent
+// loads in flight), then wave 0 adds tail(c0) and the 16 wave sums in a fixed order (deterministic whatever the
+// row's length: a univariate measurement's row spans ~300 chunks of a C2 batch). Empty rows stay as zero-filled.
+constexpr int kCombWaves = 16;
+constexpr int kCombBlocks = 256;
+__global__ __launch_bounds__(1024) void bag_combine_kernel(const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ multi, int64_t D,
                                                           const float* __restrict__ part_head,
                                                           const float* __restrict__ part_tail,
                                                           float* __restrict__ dtable) {
-  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  __shared__ float4 s_acc[kCombWaves][64];
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int n_multi = multi[0];
   const int64_t dblocks = (D + 255) / 256;
-  const int64_t v = w / dblocks;
-  if (v >= V) return;
-  const int64_t d0 = (w % dblocks) * 256 + lane_id() * 4;
-  const int64_t s = rowptr[v], e = rowptr[v + 1];
-  float* dst = dtable + v * D;
-  if (s == e) {
-    for (int64_t d = d0; d < min(D, d0 + 4); ++d) dst[d] = 0.f;
-    return;
-  }
-  const int64_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
-  if (c0 == c1) return;  // written by bag_reduce
-  for (int64_t d = d0; d < min(D, d0 + 4); ++d) {
-    float acc = part_tail[c0 * D + d];
-    for (int64_t c = c0 + 1; c <= c1; ++c) acc += part_head[c * D + d];
-    dst[d] = acc;
+  const bool vec = (D % 4 == 0);
+  for (int64_t job = blockIdx.x; job < (int64_t)n_multi * dblocks; job += gridDim.x) {
+    const int64_t v = multi[1 + job / dblocks];
+    const int64_t d0 = (job % dblocks) * 256 + lane * 4;
+    const int64_t s = rowptr[v], e = rowptr[v + 1];
+    const int64_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
+    auto load = [&](const float* p) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (vec) {
+        if (d0 < D) t = *reinterpret_cast<const float4*>(p + d0);
+      } else {
+        if (d0 < D) t.x = p[d0];
+        if (d0 + 1 < D) t.y = p[d0 + 1];
+        if (d0 + 2 < D) t.z = p[d0 + 2];
+        if (d0 + 3 < D) t.w = p[d0 + 3];
+      }
+      return t;
+    };
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int U = 8;
+    for (int64_t cb = c0 + 1 + wave; cb <= c1; cb += (int64_t)kCombWaves * U) {
+      float4 t[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t c = cb + (int64_t)kCombWaves * u;
+        t[u] = c <= c1 ? load(part_head + c * D) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc.x += t[u].x;
+        acc.y += t[u].y;
+        acc.z += t[u].z;
+        acc.w += t[u].w;
+      }
+    }
+    s_acc[wave][lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      float4 r = load(part_tail + c0 * D);
+#pragma unroll
+      for (int w = 0; w < kCombWaves; ++w) {
+        r.x += s_acc[w][lane].x;
+        r.y += s_acc[w][lane].y;
+        r.z += s_acc[w][lane].z;
+        r.w += s_acc[w][lane].w;
+      }
+      float* dst = dtable + v * D;
+      if (vec) {
+        if (d0 < D) *reinterpret_cast<float4*>(dst + d0) = r;
+      } else {
+        if (d0 < D) dst[d0] = r.x;
+        if (d0 + 1 < D) dst[d0 + 1] = r.y;
+        if (d0 + 2 < D) dst[d0 + 2] = r.z;
+        if (d0 + 3 < D) dst[d0 + 3] = r.w;
+      }
+    }
+    __syncthreads();  // s_acc is rewritten by the next job
   }
 }
 
@@ -755,13 +878,15 @@ struct BagWs {
   int32_t* counts;   // [nblk][V]: block counts, then in-place prefixes over blocks
   int32_t* total;    // [V]
   int32_t* rowptr;   // [V + 1]
+  int32_t* multi;    // [1 + V]: count, then the rows spanning several reduce chunks
   int32_t* n_valid;  // [nblk]
   int2* sorted;      // [nblk * kSortCh]
   int4* ent;         // [n_slots]
   float* part_head;  // [n_chunks][D]
   float* part_tail;  // [n_chunks][D]
   float* sub;        // [B][D]
-  int64_t nblk, n_slots, n_chunks;
+  float* sub_part;   // [B][n_sub][D]
+  int64_t nblk, n_slots, n_chunks, n_sub;
   size_t bytes;
 };
 
@@ -782,12 +907,15 @@ static BagWs carve(void* base, const esgpt_batch* bt, int64_t G, int64_t V, int6
   w.counts = (int32_t*)take(sizeof(int32_t) * w.nblk * V);
   w.total = (int32_t*)take(sizeof(int32_t) * V);
   w.rowptr = (int32_t*)take(sizeof(int32_t) * (V + 1));
+  w.multi = (int32_t*)take(sizeof(int32_t) * (V + 1));
   w.n_valid = (int32_t*)take(sizeof(int32_t) * w.nblk);
   w.sorted = (int2*)take(sizeof(int2) * w.nblk * kSortCh);
   w.ent = (int4*)take(sizeof(int4) * w.n_slots);
   w.part_head = (float*)take(sizeof(float) * w.n_chunks * D);
   w.part_tail = (float*)take(sizeof(float) * w.n_chunks * D);
   w.sub = (float*)take(sizeof(float) * bt->B * D);
+  w.n_sub = std::max<int64_t>(1, cdiv(bt->L, kSubEv));
+  w.sub_part = (float*)take(sizeof(float) * bt->B * w.n_sub * D);
   w.bytes = off;
   return w;
 }
@@ -887,12 +1015,20 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   ESGPT_REQUIRE(w.n_slots < (1ll << 31) && batch->B * batch->L * bk.G < (1ll << 31));  // int32 CSR fields
   hipStream_t st = as_stream(stream);
   BagBwdArgs a{*batch, bk, selector, flags, dyn_scale, static_scale, V};
-  if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM)
-    bag_subject_sum_kernel<<<dim3((unsigned)batch->B, (unsigned)cdiv(D, 256)), 256, 0, st>>>(*batch, bk.G, dsrc, ld,
-                                                                                          D, w.sub);
-  bag_block_sort_kernel<<<(unsigned)w.nblk, kSortThreads, 0, st>>>(a, w.n_slots, w.counts, w.sorted, w.n_valid);
-  bag_col_prefix_kernel<<<(unsigned)cdiv(V, 256), 256, 0, st>>>(w.counts, (int)w.nblk, V, w.total);
-  bag_row_scan_kernel<<<1, 1024, 0, st>>>(w.total, V, w.rowptr);
+  if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM && batch->B > 0) {
+    bag_subject_part_kernel<<<dim3((unsigned)batch->B, (unsigned)w.n_sub, (unsigned)cdiv(D, 256)), 256, 0, st>>>(
+        *batch, bk.G, dsrc, ld, D, w.sub_part);
+    bag_subject_sum_kernel<<<dim3((unsigned)batch->B, (unsigned)cdiv(D, 256)), 256, 0, st>>>(w.sub_part, w.n_sub, D,
+                                                                                          w.sub);
+  }
+  if (zero_async(w.counts, sizeof(int32_t) * w.nblk * V, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  if (zero_async(dtable, sizeof(float) * V * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;  // rows without entries
+  int end_bit = 1;
+  while (end_bit < 32 && (V >> end_bit) != 0) ++end_bit;  // keys 0 .. V (the sentinel) fit in end_bit bits
+  bag_block_sort_kernel<<<(unsigned)w.nblk, kSortThreads, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
+                                                                   w.n_valid);
+  bag_col_prefix_kernel<<<(unsigned)cdiv(V, 64), 1024, 0, st>>>(w.counts, (int)w.nblk, V, w.total);
+  bag_row_scan_kernel<<<1, 1024, 0, st>>>(w.total, V, w.rowptr, w.multi, kChunk);
   bag_scatter_kernel<<<dim3(4, (unsigned)w.nblk), 256, 0, st>>>(a, w.sorted, w.n_valid, w.counts, w.rowptr, w.ent);
   // The number of entries is data-dependent (not known on the host without a sync): launch for the upper bound;
   // chunks past rowptr[V] exit immediately.
@@ -903,8 +1039,7 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   else
     bag_reduce_kernel<1><<<g_red, 256, 0, st>>>(w.rowptr, V, w.ent, dsrc, ld, w.sub, D, dtable, w.part_head,
                                                 w.part_tail);
-  bag_combine_kernel<<<(unsigned)cdiv(V * cdiv(D, 256), kWavesPerBlock), 256, 0, st>>>(w.rowptr, V, D, w.part_head,
-                                                                                      w.part_tail, dtable);
+  bag_combine_kernel<<<kCombBlocks, 1024, 0, st>>>(w.rowptr, w.multi, D, w.part_head, w.part_tail, dtable);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -490,6 +490,12 @@ bool shapes_ok(bool akc, bool bkc, const void* A, int64_t lda, const void* B, in
 
 // Tile count of the dX product (what the grouped launch already puts on the chip): the dW split targets the rest.
 int64_t dw_target(bool has_dx, int64_t T, int64_t in) {
+  static int64_t tgt = -1;
+  if (tgt < 0) {
+    const char* e = getenv("ESGPT_GEMM_DW_TARGET");  // tuning hook: fixed dW item target (0 = the default rule)
+    tgt = e ? std::max(0, atoi(e)) : 0;
+  }
+  if (tgt > 0) return tgt;
   return has_dx ? std::max<int64_t>(64, kTarget - cdiv(T, TILE) * cdiv(in, TILE)) : kTarget;
 }
 

@@ -477,18 +477,18 @@ Tensor linear(const Tensor& x_, const Tensor& w, const optional<Tensor>& bias, a
   return y;
 }
 
-// InnerMLP up to c_proj's bias (transformer.py:378-391): pre = x·W_fcᵀ + b_fc, g = act(pre), y = g·W_projᵀ.
+// InnerMLP (transformer.py:378-391): pre = x·W_fcᵀ + b_fc, g = act(pre), y = g·W_projᵀ (+ b_proj when given).
 // Returns (y, pre, g); pre and g are kept for the backward.
 std::tuple<Tensor, Tensor, Tensor> mlp(const Tensor& x_, const Tensor& w_fc, const Tensor& w_pj, const Tensor& b_fc,
-                                       int64_t act, const Tensor& p_fc, const Tensor& p_pj, const Tensor& tickets) {
+                                       const optional<Tensor>& b_pj, int64_t act, const Tensor& p_fc,
+                                       const Tensor& p_pj, const Tensor& tickets) {
   const c10::DeviceGuard guard(x_.device());
   Tensor x = x_.contiguous();
   auto pg = linear_act(x, w_fc, b_fc, act);
   Tensor g = std::get<1>(pg);
   const int64_t T = g.size(0), F = g.size(1), D = w_pj.size(0);
   Tensor y = at::empty({T, D}, x.options());
-  gemm_into(ESGPT_GEMM_K_CONTIG, g, F, ESGPT_GEMM_K_CONTIG, w_pj, F, T, D, F, c10::nullopt, c10::nullopt, y, false,
-            tickets);
+  gemm_into(ESGPT_GEMM_K_CONTIG, g, F, ESGPT_GEMM_K_CONTIG, w_pj, F, T, D, F, b_pj, c10::nullopt, y, false, tickets);
   return {y, std::get<0>(pg), g};
 }
 
@@ -558,8 +558,8 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
         "Tensor tickets) -> (Tensor, Tensor, Tensor)");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
-  m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, int act, Tensor p_fc, Tensor p_pj, Tensor tickets) "
-        "-> (Tensor, Tensor, Tensor)");
+  m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, Tensor? b_pj, int act, Tensor p_fc, Tensor p_pj, "
+        "Tensor tickets) -> (Tensor, Tensor, Tensor)");
   m.def("head_loss(Tensor xc, Tensor? xt, " BATCH_SCHEMA ", int[] terms, int[] tte_i, float[] tte_f, int shift, "
         "int n_levels, Tensor wc, Tensor bc, Tensor? wt, Tensor? bt, Tensor[] cw, Tensor[] cb, Tensor[] tw, "
         "Tensor[] tb, Tensor err, Tensor tickets) -> (Tensor, Tensor, Tensor, Tensor)");

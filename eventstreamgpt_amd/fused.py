@@ -3,10 +3,10 @@ plain (bias-free) GEMMs, with one flat low-precision weight shadow per forward.
 
 Per layer (``InnerBlock``, ``transformer.py:394-461``; encoder loop ``:775-831``):
 
-    qkv = ln @ [Wq;Wk;Wv]ᵀ ; o = attention(qkv) ; y = o @ Woᵀ
-    h1, ln2 = ResidualLN(h, y + b_o, dropout, LN2)                         # attn residual
-    g = act(ln2 @ Wfcᵀ + b_fc) ; y2 = g @ Wprojᵀ
-    h, ln = ResidualLN(h1, y2 + b_proj, dropout, event_mask, LN1 of next layer or ln_f)
+    qkv = ln @ [Wq;Wk;Wv]ᵀ ; o = attention(qkv) ; y = o @ Woᵀ + b_o
+    h1, ln2 = ResidualLN(h, y, dropout, LN2)                               # attn residual
+    g = act(ln2 @ Wfcᵀ + b_fc) ; y2 = g @ Wprojᵀ + b_proj
+    h, ln = ResidualLN(h1, y2, dropout, event_mask, LN1 of next layer or ln_f)
 
 i.e. 4 GEMMs + attention + 3 fused elementwise kernels per layer, instead of ~20 ATen launches. Parameters are
 the modules' own (state_dict unchanged); numerics follow the reference (f32 residual stream and LayerNorm
@@ -160,15 +160,15 @@ def proj(x, w_lp, bias, params):
     return F.linear(x, w.to(dt), None if bias is None else bias.to(dt))
 
 
-def mlp_op(x, w_fc, w_pj, b_fc, act: int, p_fc, p_pj):
-    """``esgpt::mlp``: InnerMLP (transformer.py:378-391) up to c_proj's bias: y = act(x · W_fcᵀ + b_fc) · W_projᵀ in
-    two GEMM launches (c_fc's bias + activation in its epilogue; the bf16 pre-activation is kept) and two grouped
-    backward launches (c_proj: d(pre) = (dy · W_proj) · act'(pre) in the dX epilogue, + dW_proj; c_fc: dx + dW_fc +
-    db_fc as a row sum inside its dW product). c_proj's bias and the residual dropout belong to the following
-    residual_ln. ``w_fc`` / ``w_pj`` are the bf16 shadows; the f32 parameters ``p_fc`` / ``p_pj`` receive the
-    gradients."""
+def mlp_op(x, w_fc, w_pj, b_fc, act: int, p_fc, p_pj, b_pj=None):
+    """``esgpt::mlp``: InnerMLP (transformer.py:378-391): y = act(x · W_fcᵀ + b_fc) · W_projᵀ (+ b_proj) in two
+    GEMM launches (c_fc's bias + activation in its epilogue, the bf16 pre-activation kept; c_proj's bias in its
+    epilogue) and two grouped backward launches (c_proj: d(pre) = (dy · W_proj) · act'(pre) in the dX epilogue, +
+    dW_proj + db_proj; c_fc: dx + dW_fc + db_fc, the bias gradients as row sums inside the dW products). The residual
+    dropout belongs to the following residual_ln. ``w_fc`` / ``w_pj`` are the bf16 shadows; the f32 parameters
+    ``p_fc`` / ``p_pj`` receive the gradients."""
     with _timed("gemm"):
-        y, _pre, _g = _ops().mlp(x, w_fc, w_pj, b_fc, int(act), p_fc, p_pj, tickets(x.device))
+        y, _pre, _g = _ops().mlp(x, w_fc, w_pj, b_fc, b_pj, int(act), p_fc, p_pj, tickets(x.device))
     return y
 
 
@@ -178,14 +178,16 @@ class MLPFn:
     apply = staticmethod(mlp_op)
 
 
-def mlp(x, w_fc, w_pj, fc, pj, act: int):
-    """InnerMLP without c_proj's bias: ``MLPFn`` when the bf16 GEMM shapes allow it, else proj + BiasActFn + proj."""
+def mlp(x, w_fc, w_pj, fc, pj, act: int, with_bias: bool = False):
+    """InnerMLP (c_proj's bias included only with ``with_bias``): ``mlp_op`` when the bf16 GEMM shapes allow it,
+    else proj + bias_act + proj."""
     if (w_fc is not None and w_fc.dtype == torch.bfloat16
             and gemm_supported(x.shape[0], x.shape[1], w_fc.shape[0])):
-        return mlp_op(x.to(torch.bfloat16).contiguous(), w_fc, w_pj, fc.bias, act, fc.weight, pj.weight)
+        return mlp_op(x.to(torch.bfloat16).contiguous(), w_fc, w_pj, fc.bias, act, fc.weight, pj.weight,
+                      pj.bias if with_bias else None)
     f = proj(x, w_fc, None, (fc.weight,))
     g = bias_act(f, fc.bias, act)
-    return proj(g, w_pj, None, (pj.weight,))
+    return proj(g, w_pj, pj.bias if with_bias else None, (pj.weight,))
 
 
 @torch.no_grad()
@@ -308,12 +310,13 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
             qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight)).view(B, Lq, 3 * D)
             window = att.window_size if att.attention_type == "local" else 0
             o = attention(qkv, em, em, att.num_heads, window, False, p_att)
-            y = proj(o.view(N, D), wo, None, (att.out_proj.weight,))
-            h1, ln2 = residual_ln(h, y, att.out_proj.bias, blk.layer_norm.weight, blk.layer_norm.bias, None,
-                                  p_res, eps, dt)
-            y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, act)
+            # the projections' biases in the GEMM epilogues (as the reference's bf16 nn.Linear), their gradients as
+            # row sums inside the backward dW products
+            y = proj(o.view(N, D), wo, att.out_proj.bias, (att.out_proj.weight,))
+            h1, ln2 = residual_ln(h, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt)
+            y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, act, with_bias=True)
             nxt = blocks[i + 1].attn.layer_norm if i + 1 < len(blocks) else encoder.ln_f
-            h, ln = residual_ln(h1, y2, blk.mlp.c_proj.bias, nxt.weight, nxt.bias, rows, p_res, eps, dt)
+            h, ln = residual_ln(h1, y2, None, nxt.weight, nxt.bias, rows, p_res, eps, dt)
     return ln.view(B, Lq, D)
 
 
@@ -354,10 +357,9 @@ def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_fir
         qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight)).view(Bs, T, 3 * D)
         o = attention(qkv, kpm, qpm, att.num_heads, window, static_kv_first, p_att)
         Tq = T - skf
-        y = proj(o.reshape(Bs * Tq, D), wo, None, (att.out_proj.weight,))
+        y = proj(o.reshape(Bs * Tq, D), wo, att.out_proj.bias, (att.out_proj.weight,))
         res = hidden[:, skf:, :].reshape(Bs * Tq, D).float().contiguous()
-        h1, ln2 = residual_ln(res, y, att.out_proj.bias, blk.layer_norm.weight, blk.layer_norm.bias, None,
-                              p_res, eps, dt)
-        y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name])
-        out = h1 + F.dropout(y2.float() + blk.mlp.c_proj.bias, p=p_res, training=train)
+        h1, ln2 = residual_ln(res, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt)
+        y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name], with_bias=True)
+        out = h1 + F.dropout(y2.float(), p=p_res, training=train)
     return out.view(Bs, Tq, D)

@@ -196,7 +196,7 @@ def _register():
         return x.new_empty(x.shape[0], w.shape[0])
 
     @fake(lib + "mlp")
-    def _(x, w_fc, w_pj, b_fc, act, p_fc, p_pj, tickets):
+    def _(x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets):
         T = x.shape[0]
         return x.new_empty(T, w_pj.shape[0]), x.new_empty(T, w_fc.shape[0]), x.new_empty(T, w_fc.shape[0])
 
@@ -334,20 +334,23 @@ def _register():
 
     reg(lib + "linear", _li_bwd, setup_context=_li_setup)
 
-    # mlp: d x, d b_fc, d W_fc, d W_proj (activation gradient in c_proj's dX epilogue)
+    # mlp: d x, d b_fc, d b_proj, d W_fc, d W_proj (activation gradient in c_proj's dX epilogue, the bias gradients
+    # as row sums inside the dW products)
     def _ml_setup(ctx, inputs, output):
-        x, w_fc, w_pj, b_fc, act, p_fc, p_pj, tickets = inputs
+        x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets = inputs
         y, pre, g = output
         ctx.mark_non_differentiable(pre, g)
         ctx.save_for_backward(x, w_fc, w_pj, pre, g)
         ctx.act = act
+        ctx.has_bpj = b_pj is not None
 
     def _ml_bwd(ctx, dy, _dpre, _dg):
         x, w_fc, w_pj, pre, g = ctx.saved_tensors
-        dz, dw_pj, _ = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, False)
+        need_dbpj = ctx.has_bpj and ctx.needs_input_grad[4]
+        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj)
         need_dx = ctx.needs_input_grad[0]
         dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True)
-        return (dx if need_dx else None, None, None, db_fc, None, dw_fc, dw_pj, None)
+        return (dx if need_dx else None, None, None, db_fc, db_pj if need_dbpj else None, None, dw_fc, dw_pj, None)
 
     reg(lib + "mlp", _ml_bwd, setup_context=_ml_setup)
 

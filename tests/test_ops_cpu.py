@@ -104,10 +104,12 @@ def test_linear_and_mlp_autograd_route_f32_master_gradients(esgpt):
     pf, pp = torch.empty(24, 8, device=M, requires_grad=True), torch.empty(8, 24, device=M, requires_grad=True)
     bf = torch.empty(24, device=M, requires_grad=True)
     x3 = torch.empty(16, 8, dtype=torch.bfloat16, device=M, requires_grad=True)
-    y3, pre, g = esgpt.mlp(x3, pf.bfloat16(), pp.bfloat16(), bf, 0, pf, pp, _tk())
+    bp = torch.empty(8, device=M, requires_grad=True)
+    y3, pre, g = esgpt.mlp(x3, pf.bfloat16(), pp.bfloat16(), bf, bp, 0, pf, pp, _tk())
     assert y3.shape == (16, 8) and pre.shape == g.shape == (16, 24)
     y3.float().sum().backward()
     assert pf.grad.shape == pf.shape and pp.grad.shape == pp.shape and bf.grad.shape == (24,) and x3.grad is not None
+    assert bp.grad.shape == (8,)
 
 
 def test_head_loss_and_output_loss_autograd(esgpt):
