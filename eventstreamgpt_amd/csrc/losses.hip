@@ -48,35 +48,53 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void count_kernel(esgpt_batch bt, Terms terms, int32_t* __restrict__ counts,
-                                                    int32_t* __restrict__ err) {
+// Pass 1: one 1024-thread block per subject. The subject's L·M entries are read once, coalesced (thread = entry),
+// and each entry ORs the bit of every non-MULTI term it satisfies into its event's LDS word (SINGLE: measurement
+// present; MVREG / UVREG: measurement with a value); then thread = event: term t counts the event when it is an
+// event and (MULTI or bit t set); TTE counts events followed by an event. Integer LDS adds: exact, order-free.
+// Dynamic LDS: L words.
+__global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms, int32_t* __restrict__ counts,
+                                                     int32_t* __restrict__ err) {
+  extern __shared__ uint32_t s_bits[];
   __shared__ int32_t s_cnt[ESGPT_MAX_TERMS + 1];
   const int64_t b = blockIdx.x;
   const int T = terms.n;
+  const int64_t L = bt.L, M = bt.M;
   if (threadIdx.x <= T) s_cnt[threadIdx.x] = 0;
+  for (int64_t l = threadIdx.x; l < L; l += blockDim.x) s_bits[l] = 0u;
   __syncthreads();
-  for (int64_t l = threadIdx.x; l < bt.L; l += blockDim.x) {
-    const int64_t e = b * bt.L + l;
-    const bool ev = bt.event_mask[e] != 0;
-    if (ev) {
-      const int64_t* ip = bt.dyn_meas + e * bt.M;
-      const uint8_t* vp = bt.dyn_vmask + e * bt.M;
-      for (int t = 0; t < T; ++t) {
-        const esgpt_loss_term& tm = terms.t[t];
-        bool mk = false;
-        if (tm.kind == ESGPT_TERM_MULTI) mk = true;
-        else {
-          for (int64_t m = 0; m < bt.M; ++m) {
-            if (ip[m] == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vp[m])) {
-              mk = true;
-              break;
-            }
-          }
-        }
-        if (mk) atomicAdd(&s_cnt[t], 1);
-      }
+  const int64_t* meas = bt.dyn_meas + b * L * M;
+  const uint8_t* vmask = bt.dyn_vmask + b * L * M;
+  const int LM = (int)(L * M), Mi = (int)M;  // 32-bit index math (L * M < 2^31, checked on the host)
+  for (int i = threadIdx.x; i < LM; i += blockDim.x) {
+    const int64_t mi = meas[i];
+    const bool vm = vmask[i] != 0;
+    uint32_t bits = 0u;
+    for (int t = 0; t < T; ++t) {
+      const esgpt_loss_term& tm = terms.t[t];
+      if (tm.kind != ESGPT_TERM_MULTI && mi == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vm)) bits |= 1u << t;
     }
-    if (l + 1 < bt.L && ev && bt.event_mask[e + 1]) atomicAdd(&s_cnt[T], 1);
+    if (bits) atomicOr(&s_bits[i / Mi], bits);
+  }
+  __syncthreads();
+  int32_t c[ESGPT_MAX_TERMS + 1];
+#pragma unroll
+  for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) c[t] = 0;
+  const uint8_t* em = bt.event_mask + b * L;
+  for (int64_t l = threadIdx.x; l < L; l += blockDim.x) {
+    const bool ev = em[l] != 0;
+    const uint32_t bits = s_bits[l];
+#pragma unroll
+    for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
+      if (t < T && ev && (terms.t[t].kind == ESGPT_TERM_MULTI || ((bits >> t) & 1u))) ++c[t];
+    if (l + 1 < L && ev && em[l + 1]) ++c[ESGPT_MAX_TERMS];
+  }
+  // wave sums (integer: exact) -> one LDS add per wave and term
+#pragma unroll
+  for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) {
+    const int v = (int)wave_sum((float)c[t]);  // < 2^24 events per subject: exact in f32
+    const int slot = t < ESGPT_MAX_TERMS ? t : T;
+    if ((t < T || t == ESGPT_MAX_TERMS) && lane_id() == 0 && v) atomicAdd(&s_cnt[slot], v);
   }
   __syncthreads();
   if (threadIdx.x <= T) counts[b * (ESGPT_MAX_TERMS + 1) + threadIdx.x] = s_cnt[threadIdx.x];
@@ -84,6 +102,238 @@ __global__ __launch_bounds__(256) void count_kernel(esgpt_batch bt, Terms terms,
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Per-term math shared by both event kernels. `z(col)` reads a logit of the term's row (f32), `put(col, g)` adds
+// g to that column's gradient. Every lane of the wave calls these (wave-uniform control flow); returns the
+// wave-uniform per-event loss ell of the term. Entry registers: lane m < M holds entry m (e_idx, e_val, e_vm,
+// match = entry belongs to the term's measurement); mm / mv = ballots of match / match && value-present.
+template <typename ZF, typename GF>
+__device__ __forceinline__ float content_term(const esgpt_loss_term& tm, int lane, int64_t M, bool match,
+                                              uint64_t mm, uint64_t mv, int64_t e_idx, float e_val, bool e_vm,
+                                              bool mk, float scale, int32_t* err, ZF z, GF put) {
+  float ell = 0.f;
+  if (tm.kind == ESGPT_TERM_SINGLE) {
+    const int n = tm.vocab_end - tm.vocab_start;
+    int64_t lab = 0;
+    const bool has = mm != 0;
+    for (uint64_t bits = mm; bits; bits &= bits - 1) lab += readlane64(e_idx, __builtin_ctzll(bits));
+    lab = has ? lab - tm.vocab_start : 0;
+    if (mk && (lab < 0 || lab >= n)) {
+      set_err(err, ESGPT_FLAG_BAD_LABEL);
+      lab = 0;
+    }
+    float mx = -INFINITY;
+    for (int j = lane; j < n; j += 64) mx = fmaxf(mx, z(tm.col + j));
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int j = lane; j < n; j += 64) se += expf(z(tm.col + j) - mx);
+    se = wave_sum(se);
+    const float lse = mx + logf(se);
+    const float xl = z(tm.col + lab);
+    const float zo = z(tm.obs_col);
+    ell = (lse - xl) + bce_logits(zo, has ? 1.f : 0.f);
+    if (scale != 0.f) {
+      const float inv = 1.f / se;
+      for (int j = lane; j < n; j += 64) {
+        const float pj = expf(z(tm.col + j) - mx) * inv;
+        put(tm.col + j, scale * (pj - (j == lab ? 1.f : 0.f)));
+      }
+      if (lane == 0) put(tm.obs_col, scale * (sigmoidf_(zo) - (has ? 1.f : 0.f)));
+    }
+  } else if (tm.kind == ESGPT_TERM_MULTI) {
+    const int n = tm.vocab_end - tm.vocab_start;
+    // lane m < M holds entry m's label within this term (-1: another measurement); labels are broadcast
+    // with readlane (wave-uniform m) instead of re-reading the staged entries per column
+    const int my_lab = match ? (int)(e_idx - tm.vocab_start) : -1;
+    float acc = 0.f;
+    // passes of kPass column groups: the pass's logits are read before any gradient is written
+    constexpr int kPass = 16;
+    for (int j1 = 0; j1 < n; j1 += 64 * kPass) {
+      float xs[kPass];
+#pragma unroll
+      for (int it = 0; it < kPass; ++it) {
+        const int j = j1 + 64 * it + lane;
+        xs[it] = j < n ? z(tm.col + j) : 0.f;
+      }
+      // multi-hot labels of this pass group: each of the M entries marks the (column group, lane) holding its
+      // label — M readlanes per group of 64·kPass columns instead of M per column
+      uint32_t ymask = 0;
+      for (int m = 0; m < M; ++m) {
+        const int rel = __builtin_amdgcn_readlane(my_lab, m) - j1;  // my_lab = -1: not this term's entry
+        if (rel >= 0 && rel < 64 * kPass && (rel & 63) == lane) ymask |= 1u << (rel >> 6);
+      }
+#pragma unroll
+      for (int it = 0; it < kPass; ++it) {
+        const int j = j1 + 64 * it + lane;
+        if (j1 + 64 * it >= n) break;  // wave-uniform
+        const bool y = (ymask >> it) & 1u;
+        if (j < n) {
+          // BCE-with-logits and its gradient from ONE exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32):
+          // e = exp(-|x|), loss = max(x, 0) - x·y + log(1 + e), sigmoid(x) = x >= 0 ? 1/(1+e) : e/(1+e)
+          const float x = xs[it], yf = y ? 1.f : 0.f;
+          const float e = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
+          const float ope = 1.f + e;
+          acc += fmaxf(x, 0.f) - x * yf + __builtin_amdgcn_logf(ope) * 0.6931471805599453f;
+          if (scale != 0.f) {
+            const float inv = __builtin_amdgcn_rcpf(ope);
+            put(tm.col + j, scale / (float)n * ((x >= 0.f ? inv : e * inv) - yf));
+          }
+        }
+      }
+    }
+    ell = wave_sum(acc) / (float)n;
+  } else if (tm.kind == ESGPT_TERM_MVREG) {
+    // lanes 0..M-1: one entry each; duplicates of a target index accumulate into one gradient pair.
+    const int n_targets = tm.vocab_end - tm.vocab_start;
+    const bool sel = match && e_vm;
+    int64_t j = 0;
+    float nll = 0.f, gmu = 0.f, grho = 0.f;
+    if (sel) {
+      j = e_idx - tm.vocab_start;
+      if (j < 0 || j >= n_targets) {
+        set_err(err, ESGPT_FLAG_BAD_LABEL);
+        j = 0;
+      }
+      const float mu = z(tm.col + 2 * j);
+      const float rho = z(tm.col + 2 * j + 1);
+      const float sd = elu1(rho);
+      const float x = e_val;
+      const float zz = (x - mu) / sd;
+      nll = 0.5f * zz * zz + logf(sd) + kHalfLog2Pi;
+      gmu = -(x - mu) / (sd * sd);
+      grho = (1.f / sd - (x - mu) * (x - mu) / (sd * sd * sd)) * delu(rho);
+    }
+    const float nsel = (float)__popcll(mv);
+    ell = nsel > 0.f ? wave_sum(nll) / nsel : 0.f;
+    if (scale != 0.f && nsel > 0.f) {
+      const float s2 = scale / nsel;
+      // combine duplicate targets: the first lane of each target sums its group, then writes once
+      float sm = 0.f, sr = 0.f;
+      bool first = sel;
+      for (uint64_t bits = mv; bits; bits &= bits - 1) {  // the selected entries, in lane order
+        const int m = __builtin_ctzll(bits);
+        const int64_t jm = readlane64(j, m);
+        const float gm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gmu), m));
+        const float gr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(grho), m));
+        if (sel && jm == j) {
+          sm += gm;
+          sr += gr;
+          if (m < lane) first = false;
+        }
+      }
+      if (first) {
+        put(tm.col + 2 * j, s2 * sm);
+        put(tm.col + 2 * j + 1, s2 * sr);
+      }
+    }
+  } else if (tm.kind == ESGPT_TERM_UVREG) {
+    const bool has_meas = mm != 0, has_val = mv != 0;
+    float x = 0.f;
+    for (uint64_t bits = mv; bits; bits &= bits - 1)
+      x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e_val), __builtin_ctzll(bits)));
+    if (!has_val) x = 0.f;
+    const float mu = z(tm.col);
+    const float rho = z(tm.col + 1);
+    const float sd = elu1(rho);
+    const float zz = (x - mu) / sd;
+    const float zo = z(tm.obs_col);
+    ell = 0.5f * zz * zz + logf(sd) + kHalfLog2Pi + bce_logits(zo, has_meas ? 1.f : 0.f);
+    if (scale != 0.f && lane == 0) {
+      put(tm.col, scale * (-(x - mu) / (sd * sd)));
+      put(tm.col + 1, scale * (1.f / sd - (x - mu) * (x - mu) / (sd * sd * sd)) * delu(rho));
+      put(tm.obs_col, scale * (sigmoidf_(zo) - (has_meas ? 1.f : 0.f)));
+    }
+  }
+  return ell;
+}
+
+// Time-to-event log-likelihood of one observed delta x; z(k) / put(k, g) address the TTE columns relative to
+// tte.col. `scale` = d(-LL)/d ll for this event (0: no gradient). Returns ll (wave-uniform).
+template <typename ZF, typename GF>
+__device__ __forceinline__ float tte_term(const esgpt_tte_spec& tte, int lane, float x, float scale, ZF z, GF put) {
+  float ll = 0.f;
+  if (tte.kind == ESGPT_TTE_EXP) {
+    const float zz = z(0);
+    const float rate = elu1(zz);
+    ll = logf(rate) - rate * x;
+    if (lane == 0 && scale != 0.f) put(0, scale * (1.f / rate - x) * delu(zz));
+  } else {
+    // LogNormalMixture (third-party pytorch_lognormal_mixture, restated): lanes = components.
+    const int K = tte.K;
+    const bool affine = !(tte.mean_log == 0.f && tte.std_log == 1.f);
+    const float lx = logf(x);
+    const float y = affine ? (lx - tte.mean_log) / tte.std_log : lx;
+    float loc = 0.f, ls = 0.f, lw = -INFINITY, a = -INFINITY;
+    if (lane < K) {
+      loc = z(3 * lane);
+      ls = z(3 * lane + 1);
+      lw = z(3 * lane + 2);
+    }
+    const float wmax = wave_max(lw);
+    const float wse = wave_sum(lane < K ? expf(lw - wmax) : 0.f);
+    const float lsm = lw - (wmax + logf(wse));  // log_softmax(weights)
+    if (lane < K) {
+      const float sd = expf(ls);
+      const float zz = (y - loc) / sd;
+      a = lsm - 0.5f * zz * zz - ls - kHalfLog2Pi;
+    }
+    const float amax = wave_max(a);
+    const float ase = wave_sum(lane < K ? expf(a - amax) : 0.f);
+    ll = amax + logf(ase) - lx - (affine ? logf(fabsf(tte.std_log)) : 0.f);
+    if (scale != 0.f && lane < K) {
+      const float resp = expf(a - amax) / ase;  // posterior responsibility
+      const float pi = expf(lsm);
+      const float sd = expf(ls);
+      const float dz = (y - loc) / sd;
+      put(3 * lane, scale * resp * dz / sd);
+      put(3 * lane + 1, scale * resp * (dz * dz - 1.f));
+      put(3 * lane + 2, scale * (resp - pi));
+    }
+  }
+  return ll;
+}
+
+// Subjects-with-events per term (the outer safe_weighted_avg of weighted_loss) into s_nsub_inv; TTE averages over
+// all B. Called by wave 0: lane = subject, one ballot per term (all terms' count loads in flight together).
+__device__ __forceinline__ void subjects_with_events(const int32_t* __restrict__ counts, int64_t B, int NT, int lane,
+                                                     float* s_nsub_inv) {
+  int nsub[ESGPT_MAX_TERMS];
+#pragma unroll
+  for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] = 0;
+  for (int64_t b0 = 0; b0 < B; b0 += 64) {
+    const int64_t b = b0 + lane;
+    int c[ESGPT_MAX_TERMS];
+#pragma unroll
+    for (int t = 0; t < ESGPT_MAX_TERMS; ++t) c[t] = (t < NT && b < B) ? counts[b * (ESGPT_MAX_TERMS + 1) + t] : 0;
+#pragma unroll
+    for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] += __popcll(__ballot(c[t] > 0));
+  }
+#pragma unroll
+  for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
+    if (lane == t && t < NT) s_nsub_inv[t] = nsub[t] > 0 ? 1.f / (float)nsub[t] : 0.f;
+  if (lane == 0) s_nsub_inv[NT] = B > 0 ? 1.f / (float)B : 0.f;
+}
+
+// The wave's logit-row coordinates: w -> subject b, unshifted row r (-1: the bias row in shift mode) and content
+// target position p = r + shift.
+struct RowPos {
+  bool active, has_content, ev;
+  int64_t b, r, p;
+};
+__device__ __forceinline__ RowPos row_pos(const esgpt_batch& bt, int64_t w, int64_t n_rows, int shift) {
+  RowPos q;
+  q.active = w < n_rows;
+  const int64_t per_b = bt.L + shift;
+  q.b = q.active ? w / per_b : 0;
+  q.r = q.active ? (w % per_b) - shift : 0;
+  q.p = q.r + shift;
+  q.has_content = q.active && q.p < bt.L;
+  q.ev = q.has_content && bt.event_mask[q.b * bt.L + q.p] != 0;
+  return q;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Generic event kernel (any row width): one wave per (subject, logit row), logits read from and gradients written
+// to global memory column by column (the gradient buffers are zero-filled first).
 template <typename T, bool RMW>
 __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms, esgpt_tte_spec tte,
                                                     const T* __restrict__ zc, int64_t ldc, int64_t n_levels, int shift,
@@ -93,46 +343,21 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
                                                     float* __restrict__ contrib, int64_t n_rows,
                                                     int32_t* __restrict__ err) {
   __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: row math in SALU
   const int lane = lane_id();
   const int NT = terms.n;
-  const int64_t B = bt.B, L = bt.L, M = bt.M;
-
-  // subjects-with-events per term (the outer safe_weighted_avg of weighted_loss); TTE averages over all B.
-  // Wave 0: lane = subject, one ballot per term (all terms' count loads in flight together).
-  if (wave == 0) {
-    int nsub[ESGPT_MAX_TERMS];
-#pragma unroll
-    for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] = 0;
-    for (int64_t b0 = 0; b0 < B; b0 += 64) {
-      const int64_t b = b0 + lane;
-      int c[ESGPT_MAX_TERMS];
-#pragma unroll
-      for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
-        c[t] = (t < NT && b < B) ? counts[b * (ESGPT_MAX_TERMS + 1) + t] : 0;
-#pragma unroll
-      for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] += __popcll(__ballot(c[t] > 0));
-    }
-#pragma unroll
-    for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
-      if (lane == t && t < NT) s_nsub_inv[t] = nsub[t] > 0 ? 1.f / (float)nsub[t] : 0.f;
-    if (lane == 0) s_nsub_inv[NT] = B > 0 ? 1.f / (float)B : 0.f;
-  }
+  const int64_t L = bt.L, M = bt.M;
+  if (wave == 0) subjects_with_events(counts, bt.B, NT, lane, s_nsub_inv);
 
   const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
-  const bool active = w < n_rows;
-  const int64_t per_b = L + shift;
-  const int64_t b = active ? w / per_b : 0;
-  const int64_t r = active ? (w % per_b) - shift : 0;  // logit row within subject (-1: the bias row)
-  const int64_t p = r + shift;                          // content target position
-  const bool has_content = active && p < L;
-  const bool ev = has_content && bt.event_mask[b * L + p] != 0;
+  const RowPos q = row_pos(bt, w, n_rows, shift);
+  const int64_t b = q.b, r = q.r, p = q.p;
 
   // the event's M entries in registers, lane m = entry m (per-term scans are ballots / readlanes, not LDS loops)
   int64_t e_idx = 0, e_meas = INT64_MIN;
   float e_val = 0.f;
   bool e_vm = false;
-  if (has_content && lane < M) {
+  if (q.has_content && lane < M) {
     const int64_t off = (b * L + p) * M + lane;
     e_idx = bt.dyn_idx[off];
     e_meas = bt.dyn_meas[off];
@@ -149,7 +374,7 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
   for (int t = 0; t < NT; ++t) {
     const esgpt_loss_term& tm = terms.t[t];
     float c_out = 0.f;
-    if (has_content) {
+    if (q.has_content) {
       const T* zrow;
       T* gT = nullptr;
       float* gF = nullptr;
@@ -166,166 +391,31 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
         zrow = zc + row * ldc;
         gT = dzc + row * ldc;
       }
-      const bool match = e_meas == tm.meas_idx;             // this lane's entry belongs to the term
+      const bool match = e_meas == tm.meas_idx;  // this lane's entry belongs to the term
       const uint64_t mm = __ballot(match), mv = __ballot(match && e_vm);
-      const bool mk = ev && (tm.kind == ESGPT_TERM_MULTI ||
-                             (tm.kind == ESGPT_TERM_SINGLE ? mm != 0 : mv != 0));  // term_mask, restated
+      const bool mk = q.ev && (tm.kind == ESGPT_TERM_MULTI ||
+                               (tm.kind == ESGPT_TERM_SINGLE ? mm != 0 : mv != 0));  // term_mask, restated
       const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
       const float scale = (mk && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
       // Gradient columns: with disjoint term columns (checked on the host) every column of a row has exactly one
       // writer, so the zero-filled buffer is stored to without a read; otherwise read-modify-write. The bias row
       // (shift mode) is this wave's own f32 row.
-      auto put = [&](int64_t col, float g) {
-        if (gF) gF[col] += g;
-        else if (RMW) gT[col] = from_f32<T>(to_f32(gT[col]) + g);
-        else gT[col] = from_f32<T>(g);
-      };
-      float ell = 0.f;
-      if (tm.kind == ESGPT_TERM_SINGLE) {
-        const int n = tm.vocab_end - tm.vocab_start;
-        int64_t lab = 0;
-        const bool has = mm != 0;
-        for (uint64_t bits = mm; bits; bits &= bits - 1) lab += readlane64(e_idx, __builtin_ctzll(bits));
-        lab = has ? lab - tm.vocab_start : 0;
-        if (mk && (lab < 0 || lab >= n)) {
-          set_err(err, ESGPT_FLAG_BAD_LABEL);
-          lab = 0;
-        }
-        float mx = -INFINITY;
-        for (int j = lane; j < n; j += 64) mx = fmaxf(mx, to_f32(zrow[tm.col + j]));
-        mx = wave_max(mx);
-        float se = 0.f;
-        for (int j = lane; j < n; j += 64) se += expf(to_f32(zrow[tm.col + j]) - mx);
-        se = wave_sum(se);
-        const float lse = mx + logf(se);
-        const float xl = to_f32(zrow[tm.col + lab]);
-        const float zo = to_f32(zrow[tm.obs_col]);
-        ell = (lse - xl) + bce_logits(zo, has ? 1.f : 0.f);
-        if (scale != 0.f) {
-          const float inv = 1.f / se;
-          for (int j = lane; j < n; j += 64) {
-            const float pj = expf(to_f32(zrow[tm.col + j]) - mx) * inv;
-            put(tm.col + j, scale * (pj - (j == lab ? 1.f : 0.f)));
-          }
-          if (lane == 0) put(tm.obs_col, scale * (sigmoidf_(zo) - (has ? 1.f : 0.f)));
-        }
-      } else if (tm.kind == ESGPT_TERM_MULTI) {
-        const int n = tm.vocab_end - tm.vocab_start;
-        // lane m < M holds entry m's label within this term (-1: another measurement); labels are broadcast
-        // with readlane (wave-uniform m) instead of re-reading the staged entries per column
-        const int my_lab = match ? (int)(e_idx - tm.vocab_start) : -1;
-        float acc = 0.f;
-        // passes of kPass column groups: the pass's logits are loaded before any gradient is stored, so the
-        // loads overlap instead of each waiting behind the previous group's store
-        constexpr int kPass = 16;
-        for (int j1 = 0; j1 < n; j1 += 64 * kPass) {
-          float xs[kPass];
-#pragma unroll
-          for (int it = 0; it < kPass; ++it) {
-            const int j = j1 + 64 * it + lane;
-            xs[it] = j < n ? to_f32(zrow[tm.col + j]) : 0.f;
-          }
-          // multi-hot labels of this pass group: each of the M entries marks the (column group, lane) holding its
-          // label — M readlanes per group of 64·kPass columns instead of M per column
-          uint32_t ymask = 0;
-          for (int m = 0; m < M; ++m) {
-            const int rel = __builtin_amdgcn_readlane(my_lab, m) - j1;  // my_lab = -1: not this term's entry
-            if (rel >= 0 && rel < 64 * kPass && (rel & 63) == lane) ymask |= 1u << (rel >> 6);
-          }
-#pragma unroll
-          for (int it = 0; it < kPass; ++it) {
-            const int j = j1 + 64 * it + lane;
-            if (j1 + 64 * it >= n) break;  // wave-uniform
-            const bool y = (ymask >> it) & 1u;
-            if (j < n) {
-              // BCE-with-logits and its gradient from ONE exp2 / log2 / rcp (v_exp_f32, v_log_f32, v_rcp_f32):
-              // e = exp(-|x|), loss = max(x, 0) - x·y + log(1 + e), sigmoid(x) = x >= 0 ? 1/(1+e) : e/(1+e)
-              const float x = xs[it], yf = y ? 1.f : 0.f;
-              const float e = __builtin_amdgcn_exp2f(-fabsf(x) * 1.4426950408889634f);
-              const float ope = 1.f + e;
-              acc += fmaxf(x, 0.f) - x * yf + __builtin_amdgcn_logf(ope) * 0.6931471805599453f;
-              if (scale != 0.f) {
-                const float inv = __builtin_amdgcn_rcpf(ope);
-                put(tm.col + j, scale / (float)n * ((x >= 0.f ? inv : e * inv) - yf));
-              }
-            }
-          }
-        }
-        ell = wave_sum(acc) / (float)n;
-      } else if (tm.kind == ESGPT_TERM_MVREG) {
-        // lanes 0..M-1: one entry each; duplicates of a target index accumulate into one gradient pair.
-        const int n_targets = tm.vocab_end - tm.vocab_start;
-        bool sel = false;
-        int64_t j = 0;
-        float nll = 0.f, gmu = 0.f, grho = 0.f;
-        {
-          sel = match && e_vm;
-          if (sel) {
-            j = e_idx - tm.vocab_start;
-            if (j < 0 || j >= n_targets) {
-              set_err(err, ESGPT_FLAG_BAD_LABEL);
-              j = 0;
-            }
-            const float mu = to_f32(zrow[tm.col + 2 * j]);
-            const float rho = to_f32(zrow[tm.col + 2 * j + 1]);
-            const float sd = elu1(rho);
-            const float x = e_val;
-            const float zz = (x - mu) / sd;
-            nll = 0.5f * zz * zz + logf(sd) + kHalfLog2Pi;
-            gmu = -(x - mu) / (sd * sd);
-            grho = (1.f / sd - (x - mu) * (x - mu) / (sd * sd * sd)) * delu(rho);
-          }
-        }
-        const float nsel = (float)__popcll(mv);
-        ell = nsel > 0.f ? wave_sum(nll) / nsel : 0.f;
-        if (scale != 0.f && nsel > 0.f) {
-          const float s2 = scale / nsel;
-          // combine duplicate targets: the first lane of each target sums its group, then writes once
-          float sm = 0.f, sr = 0.f;
-          bool first = sel;
-          for (uint64_t bits = mv; bits; bits &= bits - 1) {  // the selected entries, in lane order
-            const int m = __builtin_ctzll(bits);
-            const bool sm_sel = true;
-            const int64_t jm = readlane64(j, m);
-            const float gm = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gmu), m));
-            const float gr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(grho), m));
-            if (sel && sm_sel && jm == j) {
-              sm += gm;
-              sr += gr;
-              if (m < lane) first = false;
-            }
-          }
-          if (first) {
-            put(tm.col + 2 * j, s2 * sm);
-            put(tm.col + 2 * j + 1, s2 * sr);
-          }
-        }
-      } else if (tm.kind == ESGPT_TERM_UVREG) {
-        const bool has_meas = mm != 0, has_val = mv != 0;
-        float x = 0.f;
-        for (uint64_t bits = mv; bits; bits &= bits - 1)
-          x += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e_val), __builtin_ctzll(bits)));
-        if (!has_val) x = 0.f;
-        const float mu = to_f32(zrow[tm.col]);
-        const float rho = to_f32(zrow[tm.col + 1]);
-        const float sd = elu1(rho);
-        const float zz = (x - mu) / sd;
-        const float zo = to_f32(zrow[tm.obs_col]);
-        ell = 0.5f * zz * zz + logf(sd) + kHalfLog2Pi + bce_logits(zo, has_meas ? 1.f : 0.f);
-        if (scale != 0.f && lane == 0) {
-          put(tm.col, scale * (-(x - mu) / (sd * sd)));
-          put(tm.col + 1, scale * (1.f / sd - (x - mu) * (x - mu) / (sd * sd * sd)) * delu(rho));
-          put(tm.obs_col, scale * (sigmoidf_(zo) - (has_meas ? 1.f : 0.f)));
-        }
-      }
+      const float ell = content_term(
+          tm, lane, M, match, mm, mv, e_idx, e_val, e_vm, mk, scale, err,
+          [&](int64_t col) { return to_f32(zrow[col]); },
+          [&](int64_t col, float g) {
+            if (gF) gF[col] += g;
+            else if (RMW) gT[col] = from_f32<T>(to_f32(gT[col]) + g);
+            else gT[col] = from_f32<T>(g);
+          });
       c_out = scale * ell;
     }
-    if (active && lane == 0) my_contrib[(int64_t)t * n_rows] = c_out;
+    if (q.active && lane == 0) my_contrib[(int64_t)t * n_rows] = c_out;
   }
 
   // ---------------- time-to-event (unshifted row r) ----------------
   float c_tte = 0.f;
-  if (active && r >= 0) {
+  if (q.active && r >= 0) {
     const int64_t e = b * L + r;
     const bool obs = (r + 1 < L) && bt.event_mask[e] && bt.event_mask[e + 1];
     const float x = obs ? bt.time_delta[e] : 1.f;
@@ -333,72 +423,201 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
     T* gz = dzt + e * ldt + tte.col;
     const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
     const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;  // d(-LL)/d ll
-    float ll = 0.f;
-    if (tte.kind == ESGPT_TTE_EXP) {
-      const float zz = to_f32(z[0]);
-      const float rate = elu1(zz);
-      ll = logf(rate) - rate * x;
-      if (lane == 0 && scale != 0.f) gz[0] = from_f32<T>(scale * (1.f / rate - x) * delu(zz));
-    } else {
-      // LogNormalMixture (third-party pytorch_lognormal_mixture, restated): lanes = components.
-      const int K = tte.K;
-      const bool affine = !(tte.mean_log == 0.f && tte.std_log == 1.f);
-      const float lx = logf(x);
-      const float y = affine ? (lx - tte.mean_log) / tte.std_log : lx;
-      float loc = 0.f, ls = 0.f, lw = -INFINITY, a = -INFINITY;
-      if (lane < K) {
-        loc = to_f32(z[3 * lane]);
-        ls = to_f32(z[3 * lane + 1]);
-        lw = to_f32(z[3 * lane + 2]);
-      }
-      const float wmax = wave_max(lw);
-      const float wse = wave_sum(lane < K ? expf(lw - wmax) : 0.f);
-      const float lsm = lw - (wmax + logf(wse));  // log_softmax(weights)
-      if (lane < K) {
-        const float sd = expf(ls);
-        const float zz = (y - loc) / sd;
-        a = lsm - 0.5f * zz * zz - ls - kHalfLog2Pi;
-      }
-      const float amax = wave_max(a);
-      const float ase = wave_sum(lane < K ? expf(a - amax) : 0.f);
-      ll = amax + logf(ase) - lx - (affine ? logf(fabsf(tte.std_log)) : 0.f);
-      if (scale != 0.f && lane < K) {
-        const float resp = expf(a - amax) / ase;  // posterior responsibility
-        const float pi = expf(lsm);
-        const float sd = expf(ls);
-        const float dz = (y - loc) / sd;
-        gz[3 * lane] = from_f32<T>(scale * resp * dz / sd);
-        gz[3 * lane + 1] = from_f32<T>(scale * resp * (dz * dz - 1.f));
-        gz[3 * lane + 2] = from_f32<T>(scale * (resp - pi));
-      }
-    }
+    const float ll = tte_term(
+        tte, lane, x, scale, [&](int k) { return to_f32(z[k]); },
+        [&](int k, float g) { gz[k] = from_f32<T>(g); });
     if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
     c_tte = obs ? -scale * ll : 0.f;  // = obs * ll / (B * cnt): LL contribution (positive sign)
   }
-  if (active && lane == 0) my_contrib[(int64_t)NT * n_rows] = c_tte;
+  if (q.active && lane == 0) my_contrib[(int64_t)NT * n_rows] = c_tte;
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Deterministic sums of the per-row contributions: every thread accumulates all terms over its rows, then wave
-// sums and a fixed-order sum over the 16 waves.
+// Row-staged event kernel (rows that fit in LDS): each wave stages its whole logit row in LDS with 16-B loads
+// issued together (the row, the event's entries and the counts in one round trip instead of one per term), the
+// terms read logits from and accumulate f32 gradients into LDS, and the complete gradient row — every column,
+// zeros included — is written back with 16-B stores, so the gradient buffer needs no zero-fill pass. In NA mode
+// (no shift, n_levels rows per event) the wave walks its event's level rows one after another. The TTE columns
+// are part of the row when zt == zc (CI); otherwise they are written to dzt directly (zero-filled).
+// LDS per wave: ldp T logits + ldp f32 gradients (ldp = ldc rounded up to 16-B chunks of T).
+template <typename T>
+__global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms terms, esgpt_tte_spec tte,
+                                                        const T* __restrict__ zc, int64_t ldc, int64_t n_levels,
+                                                        int shift, const T* __restrict__ zc_bias,
+                                                        const T* __restrict__ zt, int64_t ldt, T* __restrict__ dzc,
+                                                        T* __restrict__ dzt, float* __restrict__ dbias,
+                                                        const int32_t* __restrict__ counts, float* __restrict__ contrib,
+                                                        int64_t n_rows, int tte_in_row, int32_t* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
+  constexpr int kEl = 16 / sizeof(T);  // elements per 16-B chunk
+  const int waves = blockDim.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: row math in SALU
+  const int lane = lane_id();
+  const int NT = terms.n;
+  const int64_t L = bt.L, M = bt.M;
+  const int64_t nch = ldc / kEl;           // 16-B chunks per row (ldc % kEl == 0, checked on the host)
+  const int64_t ldp = nch * kEl;
+  T* zs = reinterpret_cast<T*>(s_dyn) + (int64_t)wave * ldp;
+  float* gs = reinterpret_cast<float*>(s_dyn + (size_t)waves * ldp * sizeof(T)) + (int64_t)wave * ldp;
+
+  if (wave == 0) subjects_with_events(counts, bt.B, NT, lane, s_nsub_inv);
+  const int64_t w = (int64_t)blockIdx.x * waves + wave;
+  const RowPos q = row_pos(bt, w, n_rows, shift);
+  const int64_t b = q.b, r = q.r, p = q.p;
+
+  int64_t e_idx = 0, e_meas = INT64_MIN;
+  float e_val = 0.f;
+  bool e_vm = false;
+  if (q.has_content && lane < M) {
+    const int64_t off = (b * L + p) * M + lane;
+    e_idx = bt.dyn_idx[off];
+    e_meas = bt.dyn_meas[off];
+    e_val = bt.dyn_vals[off];
+    e_vm = bt.dyn_vmask[off] != 0;
+  }
+  const int32_t my_cnt = (q.active && lane <= NT) ? counts[b * (ESGPT_MAX_TERMS + 1) + lane] : 0;
+  float* my_contrib = contrib + w;
+  // TTE inputs (loaded with the row)
+  const bool tte_row = q.active && r >= 0;
+  const int64_t e = b * L + (r < 0 ? 0 : r);
+  const bool obs = tte_row && (r + 1 < L) && bt.event_mask[e] && bt.event_mask[e + 1];
+  const float x_tte = obs ? bt.time_delta[e] : 1.f;
+
+  const int n_lv = shift ? 1 : (int)n_levels;
+  for (int lv = 0; lv < n_lv; ++lv) {
+    // ---- stage the row: logits -> zs, gradients -> 0 ----
+    const T* zrow = nullptr;
+    T* grow = nullptr;
+    float* frow = nullptr;
+    if (q.active) {
+      if (shift) {
+        if (r < 0) {
+          zrow = zc_bias;
+          frow = dbias + b * ldc;
+        } else {
+          zrow = zc + (b * L + r) * ldc;
+          grow = dzc + (b * L + r) * ldc;
+        }
+      } else {
+        const int64_t row = (b * L + p) * n_levels + lv;
+        zrow = zc + row * ldc;
+        grow = dzc + row * ldc;
+      }
+    }
+    if (zrow) {
+      constexpr int kBatch = 8;
+      for (int64_t c0 = 0; c0 < nch; c0 += 64 * kBatch) {
+        uint4 v[kBatch];
+#pragma unroll
+        for (int i = 0; i < kBatch; ++i) {
+          const int64_t c = c0 + 64 * i + lane;
+          if (c < nch) v[i] = reinterpret_cast<const uint4*>(zrow)[c];
+        }
+#pragma unroll
+        for (int i = 0; i < kBatch; ++i) {
+          const int64_t c = c0 + 64 * i + lane;
+          if (c < nch) reinterpret_cast<uint4*>(zs)[c] = v[i];
+        }
+      }
+      for (int64_t c = lane; c < ldp / 4; c += 64) reinterpret_cast<float4*>(gs)[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __syncthreads();  // zs / gs staged (and s_nsub_inv on the first level)
+
+    auto zget = [&](int64_t col) { return to_f32(zs[col]); };
+    auto gput = [&](int64_t col, float g) { gs[col] += g; };
+    for (int t = 0; t < NT; ++t) {
+      const esgpt_loss_term& tm = terms.t[t];
+      if (!shift && tm.level != lv) continue;  // wave-uniform
+      float c_out = 0.f;
+      if (q.has_content) {
+        const bool match = e_meas == tm.meas_idx;
+        const uint64_t mm = __ballot(match), mv = __ballot(match && e_vm);
+        const bool mk = q.ev && (tm.kind == ESGPT_TERM_MULTI || (tm.kind == ESGPT_TERM_SINGLE ? mm != 0 : mv != 0));
+        const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
+        const float scale = (mk && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
+        const float ell = content_term(tm, lane, M, match, mm, mv, e_idx, e_val, e_vm, mk, scale, err, zget, gput);
+        c_out = scale * ell;
+      }
+      if (q.active && lane == 0) my_contrib[(int64_t)t * n_rows] = c_out;
+    }
+    if (tte_in_row && lv == 0) {
+      float c_tte = 0.f;
+      if (tte_row) {
+        const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
+        const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;
+        const float ll = tte_term(
+            tte, lane, x_tte, scale, [&](int k) { return to_f32(zs[tte.col + k]); },
+            [&](int k, float g) { gs[tte.col + k] += g; });
+        if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
+        c_tte = obs ? -scale * ll : 0.f;
+      }
+      if (q.active && lane == 0) my_contrib[(int64_t)NT * n_rows] = c_tte;
+    }
+    __syncthreads();  // every lane's gradient columns in gs
+
+    // ---- write the whole gradient row ----
+    if (frow) {
+      for (int64_t c = lane; c < ldp / 4; c += 64)
+        reinterpret_cast<float4*>(frow)[c] = reinterpret_cast<const float4*>(gs)[c];
+    } else if (grow) {
+      for (int64_t c = lane; c < nch; c += 64) {
+        uint4 o;
+        if constexpr (sizeof(T) == 4) {
+          o = reinterpret_cast<const uint4*>(gs)[c];
+        } else {
+          const float4 a0 = reinterpret_cast<const float4*>(gs)[2 * c];
+          const float4 a1 = reinterpret_cast<const float4*>(gs)[2 * c + 1];
+          o.x = (uint32_t)f32_to_bf16_bits(a0.x) | ((uint32_t)f32_to_bf16_bits(a0.y) << 16);
+          o.y = (uint32_t)f32_to_bf16_bits(a0.z) | ((uint32_t)f32_to_bf16_bits(a0.w) << 16);
+          o.z = (uint32_t)f32_to_bf16_bits(a1.x) | ((uint32_t)f32_to_bf16_bits(a1.y) << 16);
+          o.w = (uint32_t)f32_to_bf16_bits(a1.z) | ((uint32_t)f32_to_bf16_bits(a1.w) << 16);
+        }
+        reinterpret_cast<uint4*>(grow)[c] = o;
+      }
+    }
+    if (lv + 1 < n_lv) __syncthreads();  // zs / gs reused by the next level
+  }
+
+  // ---- time-to-event into a separate dzt (NA) ----
+  if (!tte_in_row) {
+    float c_tte = 0.f;
+    if (tte_row) {
+      const T* z = zt + e * ldt + tte.col;
+      T* gz = dzt + e * ldt + tte.col;
+      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
+      const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;
+      const float ll = tte_term(
+          tte, lane, x_tte, scale, [&](int k) { return to_f32(z[k]); },
+          [&](int k, float g) { gz[k] = from_f32<T>(g); });
+      if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
+      c_tte = obs ? -scale * ll : 0.f;
+    }
+    if (q.active && lane == 0) my_contrib[(int64_t)NT * n_rows] = c_tte;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Deterministic sums of the per-row contributions: thread i sums rows i, i + 1024, ... of each term (8 loads in
+// flight), then wave sums and a fixed-order sum over the 16 waves.
 __global__ __launch_bounds__(1024) void reduce_kernel(const float* __restrict__ contrib, int64_t n_rows, int NT,
                                                       float* __restrict__ losses) {
   __shared__ float s[16][ESGPT_MAX_TERMS + 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float a[ESGPT_MAX_TERMS + 1];
+  for (int t = 0; t <= NT; ++t) {
+    const float* c = contrib + (int64_t)t * n_rows;
+    float a = 0.f;
+    int64_t i = threadIdx.x;
+    for (; i + 7 * 1024 < n_rows; i += 8 * 1024) {
+      float v[8];
 #pragma unroll
-  for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) a[t] = 0.f;
-  for (int64_t i = threadIdx.x; i < n_rows; i += 1024) {
+      for (int k = 0; k < 8; ++k) v[k] = c[i + k * 1024];
 #pragma unroll
-    for (int t = 0; t <= ESGPT_MAX_TERMS; ++t)
-      if (t <= NT) a[t] += contrib[(int64_t)t * n_rows + i];
-  }
-#pragma unroll
-  for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) {
-    if (t <= NT) {
-      const float v = wave_sum(a[t]);
-      if (lane == 0) s[wave][t] = v;
+      for (int k = 0; k < 8; ++k) a += v[k];
     }
+    for (; i < n_rows; i += 1024) a += c[i];
+    const float w = wave_sum(a);
+    if (lane == 0) s[wave][t] = w;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -436,6 +655,14 @@ bool disjoint_columns(const esgpt_loss_term* terms, int n_terms, int shift) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+constexpr int64_t kLdsBudget = 64 * 1024;  // row-staged event kernel: LDS bytes per block
+
+// ESGPT_LOSS_ROW_STAGE=0 forces the generic (column-by-column) event kernel (parity tests of both paths).
+bool row_stage_enabled() {
+  const char* e = getenv("ESGPT_LOSS_ROW_STAGE");
+  return !(e && e[0] == '0');
+}
+
 }  // namespace
 
 extern "C" {
@@ -456,6 +683,7 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
   ESGPT_REQUIRE(batch->M <= kMaxM && (tte->kind == ESGPT_TTE_EXP || (tte->kind == ESGPT_TTE_LNM && tte->K <= kMaxK)));
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
   ESGPT_REQUIRE(workspace_bytes >= esgpt_output_loss_workspace(batch->B, batch->L, n_terms));
+  ESGPT_REQUIRE(batch->L <= 16384 && batch->L * batch->M < (1ll << 31));  // count_kernel: LDS word per event
   const int64_t B = batch->B, L = batch->L;
   if (B == 0 || L == 0) return ESGPT_ERR_INVALID_ARG;
   hipStream_t st = as_stream(stream);
@@ -465,23 +693,52 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
   int32_t* counts = (int32_t*)workspace;
   float* contrib = (float*)((char*)workspace + align_up(sizeof(int32_t) * B * (ESGPT_MAX_TERMS + 1)));
   const size_t esz = dtype == ESGPT_F32 ? 4 : 2;
-  if (n_terms > 0 && zero_async(dzc, esz * B * L * n_levels * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if ((dzt != dzc || n_terms == 0) && zero_async(dzt, esz * B * L * ldt, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if (shift && zero_async(dbias, sizeof(float) * B * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  count_kernel<<<(unsigned)B, 256, 0, st>>>(*batch, T, counts, err);
   const int64_t n_rows = B * (L + shift);
-  const unsigned grid = (unsigned)cdiv(n_rows, kWaves);
-  const bool rmw = !disjoint_columns(terms, n_terms, shift);
+  // Row-staged kernel when a row fits: 16-B aligned rows, LDS (logits + f32 gradients) for >= 1 wave per block
+  // within kLdsBudget; waves per block = as many as fit (<= 4).
+  const int64_t kEl = 16 / (int64_t)esz;
+  const int64_t per_wave = ldc * (int64_t)(esz + 4);
+  const bool aligned = n_terms > 0 && ldc % kEl == 0 && (uintptr_t)zc % 16 == 0 && (uintptr_t)dzc % 16 == 0 &&
+                       (!shift || ((uintptr_t)zc_bias % 16 == 0 && (uintptr_t)dbias % 16 == 0));
+  // TTE columns inside the content row (CI head): handled in LDS with the row. A dzt aliasing dzc any other way
+  // would race the full-row stores, so it takes the generic kernel.
+  const bool same_row = zt == zc && dzt == dzc && ldt == ldc && n_levels == 1;
+  const bool staged = aligned && per_wave <= kLdsBudget && (dzt != dzc || same_row) && row_stage_enabled();
+  const bool tte_in_row = staged && same_row;
+  if (!staged) {
+    if (n_terms > 0 && zero_async(dzc, esz * B * L * n_levels * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    if (shift && zero_async(dbias, sizeof(float) * B * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  }
+  if (!tte_in_row && (dzt != dzc || n_terms == 0 || staged) &&
+      zero_async(dzt, esz * B * L * ldt, st) != hipSuccess)
+    return ESGPT_ERR_LAUNCH;
+  count_kernel<<<(unsigned)B, 1024, sizeof(uint32_t) * L, st>>>(*batch, T, counts, err);
+  if (staged) {
+    const int wpb = (int)std::min<int64_t>(kWaves, kLdsBudget / per_wave);
+    const unsigned grid = (unsigned)cdiv(n_rows, wpb);
+    const size_t lds = (size_t)wpb * per_wave;
+    if (dtype == ESGPT_F32)
+      event_lds_kernel<float><<<grid, 64 * wpb, lds, st>>>(*batch, T, *tte, (const float*)zc, ldc, n_levels, shift,
+                                                          (const float*)zc_bias, (const float*)zt, ldt, (float*)dzc,
+                                                          (float*)dzt, dbias, counts, contrib, n_rows, tte_in_row, err);
+    else
+      event_lds_kernel<bf16><<<grid, 64 * wpb, lds, st>>>(*batch, T, *tte, (const bf16*)zc, ldc, n_levels, shift,
+                                                         (const bf16*)zc_bias, (const bf16*)zt, ldt, (bf16*)dzc,
+                                                         (bf16*)dzt, dbias, counts, contrib, n_rows, tte_in_row, err);
+  } else {
+    const unsigned grid = (unsigned)cdiv(n_rows, kWaves);
+    const bool rmw = !disjoint_columns(terms, n_terms, shift);
 #define LAUNCH_EV(TT, RMW)                                                                                        \
   event_kernel<TT, RMW><<<grid, 256, 0, st>>>(*batch, T, *tte, (const TT*)zc, ldc, n_levels, shift,               \
                                               (const TT*)zc_bias, (const TT*)zt, ldt, (TT*)dzc, (TT*)dzt, dbias,  \
                                               counts, contrib, n_rows, err)
-  if (dtype == ESGPT_F32) {
-    if (rmw) LAUNCH_EV(float, true); else LAUNCH_EV(float, false);
-  } else {
-    if (rmw) LAUNCH_EV(bf16, true); else LAUNCH_EV(bf16, false);
-  }
+    if (dtype == ESGPT_F32) {
+      if (rmw) LAUNCH_EV(float, true); else LAUNCH_EV(float, false);
+    } else {
+      if (rmw) LAUNCH_EV(bf16, true); else LAUNCH_EV(bf16, false);
+    }
 #undef LAUNCH_EV
+  }
   reduce_kernel<<<1, 1024, 0, st>>>(contrib, n_rows, n_terms, losses);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;

@@ -272,10 +272,13 @@ def _register():
         qkv, km, qm, H, window, skf, p, seed = inputs
         o, lse = output
         ctx.mark_non_differentiable(lse)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(qkv, o, lse, km, qm, seed)
         ctx.meta = (H, window, skf, p)
 
     def _at_bwd(ctx, do, _dlse):
+        if do is None:
+            return (None,) * 8
         qkv, o, lse, km, qm, seed = ctx.saved_tensors
         H, window, skf, p = ctx.meta
         dqkv = ops.attention_bwd(qkv, o, do, lse, km, qm, H, window, skf, p, seed, _tickets(qkv.device))
@@ -340,11 +343,14 @@ def _register():
         x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets = inputs
         y, pre, g = output
         ctx.mark_non_differentiable(pre, g)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, w_fc, w_pj, pre, g)
         ctx.act = act
         ctx.has_bpj = b_pj is not None
 
     def _ml_bwd(ctx, dy, _dpre, _dg):
+        if dy is None:
+            return (None,) * 9
         x, w_fc, w_pj, pre, g = ctx.saved_tensors
         need_dbpj = ctx.has_bpj and ctx.needs_input_grad[4]
         dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj)
@@ -359,10 +365,13 @@ def _register():
         zc, zt, zc_bias = inputs[:3]
         losses, dzc, dzt, dbias = output
         ctx.mark_non_differentiable(dzc, dzt, dbias)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(dzc, dzt, dbias)
         ctx.meta = (zt is not None, zc_bias is not None)
 
     def _ol_bwd(ctx, g, *_):
+        if g is None:
+            return (None,) * 18
         dzc, dzt, dbias = ctx.saved_tensors
         has_zt, has_bias = ctx.meta
         gt = g[-1]
@@ -377,11 +386,14 @@ def _register():
         wc, bc, wt, bt, cw, cb, tw, tb = inputs[16:24]
         losses, dzc, dzt, dbias = output
         ctx.mark_non_differentiable(dzc, dzt, dbias)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(xc, xt, wc, wt, dzc, dzt, dbias)
         ctx.rows = ([w.shape[0] for w in cw], [w.shape[0] for w in tw])
         ctx.n = (len(cw), len(tw))
 
     def _hl_bwd(ctx, g, *_):
+        if g is None:
+            return (None,) * 26
         xc, xt, wc, wt, dzc, dzt, dbias = ctx.saved_tensors
         n_cw, n_tw = ctx.n
         rows_c, rows_t = ctx.rows

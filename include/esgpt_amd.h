@@ -202,9 +202,9 @@ int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const floa
                           float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
                           int64_t N, int64_t D, float* h, void* out, int out_dtype, float* mean, float* rstd,
                           void* stream);
-/* Backward: sums f32 [3, D] = (dgamma, dbeta, dbias) column sums, computed in the same launch (fixed order):
- * part: f32 workspace [esgpt_residual_ln_partials(N), 3, D]; counters: esgpt_residual_ln_counters(N) int32
- * tickets, zeroed once by the caller and left zeroed (stream-ordered use, as for esgpt_gemm_bf16). */
+/* Backward: sums f32 [3, D] = (dgamma, dbeta, dbias) column sums (per-block partials in part, then a second
+ * small launch sums them in a fixed order: deterministic). part: f32 workspace [esgpt_residual_ln_partials(N), 3,
+ * D]. counters: reserved (esgpt_residual_ln_counters returns 0; may be NULL). */
 int64_t esgpt_residual_ln_counters(int64_t N);
 int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, const float* h, const float* mean,
                           const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,

@@ -1,0 +1,84 @@
+"""esgpt_output_loss at the C2 step's head layout, per loss-term subset and per event-kernel path (row-staged /
+generic, ESGPT_LOSS_ROW_STAGE): graph-replayed launch time (count + event + reduce kernels).
+
+    python tools/loss_bench.py
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from bench import graph_time_ms  # noqa: E402
+from eventstreamgpt_amd import _lib as L  # noqa: E402
+from eventstreamgpt_amd.kernels import batch_view, err_word  # noqa: E402
+from eventstreamgpt_amd.synthetic import CONFIGS  # noqa: E402
+from eventstreamgpt_amd.transformer import model_output as MO  # noqa: E402
+from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling  # noqa
+
+
+def main():
+    dev = torch.device("cuda")
+    bc = CONFIGS["C2"]
+    model = CIPPTForGenerativeSequenceModeling(bc.model_config())
+    batch = bc.batch(0, batch_size=32).to(dev)
+    layer = model.output_layer
+    layer._layout = layer._build_layout()
+    terms, _ = layer._terms_for(MO.all_classification_measurements(layer),
+                                MO.all_regression_measurements(layer.config), 0)
+    tte = layer._tte_spec(layer._layout["n_content"])
+    lib = L.load()
+    bv = batch_view(batch)
+    B, Lq, M = bv.B, bv.L, bv.M
+    C = layer._layout["n_content"] + tte.K * (1 if tte.kind == L.TTE_EXP else 3)
+    C += (-C) % 8
+    g = torch.Generator(device=dev).manual_seed(4)
+    zc = torch.randn(B * Lq, C, device=dev, generator=g).bfloat16()
+    bias = torch.zeros(C, device=dev).bfloat16()
+    dzc = torch.empty_like(zc)
+    dbias = torch.empty(B, C, device=dev)
+    losses = torch.empty(len(terms) + 2, device=dev)
+    err = err_word(dev)
+    kinds = {L.TERM_SINGLE: "single", L.TERM_MULTI: "multi", L.TERM_MVREG: "mvreg", L.TERM_UVREG: "uvreg"}
+    print(json.dumps({"B": B, "L": Lq, "M": M, "C": C,
+                      "terms": [(kinds[t.kind], t.vocab_end - t.vocab_start) for t in terms]}))
+
+    def launcher(sub):
+        arr = (L.EsgptLossTerm * max(1, len(sub)))(*sub)
+        nb = lib.esgpt_output_loss_workspace(B, Lq, len(sub))
+        ws = torch.empty(max(1, nb), dtype=torch.uint8, device=dev)
+
+        def fwd():
+            L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), C, 1, 1, bias.data_ptr(), zc.data_ptr(), C, L.BF16,
+                                          arr, len(sub), ctypes.byref(tte), dzc.data_ptr(), dzc.data_ptr(),
+                                          dbias.data_ptr(), losses[: len(sub) + 2].data_ptr(), ws.data_ptr(), nb,
+                                          err.data_ptr(), L.stream()), "output_loss")
+        return fwd, (arr, ws)
+
+    if "--pmc" in sys.argv:  # eager launches of a term subset (counter collection): --pmc [all | i]
+        k = sys.argv[sys.argv.index("--pmc") + 1] if len(sys.argv) > sys.argv.index("--pmc") + 1 else "all"
+        fn, keep = launcher(list(terms) if k == "all" else [terms[int(k)]])
+        for _ in range(5):
+            fn()
+        torch.cuda.synchronize()
+        err.zero_()
+        return
+    subsets = {"all": list(terms)}
+    for i, t in enumerate(terms):
+        subsets[f"only_{i}_{kinds[t.kind]}"] = [t]
+    for stage in ("1", "0"):
+        os.environ["ESGPT_LOSS_ROW_STAGE"] = stage
+        for name, sub in subsets.items():
+            fn, keep = launcher(sub)
+            us = graph_time_ms(fn) * 1e3
+            print(json.dumps({"row_stage": stage, "terms": name, "us": round(us, 2)}))
+    err.zero_()
+
+
+if __name__ == "__main__":
+    main()
