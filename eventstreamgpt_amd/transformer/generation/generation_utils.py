@@ -8,8 +8,9 @@ re-concatenates its cache each step.
 
 Host reads per generated event: one combined NaN / non-finite check over the inputs (the reference issues two
 ``.any()`` reads per input field), the sampler's own reads (data-dependent widths in ``strip_unused_indices``),
-and the stopping criterion. The nested-attention model generates without caches (every graph level re-encodes the
-batch); its ``use_cache=True`` (dependency-graph caches) raises.
+and the stopping criterion. The nested-attention model walks the dependency graph per event (target 0 = TTE and
+the new event, then one graph level per call); with ``use_cache=True`` each call runs only the new event (target 0)
+or the new graph element (t > 0) against the sequence and dependency-graph caches.
 """
 from __future__ import annotations
 

@@ -1,10 +1,16 @@
-"""``StructuredAttention`` — drop-in for ``EventStream/transformer/structured_attention.py:7-219`` (training path).
+"""``StructuredAttention`` — drop-in for ``EventStream/transformer/structured_attention.py:7-219``.
 
 Differences in mechanics (same results): padded events are NOT compacted out with boolean indexing (a device→host
 sync and data-dependent shapes in the reference, ``:87-96,158-165,186-193``); every (subject, event) runs through
 the dependency-graph module — its sequences are independent — and the outputs of padded events are zeroed, which
 is exactly what the reference's scatter into a zero tensor produces. This keeps the step shape-static (capturable
 into a HIP graph).
+
+Generation with caches (``prepend_graph_with_history_embeddings`` / ``update_last_graph_el_to_history_embedding``
+False, set by the encoder from ``dep_graph_el_generation_target``): the three cases of ``:63-156`` — prefill
+(history prepended, the last graph element replaced by the contextualised event), a new event's whole-event
+element (no history: it is in the dependency-graph cache; its contextualised version replaces it) and a new graph
+element (no sequence module at all).
 """
 from __future__ import annotations
 
@@ -24,32 +30,43 @@ class StructuredAttention(torch.nn.Module):
                 dep_graph_module_kwargs: dict[str, Any] | None = None,
                 prepend_graph_with_history_embeddings: bool = True,
                 update_last_graph_el_to_history_embedding: bool = True):
-        if not (prepend_graph_with_history_embeddings and update_last_graph_el_to_history_embedding):
-            raise NotImplementedError("eventstreamgpt_amd: cached dependency-graph generation is out of scope")
         seq_module_kwargs = dict(seq_module_kwargs or {})
         dep_graph_module_kwargs = dict(dep_graph_module_kwargs or {})
         bsz, seq_len, dep_graph_len, hidden_size = hidden_states.shape
-
-        kpm = event_mask
-        if kpm is None and seq_attention_mask is not None:
-            kpm = seq_attention_mask.reshape(bsz, -1) == 0
-        per_event = hidden_states[:, :, -1, :]
-        if event_mask is not None:
-            m3 = event_mask.unsqueeze(-1)
-            per_event = torch.where(m3, per_event, 0.0)
-        ctx = self.seq_module(per_event, key_padding_mask=kpm, **seq_module_kwargs)
+        m3 = None if event_mask is None else event_mask.unsqueeze(-1)
         seq_ret = None
-        if isinstance(ctx, tuple):
-            ctx, seq_ret = ctx
-        if event_mask is not None:
-            ctx = torch.where(m3, ctx, 0.0)
 
-        history = torch.nn.functional.pad(ctx[:, :-1, :], (0, 0, 1, 0))  # [0, ctx_0 .. ctx_{L-2}]
-        # [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i]: the last graph element is replaced by the contextualised
-        # event (structured_attention.py:125-149).
-        dep_graph_seq = torch.cat((history.unsqueeze(2), hidden_states[:, :, :-1, :], ctx.unsqueeze(2)), dim=2)
-        dep_graph_seq = dep_graph_seq.reshape(bsz * seq_len, dep_graph_len + 1, hidden_size)
-        out = self.dep_graph_module(dep_graph_seq, attention_mask=None, static_kv_first=True,
+        if prepend_graph_with_history_embeddings or update_last_graph_el_to_history_embedding:
+            # key padding of the sequence module: the additive mask covers past + new events when a cache is used
+            if seq_attention_mask is not None:
+                kpm = seq_attention_mask.reshape(bsz, -1) == 0
+            else:
+                kpm = event_mask
+            per_event = hidden_states[:, :, -1, :]
+            if m3 is not None:
+                per_event = torch.where(m3, per_event, 0.0)
+            ctx = self.seq_module(per_event, key_padding_mask=kpm, **seq_module_kwargs)
+            if isinstance(ctx, tuple):
+                ctx, seq_ret = ctx
+            if m3 is not None:
+                ctx = torch.where(m3, ctx, 0.0)
+            if prepend_graph_with_history_embeddings:
+                history = torch.nn.functional.pad(ctx[:, :-1, :], (0, 0, 1, 0))  # [0, ctx_0 .. ctx_{L-2}]
+                # [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i]: the last graph element is replaced by the contextualised
+                # event (structured_attention.py:125-149).
+                dep_graph_seq = torch.cat((history.unsqueeze(2), hidden_states[:, :, :-1, :], ctx.unsqueeze(2)),
+                                          dim=2)
+                static_kv_first = True
+            else:
+                dep_graph_seq = torch.cat((hidden_states[:, :, :-1, :], ctx.unsqueeze(2)), dim=2)
+                static_kv_first = False
+        else:
+            dep_graph_seq = hidden_states
+            static_kv_first = False
+
+        G1 = dep_graph_seq.shape[2]
+        dep_graph_seq = dep_graph_seq.reshape(bsz * seq_len, G1, hidden_size)
+        out = self.dep_graph_module(dep_graph_seq, attention_mask=None, static_kv_first=static_kv_first,
                                     **dep_graph_module_kwargs)
         dep_ret = None
         if isinstance(out, tuple):
@@ -57,4 +74,9 @@ class StructuredAttention(torch.nn.Module):
         out = out.reshape(bsz, seq_len, dep_graph_len, hidden_size)
         if event_mask is not None:
             out = torch.where(event_mask[:, :, None, None], out, 0.0)
+            present = dep_ret.get("present_key_value") if isinstance(dep_ret, dict) else None
+            if present is not None and not bool(event_mask.all()):
+                # the reference scatters the present keys / values of the kept events into zeros (:186-193)
+                keep = event_mask.reshape(bsz * seq_len, 1, 1, 1)
+                dep_ret["present_key_value"] = tuple(torch.where(keep, t, 0.0) for t in present)
         return out, {"seq_module": seq_ret, "dep_graph_module": dep_ret}

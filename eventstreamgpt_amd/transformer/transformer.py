@@ -8,8 +8,9 @@ Class names, constructor/forward signatures, return types and state_dict keys fo
 Compute: the attention core (scores, causal/local band, key padding, softmax, P·V) runs in the gfx950 attention
 kernels over a packed QKV buffer (one GEMM for q/k/v); the input layer runs in the fused embedding kernels. The CI
 training path runs every block through ``fused.ci_encoder_fused`` (own GEMM / LayerNorm kernels). Generation
-(``use_cache`` / ``past``, CI encoder) keeps a preallocated KV cache per layer and attends the new events with the
-decode kernel (``csrc/decode.hip``); the NA model's caches and ``output_attentions`` are not supported and raise.
+(``use_cache`` / ``past``) keeps a preallocated KV cache per layer — the CI encoder's sequence caches, and the NA
+encoder's sequence + dependency-graph caches — and attends the new events / graph elements with the decode kernel
+(``csrc/decode.hip``); ``output_attentions`` is not supported and raises.
 """
 from __future__ import annotations
 
@@ -82,6 +83,8 @@ class InnerSelfAttention(nn.Module):
                 f"`num_heads`: {self.num_heads})."
             )
         self.max_seq_len = max_seq_len
+        # KV-cache rows preallocated per generation cache (the dependency-graph module sets its graph length + 1)
+        self.cache_cap = max_seq_len
         self.k_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=False)
         self.v_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=False)
         self.q_proj = nn.Linear(self.embed_dim, self.embed_dim, bias=False)
@@ -106,9 +109,20 @@ class InnerSelfAttention(nn.Module):
         w = self._packed_qkv_weight()
         qkv = nn.functional.linear(hidden_states, w)
         window = self.window_size if self.attention_type == "local" else 0
+        if static_kv_first and use_cache and layer_past is None:
+            # NA dependency-graph prefill (transformer.py:246-265 with static_kv_first): the graph sequences are
+            # attended as in training; present = the keys / values of every graph position, history included
+            # (the encoder keeps only the last event's last one, transformer.py:1205-1226)
+            o = attention(qkv, None, None, self.num_heads, window, True, self.attn_dropout_p if self.training else 0.0)
+            N, T, _ = qkv.shape
+            D, H = self.embed_dim, self.num_heads
+            k = qkv[..., D:2 * D].view(N, T, H, D // H).permute(0, 2, 1, 3)
+            v = qkv[..., 2 * D:].view(N, T, H, D // H).permute(0, 2, 1, 3)
+            return self.resid_dropout(self.out_proj(o)), {"present_key_value": (k, v)}
         if layer_past is not None or use_cache:
-            _unsupported(static_kv_first, "use_cache/past with static_kv_first (NA dependency-graph cache)")
-            o, present = cached_attention(qkv, layer_past, key_padding_mask, self.num_heads, window, self.max_seq_len)
+            _unsupported(static_kv_first, "a past with static_kv_first (the reference never prepends history to a "
+                                          "cached dependency graph)")
+            o, present = cached_attention(qkv, layer_past, key_padding_mask, self.num_heads, window, self.cache_cap)
             out = self.resid_dropout(self.out_proj(o))
             return out, {"present_key_value": present if use_cache else None}
         kpm = None if key_padding_mask is None else key_padding_mask.contiguous()
@@ -139,6 +153,8 @@ class InnerAttention(nn.Module):
                 f"{self.attention_layers}. Select attn layer types from ['global', 'local'] only."
             )
         self.attention = InnerSelfAttention(config, attention_type=self.attention_type, window_size=self.window_size)
+        if not is_seq and config.measurements_per_dep_graph_level:
+            self.attention.cache_cap = len(config.measurements_per_dep_graph_level) + 1  # history + graph levels
         self.layer_norm = nn.LayerNorm(config.hidden_size, eps=config.layer_norm_epsilon)
 
     def forward(self, hidden_states, attention_mask=None, layer_past=None, head_mask=None, use_cache=False,
@@ -422,7 +438,7 @@ class NestedAttentionPointProcessInputLayer(torch.nn.Module):
 
 
 class NestedAttentionPointProcessTransformer(StructuredTransformerPreTrainedModel):
-    """NA encoder (``transformer.py:939-1233``), training path (no cache)."""
+    """NA encoder (``transformer.py:939-1233``): training path and cached generation."""
 
     def __init__(self, config: StructuredTransformerConfig):
         super().__init__(config)
@@ -440,11 +456,18 @@ class NestedAttentionPointProcessTransformer(StructuredTransformerPreTrainedMode
                 seq_attention_mask: torch.Tensor | None = None, head_mask=None, use_cache: bool | None = None,
                 output_attentions: bool | None = None, output_hidden_states: bool | None = None,
                 return_dict: bool | None = None, dep_graph_past=None, dep_graph_el_generation_target=None):
-        # The reference resolves use_cache=None to config.use_cache (True by default) and then builds caches nobody
-        # reads outside generation; here None means no cache, and an explicit cache request raises.
-        _unsupported(past is not None or dep_graph_past is not None or bool(use_cache),
-                     "use_cache/past in the nested-attention encoder (pass use_cache=False)")
+        """``transformer.py:975-1233``. ``use_cache=None`` means no cache here (the reference resolves it to
+        ``config.use_cache`` and builds caches nobody reads outside generation). With ``use_cache=True`` the
+        sequence caches are per-layer KV caches (``kernels.LayerKV``: the reference's ``(key, value)`` pairs as views
+        of a preallocated cache) and the dependency-graph caches hold the graph positions of the event being
+        generated, following the reference's targets: None (prefill: both caches built, the dependency-graph cache
+        re-set to the last event's contextualised element), 0 (a completed event: sequence cache extended, graph
+        cache re-set to its contextualised element) and t > 0 (graph element t - 1 of the new event: graph cache
+        extended)."""
         _unsupported(bool(output_attentions), "output_attentions")
+        if head_mask is not None:
+            raise NotImplementedError("eventstreamgpt_amd: head_mask is not supported")
+        use_cache = bool(use_cache)
         if input_embeds is None:
             assert batch is not None
             input_embeds = self.input_layer(batch, dep_graph_el_generation_target=dep_graph_el_generation_target)
@@ -452,16 +475,73 @@ class NestedAttentionPointProcessTransformer(StructuredTransformerPreTrainedMode
         else:
             assert batch is None, "Can't specify both input_embeds and batch."
             event_mask = None
+        if seq_attention_mask is None and use_cache and event_mask is not None:
+            seq_attention_mask = expand_mask(event_mask, input_embeds.dtype)
+
+        update_seq = update_dep = re_set = False
+        prepend = update_last = True
+        if use_cache:
+            tgt = dep_graph_el_generation_target
+            if tgt is None:
+                if dep_graph_past is not None:
+                    raise ValueError(f"dep_graph_past should be None if gen target is None; got {dep_graph_past}")
+                update_seq = update_dep = re_set = True
+            elif isinstance(tgt, int) and tgt > 0:
+                if dep_graph_past is None:
+                    raise ValueError(f"dep_graph_past should not be None if dep_graph_el_generation_target is {tgt}.")
+                update_dep = True
+                prepend = update_last = False
+            elif isinstance(tgt, int) and tgt == 0:
+                update_seq = update_dep = re_set = True
+                prepend = False
+            else:
+                raise ValueError("While use_cache=True, dep graph generation target must be a non-negative int; got "
+                                 f"{tgt}.")
+        elif past is not None or dep_graph_past is not None:
+            raise ValueError("past / dep_graph_past given with use_cache=False")
+
+        n = len(self.h)
+        past = tuple([None] * n) if past is None else past
+        dep_graph_past = tuple([None] * n) if dep_graph_past is None else dep_graph_past
+        if len(past) != n or len(dep_graph_past) != n:
+            raise ValueError(f"past holds {len(past)} / {len(dep_graph_past)} layers; the encoder has {n}")
+        presents = {"seq_past": (), "dep_graph_past": ()} if use_cache else None
         hidden = input_embeds
+        bsz, seq_len = hidden.shape[:2]
         all_hidden = () if output_hidden_states else None
-        for block in self.h:
+        for block, layer_past, dep_layer_past in zip(self.h, past, dep_graph_past):
             if output_hidden_states:
                 all_hidden = all_hidden + (hidden,)
-            hidden, _ = block(hidden, seq_attention_mask=seq_attention_mask, event_mask=event_mask)
+            if not use_cache:
+                hidden, _ = block(hidden, seq_attention_mask=seq_attention_mask, event_mask=event_mask)
+                continue
+            hidden, extra = block(hidden, seq_attention_mask=seq_attention_mask, event_mask=event_mask,
+                                  prepend_graph_with_history_embeddings=prepend,
+                                  update_last_graph_el_to_history_embedding=update_last,
+                                  seq_module_kwargs=dict(layer_past=layer_past, use_cache=update_seq),
+                                  dep_graph_module_kwargs=dict(layer_past=dep_layer_past, use_cache=update_dep))
+            if update_seq:
+                presents["seq_past"] += (extra["seq_module"]["present_key_value"],)
+            if update_dep:
+                presents["dep_graph_past"] += (extra["dep_graph_module"]["present_key_value"],)
         hidden = self.ln_f(hidden)
         if output_hidden_states:
             all_hidden = all_hidden + (hidden,)
+        if use_cache:
+            if not update_seq:
+                presents["seq_past"] = past
+            if re_set:
+                # keep only the last event's last graph element: the history key / value of the next event's graph
+                # (transformer.py:1205-1226): [bsz * seq_len, H, n, hd] -> [bsz, H, 1, hd]
+                H, hd = self.config.num_attention_heads, self.config.head_dim
+
+                def last_el(t):
+                    if t.shape[0] != bsz * seq_len or t.shape[1] != H or t.shape[3] != hd:
+                        raise ValueError(f"Shape malformed! Want {(bsz * seq_len, H, '?', hd)}, Got {t.shape}")
+                    return t.reshape(bsz, seq_len, H, -1, hd)[:, -1, :, -1, :].unsqueeze(2).contiguous()
+
+                presents["dep_graph_past"] = tuple(tuple(last_el(e) for e in kv) for kv in presents["dep_graph_past"])
         if return_dict is False:
-            return tuple(v for v in (hidden, all_hidden) if v is not None)
-        return TransformerOutputWithPast(last_hidden_state=hidden, past_key_values=None, hidden_states=all_hidden,
+            return tuple(v for v in (hidden, presents, all_hidden) if v is not None)
+        return TransformerOutputWithPast(last_hidden_state=hidden, past_key_values=presents, hidden_states=all_hidden,
                                          attentions=None)

@@ -5,8 +5,10 @@ CPU: the batch-update host logic (``GenerativeSequenceModelSamples.append_to_bat
 tests/golden/make_generation_golden.py), ``repeat_batch_elements`` against the reference doctest, and the
 prediction slicing / sampling semantics. GPU (through the C ABI): the decode kernel against a plain f32 torch
 restatement of ``_attn`` (transformer.py:171-217) with a cache, the reference's KV-cache invariance property
-(test_transformer.py:209-294: step-by-step cached encodings equal the full forward's), and ``generate`` with and
-without the cache.
+(test_transformer.py:209-294: step-by-step cached encodings equal the full forward's), ``generate`` with and
+without the cache, and the nested-attention caches: the reference's NA cache property (test_transformer.py:343-435:
+prefill + graph targets 1..G-1, 0 per later event equal the uncached full forward) and cached NA ``generate``
+(lock-step encodings equal the full forward's at each graph level).
 """
 import json
 import os
@@ -364,8 +366,128 @@ def test_nested_attention_generate():
     new_meas = out.dynamic_measurement_indices[:, -3:]
     assert bool(((new_meas == et).sum(-1) == 1).all())
     assert bool(torch.isfinite(out.time_delta).all())
-    with pytest.raises(NotImplementedError):
-        model.generate(b, max_new_events=1, use_cache=True)
+
+
+def _left_pad(batch):
+    """Generation-style layout: every subject's events moved to the end (stable), padding first."""
+    order = torch.argsort(batch.event_mask.to(torch.int8), dim=1, stable=True)
+    for k in ("event_mask", "time_delta", "dynamic_indices", "dynamic_measurement_indices", "dynamic_values",
+              "dynamic_values_mask"):
+        t = getattr(batch, k)
+        idx = order.view(*order.shape, *([1] * (t.dim() - 2))).expand_as(t)
+        setattr(batch, k, t.gather(1, idx))
+    return batch
+
+
+def _na_model():
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    fx, cfg, batch = load_case("na_small")
+    cfg.measurement_configs = {m: SimpleNamespace(modality=mod, temporality="dynamic", is_dropped=False)
+                               for m, mod in _fixture()["meas"].items()}
+    model = NAPPTForGenerativeSequenceModeling(cfg)
+    model.load_state_dict(fx["state_dict"])
+    return model.cuda().eval(), cfg, _left_pad(batch)
+
+
+@pytest.mark.gpu
+def test_na_cache_matches_full_forward():
+    """The reference's NA cache property (tests/transformer/test_transformer.py:343-435): the full forward without
+    caches equals (a) the full forward with caches and (b) a prefill of the first events (target None) followed,
+    for every later event, by graph targets 1, ..., G-1, 0 on that single event against the sequence and
+    dependency-graph caches — outputs concatenated over the graph and the sequence. Also the prefill's sequence
+    cache equals the first rows of the full run's."""
+    from eventstreamgpt_amd.transformer.transformer import expand_mask, time_from_deltas
+
+    model, cfg, batch = _na_model()
+    enc = model.encoder
+    b = batch.to("cuda")
+    G = len(cfg.measurements_per_dep_graph_level)
+    tol = dict(rtol=1e-4, atol=1e-4)  # f32 through the decode kernel vs the training kernels
+    with torch.no_grad():
+        full = enc(b, use_cache=False).last_hidden_state
+        cached = enc(b, use_cache=True)
+        torch.testing.assert_close(cached.last_hidden_state, full, **tol)
+        L = b.sequence_length
+        k0 = 2
+        while not bool(b.event_mask[:, k0:].all()):
+            k0 += 1
+        assert k0 < L - 1, "fixture needs >= 2 events after the left padding"
+        src = b[:, :]
+        src.time = time_from_deltas(src)
+        sam = expand_mask(b.event_mask, full.dtype)
+        out = enc(src[:, :k0], use_cache=True, seq_attention_mask=sam[..., :k0], dep_graph_el_generation_target=None)
+        torch.testing.assert_close(out.last_hidden_state, full[:, :k0], **tol)
+        for lyr, (kv_full, kv_pre) in enumerate(zip(cached.past_key_values["seq_past"], out.past_key_values["seq_past"])):
+            for a, c in zip(kv_full, kv_pre):
+                torch.testing.assert_close(c, a[:, :, :k0], **tol, msg=lambda m: f"seq past layer {lyr}: {m}")
+        past, dep_past = out.past_key_values["seq_past"], out.past_key_values["dep_graph_past"]
+        assert all(k.shape[2] == 1 for k, _ in dep_past)
+        for t in range(k0, L):
+            ev = src[:, t: t + 1]
+            outs = []
+            for tgt in [*range(1, G), 0]:
+                o = enc(ev, use_cache=True, past=past, dep_graph_past=dep_past, dep_graph_el_generation_target=tgt,
+                        seq_attention_mask=sam[..., : t + 1])
+                past, dep_past = o.past_key_values["seq_past"], o.past_key_values["dep_graph_past"]
+                assert o.last_hidden_state.shape == (b.batch_size, 1, 1, cfg.hidden_size)
+                outs.append(o.last_hidden_state)
+            got = torch.cat(outs, dim=2)
+            torch.testing.assert_close(got, full[:, t: t + 1], **tol, msg=lambda m: f"event {t}: {m}")
+        # malformed calls (transformer.py:1062-1093)
+        with pytest.raises(ValueError):
+            enc(ev, use_cache=True, past=past, dep_graph_past=None, dep_graph_el_generation_target=1)
+        with pytest.raises(ValueError):
+            enc(ev, use_cache=True, past=past, dep_graph_past=dep_past, dep_graph_el_generation_target=None)
+
+
+@pytest.mark.gpu
+def test_na_generate_with_cache():
+    """NA generation through the sequence and dependency-graph caches: events appended with a TTE and their graph
+    levels filled in order, repeatable under a seed. (Cached and uncached NA generation are NOT expected to agree:
+    the reference's uncached calls with a graph target re-encode only the target's graph element,
+    transformer.py:924-929; the cached encodings are pinned to the full forward by test_na_cache_matches_full_forward.)
+    Each generated event's per-level predictions come from the cached encodings of the growing batch."""
+    model, cfg, batch = _na_model()
+    b = batch[:, :10].to("cuda")
+    runs = []
+    for _ in range(2):
+        torch.manual_seed(7)
+        runs.append(model.generate(b, max_new_events=3, use_cache=True))
+    a, c = runs
+    assert a.sequence_length == b.sequence_length + 3 and a.batch_size == b.batch_size
+    for k in ("time_delta", "dynamic_indices", "dynamic_measurement_indices", "dynamic_values", "event_mask"):
+        torch.testing.assert_close(getattr(a, k), getattr(c, k), rtol=0, atol=0, equal_nan=True)
+    et = cfg.measurements_idxmap["event_type"]
+    assert bool(((a.dynamic_measurement_indices[:, -3:] == et).sum(-1) == 1).all())
+    assert bool(torch.isfinite(a.time_delta[:, :-1]).all())
+    torch.testing.assert_close(a.dynamic_indices[:, :10, : b.n_data_elements], b.dynamic_indices)
+    # lock-step: every cached call's encoding equals the full uncached forward's (no target) at the same graph
+    # level of the growing batch's last event
+    levels = [{"time"}, *cfg.measurements_per_dep_graph_level[1:]]
+    kw = {"use_cache": True}
+    bb = b
+    torch.manual_seed(11)
+    with torch.no_grad():
+        for ev in range(2):
+            for tgt, fill in enumerate(levels):
+                t = None if (ev == 0 and tgt == 0) else tgt
+                inp = model.prepare_inputs_for_generation(bb, dep_graph_el_generation_target=t, **kw)
+                out = model(**inp, return_dict=True, is_generation=True)
+                kw["past"] = out["past_key_values"]
+                full = model.encoder(bb, use_cache=False).last_hidden_state[:, -1]
+                got = model.encoder(**{k: v for k, v in inp.items() if k not in ("output_attentions",
+                                                                                  "output_hidden_states")})
+                lvl = -1 if not t else t - 1
+                torch.testing.assert_close(got.last_hidden_state[:, -1, -1], full[:, lvl], rtol=1e-4, atol=1e-4)
+                nxt = out.preds.slice((slice(None), -1)).sample(bb.event_mask)
+                bb = (nxt.append_to_batch(bb, cfg) if fill == {"time"}
+                      else nxt.update_last_event_data(bb, cfg, measurements_to_fill=fill))
+    # malformed pasts (nested_attention_model.py:290-320)
+    with pytest.raises(ValueError):
+        model.prepare_inputs_for_generation(b, past=None, use_cache=True, dep_graph_el_generation_target=1)
+    with pytest.raises(ValueError):
+        model.prepare_inputs_for_generation(b, past=("x",), use_cache=True)
 
 
 @pytest.mark.gpu
