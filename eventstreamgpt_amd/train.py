@@ -131,18 +131,22 @@ class FusedAdamW:
                                   "weight_decay": self.weight_decay}]}
 
 
-def graph_safe(model) -> bool:
-    """True when the model's training step runs entirely through the fused CI path (capturable)."""
+def graph_safe(model, compute_dtype=torch.bfloat16) -> bool:
+    """True when the model's training step is capturable as one HIP graph: the CI model through the fused encoder,
+    or the NA model in bf16 (its blocks through fused.inner_block_fused; the structured-attention glue — where, pad,
+    cat — is stream-ordered ATen work with static shapes). Pinned by tests/test_train_paths.py's graph-vs-eager NA
+    test with host allocations between replays."""
     from .fused import fused_supported
     from .transformer.config import StructuredEventProcessingMode
 
     enc = getattr(model, "encoder", None)
     cfg = getattr(model, "config", None)
-    if enc is None or cfg is None:
+    if enc is None or cfg is None or not fused_supported(enc):
         return False
-    if cfg.structured_event_processing_mode != StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT:
-        return False
-    return fused_supported(enc)
+    mode = cfg.structured_event_processing_mode
+    if mode == StructuredEventProcessingMode.CONDITIONALLY_INDEPENDENT:
+        return True
+    return mode == StructuredEventProcessingMode.NESTED_ATTENTION and compute_dtype == torch.bfloat16
 
 
 class GradBuckets:
@@ -252,9 +256,9 @@ class TrainStep:
             self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
             self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, self.lr_lambda)
         self.grad_buckets = GradBuckets(params, self.world, bucket_mb) if self.distributed else None
-        # HIP-graph capture only for the fully fused CI step (every kernel ours). `_force_graph` is for diagnostics
-        # of the module-by-module paths (tools/na_graph_*.py).
-        self.use_graph = use_graph and (_force_graph or graph_safe(model))
+        # HIP-graph capture for the capturable steps (graph_safe). `_force_graph` is for diagnostics of the other
+        # paths (tools/na_graph_*.py).
+        self.use_graph = use_graph and (_force_graph or graph_safe(model, compute_dtype))
         self.max_graphs = max_graphs
         self.graphs: dict = {}  # shape signature -> (graph, static batch, static loss)
         self.check_errors = check_errors and dev.type == "cuda"

@@ -16,7 +16,9 @@ def test_graph_safe_selection():
     from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
 
     assert graph_safe(CIPPTForGenerativeSequenceModeling(ci))
-    assert not graph_safe(NAPPTForGenerativeSequenceModeling(na))
+    assert graph_safe(CIPPTForGenerativeSequenceModeling(ci), torch.float32)
+    assert graph_safe(NAPPTForGenerativeSequenceModeling(na))  # bf16: fused NA blocks
+    assert not graph_safe(NAPPTForGenerativeSequenceModeling(na), torch.float32)  # module path stays eager
 
 
 @pytest.mark.parametrize("warm,total,power,init,end", [(10, 100, 1.0, 1e-3, 0.0), (0, 50, 2.0, 1e-2, 1e-5),
@@ -157,7 +159,7 @@ def test_nested_attention_bf16_fused_blocks_match_module_path(name):
 
 @pytest.mark.gpu
 def test_nested_attention_graph_replay_matches_eager_with_allocations_between_replays():
-    """The NA training step captured as a HIP graph (forced: graph_safe() keeps NA eager by default) replays with
+    """The NA training step captured as a HIP graph (graph_safe: NA in bf16 is captured by default) replays with
     fresh batches while the host allocates and frees device memory between replays (so a buffer the graph uses but
     does not own would be reused and corrupted), and matches eager steps: losses every step, parameters after."""
     from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
@@ -170,7 +172,7 @@ def test_nested_attention_graph_replay_matches_eager_with_allocations_between_re
         torch.manual_seed(0)
         m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
         ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=100),
-                       torch.bfloat16, use_graph=graph, _force_graph=True)
+                       torch.bfloat16, use_graph=graph)
         losses, junk = [], []
         for i, b in enumerate(batches):
             losses.append(float(ts.step(b)))
