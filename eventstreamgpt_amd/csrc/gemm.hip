@@ -191,15 +191,24 @@ __device__ __forceinline__ float act_grad(float z, int act) {
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-constexpr int kMaxTileElems =
-    Tile<false, TILE>::kElems > Tile<true, TILE>::kElems ? Tile<false, TILE>::kElems : Tile<true, TILE>::kElems;
-constexpr int LDS_ELEMS = 4 * kMaxTileElems;  // two buffers x (A + B); also holds the reducer flag
 
 // One 64x64 output tile (4 waves as 2x2 of 32x32) of problem p; `lin` = the tile's index within the problem.
 // The MFMAs compute the tile transposed (A-operand = B fragment, B-operand = A fragment) so that a lane owns one
 // output ROW m and its registers hold columns n = (e&3) + 8(e>>2) + 4h: the epilogue stores 16 B per lane.
+// LDS of one tile's staging: two buffers x (A image + B image), sized for the operand layouts (the K-contig images
+// are smaller: the forward kernel fits 4 workgroups per CU instead of 3). Also holds the epilogue's C tile (f32:
+// 64 x 68 floats) and the split-K reducer flag.
 template <bool AKC, bool BKC>
+constexpr int lds_elems() {
+  constexpr int st = 2 * (Tile<AKC, TILE>::kElems + Tile<BKC, TILE>::kElems);
+  constexpr int epi = TILE * (TILE + 4) * 2;  // f32 C tile in bf16 elements
+  return st > epi ? st : epi;
+}
+
+template <bool AKC, bool BKC, int NS_ = NS>
 __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) {
+  constexpr int NS = NS_;
+  constexpr bool kRowSum = !(AKC && BKC);  // compiled out of the forward (K-contig x K-contig) instantiation
   using TA = Tile<AKC, TILE>;
   using TB = Tile<BKC, TILE>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -212,7 +221,7 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
   const __bf16* __restrict__ A = p.A;
   const __bf16* __restrict__ B = p.B;
-  const bool want_rs = p.rowsum != nullptr && bx == 0 && wn == 0;  // wave-uniform
+  const bool want_rs = kRowSum && p.rowsum != nullptr && bx == 0 && wn == 0;  // wave-uniform
 
   f32x16 acc, racc;
 #pragma unroll
@@ -223,8 +232,8 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
 
   bf16x8 ra[NS][TA::kChunks], rb[NS][TB::kChunks];
   auto consume = [&](int st, int i) {
-    __bf16* sA = smem + (i & 1) * 2 * kMaxTileElems;
-    __bf16* sB = sA + kMaxTileElems;
+    __bf16* sA = smem + (i & 1) * (TA::kElems + TB::kElems);
+    __bf16* sB = sA + TA::kElems;
     TA::store(sA, ra[st], m0, M, kb + i * BK, ke);
     TB::store(sB, rb[st], n0, N, kb + i * BK, ke);
     __syncthreads();
@@ -263,26 +272,25 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   // store is an sc1 (write-through) store, every storing wave drains it (vmcnt(0)) before the workgroup barrier and
   // one agent-scope ticket add; the workgroup whose add comes last reads every slab with sc1 loads. No L2
   // write-back fence: with the grouped dX product streaming its output through the same L2s, buffer_wbl2 per
-  // workgroup serialised on the dirty lines of the whole XCD.
+  // workgroup serialised on the dirty lines of the whole XCD. Slabs are lane-linear (fragment order: tile, wave,
+  // register group, lane): each wave-instruction writes / reads 1 KiB contiguously — whole lines, no partial-line
+  // write-through.
   if (p.splits > 1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(p.slab, (short)0, 0x7fffffff, 0x00020000);
     constexpr int kSC1 = 16;  // cache policy: sc1
-    const int rs_base = p.splits * M * N;  // row-sum slabs follow the tile slabs
-    if (rok) {
+    const int ntile = p.tm * p.tn;
+    const int rs_base = p.splits * ntile * TILE * TILE;  // row-sum slabs follow the tile slabs
+    auto slab_off = [&](int z, int g) { return 4 * ((((z * ntile + tile) * 4 + wave) * 4 + g) * 64 + lane) * 4; };
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = cb + 8 * g + 4 * h;
-        if (c < N) {
-          const u32x4 w = {__float_as_uint(acc[4 * g]), __float_as_uint(acc[4 * g + 1]),
-                           __float_as_uint(acc[4 * g + 2]), __float_as_uint(acc[4 * g + 3])};
-          __builtin_amdgcn_raw_buffer_store_b128(w, rs, 4 * (bz * M * N + row * N + c), 0, kSC1);
-        }
-      }
-      if (want_rs && h == 0)
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(racc[0]), rs, 4 * (rs_base + bz * M + row), 0, kSC1);
+    for (int g = 0; g < 4; ++g) {
+      const u32x4 w = {__float_as_uint(acc[4 * g]), __float_as_uint(acc[4 * g + 1]), __float_as_uint(acc[4 * g + 2]),
+                       __float_as_uint(acc[4 * g + 3])};
+      __builtin_amdgcn_raw_buffer_store_b128(w, rs, slab_off(bz, g), 0, kSC1);
     }
+    if (want_rs && rok && h == 0)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(racc[0]), rs, 4 * (rs_base + bz * M + row), 0, kSC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave's slab stores have drained (and the LDS tiles are no longer read)
     int* flag = reinterpret_cast<int*>(smem);
@@ -297,21 +305,16 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
     for (int z = 0; z < p.splits; ++z) {
-      if (rok) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = cb + 8 * g + 4 * h;
-          if (c < N) {
-            const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * (z * M * N + row * N + c), 0, kSC1);
-            acc[4 * g] += __uint_as_float(x[0]);
-            acc[4 * g + 1] += __uint_as_float(x[1]);
-            acc[4 * g + 2] += __uint_as_float(x[2]);
-            acc[4 * g + 3] += __uint_as_float(x[3]);
-          }
-        }
-        if (want_rs)
-          racc[0] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (rs_base + z * M + row), 0, kSC1));
+      for (int g = 0; g < 4; ++g) {
+        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(z, g), 0, kSC1);
+        acc[4 * g] += __uint_as_float(x[0]);
+        acc[4 * g + 1] += __uint_as_float(x[1]);
+        acc[4 * g + 2] += __uint_as_float(x[2]);
+        acc[4 * g + 3] += __uint_as_float(x[3]);
       }
+      if (want_rs && rok)
+        racc[0] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (rs_base + z * M + row), 0, kSC1));
     }
   }
 
@@ -329,13 +332,26 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     v[4 * g + 2] = acc[4 * g + 2] * al + bv.z;
     v[4 * g + 3] = acc[4 * g + 3] * al + bv.w;
   }
+  // The tile goes out through LDS (the staging buffers are free once every wave is past its last fragment read):
+  // written in fragment order, stored row-major with 16-B chunks, each wave-instruction covering whole 128-B lines
+  // (8 rows x 128 B in bf16, 4 rows x 256 B in f32) instead of 32-B pieces of 32 rows.
+  const int rl = wm * 32 + r, cl = wn * 32;  // this lane's row / first column within the tile
+  __syncthreads();
   if (p.out_f32) {
+    constexpr int kLd = TILE + 4;  // f32 row pitch (floats): 16-B aligned, conflict-free fragment writes
+    float* t = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int c = cb + 8 * g + 4 * h;
-      if (!rok || c >= N) continue;
-      float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)row * p.ldc + c);
-      float4 w = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(t + rl * kLd + cl + 8 * g + 4 * h) =
+          make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TILE * TILE / 4 / THREADS; ++i) {
+      const int ch = threadIdx.x + THREADS * i, tr = ch / (TILE / 4), tc = (ch % (TILE / 4)) * 4;
+      const int gr = m0 + tr, gc = n0 + tc;
+      if (gr >= M || gc >= N) continue;
+      float4 w = *reinterpret_cast<const float4*>(t + tr * kLd + tc);
+      float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)gr * p.ldc + gc);
       if (p.accumulate) {
         const float4 o = *q;
         w.x += o.x;
@@ -360,6 +376,22 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
       }
     }
   }
+  constexpr int kLdB = TILE + 8;  // bf16 row pitch (elements): 144 B, conflict-free 8-B fragment writes
+  __bf16* tb = smem;
+  // one bf16 tile out: fragment-order LDS writes, barrier, row-major 16-B chunk stores
+  auto store_tile = [&](const uint32_t (&d)[4][2], __bf16* dst, int64_t ld) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<uint2*>(tb + rl * kLdB + cl + 8 * g + 4 * h) = make_uint2(d[g][0], d[g][1]);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TILE * TILE / 8 / THREADS; ++i) {
+      const int ch = threadIdx.x + THREADS * i, tr = ch / (TILE / 8), tc = (ch % (TILE / 8)) * 8;
+      const int gr = m0 + tr, gc = n0 + tc;
+      if (gr < M && gc < N)
+        *reinterpret_cast<uint4*>(dst + (int64_t)gr * ld + gc) = *reinterpret_cast<const uint4*>(tb + tr * kLdB + tc);
+    }
+  };
   uint32_t d[4][2];
   if (p.epi == EPI_BIAS_ACT) {
     // store the pre-activation (bf16: the value the activation and its gradient see), then activate it
@@ -372,38 +404,32 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
       v[4 * g + 2] = act_fwd(bf16_lo(d[g][1]), p.act);
       v[4 * g + 3] = act_fwd(bf16_hi(d[g][1]), p.act);
     }
-#pragma unroll
-    for (int g = 0; g < 4; g += 2) {
-      const auto s0 = __builtin_amdgcn_permlane32_swap(d[g][0], d[g + 1][0], false, false);
-      const auto s1 = __builtin_amdgcn_permlane32_swap(d[g][1], d[g + 1][1], false, false);
-      const int c = cb + 8 * g + 8 * h;
-      if (rok && c < N)
-        *reinterpret_cast<uint4*>(p.aux_out + (int64_t)row * p.ld_aux + c) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-    }
+    store_tile(d, p.aux_out, p.ld_aux);
+    __syncthreads();  // the LDS tile is rewritten below
   }
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
     d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
   }
-#pragma unroll
-  for (int g = 0; g < 4; g += 2) {
-    // lanes 0-31: columns 8g..8g+7 (own group g | upper half's group g);
-    // lanes 32-63: columns 8g+8..8g+15 (lower half's group g+1 | own group g+1)
-    const auto s0 = __builtin_amdgcn_permlane32_swap(d[g][0], d[g + 1][0], false, false);
-    const auto s1 = __builtin_amdgcn_permlane32_swap(d[g][1], d[g + 1][1], false, false);
-    const int c = cb + 8 * g + 8 * h;
-    if (rok && c < N)
-      *reinterpret_cast<uint4*>(reinterpret_cast<__bf16*>(p.C) + (int64_t)row * p.ldc + c) =
-          make_uint4(s0[0], s1[0], s0[1], s1[1]);
-  }
+  store_tile(d, reinterpret_cast<__bf16*>(p.C), p.ldc);
 }
 
-template <bool AKC, bool BKC>
+template <bool AKC, bool BKC, int NS_ = NS>
 __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[LDS_ELEMS];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC>()];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile<AKC, BKC>(p, lin, smem);
+  gemm_tile<AKC, BKC, NS_>(p, lin, smem);
+}
+
+// Forward register-stage depth (2 or 3; ESGPT_GEMM_FWD_NS tuning hook, read once).
+int fwd_stages() {
+  static int ns = 0;
+  if (ns == 0) {
+    const char* e = getenv("ESGPT_GEMM_FWD_NS");
+    ns = (e && atoi(e) == 2) ? 2 : 3;
+  }
+  return ns;
 }
 
 // A projection's backward in one launch: problem 0 = dX (A = dY K-contig, B = W N-contig), problem 1 = dW (A = dYᵀ
@@ -411,7 +437,9 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
 // p0.wg0 workgroup ids, so the dispatcher deals them round-robin over all 8 XCDs first and the short dX tiles
 // fill in behind them; each problem keeps its own XCD-aware order within its id range.
 __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[LDS_ELEMS];
+  constexpr int kLds = lds_elems<false, false>() > lds_elems<true, false>() ? lds_elems<false, false>()
+                                                                             : lds_elems<true, false>();
+  __shared__ __attribute__((aligned(16))) __bf16 smem[kLds];
   const int id = blockIdx.x, n1 = p0.wg0;
   if (id < n1)
     gemm_tile<false, false>(p1, xcd_remap(id, n1), smem);
@@ -470,8 +498,11 @@ Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M
   return p;
 }
 
+// Split-K slabs: [splits][tiles][64 x 64] f32 in fragment order, then [splits][M] row sums.
 size_t slab_bytes(int64_t splits, int64_t M, int64_t N) {
-  return splits > 1 ? sizeof(float) * ((size_t)splits * M * N + (size_t)splits * M) : 0;
+  return splits > 1 ? sizeof(float) * ((size_t)splits * cdiv(M, TILE) * cdiv(N, TILE) * TILE * TILE +
+                                       (size_t)splits * M)
+                    : 0;
 }
 
 int n_wg(const Prob& p) { return p.tm * p.tn * p.splits; }
@@ -551,7 +582,8 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
     p.aux_out = reinterpret_cast<__bf16*>(pre);
     p.ld_aux = ldy;
   }
-  gemm_kernel<true, true><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
+  if (fwd_stages() == 2) gemm_kernel<true, true, 2><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
+  else gemm_kernel<true, true><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
