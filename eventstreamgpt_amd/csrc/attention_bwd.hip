@@ -248,6 +248,31 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
         constexpr float kLog2e = 1.4426950408889634f;
         // fully visible slice: every key of the wave valid and inside the causal / local band of every query
         const bool full = __ballot(kvalid) == ~0ull && qpos_lo >= kw0 + 31 && (window == 0 || qpos_hi - kw0 < window);
+        float zk[16];  // dropout multipliers of this lane's (query row, key) elements
+        if (DROP) {
+          if ((Lk & 1) == 0 && (kw0 & 1) == 0) {
+            // lanes r, r^1 hold keys 2j, 2j+1 (one hash pair) of the same query rows: for each pair of rows the
+            // even lane hashes the first row, the odd lane the second, and they swap hashes (one hash per element
+            // pair instead of per element)
+            const int odd = key & 1;
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+              const int ql = 32 * qs + acc_row(i + odd, h);
+              const uint64_t e = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)(q0 + ql)) * (uint64_t)Lk + (uint64_t)(key - odd);
+              const uint32_t mine = dropout_hash(dr.key, e >> 1);
+              const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+              const uint32_t ha = odd ? other : mine, hb = odd ? mine : other;
+              const uint32_t ua = odd ? (ha >> 16) : (ha & 0xffffu), ub = odd ? (hb >> 16) : (hb & 0xffffu);
+              zk[i] = ua >= dr.thresh ? dr.scale : 0.f;
+              zk[i + 1] = ub >= dr.thresh ? dr.scale : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              zk[i] = dropout_mult(dr, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)(q0 + 32 * qs + acc_row(i, h))) *
+                                           (uint64_t)Lk + (uint64_t)key);
+          }
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int ql = 32 * qs + acc_row(i, h);
@@ -256,8 +281,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
           const bool ok = full | (kvalid & (key <= qpos) & ((window == 0) | (qpos - key < window)));
           const float p = ok ? e : 0.f;
           if (DROP) {
-            const float z = dropout_mult(dr, ((uint64_t)bh * (uint64_t)Lq + (uint64_t)(q0 + ql)) * (uint64_t)Lk +
-                                                 (uint64_t)key);
+            const float z = zk[i];
             const float dl = sDl[ql];
             s[i] = p * z;                          // P∘Z (feeds dV)
             dp[i] = p * (z * (dp[i] + dl) - dl);   // dS

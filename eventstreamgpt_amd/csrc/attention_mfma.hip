@@ -245,8 +245,28 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(s[c][i] - msub);  // exp2(-inf) = 0
         rs += p;  // normaliser over undropped probabilities
-        s[c][i] = DROP ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, qi, t0 + 32 * c + acc_row(i, h))) : p;
+        s[c][i] = p;
       }
+    if (DROP) {
+      // registers (i, i+1), i even, hold consecutive keys: one hash per pair when the pair is aligned
+      const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+      const bool aligned = (rowbase & 1) == 0;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 16; i += 2) {
+          const uint64_t e = rowbase + (uint64_t)(t0 + 32 * c + acc_row(i, h));
+          float m0, m1;
+          if (aligned) {
+            dropout_mult2(dr, e, m0, m1);
+          } else {
+            m0 = dropout_mult(dr, e);
+            m1 = dropout_mult(dr, e + 1);
+          }
+          s[c][i] *= m0;
+          s[c][i + 1] *= m1;
+        }
+    }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
     m = mnew;

@@ -95,13 +95,15 @@ __device__ __forceinline__ void set_bad_index(int32_t* err, int64_t idx) {
 }
 
 // Dropout (attention probabilities, residual / input): a counter-based hash of (seed, element index), so the
-// forward and backward regenerate the same keep-mask without storing it. 32-bit arithmetic only (no 64-bit
-// multiplies in the hot loops): key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)) once per kernel, then per
-// element h = mix32(idx_lo ^ key ^ idx_hi * 0x9E3779B9) ("lowbias32" finaliser); keep <=> h >= p * 2^32.
+// forward and backward regenerate the same keep-mask without storing it. One hash per PAIR of elements: element idx
+// takes the 16-bit half (idx & 1) of h = mix32(pair_lo ^ key ^ pair_hi * 0x9E3779B9), pair = idx >> 1 ("lowbias32"
+// finaliser; key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)) once per kernel); keep <=> half >= thresh =
+// round(p * 2^16) (drop probability quantised to 2^-16; kept values scaled by 1 / (1 - p)). Two integer multiplies
+// (quarter-rate on CDNA) per two elements; the hot loops take both halves of one hash (dropout_mult2).
 struct DropoutSpec {
   float p;          // drop probability (0 = off)
   float scale;      // 1 / (1 - p)
-  uint32_t thresh;  // p * 2^32
+  uint32_t thresh;  // round(p * 2^16)
   uint32_t key;
 };
 
@@ -118,19 +120,29 @@ __host__ __device__ __forceinline__ uint32_t dropout_key(uint64_t seed) {
   return mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) ^ 0x9E3779B9u));
 }
 
-__host__ __device__ __forceinline__ uint32_t dropout_hash(uint32_t key, uint64_t idx) {
-  return mix32((uint32_t)idx ^ key ^ ((uint32_t)(idx >> 32) * 0x9E3779B9u));
+// 32 random bits for the element pair (2 * pair, 2 * pair + 1)
+__host__ __device__ __forceinline__ uint32_t dropout_hash(uint32_t key, uint64_t pair) {
+  return mix32((uint32_t)pair ^ key ^ ((uint32_t)(pair >> 32) * 0x9E3779B9u));
 }
 
 __device__ __forceinline__ float dropout_mult(const DropoutSpec& d, uint64_t idx) {
-  return (dropout_hash(d.key, idx) >= d.thresh) ? d.scale : 0.f;
+  const uint32_t hh = dropout_hash(d.key, idx >> 1);
+  const uint32_t half = (idx & 1) ? (hh >> 16) : (hh & 0xffffu);
+  return half >= d.thresh ? d.scale : 0.f;
+}
+
+// Both elements of the pair starting at the EVEN index idx: m0 for idx, m1 for idx + 1.
+__device__ __forceinline__ void dropout_mult2(const DropoutSpec& d, uint64_t idx, float& m0, float& m1) {
+  const uint32_t hh = dropout_hash(d.key, idx >> 1);
+  m0 = (hh & 0xffffu) >= d.thresh ? d.scale : 0.f;
+  m1 = (hh >> 16) >= d.thresh ? d.scale : 0.f;
 }
 
 __device__ __forceinline__ DropoutSpec make_dropout(float p, const uint64_t* seed_ptr) {
   DropoutSpec d;
   d.p = p;
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  d.thresh = p > 0.f ? (uint32_t)fminf(p * 4294967296.f, 4294967295.f) : 0u;
+  d.thresh = p > 0.f ? (uint32_t)fminf(rintf(p * 65536.f), 65536.f) : 0u;
   d.key = dropout_key((p > 0.f && seed_ptr) ? *seed_ptr : 0ull);
   return d;
 }

@@ -84,10 +84,15 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
       if (x) v[k] = load4(x + row * D + c);
       if (y) {
         V4 t = load4(y + row * D + c);
+        float z[4] = {1.f, 1.f, 1.f, 1.f};
+        if (dr.p > 0.f) {  // row * D + c is even (D % 4 == 0): two element pairs
+          dropout_mult2(dr, drop_idx(row, D, c), z[0], z[1]);
+          dropout_mult2(dr, drop_idx(row, D, c + 2), z[2], z[3]);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           float u = t.v[j] + (bias ? bias[c + j] : 0.f);
-          if (dr.p > 0.f) u *= dropout_mult(dr, drop_idx(row, D, c + j));
+          if (dr.p > 0.f) u *= z[j];
           v[k].v[j] += u;
         }
       }
@@ -207,9 +212,14 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
         if (dx) store4(dx + row * D + c, d);
         if (dy) {
           V4 e;
+          float z[4] = {1.f, 1.f, 1.f, 1.f};
+          if (dr.p > 0.f) {
+            dropout_mult2(dr, drop_idx(row, D, c), z[0], z[1]);
+            dropout_mult2(dr, drop_idx(row, D, c + 2), z[2], z[3]);
+          }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            e.v[j] = dr.p > 0.f ? d.v[j] * dropout_mult(dr, drop_idx(row, D, c + j)) : d.v[j];
+            e.v[j] = dr.p > 0.f ? d.v[j] * z[j] : d.v[j];
             py[k].v[j] += e.v[j];
           }
           store4(dy + row * D + c, e);

@@ -221,18 +221,21 @@ def _np_mix32(x):
 
 
 def _np_keep(seed: int, B: int, H: int, Lq: int, Lk: int, p: float):
-    """Host restatement of the kernels' dropout keep-mask (csrc/common.h dropout_hash: lowbias32 of
-    idx_lo ^ key ^ idx_hi * 0x9E3779B9, key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)), idx = (bh*Lq+i)*Lk+j)."""
+    """Host restatement of the kernels' dropout keep-mask (csrc/common.h: element idx = (bh*Lq+i)*Lk+j takes the
+    16-bit half (idx & 1) of lowbias32(pair_lo ^ key ^ pair_hi * 0x9E3779B9), pair = idx >> 1,
+    key = mix32(seed_lo ^ mix32(seed_hi ^ 0x9E3779B9)); kept iff half >= round(p * 2^16))."""
     import numpy as np
 
     with np.errstate(over="ignore"):
         key = _np_mix32(np.uint64(seed & 0xFFFFFFFF) ^ _np_mix32(np.uint64(((seed >> 32) ^ 0x9E3779B9) & 0xFFFFFFFF)))
         idx = np.arange(B * H * Lq * Lk, dtype=np.uint64)
-        lo = idx & np.uint64(0xFFFFFFFF)
-        hi = ((idx >> np.uint64(32)) * np.uint64(0x9E3779B9)) & np.uint64(0xFFFFFFFF)
+        pair = idx >> np.uint64(1)
+        lo = pair & np.uint64(0xFFFFFFFF)
+        hi = ((pair >> np.uint64(32)) * np.uint64(0x9E3779B9)) & np.uint64(0xFFFFFFFF)
         h = _np_mix32(lo ^ key ^ hi)
-    thresh = int(np.float32(p) * np.float32(4294967296.0))
-    return torch.from_numpy((h >= thresh).reshape(B, H, Lq, Lk))
+        half = np.where((idx & np.uint64(1)) == 1, h >> np.uint64(16), h & np.uint64(0xFFFF))
+    thresh = int(np.rint(np.float32(p) * np.float32(65536.0)))
+    return torch.from_numpy((half >= thresh).reshape(B, H, Lq, Lk))
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
