@@ -21,6 +21,7 @@
 // MFMA v_mfma_f32_32x32x16_bf16; register-staged global->LDS with NS-1 k-tiles in flight during the MFMAs.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -108,6 +109,32 @@ struct Tile {
     }
   }
 
+  // Fast path (whole tiles, operand < 2 GiB): per-lane byte offsets within a k-tile computed once; each k-tile
+  // is one uniform (SGPR) offset on buffer loads — no per-chunk address math, clamps or zero selects.
+  __device__ __forceinline__ static void lane_offsets(int (&vo)[kChunks], int64_t ld, int row0) {
+#pragma unroll
+    for (int i = 0; i < kChunks; ++i) {
+      int a, b;
+      coords(i, a, b);
+      vo[i] = KC ? (int)(((int64_t)(row0 + a) * ld + b) * 2) : (int)(((int64_t)a * ld + row0 + b) * 2);
+    }
+  }
+  __device__ __forceinline__ static int k_offset(int k0, int64_t ld) { return KC ? k0 * 2 : (int)(k0 * ld * 2); }
+  __device__ __forceinline__ static void load_fast(bf16x8 (&reg)[kChunks], __amdgpu_buffer_rsrc_t rs,
+                                                   const int (&vo)[kChunks], int so) {
+#pragma unroll
+    for (int i = 0; i < kChunks; ++i)
+      reg[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, vo[i], so, 0));
+  }
+  __device__ __forceinline__ static void store_fast(__bf16* s, const bf16x8 (&reg)[kChunks]) {
+#pragma unroll
+    for (int i = 0; i < kChunks; ++i) {
+      int a, b;
+      coords(i, a, b);
+      *reinterpret_cast<bf16x8*>(s + a * (KC ? KC_LD : MN_LD) + b) = reg[i];
+    }
+  }
+
   // MFMA operand fragment for rows sub0 .. sub0+31 of the tile and k-step t (k = 16t .. 16t+15):
   // lane (r = l&31, h = l>>5) gets row sub0 + r, k = 16t + 8h + j, j = 0..7.
   __device__ __forceinline__ static bf16x8 frag(const __bf16* s, int sub0, int t) {
@@ -160,8 +187,10 @@ struct Prob {
   __bf16* aux_out;     // EPI_BIAS_ACT: pre-activation output [M][ld_aux]
   int64_t ld_aux;
   float* rowsum;       // optional [M] f32: alpha · Σ_k A[m][k] (the bias gradient of a dW product)
-  float* slab;         // split-K: f32 [splits][M][N] (+ [splits][M] row sums)
-  int* counters;       // split-K: one zeroed ticket per tile (left zeroed)
+  float* slab;         // split-K: f32 [splits][tiles][64 x 64] fragment order (+ [splits][M] row sums)
+  int* counters;       // split-K, in-launch reduction: one zeroed ticket per tile (left zeroed)
+  int ext_reduce;      // split-K: slabs summed by slab_reduce_kernel (a second launch) instead of in-launch
+  int fast;            // A and B each < 2 GiB: whole tiles take the buffer-load fast path
 };
 
 __device__ __forceinline__ float act_fwd(float z, int act) {
@@ -231,37 +260,73 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
   bf16x8 ra[NS][TA::kChunks], rb[NS][TB::kChunks];
-  auto consume = [&](int st, int i) {
-    __bf16* sA = smem + (i & 1) * (TA::kElems + TB::kElems);
-    __bf16* sB = sA + TA::kElems;
-    TA::store(sA, ra[st], m0, M, kb + i * BK, ke);
-    TB::store(sB, rb[st], n0, N, kb + i * BK, ke);
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < BK / 16; ++t) {
-      const bf16x8 af = TA::frag(sA, wm * 32, t);
-      const bf16x8 bfr = TB::frag(sB, wn * 32, t);
-      acc = mfma(bfr, af, acc);
-      if (want_rs) racc = mfma(ones, af, racc);
+  // the k loop in four compiled forms: whole tile or edge tile x with or without the bias-gradient MFMA (both
+  // conditions workgroup- / wave-uniform, decided once)
+  auto mainloop = [&](auto fast_c, auto rs_c) {
+    constexpr bool FAST = decltype(fast_c)::value, RS = decltype(rs_c)::value;
+    int voA[TA::kChunks], voB[TB::kChunks];
+    __amdgpu_buffer_rsrc_t rsA, rsB;
+    if constexpr (FAST) {
+      TA::lane_offsets(voA, p.lda, m0);
+      TB::lane_offsets(voB, p.ldb, n0);
+      rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
+      rsB = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
     }
+    const int klast = ke - BK;  // FAST: prefetches past the range re-read the last k-tile (never consumed)
+    auto load = [&](int st, int i) {
+      const int k0 = kb + i * BK;
+      if constexpr (FAST) {
+        const int kk = min(k0, klast);
+        TA::load_fast(ra[st], rsA, voA, TA::k_offset(kk, p.lda));
+        TB::load_fast(rb[st], rsB, voB, TB::k_offset(kk, p.ldb));
+      } else {
+        TA::load(ra[st], A, p.lda, m0, M, k0, ke);
+        TB::load(rb[st], B, p.ldb, n0, N, k0, ke);
+      }
+    };
+    auto consume = [&](int st, int i) {
+      __bf16* sA = smem + (i & 1) * (TA::kElems + TB::kElems);
+      __bf16* sB = sA + TA::kElems;
+      if constexpr (FAST) {
+        TA::store_fast(sA, ra[st]);
+        TB::store_fast(sB, rb[st]);
+      } else {
+        TA::store(sA, ra[st], m0, M, kb + i * BK, ke);
+        TB::store(sB, rb[st], n0, N, kb + i * BK, ke);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < BK / 16; ++t) {
+        const bf16x8 af = TA::frag(sA, wm * 32, t);
+        const bf16x8 bfr = TB::frag(sB, wn * 32, t);
+        acc = mfma(bfr, af, acc);
+        if constexpr (RS) racc = mfma(ones, af, racc);
+      }
+    };
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st) load(st, st);
+    int i0 = 0;
+    for (; i0 + NS <= nk; i0 += NS) {
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        load((st + NS - 1) % NS, i0 + st + NS - 1);
+        consume(st, i0 + st);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+      if (i0 + st < nk) consume(st, i0 + st);
   };
-#pragma unroll
-  for (int st = 0; st < NS - 1; ++st) {
-    TA::load(ra[st], A, p.lda, m0, M, kb + st * BK, ke);
-    TB::load(rb[st], B, p.ldb, n0, N, kb + st * BK, ke);
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const bool fast = p.fast && m0 + TILE <= M && n0 + TILE <= N && nk > 0 && (ke - kb) % BK == 0;
+  if (fast) {
+    if (want_rs) mainloop(T_{}, T_{});
+    else mainloop(T_{}, F_{});
+  } else {
+    if (want_rs) mainloop(F_{}, T_{});
+    else mainloop(F_{}, F_{});
   }
-  int i0 = 0;
-  for (; i0 + NS <= nk; i0 += NS) {
-#pragma unroll
-    for (int st = 0; st < NS; ++st) {
-      TA::load(ra[(st + NS - 1) % NS], A, p.lda, m0, M, kb + (i0 + st + NS - 1) * BK, ke);
-      TB::load(rb[(st + NS - 1) % NS], B, p.ldb, n0, N, kb + (i0 + st + NS - 1) * BK, ke);
-      consume(st, i0 + st);
-    }
-  }
-#pragma unroll
-  for (int st = 0; st < NS - 1; ++st)
-    if (i0 + st < nk) consume(st, i0 + st);
 
   const int row = m0 + wm * 32 + r;
   const bool rok = row < M;
@@ -275,6 +340,16 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   // workgroup serialised on the dirty lines of the whole XCD. Slabs are lane-linear (fragment order: tile, wave,
   // register group, lane): each wave-instruction writes / reads 1 KiB contiguously — whole lines, no partial-line
   // write-through.
+  if (p.splits > 1 && p.ext_reduce) {
+    // slabs only (plain stores: the kernel boundary orders them before slab_reduce_kernel)
+    const int ntile = p.tm * p.tn;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<float4*>(p.slab + ((((int64_t)bz * ntile + tile) * 4 + wave) * 4 + g) * 256 + 4 * lane) =
+          make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+    if (want_rs && rok && h == 0) p.slab[(int64_t)p.splits * ntile * TILE * TILE + (int64_t)bz * M + row] = racc[0];
+    return;
+  }
   if (p.splits > 1) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t rs =
@@ -304,17 +379,33 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     if (!*flag) return;
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
-    for (int z = 0; z < p.splits; ++z) {
+    // slabs in batches of kRB: every load of a batch in flight before the (z-ordered, deterministic) adds — one
+    // memory round trip per batch instead of one per slab
+    constexpr int kRB = 4;
+    for (int z0 = 0; z0 < p.splits; z0 += kRB) {
+      u32x4 x[kRB][4];
+      float rv[kRB];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(z, g), 0, kSC1);
-        acc[4 * g] += __uint_as_float(x[0]);
-        acc[4 * g + 1] += __uint_as_float(x[1]);
-        acc[4 * g + 2] += __uint_as_float(x[2]);
-        acc[4 * g + 3] += __uint_as_float(x[3]);
+      for (int u = 0; u < kRB; ++u) {
+        const int z = min(z0 + u, p.splits - 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) x[u][g] = __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(z, g), 0, kSC1);
+        rv[u] = (want_rs && rok)
+                    ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (rs_base + z * M + row), 0, kSC1))
+                    : 0.f;
       }
-      if (want_rs && rok)
-        racc[0] += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (rs_base + z * M + row), 0, kSC1));
+#pragma unroll
+      for (int u = 0; u < kRB; ++u) {
+        if (z0 + u >= p.splits) break;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          acc[4 * g] += __uint_as_float(x[u][g][0]);
+          acc[4 * g + 1] += __uint_as_float(x[u][g][1]);
+          acc[4 * g + 2] += __uint_as_float(x[u][g][2]);
+          acc[4 * g + 3] += __uint_as_float(x[u][g][3]);
+        }
+        racc[0] += rv[u];
+      }
     }
   }
 
@@ -447,6 +538,84 @@ __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1
     gemm_tile<true, false>(p0, xcd_remap(id - n1, gridDim.x - n1), smem);
 }
 
+// Split-K reduction as its own launch (large slab sets: one last-arriving workgroup reading every slab of its tile
+// is a serial memory-latency chain on one CU; here every CU takes a share). f32 output, plain store epilogue (the
+// weight-gradient products): thread = one 16-B fragment chunk (tile, wave, register group, lane) of the output,
+// summing its splits in z order (deterministic), then alpha, bias, accumulate, and the 4 columns stored; threads
+// past the tiles sum the row-sum slabs into p.rowsum.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(Prob p) {
+  const int64_t ntile = (int64_t)p.tm * p.tn, nch = ntile * TILE * TILE / 4;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float al = p.alpha ? *p.alpha : 1.f;
+  if (t < nch) {
+    const int lane = (int)(t & 63), g = (int)((t >> 6) & 3), wave = (int)((t >> 8) & 3);
+    const int64_t tile = t >> 10;
+    const int bx = (int)(tile % p.tn), by = (int)(tile / p.tn);
+    const int row = by * TILE + (wave >> 1) * 32 + (lane & 31);
+    const int col = bx * TILE + (wave & 1) * 32 + 8 * g + 4 * (lane >> 5);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    constexpr int kU = 8;
+    for (int z0 = 0; z0 < p.splits; z0 += kU) {
+      float4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int z = min(z0 + u, p.splits - 1);
+        v[u] = *reinterpret_cast<const float4*>(p.slab + ((int64_t)z * nch + t) * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (z0 + u >= p.splits) break;
+        a.x += v[u].x;
+        a.y += v[u].y;
+        a.z += v[u].z;
+        a.w += v[u].w;
+      }
+    }
+    if (row < p.M && col < p.N) {
+      float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)row * p.ldc + col);
+      float4 w = make_float4(a.x * al, a.y * al, a.z * al, a.w * al);
+      if (p.bias) {
+        const float4 b = *reinterpret_cast<const float4*>(p.bias + col);
+        w.x += b.x;
+        w.y += b.y;
+        w.z += b.z;
+        w.w += b.w;
+      }
+      if (p.accumulate) {
+        const float4 o = *q;
+        w.x += o.x;
+        w.y += o.y;
+        w.z += o.z;
+        w.w += o.w;
+      }
+      *q = w;
+    }
+  } else if (p.rowsum && t - nch < p.M) {
+    const int64_t m = t - nch;
+    const float* rs = p.slab + (int64_t)p.splits * ntile * TILE * TILE;
+    float a = 0.f;
+    for (int z = 0; z < p.splits; ++z) a += rs[(int64_t)z * p.M + m];
+    p.rowsum[m] = a * al;
+  }
+}
+
+void launch_slab_reduce(const Prob& p, hipStream_t st) {
+  const int64_t n = (int64_t)p.tm * p.tn * TILE * TILE / 4 + (p.rowsum ? p.M : 0);
+  slab_reduce_kernel<<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
+}
+
+// Slab sets above this many splits are reduced by slab_reduce_kernel (f32 outputs without an epilogue); smaller
+// ones by the tile's last-arriving workgroup (ESGPT_GEMM_INLAUNCH_SPLITS tuning hook, read once; measured at C2:
+// in-launch for the grouped backward pairs (8 splits) is 0.09 ms per step faster than the separate launch).
+int in_launch_splits() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ESGPT_GEMM_INLAUNCH_SPLITS");
+    v = e ? std::max(1, atoi(e)) : 32;
+  }
+  return v;
+}
+
 struct Plan {
   int splits, kchunk;
 };
@@ -495,6 +664,9 @@ Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M
   p.accumulate = accumulate;
   p.bias = bias;
   p.alpha = alpha;
+  // operand extents in bytes (K-contig: rows x ld; M/N-contig: K rows x ld) within the 32-bit buffer offsets
+  const int64_t lim = (int64_t)1 << 31;
+  p.fast = (std::max(M, K) * lda * 2 < lim && std::max(N, K) * ldb * 2 < lim) ? 1 : 0;
   return p;
 }
 
@@ -553,7 +725,8 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   if (M == 0 || N == 0) return ESGPT_OK;
   Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget);
   if (p.splits > 1) {
-    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N) && counters);
+    p.ext_reduce = f32 && p.splits > in_launch_splits();
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N) && (p.ext_reduce || counters));
     ESGPT_REQUIRE(slab_bytes(p.splits, M, N) < (1ull << 31));  // 32-bit buffer offsets
     p.slab = reinterpret_cast<float*>(workspace);
     p.counters = counters;
@@ -564,6 +737,7 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   else if (akc) gemm_kernel<true, false><<<grid, THREADS, 0, st>>>(p);
   else if (bkc) gemm_kernel<false, true><<<grid, THREADS, 0, st>>>(p);
   else gemm_kernel<false, false><<<grid, THREADS, 0, st>>>(p);
+  if (p.ext_reduce) launch_slab_reduce(p, st);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
@@ -622,7 +796,8 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
   Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in));
   p1.rowsum = db;
   if (p1.splits > 1) {
-    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in) && counters);
+    p1.ext_reduce = p1.splits > in_launch_splits();
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in) && (p1.ext_reduce || counters));
     ESGPT_REQUIRE(slab_bytes(p1.splits, out, in) < (1ull << 31));  // 32-bit buffer offsets
     p1.slab = reinterpret_cast<float*>(workspace);
     p1.counters = counters;
@@ -633,6 +808,7 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
   } else {
     gemm_kernel<false, false><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
   }
+  if (p1.ext_reduce) launch_slab_reduce(p1, st);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
