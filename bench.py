@@ -367,7 +367,7 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_c
     add("attn_bwd", f"attn_bwd_kernel<{hd}, {drop}>", "mfma", 8.0 * H * hd * T_pairs, ba,
         {"shape": f"C2 layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"})
     gf, gb, _keep_g = _gemm_launchers(B * Lq, D, F, dev)
-    add("gemm_fc_fwd", "gemm_kernel<true, true>", "mfma", 2.0 * B * Lq * D * F, gf,
+    add("gemm_fc_fwd", "gemm_kernel<true, true, 3>", "mfma", 2.0 * B * Lq * D * F, gf,
         {"shape": f"c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"})
     add("gemm_fc_bwd", "gemm_bwd_pair_kernel", "mfma", 4.0 * B * Lq * D * F, gb,
         {"shape": f"c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"})
@@ -380,7 +380,8 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_c
 
     add("embed_joint_fwd", "embed_joint_fwd_kernel<4, 1>", "hbm", embed_fwd_bytes(batch, cfg), emb_fwd)
     eb, _keep_eb = _embed_bwd_launcher(model, batch)
-    add("embed_joint_bwd", "bag_count/scan/fill/reduce/subject kernels (esgpt_embed_bag_bwd)", "hbm",
+    add("embed_joint_bwd", "bag_block_sort/col_prefix/row_scan/scatter/reduce/combine/subject kernels "
+        "(esgpt_embed_bag_bwd)", "hbm",
         embed_bwd_bytes(batch, cfg), eb, {"traffic_key": "embed_bag_bwd"})
     lf, lbytes, _keep_lf = _loss_launcher(model, batch)
     add("output_loss", "count + event + reduce kernels (esgpt_output_loss)", "hbm", lbytes, lf,

@@ -15,23 +15,51 @@ import sys
 from collections import defaultdict
 
 SYMBOLS = ["attn_fwd_mfma_kernel<64, true>", "attn_fwd_mfma_kernel<64, false>", "attn_bwd_kernel<64, true>",
-           "gemm_kernel<true, true>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>",
+           "gemm_kernel<true, true, 3>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>",
            "attn_decode_kernel<float, 64>"]
 # kernels launched at several shapes by bench.py: keyed "<symbol>@grid<work-items>"
 BY_GRID = {"attn_decode_kernel<float, 64>"}
+# the C5 embedding microbench runs the JOINT kernel on a grid far larger than C2's: its dispatches are keyed "@c5"
+C5_GRID_MIN = 4 << 20
+# multi-kernel launch sets: bytes per set = the sum over the member kernels' dispatches / the anchor's dispatches
+GROUPS = {
+    "embed_bag_bwd": (["bag_block_sort_kernel", "bag_col_prefix_kernel", "bag_row_scan_kernel", "bag_scatter_kernel",
+                       "bag_reduce_kernel", "bag_combine_kernel", "bag_subject_part_kernel", "bag_subject_sum_kernel"],
+                      "bag_block_sort_kernel"),
+    "output_loss": (["::count_kernel(", "::event_lds_kernel<", "::event_kernel<", "::reduce_kernel(float const*"],
+                    "::count_kernel("),
+}
 
 
 def averages(d: str, counter: str) -> dict:
     acc = defaultdict(list)
+    group_sum = defaultdict(float)
+    group_n = defaultdict(int)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
+            name, val = r["Kernel_Name"], float(r["Counter_Value"])
+            grid = int(r.get("Grid_Size", 0) or 0)
             for s in SYMBOLS:
-                if s in r["Kernel_Name"]:
-                    key = f"{s}@grid{r.get('Grid_Size', '?')}" if s in BY_GRID else s
-                    acc[key].append(float(r["Counter_Value"]))
-    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+                if s in name:
+                    if s in BY_GRID:
+                        key = f"{s}@grid{r.get('Grid_Size', '?')}"
+                    elif s.startswith("embed_joint_fwd_kernel") and grid >= C5_GRID_MIN:
+                        key = "embed_joint_fwd_kernel@c5"
+                    else:
+                        key = s
+                    acc[key].append(val)
+            for g, (members, anchor) in GROUPS.items():
+                if any(m in name for m in members):
+                    group_sum[g] += val
+                if anchor in name:
+                    group_n[g] += 1
+    out = {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
+    for g in group_sum:
+        if group_n[g]:
+            out[g] = (group_sum[g] / group_n[g], group_n[g])
+    return out
 
 
 def main():
