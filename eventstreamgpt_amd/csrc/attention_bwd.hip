@@ -31,7 +31,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ uint64_t g_stamps[64];
 #define STAMP(i)                                                                              \
   do {                                                                                        \
-    if (blockIdx.x == 0 && blockIdx.y == 5 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memtime(); \
+    if (blockIdx.x == 40 && threadIdx.x == 0) g_stamps[i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define STAMP(i)
@@ -138,10 +138,12 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;  // transposed-read lane roles
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int nxb = ((Lk + KB - 1) / KB) * nsplit;       // workgroups per (batch, head)
+  const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the key-block halves of one (batch, head) share an XCD
+  const int bh = lin / nxb, b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
-  const int kblk = blockIdx.x / nsplit, qsplit = blockIdx.x % nsplit;  // key block; query-tile parity
+  const int kblk = (lin % nxb) / nsplit, qsplit = (lin % nxb) % nsplit;  // key block; query-tile parity
   const int kb0 = kblk * KB;
   const int kw0 = kb0 + 32 * wave;  // this wave's first key
   const int key = kw0 + r;
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   // polls the flag (relaxed sc1 loads + s_sleep), reads the partial with sc1 loads, adds it in registers and stores
   // the bf16 result. Two-term f32 sums commute, so the result does not depend on which one finishes first.
   if (nsplit > 1) {
-    const int64_t id = (int64_t)bh * (gridDim.x / nsplit) + kblk;
+    const int64_t id = (int64_t)bh * (nxb / nsplit) + kblk;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     constexpr int kSC1 = 16;  // buffer cache policy: sc1 (write-through stores, L1-bypassing loads)
     // [dk | dv] f32 slab of this pair, [wave][dt][i/4][lane] x 16 B (coalesced per store / load instruction)
@@ -470,7 +472,7 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   const int nsplit = (counters && Lq > Cfg<HD>::QT) ? 2 : 1;
   float* xbuf = dq32 + (nkb > 1 ? (size_t)(B * H * Lq * HD) : 0);
   if (acc && zero_async(acc, sizeof(float) * (size_t)(B * H * Lq * HD), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  const dim3 grid((unsigned)(nkb * nsplit), (unsigned)(B * H));
+  const dim3 grid((unsigned)(nkb * nsplit * B * H));  // 1-D: XCD-aware order in the kernel
   if (drop_p > 0.f)
     attn_bwd_kernel<HD, true><<<grid, THREADS, lds, st>>>(
         (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,

@@ -136,10 +136,12 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int qh = wave & 1, kp = wave >> 1;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H;
+  const int nqb = (Lq + ROWS - 1) / ROWS;
+  const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the query blocks of one (batch, head) share an XCD
+  const int bh = lin / nqb, b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int off = Lk - Lq;
-  const int qb = blockIdx.x * ROWS;
+  const int qb = (lin % nqb) * ROWS;
   const int qi = qb + qh * 32 + r;
   const bool qin = qi < Lq;
   const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
@@ -364,7 +366,7 @@ static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, 
 int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
                         float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
                         int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st) {
-  dim3 grid((unsigned)cdiv(Lq, ROWS), (unsigned)(B * H));
+  dim3 grid((unsigned)(cdiv(Lq, ROWS) * B * H));  // 1-D: XCD-aware (query block, batch-head) order in the kernel
   if (hd == 32)
     launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
   else if (hd == 64)

@@ -94,6 +94,15 @@ __device__ __forceinline__ void set_bad_index(int32_t* err, int64_t idx) {
   }
 }
 
+// XCD-aware workgroup order: the dispatcher deals consecutive workgroup ids round-robin over the 8 XCDs (each with
+// its own L2), so id -> (xcd = id % 8, slot = id / 8) is remapped (bijectively) to a linear index that gives every
+// XCD a contiguous run: workgroups with neighbouring linear indices (the query blocks of one (batch, head), the two
+// halves of a key block) share an L2.
+__device__ __forceinline__ int xcd_linear(int id, int nwg) {
+  const int q = nwg >> 3, rr = nwg & 7, xcd = id & 7, slot = id >> 3;
+  return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
+}
+
 // Dropout (attention probabilities, residual / input): a counter-based hash of (seed, element index), so the
 // forward and backward regenerate the same keep-mask without storing it. One hash per PAIR of elements: element idx
 // takes the 16-bit half (idx & 1) of h = mix32(pair_lo ^ key ^ pair_hi * 0x9E3779B9), pair = idx >> 1 ("lowbias32"
