@@ -367,7 +367,7 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_c
     add("attn_bwd", f"attn_bwd_kernel<{hd}, {drop}>", "mfma", 8.0 * H * hd * T_pairs, ba,
         {"shape": f"C2 layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"})
     gf, gb, _keep_g = _gemm_launchers(B * Lq, D, F, dev)
-    add("gemm_fc_fwd", "gemm_kernel<true, true, 3>", "mfma", 2.0 * B * Lq * D * F, gf,
+    add("gemm_fc_fwd", "gemm_kernel<true, true, 3, 1, 1>", "mfma", 2.0 * B * Lq * D * F, gf,
         {"shape": f"c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"})
     add("gemm_fc_bwd", "gemm_bwd_pair_kernel", "mfma", 4.0 * B * Lq * D * F, gb,
         {"shape": f"c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"})

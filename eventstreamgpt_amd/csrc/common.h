@@ -103,6 +103,52 @@ __device__ __forceinline__ int xcd_linear(int id, int nwg) {
   return (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + slot;
 }
 
+// Activations of the GEMM / bias epilogues (act: 0 erf-GELU, 1 tanh-GELU, 2 ReLU) and their derivatives.
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 for the CDF): one reciprocal and one exp2, the exp2 shared
+// with the normal density of the derivative; tanh as 1 - 2 / (1 + e^{2u}). The library erff / tanhf (branchy
+// polynomials) made the c_fc epilogue VALU-bound: 8.4 M activations per C2 layer.
+__device__ __forceinline__ void normal_cdf_pdf(float z, float& cdf, float& pdf) {
+  const float u = fabsf(z) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.f));
+  const float e = __builtin_amdgcn_exp2f(z * z * -0.72134752044448170368f);  // exp(-z^2 / 2)
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float q = 0.5f * poly * e;  // (1 - erf(|z| / sqrt 2)) / 2
+  cdf = z >= 0.f ? 1.f - q : q;
+  pdf = 0.39894228040143267794f * e;
+}
+
+__device__ __forceinline__ float fast_tanh(float u) {
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * 2.88539008177792681472f));
+}
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  if (act == 0) {
+    float cdf, pdf;
+    normal_cdf_pdf(z, cdf, pdf);
+    return z * cdf;
+  }
+  if (act == 1) {
+    const float k = 0.79788456080286535588f;  // sqrt(2/pi)
+    return 0.5f * z * (1.f + fast_tanh(k * (z + 0.044715f * z * z * z)));
+  }
+  return z > 0.f ? z : 0.f;
+}
+
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == 0) {
+    float cdf, pdf;
+    normal_cdf_pdf(z, cdf, pdf);
+    return cdf + z * pdf;
+  }
+  if (act == 1) {
+    const float k = 0.79788456080286535588f;
+    const float t = fast_tanh(k * (z + 0.044715f * z * z * z));
+    return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * z * z);
+  }
+  return z > 0.f ? 1.f : 0.f;
+}
+
 // Dropout (attention probabilities, residual / input): a counter-based hash of (seed, element index), so the
 // forward and backward regenerate the same keep-mask without storing it. One hash per PAIR of elements: element idx
 // takes the 16-bit half (idx & 1) of h = mix32(pair_lo ^ key ^ pair_hi * 0x9E3779B9), pair = idx >> 1 ("lowbias32"

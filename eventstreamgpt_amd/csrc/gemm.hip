@@ -4,8 +4,9 @@
 //   C[M, N] = alpha · A · B (+ bias[n]) (+ epilogue),   bf16 operands, f32 accumulation, C bf16 or f32.
 //
 // The step's shapes are skinny: M = B·L tokens (8192 for the C2 workload) with N, K in {256 … 1624}, and the
-// weight gradients are [out, in] products with K = tokens. Tiles are 64x64 (4 waves of 32x32; measured best at
-// these sizes: more resident workgroups hide the load / store latency that dominates). Products with few tiles or
+// weight gradients are [out, in] products with K = tokens. Tiles are (64·fm) x (64·fn), 4 waves of fm x fn 32x32
+// fragments; 64x64 measured best at these sizes (more resident workgroups hide the load / store latency that
+// dominates at K = 256; 128x128 forward / dX tiles were 10-100 % slower), 128x128 for the largest weight gradients. Products with few tiles or
 // a long K split K into f32 slabs that the LAST-arriving workgroup of each tile sums in a fixed order (agent-scope
 // release / acquire ticket, cdna_hip_programming.md's in-launch split-K recipe; deterministic, no second launch).
 // Epilogues fuse what the step needs around a GEMM: bias + activation (c_fc: stores the pre-activation too), the
@@ -38,7 +39,6 @@ constexpr int BK = 64;
 constexpr int KC_LD = BK + 8;  // K-contig image row stride (elements)
 constexpr int THREADS = 256;
 constexpr int NS = 3;          // register stages: NS-1 k-tiles in flight while one is written to LDS
-constexpr int TILE = 64;
 
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -191,70 +191,55 @@ struct Prob {
   int* counters;       // split-K, in-launch reduction: one zeroed ticket per tile (left zeroed)
   int ext_reduce;      // split-K: slabs summed by slab_reduce_kernel (a second launch) instead of in-launch
   int fast;            // A and B each < 2 GiB: whole tiles take the buffer-load fast path
+  int fm, fn;          // tile = (64·fm) x (64·fn): each of the 4 waves holds fm x fn 32x32 fragments
 };
-
-__device__ __forceinline__ float act_fwd(float z, int act) {
-  if (act == 0) return 0.5f * z * (1.f + erff(z * 0.70710678118654752440f));
-  if (act == 1) {
-    const float k = 0.79788456080286535588f;
-    return 0.5f * z * (1.f + tanhf(k * (z + 0.044715f * z * z * z)));
-  }
-  return z > 0.f ? z : 0.f;
-}
-
-__device__ __forceinline__ float act_grad(float z, int act) {
-  if (act == 0) {
-    const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752440f));
-    const float pdf = 0.39894228040143267794f * expf(-0.5f * z * z);
-    return cdf + z * pdf;
-  }
-  if (act == 1) {
-    const float k = 0.79788456080286535588f;
-    const float u = k * (z + 0.044715f * z * z * z);
-    const float t = tanhf(u);
-    return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * z * z);
-  }
-  return z > 0.f ? 1.f : 0.f;
-}
 
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
 
-// One 64x64 output tile (4 waves as 2x2 of 32x32) of problem p; `lin` = the tile's index within the problem.
-// The MFMAs compute the tile transposed (A-operand = B fragment, B-operand = A fragment) so that a lane owns one
-// output ROW m and its registers hold columns n = (e&3) + 8(e>>2) + 4h: the epilogue stores 16 B per lane.
-// LDS of one tile's staging: two buffers x (A image + B image), sized for the operand layouts (the K-contig images
-// are smaller: the forward kernel fits 4 workgroups per CU instead of 3). Also holds the epilogue's C tile (f32:
-// 64 x 68 floats) and the split-K reducer flag.
-template <bool AKC, bool BKC>
+// One (64·FM)x(64·FN) output tile of problem p (4 waves as 2x2, each wave FM x FN fragments of 32x32);
+// `lin` = the tile's index within the problem. The MFMAs compute each fragment transposed (A-operand = B fragment,
+// B-operand = A fragment) so that a lane owns one output ROW m and its registers hold columns
+// n = (e&3) + 8(e>>2) + 4h: the epilogue stores 16 B per lane. LDS of one tile's staging: two buffers x (A image +
+// B image), sized for the operand layouts (the K-contig images are smaller: the 64x64 forward kernel fits 4
+// workgroups per CU instead of 3). Also holds the epilogue's C tile (f32: BM x (BN + 4) floats) and the split-K
+// reducer flag.
+template <bool AKC, bool BKC, int FM, int FN>
 constexpr int lds_elems() {
-  constexpr int st = 2 * (Tile<AKC, TILE>::kElems + Tile<BKC, TILE>::kElems);
-  constexpr int epi = TILE * (TILE + 4) * 2;  // f32 C tile in bf16 elements
+  constexpr int st = 2 * (Tile<AKC, 64 * FM>::kElems + Tile<BKC, 64 * FN>::kElems);
+  constexpr int epi = 64 * FM * (64 * FN + 4) * 2;  // f32 C tile in bf16 elements
   return st > epi ? st : epi;
 }
 
-template <bool AKC, bool BKC, int NS_ = NS>
+template <bool AKC, bool BKC, int NS_, int FM, int FN>
 __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) {
-  constexpr int NS = NS_;
+  constexpr int NS = NS_, BM = 64 * FM, BN = 64 * FN, F = FM * FN;
   constexpr bool kRowSum = !(AKC && BKC);  // compiled out of the forward (K-contig x K-contig) instantiation
-  using TA = Tile<AKC, TILE>;
-  using TB = Tile<BKC, TILE>;
+  using TA = Tile<AKC, BM>;
+  using TB = Tile<BKC, BN>;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
   const int bz = lin % p.splits, tile = lin / p.splits;
   const int bx = tile % p.tn, by = tile / p.tn;
   const int M = p.M, N = p.N;
-  const int m0 = by * TILE, n0 = bx * TILE;
+  const int m0 = by * BM, n0 = bx * BN;
   const int kb = bz * p.kchunk, ke = min(p.K, kb + p.kchunk);
   const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
   const __bf16* __restrict__ A = p.A;
   const __bf16* __restrict__ B = p.B;
   const bool want_rs = kRowSum && p.rowsum != nullptr && bx == 0 && wn == 0;  // wave-uniform
 
-  f32x16 acc, racc;
+  f32x16 acc[FM][FN], racc[FM];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
+  for (int e = 0; e < 16; ++e) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      racc[i][e] = 0.f;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j][e] = 0.f;
+    }
+  }
   bf16x8 ones;
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
@@ -297,10 +282,17 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
       __syncthreads();
 #pragma unroll
       for (int t = 0; t < BK / 16; ++t) {
-        const bf16x8 af = TA::frag(sA, wm * 32, t);
-        const bf16x8 bfr = TB::frag(sB, wn * 32, t);
-        acc = mfma(bfr, af, acc);
-        if constexpr (RS) racc = mfma(ones, af, racc);
+        bf16x8 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = TA::frag(sA, wm * 32 * FM + 32 * i, t);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = TB::frag(sB, wn * 32 * FN + 32 * j, t);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma(bfr[j], af[i], acc[i][j]);
+          if constexpr (RS) racc[i] = mfma(ones, af[i], racc[i]);
+        }
       }
     };
 #pragma unroll
@@ -319,7 +311,7 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  const bool fast = p.fast && m0 + TILE <= M && n0 + TILE <= N && nk > 0 && (ke - kb) % BK == 0;
+  const bool fast = p.fast && m0 + BM <= M && n0 + BN <= N && nk > 0 && (ke - kb) % BK == 0;
   if (fast) {
     if (want_rs) mainloop(T_{}, T_{});
     else mainloop(T_{}, F_{});
@@ -328,9 +320,9 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     else mainloop(F_{}, F_{});
   }
 
-  const int row = m0 + wm * 32 + r;
-  const bool rok = row < M;
-  const int cb = n0 + wn * 32;
+  // this lane's output row of fragment row i, and the first column of fragment column j (within the tile)
+  auto lrow = [&](int i) { return wm * 32 * FM + 32 * i + r; };
+  auto lcol = [&](int j) { return wn * 32 * FN + 32 * j; };
 
   // ---- split-K: slab, ticket, the last arriver reduces in z order ----
   // Hand-off in its write-through form (MI355X_MICROARCH.md, inter-workgroup visibility, valid forms): every slab
@@ -338,16 +330,27 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   // one agent-scope ticket add; the workgroup whose add comes last reads every slab with sc1 loads. No L2
   // write-back fence: with the grouped dX product streaming its output through the same L2s, buffer_wbl2 per
   // workgroup serialised on the dirty lines of the whole XCD. Slabs are lane-linear (fragment order: tile, wave,
-  // register group, lane): each wave-instruction writes / reads 1 KiB contiguously — whole lines, no partial-line
-  // write-through.
+  // fragment, register group, lane): each wave-instruction writes / reads 1 KiB contiguously — whole lines, no
+  // partial-line write-through.
+  const int ntile = p.tm * p.tn;
+  auto slab_idx = [&](int z, int f, int g) {  // float index of this lane's 4 values
+    return 4 * (((((z * ntile + tile) * 4 + wave) * F + f) * 4 + g) * 64 + lane);
+  };
+  const int rs_base = p.splits * ntile * BM * BN;  // row-sum slabs follow the tile slabs
   if (p.splits > 1 && p.ext_reduce) {
     // slabs only (plain stores: the kernel boundary orders them before slab_reduce_kernel)
-    const int ntile = p.tm * p.tn;
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<float4*>(p.slab + ((((int64_t)bz * ntile + tile) * 4 + wave) * 4 + g) * 256 + 4 * lane) =
-          make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
-    if (want_rs && rok && h == 0) p.slab[(int64_t)p.splits * ntile * TILE * TILE + (int64_t)bz * M + row] = racc[0];
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(p.slab + slab_idx(bz, i * FN + j, g)) =
+              make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+    if (want_rs && h == 0)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        if (m0 + lrow(i) < M) p.slab[rs_base + (int64_t)bz * M + m0 + lrow(i)] = racc[i][0];
     return;
   }
   if (p.splits > 1) {
@@ -355,17 +358,22 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(p.slab, (short)0, 0x7fffffff, 0x00020000);
     constexpr int kSC1 = 16;  // cache policy: sc1
-    const int ntile = p.tm * p.tn;
-    const int rs_base = p.splits * ntile * TILE * TILE;  // row-sum slabs follow the tile slabs
-    auto slab_off = [&](int z, int g) { return 4 * ((((z * ntile + tile) * 4 + wave) * 4 + g) * 64 + lane) * 4; };
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const u32x4 w = {__float_as_uint(acc[4 * g]), __float_as_uint(acc[4 * g + 1]), __float_as_uint(acc[4 * g + 2]),
-                       __float_as_uint(acc[4 * g + 3])};
-      __builtin_amdgcn_raw_buffer_store_b128(w, rs, slab_off(bz, g), 0, kSC1);
-    }
-    if (want_rs && rok && h == 0)
-      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(racc[0]), rs, 4 * (rs_base + bz * M + row), 0, kSC1);
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const u32x4 w = {__float_as_uint(acc[i][j][4 * g]), __float_as_uint(acc[i][j][4 * g + 1]),
+                           __float_as_uint(acc[i][j][4 * g + 2]), __float_as_uint(acc[i][j][4 * g + 3])};
+          __builtin_amdgcn_raw_buffer_store_b128(w, rs, 4 * slab_idx(bz, i * FN + j, g), 0, kSC1);
+        }
+    if (want_rs && h == 0)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        if (m0 + lrow(i) < M)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(racc[i][0]), rs,
+                                                4 * (rs_base + bz * M + m0 + lrow(i)), 0, kSC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave's slab stores have drained (and the LDS tiles are no longer read)
     int* flag = reinterpret_cast<int*>(smem);
@@ -378,139 +386,183 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     __syncthreads();
     if (!*flag) return;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = racc[e] = 0.f;
+    for (int e = 0; e < 16; ++e) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        racc[i][e] = 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j][e] = 0.f;
+      }
+    }
     // slabs in batches of kRB: every load of a batch in flight before the (z-ordered, deterministic) adds — one
     // memory round trip per batch instead of one per slab
-    constexpr int kRB = 4;
+    constexpr int kRB = F >= 4 ? 1 : 4 / F;
     for (int z0 = 0; z0 < p.splits; z0 += kRB) {
-      u32x4 x[kRB][4];
-      float rv[kRB];
+      u32x4 x[kRB][F][4];
+      float rv[kRB][FM];
 #pragma unroll
       for (int u = 0; u < kRB; ++u) {
         const int z = min(z0 + u, p.splits - 1);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) x[u][g] = __builtin_amdgcn_raw_buffer_load_b128(rs, slab_off(z, g), 0, kSC1);
-        rv[u] = (want_rs && rok)
-                    ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (rs_base + z * M + row), 0, kSC1))
-                    : 0.f;
+        for (int f = 0; f < F; ++f)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) x[u][f][g] = __builtin_amdgcn_raw_buffer_load_b128(rs, 4 * slab_idx(z, f, g), 0, kSC1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          rv[u][i] = (want_rs && m0 + lrow(i) < M) ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                                                          rs, 4 * (rs_base + z * M + m0 + lrow(i)), 0, kSC1))
+                                                    : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < kRB; ++u) {
         if (z0 + u >= p.splits) break;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          acc[4 * g] += __uint_as_float(x[u][g][0]);
-          acc[4 * g + 1] += __uint_as_float(x[u][g][1]);
-          acc[4 * g + 2] += __uint_as_float(x[u][g][2]);
-          acc[4 * g + 3] += __uint_as_float(x[u][g][3]);
+        for (int i = 0; i < FM; ++i) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              acc[i][j][4 * g] += __uint_as_float(x[u][i * FN + j][g][0]);
+              acc[i][j][4 * g + 1] += __uint_as_float(x[u][i * FN + j][g][1]);
+              acc[i][j][4 * g + 2] += __uint_as_float(x[u][i * FN + j][g][2]);
+              acc[i][j][4 * g + 3] += __uint_as_float(x[u][i * FN + j][g][3]);
+            }
+          racc[i][0] += rv[u][i];
         }
-        racc[0] += rv[u];
       }
     }
   }
 
-  // ---- epilogue: lane = row, register group g = columns cb + 8g + 4h + {0..3} ----
+  // ---- epilogue: lane = row, register group g = columns lcol(j) + 8g + 4h + {0..3} ----
   const float al = p.alpha ? *p.alpha : 1.f;
-  if (want_rs && rok && h == 0) p.rowsum[row] = racc[0] * al;
-  float v[16];
+  if (want_rs && h == 0)
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int c = cb + 8 * g + 4 * h;
-    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (p.bias && c < N) bv = *reinterpret_cast<const float4*>(p.bias + c);
-    v[4 * g + 0] = acc[4 * g + 0] * al + bv.x;
-    v[4 * g + 1] = acc[4 * g + 1] * al + bv.y;
-    v[4 * g + 2] = acc[4 * g + 2] * al + bv.z;
-    v[4 * g + 3] = acc[4 * g + 3] * al + bv.w;
-  }
+    for (int i = 0; i < FM; ++i)
+      if (m0 + lrow(i) < M) p.rowsum[m0 + lrow(i)] = racc[i][0] * al;
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = n0 + lcol(j) + 8 * g + 4 * h;
+      float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (p.bias && c < N) bv = *reinterpret_cast<const float4*>(p.bias + c);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        acc[i][j][4 * g + 0] = acc[i][j][4 * g + 0] * al + bv.x;
+        acc[i][j][4 * g + 1] = acc[i][j][4 * g + 1] * al + bv.y;
+        acc[i][j][4 * g + 2] = acc[i][j][4 * g + 2] * al + bv.z;
+        acc[i][j][4 * g + 3] = acc[i][j][4 * g + 3] * al + bv.w;
+      }
+    }
   // The tile goes out through LDS (the staging buffers are free once every wave is past its last fragment read):
   // written in fragment order, stored row-major with 16-B chunks, each wave-instruction covering whole 128-B lines
-  // (8 rows x 128 B in bf16, 4 rows x 256 B in f32) instead of 32-B pieces of 32 rows.
-  const int rl = wm * 32 + r, cl = wn * 32;  // this lane's row / first column within the tile
+  // instead of 32-B pieces of 32 rows.
   __syncthreads();
   if (p.out_f32) {
-    constexpr int kLd = TILE + 4;  // f32 row pitch (floats): 16-B aligned, conflict-free fragment writes
+    constexpr int kLd = BN + 4;  // f32 row pitch (floats): 16-B aligned, conflict-free fragment writes
     float* t = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<float4*>(t + rl * kLd + cl + 8 * g + 4 * h) =
-          make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(t + lrow(i) * kLd + lcol(j) + 8 * g + 4 * h) =
+              make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < TILE * TILE / 4 / THREADS; ++i) {
-      const int ch = threadIdx.x + THREADS * i, tr = ch / (TILE / 4), tc = (ch % (TILE / 4)) * 4;
+    for (int q = 0; q < BM * BN / 4 / THREADS; ++q) {
+      const int ch = threadIdx.x + THREADS * q, tr = ch / (BN / 4), tc = (ch % (BN / 4)) * 4;
       const int gr = m0 + tr, gc = n0 + tc;
       if (gr >= M || gc >= N) continue;
       float4 w = *reinterpret_cast<const float4*>(t + tr * kLd + tc);
-      float4* q = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)gr * p.ldc + gc);
+      float4* o4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)gr * p.ldc + gc);
       if (p.accumulate) {
-        const float4 o = *q;
+        const float4 o = *o4;
         w.x += o.x;
         w.y += o.y;
         w.z += o.z;
         w.w += o.w;
       }
-      *q = w;
+      *o4 = w;
     }
     return;
   }
   if (p.epi == EPI_ACT_GRAD) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int c = cb + 8 * g + 4 * h;
-      if (rok && c < N) {
-        const uint2 f = *reinterpret_cast<const uint2*>(p.aux + (int64_t)row * p.ld_aux + c);
-        v[4 * g + 0] *= act_grad(bf16_lo(f.x), p.act);
-        v[4 * g + 1] *= act_grad(bf16_hi(f.x), p.act);
-        v[4 * g + 2] *= act_grad(bf16_lo(f.y), p.act);
-        v[4 * g + 3] *= act_grad(bf16_hi(f.y), p.act);
-      }
+    for (int i = 0; i < FM; ++i) {
+      const int row = m0 + lrow(i);
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = n0 + lcol(j) + 8 * g + 4 * h;
+          if (row < M && c < N) {
+            const uint2 f = *reinterpret_cast<const uint2*>(p.aux + (int64_t)row * p.ld_aux + c);
+            acc[i][j][4 * g + 0] *= act_grad(bf16_lo(f.x), p.act);
+            acc[i][j][4 * g + 1] *= act_grad(bf16_hi(f.x), p.act);
+            acc[i][j][4 * g + 2] *= act_grad(bf16_lo(f.y), p.act);
+            acc[i][j][4 * g + 3] *= act_grad(bf16_hi(f.y), p.act);
+          }
+        }
     }
   }
-  constexpr int kLdB = TILE + 8;  // bf16 row pitch (elements): 144 B, conflict-free 8-B fragment writes
+  constexpr int kLdB = BN + 8;  // bf16 row pitch (elements): conflict-free 8-B fragment writes
   __bf16* tb = smem;
   // one bf16 tile out: fragment-order LDS writes, barrier, row-major 16-B chunk stores
-  auto store_tile = [&](const uint32_t (&d)[4][2], __bf16* dst, int64_t ld) {
+  auto store_tile = [&](const uint32_t (&d)[FM][FN][4][2], __bf16* dst, int64_t ld) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-      *reinterpret_cast<uint2*>(tb + rl * kLdB + cl + 8 * g + 4 * h) = make_uint2(d[g][0], d[g][1]);
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<uint2*>(tb + lrow(i) * kLdB + lcol(j) + 8 * g + 4 * h) = make_uint2(d[i][j][g][0], d[i][j][g][1]);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < TILE * TILE / 8 / THREADS; ++i) {
-      const int ch = threadIdx.x + THREADS * i, tr = ch / (TILE / 8), tc = (ch % (TILE / 8)) * 8;
+    for (int q = 0; q < BM * BN / 8 / THREADS; ++q) {
+      const int ch = threadIdx.x + THREADS * q, tr = ch / (BN / 8), tc = (ch % (BN / 8)) * 8;
       const int gr = m0 + tr, gc = n0 + tc;
       if (gr < M && gc < N)
         *reinterpret_cast<uint4*>(dst + (int64_t)gr * ld + gc) = *reinterpret_cast<const uint4*>(tb + tr * kLdB + tc);
     }
   };
-  uint32_t d[4][2];
+  uint32_t d[FM][FN][4][2];
   if (p.epi == EPI_BIAS_ACT) {
     // store the pre-activation (bf16: the value the activation and its gradient see), then activate it
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
-      d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
-      v[4 * g + 0] = act_fwd(bf16_lo(d[g][0]), p.act);
-      v[4 * g + 1] = act_fwd(bf16_hi(d[g][0]), p.act);
-      v[4 * g + 2] = act_fwd(bf16_lo(d[g][1]), p.act);
-      v[4 * g + 3] = act_fwd(bf16_hi(d[g][1]), p.act);
-    }
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          d[i][j][g][0] = pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]);
+          d[i][j][g][1] = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+          acc[i][j][4 * g + 0] = act_fwd(bf16_lo(d[i][j][g][0]), p.act);
+          acc[i][j][4 * g + 1] = act_fwd(bf16_hi(d[i][j][g][0]), p.act);
+          acc[i][j][4 * g + 2] = act_fwd(bf16_lo(d[i][j][g][1]), p.act);
+          acc[i][j][4 * g + 3] = act_fwd(bf16_hi(d[i][j][g][1]), p.act);
+        }
     store_tile(d, p.aux_out, p.ld_aux);
     __syncthreads();  // the LDS tile is rewritten below
   }
 #pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    d[g][0] = pack_bf16x2(v[4 * g], v[4 * g + 1]);
-    d[g][1] = pack_bf16x2(v[4 * g + 2], v[4 * g + 3]);
-  }
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        d[i][j][g][0] = pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]);
+        d[i][j][g][1] = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+      }
   store_tile(d, reinterpret_cast<__bf16*>(p.C), p.ldc);
 }
 
-template <bool AKC, bool BKC, int NS_ = NS>
+template <bool AKC, bool BKC, int NS_, int FM, int FN>
 __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC>()];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC, FM, FN>()];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile<AKC, BKC, NS_>(p, lin, smem);
+  gemm_tile<AKC, BKC, NS_, FM, FN>(p, lin, smem);
 }
 
 // Forward register-stage depth (2 or 3; ESGPT_GEMM_FWD_NS tuning hook, read once).
@@ -527,32 +579,43 @@ int fwd_stages() {
 // M-contig, B = X N-contig, + the bias gradient). The dW workgroups (the long K = tokens chains) take the first
 // p0.wg0 workgroup ids, so the dispatcher deals them round-robin over all 8 XCDs first and the short dX tiles
 // fill in behind them; each problem keeps its own XCD-aware order within its id range.
+// Register stages of the backward products: 2 for the 4-fragment tiles (3 would leave 1 wave per SIMD).
+template <int FM, int FN>
+constexpr int bwd_stages() {
+  return FM * FN >= 4 ? 2 : NS;
+}
+
+template <int XM, int XN, int WM, int WN>
 __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1) {
-  constexpr int kLds = lds_elems<false, false>() > lds_elems<true, false>() ? lds_elems<false, false>()
-                                                                             : lds_elems<true, false>();
+  constexpr int kLds = lds_elems<false, false, WM, WN>() > lds_elems<true, false, XM, XN>()
+                           ? lds_elems<false, false, WM, WN>()
+                           : lds_elems<true, false, XM, XN>();
   __shared__ __attribute__((aligned(16))) __bf16 smem[kLds];
   const int id = blockIdx.x, n1 = p0.wg0;
   if (id < n1)
-    gemm_tile<false, false>(p1, xcd_remap(id, n1), smem);
+    gemm_tile<false, false, bwd_stages<WM, WN>(), WM, WN>(p1, xcd_remap(id, n1), smem);
   else
-    gemm_tile<true, false>(p0, xcd_remap(id - n1, gridDim.x - n1), smem);
+    gemm_tile<true, false, bwd_stages<XM, XN>(), XM, XN>(p0, xcd_remap(id - n1, gridDim.x - n1), smem);
 }
 
 // Split-K reduction as its own launch (large slab sets: one last-arriving workgroup reading every slab of its tile
 // is a serial memory-latency chain on one CU; here every CU takes a share). f32 output, plain store epilogue (the
-// weight-gradient products): thread = one 16-B fragment chunk (tile, wave, register group, lane) of the output,
-// summing its splits in z order (deterministic), then alpha, bias, accumulate, and the 4 columns stored; threads
-// past the tiles sum the row-sum slabs into p.rowsum.
+// weight-gradient products): thread = one 16-B fragment chunk (tile, wave, fragment, register group, lane) of the
+// output, summing its splits in z order (deterministic), then alpha, bias, accumulate, and the 4 columns stored;
+// threads past the tiles sum the row-sum slabs into p.rowsum.
 __global__ __launch_bounds__(256) void slab_reduce_kernel(Prob p) {
-  const int64_t ntile = (int64_t)p.tm * p.tn, nch = ntile * TILE * TILE / 4;
+  const int F = p.fm * p.fn, BM = 64 * p.fm, BN = 64 * p.fn;
+  const int64_t ntile = (int64_t)p.tm * p.tn, nch = ntile * BM * BN / 4;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float al = p.alpha ? *p.alpha : 1.f;
   if (t < nch) {
-    const int lane = (int)(t & 63), g = (int)((t >> 6) & 3), wave = (int)((t >> 8) & 3);
-    const int64_t tile = t >> 10;
+    const int lane = (int)(t & 63), g = (int)((t >> 6) & 3);
+    const int64_t wf = t >> 8;  // (tile, wave, fragment)
+    const int f = (int)(wf % F), wave = (int)((wf / F) & 3);
+    const int64_t tile = wf / F / 4;
     const int bx = (int)(tile % p.tn), by = (int)(tile / p.tn);
-    const int row = by * TILE + (wave >> 1) * 32 + (lane & 31);
-    const int col = bx * TILE + (wave & 1) * 32 + 8 * g + 4 * (lane >> 5);
+    const int row = by * BM + (wave >> 1) * 32 * p.fm + (f / p.fn) * 32 + (lane & 31);
+    const int col = bx * BN + (wave & 1) * 32 * p.fn + (f % p.fn) * 32 + 8 * g + 4 * (lane >> 5);
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr int kU = 8;
     for (int z0 = 0; z0 < p.splits; z0 += kU) {
@@ -592,7 +655,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(Prob p) {
     }
   } else if (p.rowsum && t - nch < p.M) {
     const int64_t m = t - nch;
-    const float* rs = p.slab + (int64_t)p.splits * ntile * TILE * TILE;
+    const float* rs = p.slab + (int64_t)p.splits * nch * 4;
     float a = 0.f;
     for (int z = 0; z < p.splits; ++z) a += rs[(int64_t)z * p.M + m];
     p.rowsum[m] = a * al;
@@ -600,7 +663,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(Prob p) {
 }
 
 void launch_slab_reduce(const Prob& p, hipStream_t st) {
-  const int64_t n = (int64_t)p.tm * p.tn * TILE * TILE / 4 + (p.rowsum ? p.M : 0);
+  const int64_t n = (int64_t)p.tm * p.tn * 64 * p.fm * 64 * p.fn / 4 + (p.rowsum ? p.M : 0);
   slab_reduce_kernel<<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p);
 }
 
@@ -616,23 +679,64 @@ int in_launch_splits() {
   return v;
 }
 
+constexpr int64_t kMaxChunk = 1024;
+constexpr int64_t kTarget = 480;  // about two resident 64x64 tiles per CU
+
+// Tile shape of a product: (64·fm) x (64·fn). Larger tiles read each operand fewer times through L2 (the 64x64
+// tile's k-loop is bound by the L2 -> CU rate at ≈32 B per MFMA-cycle) but put fewer workgroups on the chip.
+struct TileCfg {
+  int fm, fn;
+};
+
+// ESGPT_GEMM_TILE_FWD / _DX / _DW = "<fm><fn>" (e.g. "22"): tuning hooks, read once; only compiled shapes accepted.
+TileCfg env_tile(const char* name, TileCfg def, const int* allowed, int n_allowed) {
+  const char* e = getenv(name);
+  if (!e) return def;
+  const int code = atoi(e);
+  for (int i = 0; i < n_allowed; ++i)
+    if (allowed[i] == code) return TileCfg{code / 10, code % 10};
+  return def;
+}
+constexpr int kFwdTiles[] = {11, 21, 12, 22};
+constexpr int kDxTiles[] = {11, 21, 22};
+constexpr int kDwTiles[] = {11, 22};
+
+TileCfg fwd_tile(int64_t /*M*/, int64_t /*N*/, int64_t /*K*/) {
+  static const TileCfg t = env_tile("ESGPT_GEMM_TILE_FWD", TileCfg{1, 1}, kFwdTiles, 4);
+  return t;
+}
+TileCfg dx_tile(int64_t /*T*/, int64_t /*in*/, int64_t /*out*/) {
+  static const TileCfg t = env_tile("ESGPT_GEMM_TILE_DX", TileCfg{1, 1}, kDxTiles, 3);
+  return t;
+}
+// dW [out, in] over K = T tokens: 128x128 tiles once the 64x64 plan (at its minimum split count, one split per
+// kMaxChunk of tokens) would put more than three workgroups per CU on the chip — their f32 slab traffic then costs
+// more than the fewer workgroups (C2: the generative head's [1624, 256] 45 -> 37 us; c_fc's [1024, 256] stays
+// 64x64: 24 vs 27 us).
+TileCfg dw_tile(int64_t T, int64_t in, int64_t out) {
+  static const TileCfg forced = env_tile("ESGPT_GEMM_TILE_DW", TileCfg{0, 0}, kDwTiles, 2);
+  if (forced.fm) return forced;
+  const int64_t wg = cdiv(out, 64) * cdiv(in, 64) * std::max<int64_t>(1, T / kMaxChunk);
+  return wg > 3 * 256 ? TileCfg{2, 2} : TileCfg{1, 1};
+}
+
+int64_t n_tiles(int64_t M, int64_t N, TileCfg c) { return cdiv(M, 64 * c.fm) * cdiv(N, 64 * c.fn); }
+
 struct Plan {
   int splits, kchunk;
 };
 
 // Split-K: enough workgroups for `target` (<= 0: never split), and no workgroup walks more than kMaxChunk of K
 // (a long K is one long serial chain: 8192 tokens = 128 k-tiles), never below 256 of K per split.
-constexpr int64_t kMaxChunk = 1024;
-constexpr int64_t kTarget = 480;  // about two resident 64x64 tiles per CU
 
-Plan plan(int64_t M, int64_t N, int64_t K, int64_t target) {
+Plan plan(int64_t M, int64_t N, int64_t K, int64_t target, TileCfg c) {
   Plan p{1, (int)(cdiv(K, BK) * BK)};
   if (K == 0 || target <= 0) return p;
   int64_t splits = 1;
   if (const char* e = getenv("ESGPT_GEMM_SPLITS")) {  // tuning hook
     splits = std::max<int64_t>(1, atoi(e));
   } else {
-    const int64_t tiles = cdiv(M, TILE) * cdiv(N, TILE);
+    const int64_t tiles = n_tiles(M, N, c);
     if (tiles < target) splits = cdiv(target, tiles);
     splits = std::max<int64_t>(splits, K / kMaxChunk);
     splits = std::min<int64_t>(splits, std::max<int64_t>(1, K / 256));
@@ -644,7 +748,8 @@ Plan plan(int64_t M, int64_t N, int64_t K, int64_t target) {
 }
 
 Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K, void* C,
-               int64_t ldc, int out_f32, int accumulate, const float* bias, const float* alpha, int64_t target) {
+               int64_t ldc, int out_f32, int accumulate, const float* bias, const float* alpha, int64_t target,
+               TileCfg c) {
   Prob p{};
   p.A = reinterpret_cast<const __bf16*>(A);
   p.B = reinterpret_cast<const __bf16*>(B);
@@ -653,9 +758,11 @@ Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M
   p.M = (int)M;
   p.N = (int)N;
   p.K = (int)K;
-  p.tm = (int)cdiv(M, TILE);
-  p.tn = (int)cdiv(N, TILE);
-  const Plan pl = plan(M, N, K, target);
+  p.fm = c.fm;
+  p.fn = c.fn;
+  p.tm = (int)cdiv(M, 64 * c.fm);
+  p.tn = (int)cdiv(N, 64 * c.fn);
+  const Plan pl = plan(M, N, K, target, c);
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.C = C;
@@ -670,10 +777,9 @@ Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M
   return p;
 }
 
-// Split-K slabs: [splits][tiles][64 x 64] f32 in fragment order, then [splits][M] row sums.
-size_t slab_bytes(int64_t splits, int64_t M, int64_t N) {
-  return splits > 1 ? sizeof(float) * ((size_t)splits * cdiv(M, TILE) * cdiv(N, TILE) * TILE * TILE +
-                                       (size_t)splits * M)
+// Split-K slabs: [splits][tiles][BM x BN] f32 in fragment order, then [splits][M] row sums.
+size_t slab_bytes(int64_t splits, int64_t M, int64_t N, TileCfg c) {
+  return splits > 1 ? sizeof(float) * ((size_t)splits * n_tiles(M, N, c) * 64 * c.fm * 64 * c.fn + (size_t)splits * M)
                     : 0;
 }
 
@@ -691,15 +797,37 @@ bool shapes_ok(bool akc, bool bkc, const void* A, int64_t lda, const void* B, in
   return N % cgrp == 0 && ldc % cgrp == 0;
 }
 
-// Tile count of the dX product (what the grouped launch already puts on the chip): the dW split targets the rest.
-int64_t dw_target(bool has_dx, int64_t T, int64_t in) {
+// Workgroups of the dX product (what the grouped launch already puts on the chip): the dW split targets the rest.
+int64_t dw_target(bool has_dx, int64_t T, int64_t in, int64_t out) {
   static int64_t tgt = -1;
   if (tgt < 0) {
     const char* e = getenv("ESGPT_GEMM_DW_TARGET");  // tuning hook: fixed dW item target (0 = the default rule)
     tgt = e ? std::max(0, atoi(e)) : 0;
   }
   if (tgt > 0) return tgt;
-  return has_dx ? std::max<int64_t>(64, kTarget - cdiv(T, TILE) * cdiv(in, TILE)) : kTarget;
+  return has_dx ? std::max<int64_t>(64, kTarget - n_tiles(T, in, dx_tile(T, in, out))) : kTarget;
+}
+
+template <int FM, int FN>
+void launch_fwd(const Prob& p, hipStream_t st) {
+  const dim3 grid((unsigned)n_wg(p));
+  if (fwd_stages() == 2) gemm_kernel<true, true, 2, FM, FN><<<grid, THREADS, 0, st>>>(p);
+  else gemm_kernel<true, true, 3, FM, FN><<<grid, THREADS, 0, st>>>(p);
+}
+
+template <int XM, int XN>
+void launch_pair_x(const Prob& p0, const Prob& p1, hipStream_t st) {
+  const dim3 grid((unsigned)(n_wg(p0) + n_wg(p1)));
+  if (p1.fm == 2) gemm_bwd_pair_kernel<XM, XN, 2, 2><<<grid, THREADS, 0, st>>>(p0, p1);
+  else gemm_bwd_pair_kernel<XM, XN, 1, 1><<<grid, THREADS, 0, st>>>(p0, p1);
+}
+
+void launch_pair(const Prob& p0, const Prob& p1, hipStream_t st) {
+  switch (p0.fm * 10 + p0.fn) {
+    case 21: launch_pair_x<2, 1>(p0, p1, st); break;
+    case 22: launch_pair_x<2, 2>(p0, p1, st); break;
+    default: launch_pair_x<1, 1>(p0, p1, st); break;
+  }
 }
 
 }  // namespace
@@ -707,10 +835,10 @@ int64_t dw_target(bool has_dx, int64_t T, int64_t in) {
 extern "C" {
 
 size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K) {
-  return slab_bytes(plan(M, N, K, kTarget).splits, M, N);
+  return slab_bytes(plan(M, N, K, kTarget, TileCfg{1, 1}).splits, M, N, TileCfg{1, 1});
 }
 
-int64_t esgpt_gemm_counters(int64_t M, int64_t N) { return cdiv(M, TILE) * cdiv(N, TILE); }
+int64_t esgpt_gemm_counters(int64_t M, int64_t N) { return cdiv(M, 64) * cdiv(N, 64); }
 
 int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, const void* B, int64_t ldb, int64_t M,
                     int64_t N, int64_t K, const float* bias, const float* alpha, void* C, int64_t ldc, int c_dtype,
@@ -723,20 +851,21 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   ESGPT_REQUIRE(shapes_ok(akc, bkc, A, lda, B, ldb, M, N, K, C, ldc, f32));
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   if (M == 0 || N == 0) return ESGPT_OK;
-  Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget);
+  const TileCfg tc{1, 1};
+  Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget, tc);
   if (p.splits > 1) {
     p.ext_reduce = f32 && p.splits > in_launch_splits();
-    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N) && (p.ext_reduce || counters));
-    ESGPT_REQUIRE(slab_bytes(p.splits, M, N) < (1ull << 31));  // 32-bit buffer offsets
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N, tc) && (p.ext_reduce || counters));
+    ESGPT_REQUIRE(slab_bytes(p.splits, M, N, tc) < (1ull << 31));  // 32-bit buffer offsets
     p.slab = reinterpret_cast<float*>(workspace);
     p.counters = counters;
   }
   hipStream_t st = as_stream(stream);
   const dim3 grid((unsigned)n_wg(p));
-  if (akc && bkc) gemm_kernel<true, true><<<grid, THREADS, 0, st>>>(p);
-  else if (akc) gemm_kernel<true, false><<<grid, THREADS, 0, st>>>(p);
-  else if (bkc) gemm_kernel<false, true><<<grid, THREADS, 0, st>>>(p);
-  else gemm_kernel<false, false><<<grid, THREADS, 0, st>>>(p);
+  if (akc && bkc) gemm_kernel<true, true, NS, 1, 1><<<grid, THREADS, 0, st>>>(p);
+  else if (akc) gemm_kernel<true, false, NS, 1, 1><<<grid, THREADS, 0, st>>>(p);
+  else if (bkc) gemm_kernel<false, true, NS, 1, 1><<<grid, THREADS, 0, st>>>(p);
+  else gemm_kernel<false, false, NS, 1, 1><<<grid, THREADS, 0, st>>>(p);
   if (p.ext_reduce) launch_slab_reduce(p, st);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
@@ -749,21 +878,28 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
   if (T == 0 || out == 0) return ESGPT_OK;
-  Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 0, 0, bias, nullptr, 0);  // never split
+  const TileCfg tc = fwd_tile(T, out, in);
+  Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 0, 0, bias, nullptr, 0, tc);  // never split
   if (act >= 0) {
     p.epi = EPI_BIAS_ACT;
     p.act = act;
     p.aux_out = reinterpret_cast<__bf16*>(pre);
     p.ld_aux = ldy;
   }
-  if (fwd_stages() == 2) gemm_kernel<true, true, 2><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
-  else gemm_kernel<true, true><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
+  hipStream_t st = as_stream(stream);
+  switch (tc.fm * 10 + tc.fn) {
+    case 21: launch_fwd<2, 1>(p, st); break;
+    case 12: launch_fwd<1, 2>(p, st); break;
+    case 22: launch_fwd<2, 2>(p, st); break;
+    default: launch_fwd<1, 1>(p, st); break;
+  }
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
 
 size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx) {
-  return slab_bytes(plan(out, in, T, dw_target(has_dx != 0, T, in)).splits, out, in);
+  const TileCfg wc = dw_tile(T, in, out);
+  return slab_bytes(plan(out, in, T, dw_target(has_dx != 0, T, in, out), wc).splits, out, in, wc);
 }
 
 int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
@@ -785,7 +921,7 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
   ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
   Prob p0{};
   if (has_dx) {
-    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0);
+    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0, dx_tile(T, in, out));
     if (act >= 0) {
       p0.epi = EPI_ACT_GRAD;
       p0.act = act;
@@ -793,20 +929,24 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
       p0.ld_aux = ldpre;
     }
   }
-  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in));
+  const TileCfg wc = dw_tile(T, in, out);
+  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in, out), wc);
   p1.rowsum = db;
   if (p1.splits > 1) {
     p1.ext_reduce = p1.splits > in_launch_splits();
-    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in) && (p1.ext_reduce || counters));
-    ESGPT_REQUIRE(slab_bytes(p1.splits, out, in) < (1ull << 31));  // 32-bit buffer offsets
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in, wc) &&
+                  (p1.ext_reduce || counters));
+    ESGPT_REQUIRE(slab_bytes(p1.splits, out, in, wc) < (1ull << 31));  // 32-bit buffer offsets
     p1.slab = reinterpret_cast<float*>(workspace);
     p1.counters = counters;
   }
   if (has_dx) {
     p0.wg0 = n_wg(p1);
-    gemm_bwd_pair_kernel<<<dim3((unsigned)(n_wg(p0) + n_wg(p1))), THREADS, 0, st>>>(p0, p1);
+    launch_pair(p0, p1, st);
+  } else if (wc.fm == 2) {
+    gemm_kernel<false, false, bwd_stages<2, 2>(), 2, 2><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
   } else {
-    gemm_kernel<false, false><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
+    gemm_kernel<false, false, NS, 1, 1><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
   }
   if (p1.ext_reduce) launch_slab_reduce(p1, st);
   ESGPT_LAUNCH_CHECK();

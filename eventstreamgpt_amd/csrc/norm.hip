@@ -5,7 +5,7 @@
 //                     out = LayerNorm(h) * w + b                         (f32 or bf16: the next GEMM's operand)
 //   residual_ln_bwd   dh  = rowmask ? dh_in + LN'(dout) : 0 ; dx = dh ; dy = dropout'(dh)
 //                     + the column sums dgamma, dbeta, dbias (block partials, then a fixed-order colsum launch)
-//   bias_act_fwd/bwd  g = act(f + bias) (exact-erf GELU, tanh GELU or ReLU), dbias partials -> colsum
+//   bias_act_fwd/bwd  g = act(f + bias) (erf GELU, tanh GELU or ReLU: common.h), dbias partials -> colsum
 //
 // Layout: one wave per row; lane l owns the 4-column chunks {4l + 256k}, k < KC = ceil(D / 256) (a template
 // parameter: registers sized for the row), loaded as 16-B (f32) / 8-B (bf16) vectors; statistics in registers
@@ -309,30 +309,6 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
   }
 }
 
-__device__ __forceinline__ float act_f(float z, int act) {
-  if (act == 0) return 0.5f * z * (1.f + erff(z * 0.70710678118654752440f));
-  if (act == 1) {
-    const float k = 0.79788456080286535588f;  // sqrt(2/pi)
-    return 0.5f * z * (1.f + tanhf(k * (z + 0.044715f * z * z * z)));
-  }
-  return z > 0.f ? z : 0.f;
-}
-
-__device__ __forceinline__ float act_d(float z, int act) {
-  if (act == 0) {
-    const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752440f));
-    const float pdf = 0.39894228040143267794f * expf(-0.5f * z * z);
-    return cdf + z * pdf;
-  }
-  if (act == 1) {
-    const float k = 0.79788456080286535588f;
-    const float u = k * (z + 0.044715f * z * z * z);
-    const float t = tanhf(u);
-    return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * z * z);
-  }
-  return z > 0.f ? 1.f : 0.f;
-}
-
 // 4 consecutive elements per thread (F % 4 == 0).
 template <typename T>
 __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__ f, const float* __restrict__ bias,
@@ -344,7 +320,7 @@ __global__ __launch_bounds__(256) void bias_act_fwd_kernel(const T* __restrict__
   const V4 bv = load4(bias + c);
   V4 o;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) o.v[j] = act_f(z.v[j] + bv.v[j], act);
+  for (int j = 0; j < 4; ++j) o.v[j] = act_fwd(z.v[j] + bv.v[j], act);
   store4(g + i, o);
 }
 
@@ -369,7 +345,7 @@ __global__ __launch_bounds__(256) void bias_act_bwd_kernel(const T* __restrict__
       V4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        o.v[j] = d.v[j] * act_d(z.v[j] + bv.v[j], act);
+        o.v[j] = d.v[j] * act_grad(z.v[j] + bv.v[j], act);
         s.v[j] += o.v[j];
       }
       store4(dz + r * F + c, o);

@@ -15,7 +15,7 @@ import sys
 from collections import defaultdict
 
 SYMBOLS = ["attn_fwd_mfma_kernel<64, true>", "attn_fwd_mfma_kernel<64, false>", "attn_bwd_kernel<64, true>",
-           "gemm_kernel<true, true, 3>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>",
+           "gemm_kernel<true, true, 3, 1, 1>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>",
            "attn_decode_kernel<float, 64>"]
 # kernels launched at several shapes by bench.py: keyed "<symbol>@grid<work-items>"
 BY_GRID = {"attn_decode_kernel<float, 64>"}
