@@ -59,11 +59,18 @@ class EsgptTTESpec(ctypes.Structure):
 _PB = ctypes.POINTER(EsgptBatch)
 _PK = ctypes.POINTER(EsgptBuckets)
 
+
+class EsgptPackSeg(ctypes.Structure):
+    """``esgpt_pack_seg``: dst[0 .. n) = cast(src[0 .. n)), dst[n .. n_pad) = 0."""
+    _fields_ = [("src", _vp), ("dst", _vp), ("n", _i64), ("n_pad", _i64), ("dst_dtype", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
 SIGNATURES = {
     "esgpt_version": (ctypes.c_char_p, []),
     "esgpt_adamw_chunk": (_i64, []),
     "esgpt_adamw": (_int, [_vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i64, _vp, _vp, _vp]),
     "esgpt_device_arch_ok": (_int, []),
+    "esgpt_pack": (_int, [_vp, _i64, _vp]),
     "esgpt_embed_joint_fwd": (_int, [_PB, _PK, _vp, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_embed_split_bags_fwd": (_int, [_PB, _PK, _vp, _i64, _vp, _i64, _i64, _int, _f32, _f32, _f32, _vp, _vp,
                                           _vp]),
@@ -97,6 +104,8 @@ SIGNATURES = {
     "esgpt_linear_bwd_workspace": (_sz, [_i64, _i64, _i64, _int]),
     "esgpt_linear_bwd": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64, _vp,
                                 _vp, _vp, _sz, _vp, _vp]),
+    "esgpt_linear_bwd_ex": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64, _vp,
+                                   _vp, _vp, _sz, _vp, _vp, _i64, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_collate_shape": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -192,7 +192,16 @@ struct Prob {
   int ext_reduce;      // split-K: slabs summed by slab_reduce_kernel (a second launch) instead of in-launch
   int fast;            // A and B each < 2 GiB: whole tiles take the buffer-load fast path
   int fm, fn;          // tile = (64·fm) x (64·fn): each of the 4 waves holds fm x fn 32x32 fragments
+  const float* rs_extra;  // optional [rs_extra_n][M] f32 rows added into rowsum before alpha
+  int rs_extra_n;
 };
+
+// Σ_b extra[b][m] (fixed order) of the optional row-sum addend.
+__device__ __forceinline__ float rowsum_extra(const Prob& p, int m) {
+  float a = 0.f;
+  for (int b = 0; b < p.rs_extra_n; ++b) a += p.rs_extra[(int64_t)b * p.M + m];
+  return a;
+}
 
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
@@ -438,7 +447,7 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   if (want_rs && h == 0)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
-      if (m0 + lrow(i) < M) p.rowsum[m0 + lrow(i)] = racc[i][0] * al;
+      if (m0 + lrow(i) < M) p.rowsum[m0 + lrow(i)] = (racc[i][0] + rowsum_extra(p, m0 + lrow(i))) * al;
 #pragma unroll
   for (int j = 0; j < FN; ++j)
 #pragma unroll
@@ -658,7 +667,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(Prob p) {
     const float* rs = p.slab + (int64_t)p.splits * nch * 4;
     float a = 0.f;
     for (int z = 0; z < p.splits; ++z) a += rs[(int64_t)z * p.M + m];
-    p.rowsum[m] = a * al;
+    p.rowsum[m] = (a + rowsum_extra(p, (int)m)) * al;
   }
 }
 
@@ -906,7 +915,17 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
                      int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
                      int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
                      void* stream) {
+  return esgpt_linear_bwd_ex(dy, lddy, x, ldx, w, T, in, out, alpha, act, pre, ldpre, dx, lddx, dw, db, workspace,
+                             workspace_bytes, counters, nullptr, 0, stream);
+}
+
+int esgpt_linear_bwd_ex(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T,
+                        int64_t in, int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre,
+                        void* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                        int32_t* counters, const float* db_extra, int64_t n_extra, void* stream) {
   ESGPT_REQUIRE(T >= 0 && in >= 0 && out >= 0);
+  ESGPT_REQUIRE(n_extra >= 0 && n_extra < (1 << 20) &&
+                (n_extra == 0 || (db_extra != nullptr && db != nullptr && T > 0)));
   hipStream_t st = as_stream(stream);
   if (in == 0 || out == 0) return ESGPT_OK;
   ESGPT_REQUIRE(dw != nullptr);
@@ -932,6 +951,8 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
   const TileCfg wc = dw_tile(T, in, out);
   Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in, out), wc);
   p1.rowsum = db;
+  p1.rs_extra = n_extra ? db_extra : nullptr;
+  p1.rs_extra_n = (int)n_extra;
   if (p1.splits > 1) {
     p1.ext_reduce = p1.splits > in_launch_splits();
     ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in, wc) &&

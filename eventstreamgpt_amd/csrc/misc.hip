@@ -67,6 +67,56 @@ __global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __r
     for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) upd(t.p[i], t.g[i], t.m[i], t.v[i]);
   }
 }
+
+// Parameter packing (esgpt_pack): one workgroup per kPackChunk elements of one segment; segment descriptors and
+// their first-chunk prefix are kernel arguments (kPackSegs per launch).
+constexpr int kPackSegs = 48;
+constexpr int kPackChunk = 2048;  // 256 threads x 8 elements
+struct PackArgs {
+  esgpt_pack_seg s[kPackSegs];
+  int64_t c0[kPackSegs + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void pack_kernel(const PackArgs a) {
+  const int64_t blk = blockIdx.x;
+  int s = 0;
+  while (s + 1 < a.n && a.c0[s + 1] <= blk) ++s;  // workgroup-uniform
+  const esgpt_pack_seg g = a.s[s];
+  const int64_t e0 = (blk - a.c0[s]) * kPackChunk + 8 * (int64_t)threadIdx.x;
+  if (e0 >= g.n_pad) return;
+  float v[8];
+  if (g.src && e0 + 8 <= g.n && (reinterpret_cast<uintptr_t>(g.src) & 15) == 0) {
+    const float4 x = *reinterpret_cast<const float4*>(g.src + e0), y = *reinterpret_cast<const float4*>(g.src + e0 + 4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (g.src && e0 + j < g.n) ? g.src[e0 + j] : 0.f;
+  }
+  const bool whole = e0 + 8 <= g.n_pad;
+  if (g.dst_dtype == ESGPT_BF16) {
+    uint16_t* d = reinterpret_cast<uint16_t*>(g.dst) + e0;
+    if (whole && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+      uint4 w;
+      w.x = (uint32_t)f32_to_bf16_bits(v[0]) | ((uint32_t)f32_to_bf16_bits(v[1]) << 16);
+      w.y = (uint32_t)f32_to_bf16_bits(v[2]) | ((uint32_t)f32_to_bf16_bits(v[3]) << 16);
+      w.z = (uint32_t)f32_to_bf16_bits(v[4]) | ((uint32_t)f32_to_bf16_bits(v[5]) << 16);
+      w.w = (uint32_t)f32_to_bf16_bits(v[6]) | ((uint32_t)f32_to_bf16_bits(v[7]) << 16);
+      *reinterpret_cast<uint4*>(d) = w;
+    } else {
+      for (int j = 0; j < 8 && e0 + j < g.n_pad; ++j) d[j] = f32_to_bf16_bits(v[j]);
+    }
+  } else {
+    float* d = reinterpret_cast<float*>(g.dst) + e0;
+    if (whole && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+      *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    } else {
+      for (int j = 0; j < 8 && e0 + j < g.n_pad; ++j) d[j] = v[j];
+    }
+  }
+}
 }  // namespace
 
 hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
@@ -100,6 +150,27 @@ int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n
                                                                    weight_decay, (float)(lr / bc1),
                                                                    (float)sqrt(bc2), per_tensor, err);
   ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_pack(const esgpt_pack_seg* segs, int64_t n_segs, void* stream) {
+  ESGPT_REQUIRE(n_segs >= 0 && (n_segs == 0 || segs != nullptr));
+  for (int64_t i = 0; i < n_segs; ++i)
+    ESGPT_REQUIRE(segs[i].n >= 0 && segs[i].n_pad >= segs[i].n && (segs[i].n == 0 || segs[i].src != nullptr) &&
+                  (segs[i].n_pad == 0 || segs[i].dst != nullptr) &&
+                  (segs[i].dst_dtype == ESGPT_F32 || segs[i].dst_dtype == ESGPT_BF16));
+  for (int64_t b = 0; b < n_segs; b += esgpt::kPackSegs) {
+    esgpt::PackArgs a{};
+    a.n = (int)(n_segs - b < esgpt::kPackSegs ? n_segs - b : esgpt::kPackSegs);
+    a.c0[0] = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.s[i] = segs[b + i];
+      a.c0[i + 1] = a.c0[i] + esgpt::cdiv(a.s[i].n_pad, esgpt::kPackChunk);
+    }
+    if (a.c0[a.n] == 0) continue;
+    esgpt::pack_kernel<<<(unsigned)a.c0[a.n], 256, 0, esgpt::as_stream(stream)>>>(a);
+    ESGPT_LAUNCH_CHECK();
+  }
   return ESGPT_OK;
 }
 

@@ -443,9 +443,15 @@ std::tuple<Tensor, Tensor> linear_act(const Tensor& x, const Tensor& w, const op
 // (dx bf16 [T, in] | empty, dw f32 [out, in], db f32 [out] | empty) of y = x·wᵀ (one grouped launch)
 std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x, const Tensor& w,
                                               const optional<Tensor>& alpha, int64_t act, const optional<Tensor>& pre,
-                                              bool need_dx, bool need_db, const Tensor& tickets) {
+                                              bool need_dx, bool need_db, const Tensor& tickets,
+                                              const optional<Tensor>& db_extra_) {
   const c10::DeviceGuard guard(x.device());
   Tensor dy = dy_.contiguous();
+  Tensor db_extra;
+  if (db_extra_.has_value() && db_extra_->defined() && db_extra_->numel()) {
+    db_extra = as(*db_extra_, at::kFloat);
+    TORCH_CHECK(need_db && db_extra.dim() == 2 && db_extra.size(1) == dy.size(1), "linear_bwd: db_extra [n, out]");
+  }
   const int64_t T = dy.size(0), dout = dy.size(1), din = x.size(1);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dw = at::empty({dout, din}, f32);
@@ -455,11 +461,13 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
   Tensor ws = nb ? at::empty({(int64_t)nb}, x.options().dtype(at::kByte)) : Tensor();
   TORCH_CHECK(!nb || esgpt_gemm_counters(dout, din) <= tickets.numel(), "GEMM tile grid exceeds the ticket array");
   const bool has_pre = pre.has_value() && pre->defined();
-  check(esgpt_linear_bwd(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
-                         optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
-                         has_pre ? pre->stride(0) : 0, need_dx ? dx.data_ptr() : nullptr, need_dx ? din : 0,
-                         ptr<float>(dw), need_db ? ptr<float>(db) : nullptr, ws.defined() ? ws.data_ptr() : nullptr, nb,
-                         ptr<int32_t>(tickets), stream_of(x)),
+  check(esgpt_linear_bwd_ex(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
+                            optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
+                            has_pre ? pre->stride(0) : 0, need_dx ? dx.data_ptr() : nullptr, need_dx ? din : 0,
+                            ptr<float>(dw), need_db ? ptr<float>(db) : nullptr,
+                            ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tickets),
+                            db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
+                            db_extra.defined() ? db_extra.size(0) : 0, stream_of(x)),
         "linear_bwd");
   return {dx, dw, db};
 }
@@ -502,14 +510,54 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> head_loss(const Tensor& xc, const opt
                                                      const Tensor& wc, const Tensor& bc, const optional<Tensor>& wt,
                                                      const optional<Tensor>& bt, at::TensorList cw, at::TensorList cb,
                                                      at::TensorList tw, at::TensorList tb, const Tensor& err,
-                                                     const Tensor& tickets) {
+                                                     const Tensor& tickets, const optional<Tensor>& zb_in) {
   const c10::DeviceGuard guard(xc.device());
   Tensor zc = linear(xc, wc, bc, {}, tickets);
   optional<Tensor> zt;
   if (wt.has_value() && wt->defined()) zt = linear(*xt, *wt, bt, {}, tickets);
-  optional<Tensor> zb;
-  if (shift) zb = bc.to(at::kBFloat16);
+  optional<Tensor> zb;  // the head bias in the logits' dtype: position 0 reads Linear(zeros) = bias
+  if (shift) zb = (zb_in.has_value() && zb_in->defined()) ? *zb_in : bc.to(at::kBFloat16);
   return output_loss(zc, zt, zb, BATCH_PASS, n_levels, shift, terms, tte_i, tte_f, err);
+}
+
+// ---- parameter packing -----------------------------------------------------------------------------------------
+// One launch: group g = srcs[o_g .. o_g + group_sizes[g]) flattened and concatenated into a new 1-D tensor of dtype
+// code dtypes[g] (ESGPT_F32 / ESGPT_BF16) followed by tails[g] zeros. srcs: contiguous f32 device tensors.
+std::vector<Tensor> pack(at::TensorList srcs, at::IntArrayRef group_sizes, at::IntArrayRef tails,
+                         at::IntArrayRef dtypes) {
+  TORCH_CHECK(!srcs.empty() && group_sizes.size() == tails.size() && tails.size() == dtypes.size(), "pack: arguments");
+  const c10::DeviceGuard guard(srcs[0].device());
+  std::vector<Tensor> outs;
+  std::vector<esgpt_pack_seg> segs;
+  size_t k = 0;
+  for (size_t gi = 0; gi < group_sizes.size(); ++gi) {
+    TORCH_CHECK(dtypes[gi] == ESGPT_F32 || dtypes[gi] == ESGPT_BF16, "pack: dtype code");
+    TORCH_CHECK(group_sizes[gi] >= 0 && tails[gi] >= 0 && k + group_sizes[gi] <= srcs.size(), "pack: group sizes");
+    int64_t n = 0;
+    for (int64_t j = 0; j < group_sizes[gi]; ++j) {
+      const Tensor& t = srcs[k + j];
+      require_hip(t, "pack");
+      TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous(), "pack: contiguous f32 sources expected");
+      n += t.numel();
+    }
+    const bool bf = dtypes[gi] == ESGPT_BF16;
+    Tensor out = at::empty({n + tails[gi]}, srcs[0].options().dtype(bf ? at::kBFloat16 : at::kFloat));
+    const size_t esz = bf ? 2 : 4;
+    int64_t off = 0;
+    for (int64_t j = 0; j < group_sizes[gi]; ++j, ++k) {
+      const Tensor& t = srcs[k];
+      const bool last = j + 1 == group_sizes[gi];
+      segs.push_back(esgpt_pack_seg{t.data_ptr<float>(), static_cast<char*>(out.data_ptr()) + off * esz, t.numel(),
+                                    t.numel() + (last ? tails[gi] : 0), (int32_t)dtypes[gi], 0});
+      off += t.numel();
+    }
+    if (group_sizes[gi] == 0 && tails[gi] > 0)
+      segs.push_back(esgpt_pack_seg{nullptr, out.data_ptr(), 0, tails[gi], (int32_t)dtypes[gi], 0});
+    outs.push_back(out);
+  }
+  TORCH_CHECK(k == srcs.size(), "pack: group sizes do not cover srcs");
+  check(esgpt_pack(segs.data(), (int64_t)segs.size(), stream_of(srcs[0])), "pack");
+  return outs;
 }
 
 // ---- optimizer -------------------------------------------------------------------------------------------------------
@@ -556,13 +604,14 @@ TORCH_LIBRARY(esgpt, m) {
         "Tensor? bias, Tensor? alpha, bool accumulate, Tensor tickets) -> ()");
   m.def("linear_act(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
-        "Tensor tickets) -> (Tensor, Tensor, Tensor)");
+        "Tensor tickets, Tensor? db_extra=None) -> (Tensor, Tensor, Tensor)");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
   m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, Tensor? b_pj, int act, Tensor p_fc, Tensor p_pj, "
         "Tensor tickets) -> (Tensor, Tensor, Tensor)");
   m.def("head_loss(Tensor xc, Tensor? xt, " BATCH_SCHEMA ", int[] terms, int[] tte_i, float[] tte_f, int shift, "
         "int n_levels, Tensor wc, Tensor bc, Tensor? wt, Tensor? bt, Tensor[] cw, Tensor[] cb, Tensor[] tw, "
-        "Tensor[] tb, Tensor err, Tensor tickets) -> (Tensor, Tensor, Tensor, Tensor)");
+        "Tensor[] tb, Tensor err, Tensor tickets, Tensor? zb) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("pack(Tensor[] srcs, int[] group_sizes, int[] tails, int[] dtypes) -> Tensor[]");
   m.def("adamw(Tensor table, Tensor blocks, float lr, float beta1, float beta2, float eps, float weight_decay, "
         "int step, Tensor? per_tensor, Tensor err) -> ()");
 }
@@ -590,5 +639,6 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("linear", &linear);
   m.impl("mlp", &mlp);
   m.impl("head_loss", &head_loss);
+  m.impl("pack", &pack);
   m.impl("adamw", &adamw);
 }

@@ -200,7 +200,10 @@ def weight_shadow(blocks, dtype):
         a = b.attn.attention
         ws += [a.q_proj.weight, a.k_proj.weight, a.v_proj.weight, a.out_proj.weight, b.mlp.c_fc.weight,
                b.mlp.c_proj.weight]
-    flat = torch.cat([w.reshape(-1) for w in ws]).to(dtype)
+    if dtype == torch.bfloat16:  # one esgpt::pack launch (a cat + a cast otherwise)
+        flat = _ops().pack([w.detach() for w in ws], [len(ws)], [0], [L.BF16])[0]
+    else:
+        flat = torch.cat([w.reshape(-1) for w in ws]).to(dtype)
     out, off = [], 0
     for i in range(len(blocks)):
         q, k, v, o, fc, pj = ws[6 * i: 6 * i + 6]
@@ -227,25 +230,6 @@ def linear_bias(x: torch.Tensor, params, biases) -> torch.Tensor:
         return proj(x.to(dt), None, b, params)
 
 
-_ZPAD: dict = {}
-
-
-def _pad_rows(ts, mult: int = 8):
-    """Row-concatenation of ``ts`` (same dtype / trailing dim) padded with zero rows to a multiple of ``mult``
-    (one cat kernel; the zero block is cached)."""
-    n = sum(t.shape[0] for t in ts)
-    pad = (-n) % mult
-    if pad:
-        t0 = ts[0]
-        key = (pad, tuple(t0.shape[1:]), t0.dtype, t0.device)
-        z = _ZPAD.get(key)
-        if z is None:
-            z = torch.zeros((pad,) + tuple(t0.shape[1:]), dtype=t0.dtype, device=t0.device)
-            _ZPAD[key] = z
-        ts = list(ts) + [z]
-    return torch.cat(list(ts), 0) if len(ts) > 1 else ts[0]
-
-
 def head_loss_op(xc, xt, batch, terms, tte, shift: int, n_levels: int, cw, cb, tw, tb):
     """``esgpt::head_loss``: bf16 generative heads + fused losses in one autograd node (model_output.py:1253-1721):
     z = x · W_padᵀ + b_pad with the HIP GEMM (the head's output columns padded to a multiple of 8 with zero
@@ -254,16 +238,35 @@ def head_loss_op(xc, xt, batch, terms, tte, shift: int, n_levels: int, cw, cb, t
     sync. ``xt`` / ``tw`` / ``tb`` are None / empty when the TTE columns are part of the content head (CI). Returns
     f32 [n_terms + 2] like ``output_loss``."""
     with torch.no_grad():
-        wc = _pad_rows([w.detach() for w in cw]).to(torch.bfloat16)
-        bc = _pad_rows([b.detach().float() for b in cb]).contiguous()
-        wt = _pad_rows([w.detach() for w in tw]).to(torch.bfloat16) if tw else None
-        bt = _pad_rows([b.detach().float() for b in tb]).contiguous() if tw else None
+        # every padded head weight / bias copy in one esgpt::pack launch: [W_c | 0] bf16, [b_c | 0] f32 and bf16
+        # (the position-0 logits when shifted), [W_t | 0] bf16, [b_t | 0] f32
+        D = cw[0].shape[1]
+        nc = sum(w.shape[0] for w in cw)
+        pc = (-nc) % 8
+        srcs = [w.detach() for w in cw] + [b.detach() for b in cb] + ([b.detach() for b in cb] if shift else [])
+        groups, tails, codes = [len(cw), len(cb)], [pc * D, pc], [L.BF16, L.F32]
+        if shift:
+            groups.append(len(cb))
+            tails.append(pc)
+            codes.append(L.BF16)
+        if tw:
+            nt = sum(w.shape[0] for w in tw)
+            pt = (-nt) % 8
+            srcs += [w.detach() for w in tw] + [b.detach() for b in tb]
+            groups += [len(tw), len(tb)]
+            tails += [pt * D, pt]
+            codes += [L.BF16, L.F32]
+        out = _ops().pack([t.float().contiguous() for t in srcs], groups, tails, codes)
+        wc, bc = out[0].view(nc + pc, D), out[1]
+        zb = out[2] if shift else None
+        wt = out[-2].view(-1, D) if tw else None
+        bt = out[-1] if tw else None
     ti, tf = tte_lists(tte)
     dev = xc.device
     with _timed("output_loss"):
         losses, _, _, _ = _ops().head_loss(xc, xt, *batch_args(batch), terms_list(terms), ti, tf, int(shift),
                                            int(n_levels), wc, bc, wt, bt, list(cw), list(cb), list(tw), list(tb),
-                                           err_word(dev), tickets(dev))
+                                           err_word(dev), tickets(dev), zb)
     return losses
 
 

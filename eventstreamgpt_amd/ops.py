@@ -24,7 +24,8 @@ Differentiable operators and the reference code they replace:
 
 Non-differentiable: ``embed_bag_bwd``, ``embed_epilogue_bwd``, ``attention_bwd``, ``residual_ln_bwd``,
 ``bias_act_bwd``, ``linear_act``, ``linear_bwd``, ``gemm`` / ``gemm_``, ``column_sum``, ``kv_append``,
-``attn_decode`` (generation) and ``adamw`` (generative_modeling.py:460-485).
+``attn_decode`` (generation), ``pack`` (the compute-dtype parameter copies) and ``adamw``
+(generative_modeling.py:460-485).
 
 There is no CPU kernel: calling an operator on CPU tensors raises (no fallback).
 """
@@ -43,7 +44,7 @@ _state = {"loaded": False}
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
-       "adamw")
+       "pack", "adamw")
 
 
 def load():
@@ -67,14 +68,14 @@ def _tickets(device):
     return tickets(device)
 
 
-def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db):
+def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None):
     """``esgpt::linear_bwd`` from a registered backward (records the launch shape for bench.py when asked)."""
     from . import fused
 
     if fused.SHAPES["enabled"]:
         fused.SHAPES["linear_bwd"].append((dy.shape[0], x.shape[1], dy.shape[1], bool(need_dx), int(act),
                                            bool(need_db)))
-    return torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device))
+    return torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device), db_extra)
 
 
 def _batch_d(args, start):
@@ -139,7 +140,7 @@ def _register():
 
     @fake(lib + "head_loss")
     def _(xc, xt, em, td, tm, di, dm, dv, dvm, si, sm, terms, tte_i, tte_f, shift, n_levels, wc, bc, wt, bt, cw, cb,
-          tw, tb, err, tickets):
+          tw, tb, err, tickets, zb):
         zc = xc.new_empty(xc.shape[0], wc.shape[0])
         zt = None if wt is None else xt.new_empty(xt.shape[0], wt.shape[0])
         return _loss_fake(zc, zt, shift, len(terms) // 8, di.shape[0])
@@ -185,11 +186,20 @@ def _register():
         return (x.new_empty(x.shape[0], w.shape[0]) if act >= 0 else x.new_empty(0)), y
 
     @fake(lib + "linear_bwd")
-    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets):
+    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None):
         f32 = torch.float32
         return (x.new_empty(dy.shape[0], x.shape[1], dtype=dy.dtype) if need_dx else x.new_empty(0, dtype=dy.dtype),
                 x.new_empty(dy.shape[1], x.shape[1], dtype=f32),
                 x.new_empty(dy.shape[1], dtype=f32) if need_db else x.new_empty(0, dtype=f32))
+
+    @fake(lib + "pack")
+    def _(srcs, group_sizes, tails, dtypes):
+        outs, k = [], 0
+        for n_src, tail, code in zip(group_sizes, tails, dtypes):
+            n = sum(t.numel() for t in srcs[k: k + n_src])
+            k += n_src
+            outs.append(srcs[0].new_empty(n + tail, dtype=torch.bfloat16 if code == L.BF16 else torch.float32))
+        return outs
 
     @fake(lib + "linear")
     def _(x, w, bias, masters, tickets):
@@ -393,14 +403,13 @@ def _register():
 
     def _hl_bwd(ctx, g, *_):
         if g is None:
-            return (None,) * 26
+            return (None,) * 27
         xc, xt, wc, wt, dzc, dzt, dbias = ctx.saved_tensors
         n_cw, n_tw = ctx.n
         rows_c, rows_t = ctx.rows
         alpha = g.contiguous()[-1:]
-        dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True)
-        if dbias.numel():
-            dbc = dbc + dbias.sum(0) * alpha
+        # the loss kernel's per-subject position-0 bias rows are summed into db inside the same launch
+        dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, dbias if dbias.numel() else None)
         nc = sum(rows_c)
         gw_c = list(torch.split(dwc[:nc], rows_c, 0))
         gb_c = list(torch.split(dbc[:nc], rows_c, 0))
@@ -411,6 +420,6 @@ def _register():
             gw_t = list(torch.split(dwt[:nt], rows_t, 0))
             gb_t = list(torch.split(dbt[:nt], rows_t, 0))
         return (dxc, dxt) + (None,) * 14 + (None, None, None, None, gw_c, gb_c, gw_t, gb_t,
-                                             None, None)
+                                             None, None, None)
 
     reg(lib + "head_loss", _hl_bwd, setup_context=_hl_setup)

@@ -253,7 +253,10 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
  *     gradient w.r.t. the pre-activation of an input x = act(pre)), dw = alpha·dyᵀ·x (f32 [out, in]) and
  *     db = alpha·Σ_rows dy (f32 [out], optional). dx = NULL skips the input gradient. Split-K workspace:
  *     esgpt_linear_bwd_workspace(T, in, out, dx != NULL) bytes; counters as for esgpt_gemm_bf16 with
- *     esgpt_gemm_counters(out, in) entries. T == 0 zero-fills dw and db. */
+ *     esgpt_gemm_counters(out, in) entries. T == 0 zero-fills dw and db.
+ *   esgpt_linear_bwd_ex: the same plus n_extra f32 rows db_extra [n_extra, out] added into db before the alpha
+ *     scaling, db = alpha·(Σ_rows dy + Σ_b db_extra[b]) — the generative head's bias gradient, whose position-0
+ *     rows the loss kernel accumulates per subject (model_output.py:1253-1721; replaces a sum + scale + add). */
 int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64_t in, int64_t out,
                      const float* bias, int act, void* pre, void* y, int64_t ldy, void* stream);
 size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx);
@@ -261,6 +264,25 @@ int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
                      int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
                      int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
                      void* stream);
+int esgpt_linear_bwd_ex(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
+                        int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
+                        int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                        int32_t* counters, const float* db_extra, int64_t n_extra, void* stream);
+
+/* ---- Parameter packing -------------------------------------------------------------------------------------
+ * The compute-dtype copies of the f32 parameters a step reads, in ONE launch: the blocks' flat bf16 weight shadow
+ * and the generative head's row-concatenated weights / biases (zero rows up to a multiple of 8; model_output.py
+ * concatenates nothing — its heads are separate nn.Linear modules). Segment s writes dst[0 .. n) = src[0 .. n)
+ * converted to dst_dtype (ESGPT_F32 or ESGPT_BF16, round-to-nearest-even) and dst[n .. n_pad) = 0; src = NULL
+ * writes zeros only. Replaces torch.cat + .to(bfloat16) pairs (one launch each). */
+typedef struct esgpt_pack_seg {
+  const float* src;
+  void* dst;
+  int64_t n, n_pad;
+  int32_t dst_dtype;
+  int32_t reserved;
+} esgpt_pack_seg;
+int esgpt_pack(const esgpt_pack_seg* segs, int64_t n_segs, void* stream);
 
 /* ---- Optimizer ------------------------------------------------------------------------------------------
  * Fused AdamW step (torch.optim.AdamW semantics: decoupled weight decay, bias-corrected moments;

@@ -122,7 +122,7 @@ def test_head_loss_and_output_loss_autograd(esgpt):
     wc = torch.empty(16, 8, dtype=torch.bfloat16, device=M)
     bc = torch.empty(16, device=M)
     losses, dzc, dzt, dbias = esgpt.head_loss(xc, None, *_batch(), terms, [1, 1, 13], [0.0, 1.0], 1, 1, wc, bc, None,
-                                              None, cw, cb, [], [], _err(), _tk())
+                                              None, cw, cb, [], [], _err(), _tk(), None)
     assert losses.shape == (3,) and dzc.shape == (10, 16) and dbias.shape == (2, 16)
     losses[-1].backward()
     assert xc.grad.shape == xc.shape and all(p.grad is not None for p in cw + cb)

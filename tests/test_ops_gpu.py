@@ -158,3 +158,51 @@ def test_adamw_op_equals_c_abi(env):
                             0.01, 1, None, None, L.stream()), "adamw")
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
+
+
+def test_pack_equals_cat_cast_and_c_abi(env):
+    """esgpt::pack (one launch) = torch.cat + zero tail + cast, bit for bit (bf16 round-to-nearest-even), over
+    more segments than one launch carries (48), odd lengths and unaligned starts; and = the raw C ABI."""
+    esgpt, lib = env
+    g = _g(21)
+    ts = [torch.randn(n, device=DEV, generator=g) * 3 for n in [5, 256 * 7, 1, 2049, 64, 3] * 9]  # 54 segments
+    ts[7][0] = float("nan")
+    groups, tails, codes = [30, 24, 24], [13, 0, 5], [L.BF16, L.F32, L.BF16]
+    srcs = ts[:30] + ts[30:] + ts[30:]
+    out = esgpt.pack(srcs, groups, tails, codes)
+    k = 0
+    for o, n_src, tail, code in zip(out, groups, tails, codes):
+        ref = torch.cat([t.reshape(-1) for t in srcs[k: k + n_src]] + [torch.zeros(tail, device=DEV)])
+        k += n_src
+        ref = ref.to(torch.bfloat16 if code == L.BF16 else torch.float32)
+        assert o.dtype == ref.dtype and o.shape == ref.shape
+        assert torch.equal(o.view(torch.int16) if code == L.BF16 else o.view(torch.int32),
+                           ref.view(torch.int16) if code == L.BF16 else ref.view(torch.int32))
+    # raw C ABI: the first group's segments, the tail on the last one
+    dst = torch.full((out[0].numel(),), 7.0, device=DEV).bfloat16()
+    segs, off = [], 0
+    for j, t in enumerate(srcs[:30]):
+        n = t.numel()
+        segs.append(L.EsgptPackSeg(t.data_ptr(), dst.data_ptr() + 2 * off, n, n + (13 if j == 29 else 0), L.BF16, 0))
+        off += n
+    arr = (L.EsgptPackSeg * len(segs))(*segs)
+    L.check(lib.esgpt_pack(arr, len(segs), L.stream()), "pack")
+    assert torch.equal(dst.view(torch.int16), out[0].view(torch.int16))
+
+
+def test_linear_bwd_row_sum_addend(env):
+    """esgpt_linear_bwd_ex's db_extra: db = alpha·(Σ_rows dy + Σ_b extra[b]) in the same launch (the head's
+    position-0 bias rows), for a split-K plan and a whole-K plan; dx / dw unchanged."""
+    esgpt, _ = env
+    t = tickets(torch.device(DEV))
+    for T, din, dout in [(8192, 256, 1624), (256, 64, 24)]:
+        x = torch.randn(T, din, device=DEV, generator=_g(31)).bfloat16()
+        w = (0.05 * torch.randn(dout, din, device=DEV, generator=_g(32))).bfloat16()
+        dy = torch.randn(T, dout, device=DEV, generator=_g(33)).bfloat16()
+        extra = torch.randn(32, dout, device=DEV, generator=_g(34))
+        alpha = torch.tensor([0.75], device=DEV)
+        dx, dw, db = esgpt.linear_bwd(dy, x, w, alpha, -1, None, True, True, t)
+        dx2, dw2, db2 = esgpt.linear_bwd(dy, x, w, alpha, -1, None, True, True, t, extra)
+        assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
+        ref = db.double() + extra.double().sum(0) * 0.75
+        assert float((db2.double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max()), (T, din, dout)
