@@ -839,6 +839,79 @@ void launch_pair(const Prob& p0, const Prob& p1, hipStream_t st) {
   }
 }
 
+template <int XM, int XN>
+void launch_dx_only(const Prob& p0, hipStream_t st) {
+  gemm_kernel<true, false, bwd_stages<XM, XN>(), XM, XN><<<dim3((unsigned)n_wg(p0)), THREADS, 0, st>>>(p0);
+}
+
+// The backward of one projection. st_dw == nullptr: dX and dW (+ db) in ONE grouped launch on st. Otherwise
+// split: dX on st, dW (+ db, its split-K workspace and counters) on st_dw after it waits for the work queued on st
+// so far — the weight gradient leaves the critical path of backward and runs beside the next layers' kernels. Both
+// forms use the same tiles and split plan (the dW target counts the dX tiles either way): bitwise equal results.
+int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
+                    int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx, int64_t lddx,
+                    float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
+                    const float* db_extra, int64_t n_extra, hipStream_t st, hipStream_t st_dw) {
+  ESGPT_REQUIRE(T >= 0 && in >= 0 && out >= 0);
+  ESGPT_REQUIRE(n_extra >= 0 && n_extra < (1 << 20) &&
+                (n_extra == 0 || (db_extra != nullptr && db != nullptr && T > 0)));
+  if (in == 0 || out == 0) return ESGPT_OK;
+  ESGPT_REQUIRE(dw != nullptr);
+  const bool has_dx = dx != nullptr;
+  hipStream_t sw = st_dw ? st_dw : st;
+  if (st_dw && esgpt_stream_wait(st_dw, st) != ESGPT_OK) return ESGPT_ERR_LAUNCH;
+  if (T == 0) {  // empty batch (the operands may be empty allocations): zero weight / bias gradients
+    if (zero_async(dw, sizeof(float) * out * in, sw) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    if (db && zero_async(db, sizeof(float) * out, sw) != hipSuccess) return ESGPT_ERR_LAUNCH;
+    return ESGPT_OK;
+  }
+  ESGPT_REQUIRE(shapes_ok(false, false, dy, lddy, x, ldx, out, in, T, dw, in, true));
+  if (has_dx) ESGPT_REQUIRE(shapes_ok(true, false, dy, lddy, w, in, T, in, out, dx, lddx, false));
+  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
+  Prob p0{};
+  if (has_dx) {
+    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0, dx_tile(T, in, out));
+    if (act >= 0) {
+      p0.epi = EPI_ACT_GRAD;
+      p0.act = act;
+      p0.aux = reinterpret_cast<const __bf16*>(pre);
+      p0.ld_aux = ldpre;
+    }
+  }
+  const TileCfg wc = dw_tile(T, in, out);
+  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in, out), wc);
+  p1.rowsum = db;
+  p1.rs_extra = n_extra ? db_extra : nullptr;
+  p1.rs_extra_n = (int)n_extra;
+  if (p1.splits > 1) {
+    p1.ext_reduce = p1.splits > in_launch_splits();
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in, wc) &&
+                  (p1.ext_reduce || counters));
+    ESGPT_REQUIRE(slab_bytes(p1.splits, out, in, wc) < (1ull << 31));  // 32-bit buffer offsets
+    p1.slab = reinterpret_cast<float*>(workspace);
+    p1.counters = counters;
+  }
+  if (has_dx && !st_dw) {
+    p0.wg0 = n_wg(p1);
+    launch_pair(p0, p1, st);
+  } else {
+    if (has_dx) {
+      switch (p0.fm * 10 + p0.fn) {
+        case 21: launch_dx_only<2, 1>(p0, st); break;
+        case 22: launch_dx_only<2, 2>(p0, st); break;
+        default: launch_dx_only<1, 1>(p0, st); break;
+      }
+    }
+    if (wc.fm == 2)
+      gemm_kernel<false, false, bwd_stages<2, 2>(), 2, 2><<<dim3((unsigned)n_wg(p1)), THREADS, 0, sw>>>(p1);
+    else
+      gemm_kernel<false, false, NS, 1, 1><<<dim3((unsigned)n_wg(p1)), THREADS, 0, sw>>>(p1);
+  }
+  if (p1.ext_reduce) launch_slab_reduce(p1, sw);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -923,55 +996,18 @@ int esgpt_linear_bwd_ex(const void* dy, int64_t lddy, const void* x, int64_t ldx
                         int64_t in, int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre,
                         void* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
                         int32_t* counters, const float* db_extra, int64_t n_extra, void* stream) {
-  ESGPT_REQUIRE(T >= 0 && in >= 0 && out >= 0);
-  ESGPT_REQUIRE(n_extra >= 0 && n_extra < (1 << 20) &&
-                (n_extra == 0 || (db_extra != nullptr && db != nullptr && T > 0)));
-  hipStream_t st = as_stream(stream);
-  if (in == 0 || out == 0) return ESGPT_OK;
-  ESGPT_REQUIRE(dw != nullptr);
-  if (T == 0) {  // empty batch (the operands may be empty allocations): zero weight / bias gradients
-    if (zero_async(dw, sizeof(float) * out * in, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-    if (db && zero_async(db, sizeof(float) * out, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-    return ESGPT_OK;
-  }
-  ESGPT_REQUIRE(shapes_ok(false, false, dy, lddy, x, ldx, out, in, T, dw, in, true));
-  const bool has_dx = dx != nullptr;
-  if (has_dx) ESGPT_REQUIRE(shapes_ok(true, false, dy, lddy, w, in, T, in, out, dx, lddx, false));
-  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
-  Prob p0{};
-  if (has_dx) {
-    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0, dx_tile(T, in, out));
-    if (act >= 0) {
-      p0.epi = EPI_ACT_GRAD;
-      p0.act = act;
-      p0.aux = reinterpret_cast<const __bf16*>(pre);
-      p0.ld_aux = ldpre;
-    }
-  }
-  const TileCfg wc = dw_tile(T, in, out);
-  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in, out), wc);
-  p1.rowsum = db;
-  p1.rs_extra = n_extra ? db_extra : nullptr;
-  p1.rs_extra_n = (int)n_extra;
-  if (p1.splits > 1) {
-    p1.ext_reduce = p1.splits > in_launch_splits();
-    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p1.splits, out, in, wc) &&
-                  (p1.ext_reduce || counters));
-    ESGPT_REQUIRE(slab_bytes(p1.splits, out, in, wc) < (1ull << 31));  // 32-bit buffer offsets
-    p1.slab = reinterpret_cast<float*>(workspace);
-    p1.counters = counters;
-  }
-  if (has_dx) {
-    p0.wg0 = n_wg(p1);
-    launch_pair(p0, p1, st);
-  } else if (wc.fm == 2) {
-    gemm_kernel<false, false, bwd_stages<2, 2>(), 2, 2><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
-  } else {
-    gemm_kernel<false, false, NS, 1, 1><<<dim3((unsigned)n_wg(p1)), THREADS, 0, st>>>(p1);
-  }
-  if (p1.ext_reduce) launch_slab_reduce(p1, st);
-  ESGPT_LAUNCH_CHECK();
-  return ESGPT_OK;
+  return linear_bwd_impl(dy, lddy, x, ldx, w, T, in, out, alpha, act, pre, ldpre, dx, lddx, dw, db, workspace,
+                         workspace_bytes, counters, db_extra, n_extra, as_stream(stream), nullptr);
+}
+
+int esgpt_linear_bwd_split(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T,
+                           int64_t in, int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre,
+                           void* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                           int32_t* counters, const float* db_extra, int64_t n_extra, void* stream,
+                           void* stream_dw) {
+  ESGPT_REQUIRE(stream_dw != nullptr && stream_dw != stream);
+  return linear_bwd_impl(dy, lddy, x, ldx, w, T, in, out, alpha, act, pre, ldpre, dx, lddx, dw, db, workspace,
+                         workspace_bytes, counters, db_extra, n_extra, as_stream(stream), as_stream(stream_dw));
 }
 
 }  // extern "C"

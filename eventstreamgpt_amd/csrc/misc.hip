@@ -174,6 +174,23 @@ int esgpt_pack(const esgpt_pack_seg* segs, int64_t n_segs, void* stream) {
   return ESGPT_OK;
 }
 
+// `waiter` waits (on the device) for every piece of work queued on `signaller` so far: one event from a per-device
+// ring (an event may be re-recorded as soon as the wait on it has been enqueued; under HIP-graph capture each record
+// / wait pair becomes a graph edge, so this forks and joins captured streams).
+int esgpt_stream_wait(void* waiter, void* signaller) {
+  constexpr int kRing = 64, kDevs = 16;
+  static hipEvent_t ring[kDevs][kRing] = {};
+  static int next[kDevs] = {};
+  ESGPT_REQUIRE(waiter != signaller);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevs) return ESGPT_ERR_LAUNCH;
+  hipEvent_t& ev = ring[dev][next[dev]];
+  next[dev] = (next[dev] + 1) % kRing;
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  if (hipEventRecord(ev, esgpt::as_stream(signaller)) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  return hipStreamWaitEvent(esgpt::as_stream(waiter), ev, 0) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+}
+
 int esgpt_device_arch_ok(void) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, 0) != hipSuccess) return 0;

@@ -15,6 +15,8 @@
 // registered from Python (eventstreamgpt_amd/ops.py).
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -441,11 +443,35 @@ std::tuple<Tensor, Tensor> linear_act(const Tensor& x, const Tensor& w, const op
 }
 
 // (dx bf16 [T, in] | empty, dw f32 [out, in], db f32 [out] | empty) of y = x·wᵀ (one grouped launch)
+// The weight-gradient stream of a device: one pool stream per device for the life of the process (every split
+// backward's dW launch is ordered on it, so they may share one split-K workspace pool and ticket array).
+c10::hip::HIPStream weight_grad_stream(c10::DeviceIndex dev) {
+  static std::vector<optional<c10::hip::HIPStream>> streams(64);
+  TORCH_CHECK(dev >= 0 && dev < 64, "eventstreamgpt_amd: device index out of range");
+  if (!streams[dev].has_value()) streams[dev] = c10::hip::getStreamFromPool(false, dev);
+  return *streams[dev];
+}
+
+// The current stream waits for every weight-gradient launch queued so far (before dW / db are read).
+void weight_grad_join(const Tensor& like) {
+  const c10::DeviceGuard guard(like.device());
+  const auto side = weight_grad_stream(like.device().index());
+  check(esgpt_stream_wait(stream_of(like), reinterpret_cast<void*>(side.stream())), "weight_grad_join");
+}
+
+// Keeps a tensor's memory from being reused by other streams' allocations until the work queued on `s` is done.
+void used_on(const Tensor& t, const c10::hip::HIPStream& s) {
+  if (t.defined() && t.numel()) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), s);
+}
+
 std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x, const Tensor& w,
                                               const optional<Tensor>& alpha, int64_t act, const optional<Tensor>& pre,
                                               bool need_dx, bool need_db, const Tensor& tickets,
-                                              const optional<Tensor>& db_extra_) {
+                                              const optional<Tensor>& db_extra_, const optional<Tensor>& dw_tickets) {
   const c10::DeviceGuard guard(x.device());
+  // dw_tickets given: split form — dX on the current stream, dW / db on the device's weight-gradient stream (with
+  // their own ticket array, workspace and outputs allocated in that stream's order); weight_grad_join before use
+  const bool split = dw_tickets.has_value() && dw_tickets->defined();
   Tensor dy = dy_.contiguous();
   Tensor db_extra;
   if (db_extra_.has_value() && db_extra_->defined() && db_extra_->numel()) {
@@ -454,21 +480,52 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
   }
   const int64_t T = dy.size(0), dout = dy.size(1), din = x.size(1);
   auto f32 = x.options().dtype(at::kFloat);
-  Tensor dw = at::empty({dout, din}, f32);
   Tensor dx = need_dx ? at::empty({T, din}, dy.options()) : at::empty({0}, dy.options());
-  Tensor db = need_db ? at::empty({dout}, f32) : at::empty({0}, f32);
   const size_t nb = esgpt_linear_bwd_workspace(T, din, dout, need_dx ? 1 : 0);
-  Tensor ws = nb ? at::empty({(int64_t)nb}, x.options().dtype(at::kByte)) : Tensor();
-  TORCH_CHECK(!nb || esgpt_gemm_counters(dout, din) <= tickets.numel(), "GEMM tile grid exceeds the ticket array");
+  const Tensor& tk = split ? *dw_tickets : tickets;
+  TORCH_CHECK(!nb || esgpt_gemm_counters(dout, din) <= tk.numel(), "GEMM tile grid exceeds the ticket array");
   const bool has_pre = pre.has_value() && pre->defined();
-  check(esgpt_linear_bwd_ex(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
-                            optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
-                            has_pre ? pre->stride(0) : 0, need_dx ? dx.data_ptr() : nullptr, need_dx ? din : 0,
-                            ptr<float>(dw), need_db ? ptr<float>(db) : nullptr,
-                            ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tickets),
-                            db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
-                            db_extra.defined() ? db_extra.size(0) : 0, stream_of(x)),
-        "linear_bwd");
+  const auto cur = c10::hip::getCurrentHIPStream(x.device().index());
+  const auto side = split ? weight_grad_stream(x.device().index()) : cur;
+  Tensor dw, db, ws;
+  void* s_cur = reinterpret_cast<void*>(cur.stream());
+  // fork first: under HIP-graph capture the side stream must have joined the capture before it allocates, so that
+  // its blocks come from the graph's private pool (and no allocation reaches the driver mid-capture)
+  if (split) check(esgpt_stream_wait(reinterpret_cast<void*>(side.stream()), s_cur), "linear_bwd fork");
+  {
+    const c10::hip::HIPStreamGuard sg(side);  // the dW product's allocations in its stream's order
+    dw = at::empty({dout, din}, f32);
+    db = need_db ? at::empty({dout}, f32) : at::empty({0}, f32);
+    ws = nb ? at::empty({(int64_t)nb}, x.options().dtype(at::kByte)) : Tensor();
+  }
+  const void* dxp = need_dx ? dx.data_ptr() : nullptr;
+  if (split) {
+    check(esgpt_linear_bwd_split(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
+                                 optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
+                                 has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0,
+                                 ptr<float>(dw), need_db ? ptr<float>(db) : nullptr,
+                                 ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tk),
+                                 db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
+                                 db_extra.defined() ? db_extra.size(0) : 0, s_cur,
+                                 reinterpret_cast<void*>(side.stream())),
+          "linear_bwd");
+    // operands the weight-gradient stream reads: not reused by the current stream's later allocations until
+    // that stream's reads are done (under graph capture: not reused within the capture)
+    used_on(dy, side);
+    used_on(x, side);
+    used_on(dy_, side);
+    if (alpha.has_value()) used_on(*alpha, side);
+    used_on(db_extra, side);
+  } else {
+    check(esgpt_linear_bwd_ex(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
+                              optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
+                              has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0,
+                              ptr<float>(dw), need_db ? ptr<float>(db) : nullptr,
+                              ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tickets),
+                              db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
+                              db_extra.defined() ? db_extra.size(0) : 0, s_cur),
+          "linear_bwd");
+  }
   return {dx, dw, db};
 }
 
@@ -604,7 +661,8 @@ TORCH_LIBRARY(esgpt, m) {
         "Tensor? bias, Tensor? alpha, bool accumulate, Tensor tickets) -> ()");
   m.def("linear_act(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
-        "Tensor tickets, Tensor? db_extra=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None) -> (Tensor, Tensor, Tensor)");
+  m.def("weight_grad_join(Tensor like) -> ()");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
   m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, Tensor? b_pj, int act, Tensor p_fc, Tensor p_pj, "
         "Tensor tickets) -> (Tensor, Tensor, Tensor)");
@@ -636,6 +694,7 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("gemm_", &gemm_);
   m.impl("linear_act", &linear_act);
   m.impl("linear_bwd", &linear_bwd);
+  m.impl("weight_grad_join", &weight_grad_join);
   m.impl("linear", &linear);
   m.impl("mlp", &mlp);
   m.impl("head_loss", &head_loss);

@@ -156,22 +156,63 @@ def check_errors(device: torch.device | None = None, n_total_embeddings: int | N
         raise_for_error(code, mx, n_total_embeddings, batch)
 
 
-_TICKETS: dict[int, torch.Tensor] = {}
+_TICKETS: dict[tuple[int, int], torch.Tensor] = {}
 TICKETS_LEN = 1 << 16
 
 
-def tickets(device: torch.device) -> torch.Tensor:
+def tickets(device: torch.device, slot: int = 0) -> torch.Tensor:
     """Per-device int32 counters of the kernels' in-launch last-arriver reductions (split-K GEMM tiles, column
-    sums). Zeroed once here; every launch leaves the counters it used at zero. The launches that use them are
-    stream-ordered (one stream per device in the training step)."""
+    sums). Zeroed once here; every launch leaves the counters it used at zero. The launches that use one array are
+    stream-ordered: slot 0 = the step's stream, slot 1 = the weight-gradient stream (``weight_grad_overlap``)."""
     if device.type != "cuda":  # fake / meta tracing of the operators
         return torch.empty(TICKETS_LEN, dtype=torch.int32, device=device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    t = _TICKETS.get(idx)
+    t = _TICKETS.get((idx, slot))
     if t is None:
         t = torch.zeros(TICKETS_LEN, dtype=torch.int32, device=torch.device("cuda", idx))
-        _TICKETS[idx] = t
+        _TICKETS[(idx, slot)] = t
     return t
+
+
+_OVERLAP: set[int] = set()  # device indices whose projection backwards put dW on the weight-gradient stream
+
+
+def weight_grad_overlap_active(device: torch.device) -> bool:
+    return bool(_OVERLAP) and device.type == "cuda" and (
+        device.index if device.index is not None else torch.cuda.current_device()) in _OVERLAP
+
+
+class weight_grad_overlap:
+    """Context of one backward pass: every projection backward (``esgpt::linear_bwd``) launches its input gradient
+    on the current stream and its weight / bias gradient on the device's weight-gradient stream, so the dW products
+    run beside the following layers' kernels instead of on backward's critical path. On exit (and whenever
+    ``join`` is called, e.g. before a DDP bucket reads gradients) the current stream waits for that stream. Usable
+    under HIP-graph capture (the fork / join become graph edges)."""
+
+    def __init__(self, device: torch.device, enabled: bool = True):
+        self.device = device
+        self.enabled = enabled and device.type == "cuda"
+        self.idx = (device.index if device.index is not None else torch.cuda.current_device()) if self.enabled else -1
+
+    def __enter__(self):
+        if self.enabled:
+            _OVERLAP.add(self.idx)
+        return self
+
+    def join(self):
+        if self.enabled:
+            join_weight_grads(self.device)
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            _OVERLAP.discard(self.idx)
+            join_weight_grads(self.device)
+        return False
+
+
+def join_weight_grads(device: torch.device) -> None:
+    """The current stream waits for every weight-gradient launch queued so far on ``device``."""
+    _ops().weight_grad_join(tickets(device, 1))
 
 
 def buckets_struct(groups: list[list] | None):

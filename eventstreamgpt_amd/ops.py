@@ -23,7 +23,8 @@ Differentiable operators and the reference code they replace:
 ====================  =====================================================================================
 
 Non-differentiable: ``embed_bag_bwd``, ``embed_epilogue_bwd``, ``attention_bwd``, ``residual_ln_bwd``,
-``bias_act_bwd``, ``linear_act``, ``linear_bwd``, ``gemm`` / ``gemm_``, ``column_sum``, ``kv_append``,
+``bias_act_bwd``, ``linear_act``, ``linear_bwd`` (+ ``weight_grad_join``: with ``dw_tickets`` the weight gradient
+runs on a second stream, joined by that op), ``gemm`` / ``gemm_``, ``column_sum``, ``kv_append``,
 ``attn_decode`` (generation), ``pack`` (the compute-dtype parameter copies) and ``adamw``
 (generative_modeling.py:460-485).
 
@@ -44,7 +45,7 @@ _state = {"loaded": False}
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
-       "pack", "adamw")
+       "pack", "adamw", "weight_grad_join")
 
 
 def load():
@@ -68,14 +69,27 @@ def _tickets(device):
     return tickets(device)
 
 
-def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None):
-    """``esgpt::linear_bwd`` from a registered backward (records the launch shape for bench.py when asked)."""
+def _leaves(*ts) -> bool:
+    """Every gradient recipient is a leaf (a parameter): its gradient goes to AccumulateGrad, which steals it
+    without a kernel — so a weight gradient still in flight on the weight-gradient stream is not read by the
+    current stream before the join (TrainStep's parameter hooks join before any accumulation that would)."""
+    return all(t is None or t.is_leaf for t in ts)
+
+
+def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None, split_ok=False):
+    """``esgpt::linear_bwd`` from a registered backward (records the launch shape for bench.py when asked). With
+    ``split_ok`` (the weight / bias gradients go straight to leaf parameters) and inside ``weight_grad_overlap``,
+    the weight gradient runs on the weight-gradient stream."""
     from . import fused
 
     if fused.SHAPES["enabled"]:
         fused.SHAPES["linear_bwd"].append((dy.shape[0], x.shape[1], dy.shape[1], bool(need_dx), int(act),
                                            bool(need_db)))
-    return torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device), db_extra)
+    from .kernels import tickets, weight_grad_overlap_active
+
+    dw_tickets = tickets(x.device, 1) if (split_ok and weight_grad_overlap_active(x.device)) else None
+    return torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device), db_extra,
+                                      dw_tickets)
 
 
 def _batch_d(args, start):
@@ -185,8 +199,12 @@ def _register():
         y = x.new_empty(x.shape[0], w.shape[0])
         return (x.new_empty(x.shape[0], w.shape[0]) if act >= 0 else x.new_empty(0)), y
 
+    @fake(lib + "weight_grad_join")
+    def _(like):
+        return None
+
     @fake(lib + "linear_bwd")
-    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None):
+    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None, dw_tickets=None):
         f32 = torch.float32
         return (x.new_empty(dy.shape[0], x.shape[1], dtype=dy.dtype) if need_dx else x.new_empty(0, dtype=dy.dtype),
                 x.new_empty(dy.shape[1], x.shape[1], dtype=f32),
@@ -337,11 +355,12 @@ def _register():
         ctx.save_for_backward(x, w)
         ctx.rows = [m.shape[0] for m in masters]
         ctx.has_bias = bias is not None
+        ctx.split_ok = _leaves(bias, *masters)
 
     def _li_bwd(ctx, dy):
         x, w = ctx.saved_tensors
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
-        dx, dw, db = _linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db)
+        dx, dw, db = _linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db, split_ok=ctx.split_ok)
         return (dx if ctx.needs_input_grad[0] else None, None, db if need_db else None,
                 list(torch.split(dw, ctx.rows, 0)), None)
 
@@ -357,15 +376,16 @@ def _register():
         ctx.save_for_backward(x, w_fc, w_pj, pre, g)
         ctx.act = act
         ctx.has_bpj = b_pj is not None
+        ctx.split_ok = _leaves(b_fc, b_pj, p_fc, p_pj)
 
     def _ml_bwd(ctx, dy, _dpre, _dg):
         if dy is None:
             return (None,) * 9
         x, w_fc, w_pj, pre, g = ctx.saved_tensors
         need_dbpj = ctx.has_bpj and ctx.needs_input_grad[4]
-        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj)
+        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj, split_ok=ctx.split_ok)
         need_dx = ctx.needs_input_grad[0]
-        dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True)
+        dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True, split_ok=ctx.split_ok)
         return (dx if need_dx else None, None, None, db_fc, db_pj if need_dbpj else None, None, dw_fc, dw_pj, None)
 
     reg(lib + "mlp", _ml_bwd, setup_context=_ml_setup)
@@ -400,6 +420,7 @@ def _register():
         ctx.save_for_backward(xc, xt, wc, wt, dzc, dzt, dbias)
         ctx.rows = ([w.shape[0] for w in cw], [w.shape[0] for w in tw])
         ctx.n = (len(cw), len(tw))
+        ctx.split_ok = _leaves(*cw, *cb, *tw, *tb)
 
     def _hl_bwd(ctx, g, *_):
         if g is None:
@@ -409,13 +430,14 @@ def _register():
         rows_c, rows_t = ctx.rows
         alpha = g.contiguous()[-1:]
         # the loss kernel's per-subject position-0 bias rows are summed into db inside the same launch
-        dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, dbias if dbias.numel() else None)
+        dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, dbias if dbias.numel() else None,
+                                    split_ok=ctx.split_ok)
         nc = sum(rows_c)
         gw_c = list(torch.split(dwc[:nc], rows_c, 0))
         gb_c = list(torch.split(dbc[:nc], rows_c, 0))
         dxt, gw_t, gb_t = None, [], []
         if n_tw:
-            dxt, dwt, dbt = _linear_bwd(dzt, xt, wt, alpha, -1, None, True, True)
+            dxt, dwt, dbt = _linear_bwd(dzt, xt, wt, alpha, -1, None, True, True, split_ok=ctx.split_ok)
             nt = sum(rows_t)
             gw_t = list(torch.split(dwt[:nt], rows_t, 0))
             gb_t = list(torch.split(dbt[:nt], rows_t, 0))

@@ -15,6 +15,8 @@
   the step as a view into one flat f32 buffer laid out last-layer-first and cut into ~25 MB buckets; a bucket is
   all-reduced (average) in place as soon as backward has produced all of its gradients (post-accumulate-grad hooks),
   so the exchange overlaps the rest of backward (SURVEY.md §8e);
+* optionally (``overlap_weight_grads``) the projections' weight / bias gradients run on a second stream (joined
+  before the exchange and AdamW), off backward's critical path;
 * optional HIP-graph capture of forward+backward, one graph per batch shape signature (static shapes; batches are
   copied into the graph's static buffers). A batch whose signature matches no captured graph is captured (up to
   ``max_graphs``) or run eagerly — never broadcast into the wrong buffers.
@@ -27,7 +29,8 @@ import torch
 import torch.distributed as dist
 
 from .data.types import PytorchBatch
-from .kernels import begin_dropout_step, check_errors, end_dropout_step, err_word, raise_for_error
+from .kernels import (begin_dropout_step, check_errors, end_dropout_step, err_word, join_weight_grads,
+                      raise_for_error, weight_grad_overlap, weight_grad_overlap_active)
 from .transformer.config import OptimizationConfig
 
 
@@ -204,6 +207,9 @@ class GradBuckets:
     def _launch(self, b: int):
         idx, s, e = self.buckets[b]
         src, dst = [], []
+        dev = self.flat.device
+        if weight_grad_overlap_active(dev):  # the bucket's weight gradients may still be in flight on their stream
+            join_weight_grads(dev)
         with torch.no_grad():
             for i in idx:
                 p, v = self.params[i], self.views[i]
@@ -235,7 +241,7 @@ class GradBuckets:
 class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
-                 max_graphs: int = 4, _force_graph: bool = False):
+                 max_graphs: int = 4, overlap_weight_grads: bool = False, _force_graph: bool = False):
         self.model = model
         self.cfg = opt_cfg
         self.dtype = compute_dtype
@@ -262,12 +268,30 @@ class TrainStep:
         self.max_graphs = max_graphs
         self.graphs: dict = {}  # shape signature -> (graph, static batch, static loss)
         self.check_errors = check_errors and dev.type == "cuda"
+        # projection weight gradients on a second stream beside the rest of backward (kernels.weight_grad_overlap).
+        # Off by default: measured on the C2 step (HIP graph) it gains nothing — the graph executor starts the side
+        # chain late and every fork costs the main stream a ~4.5 us barrier gap.
+        self.overlap_weight_grads = overlap_weight_grads and dev.type == "cuda"
+        if self.overlap_weight_grads:
+            # a second gradient contribution to a parameter is added on the current stream: join the weight-gradient
+            # stream first (the first contribution may still be in flight there)
+            for p in params:
+                p.register_hook(self._make_accumulate_guard(p))
         self._pending: deque = deque()  # (event, pinned error block copy, batch) of submitted steps
         self._vocab = getattr(getattr(model, "config", None), "vocab_size", None)
         self._copy_stream = None
         self._staging: dict = {}
         self._prefetched = None
         self._release = None
+
+    @staticmethod
+    def _make_accumulate_guard(p):
+        def hook(grad):
+            if p.grad is not None and weight_grad_overlap_active(grad.device):
+                join_weight_grads(grad.device)
+            return None
+
+        return hook
 
     # --------------------------------------------------------------------------------------------------------
     def _fwd_bwd(self, batch: PytorchBatch, autocast_cache: bool = True):
@@ -277,7 +301,8 @@ class TrainStep:
         # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
         with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32, cache_enabled=autocast_cache):
             out = self.model(batch)
-        out.loss.backward()
+        with weight_grad_overlap(dev, enabled=self.overlap_weight_grads):
+            out.loss.backward()
         if dev.type == "cuda":
             end_dropout_step(dev)
         return out.loss.detach()

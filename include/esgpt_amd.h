@@ -256,7 +256,12 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
  *     esgpt_gemm_counters(out, in) entries. T == 0 zero-fills dw and db.
  *   esgpt_linear_bwd_ex: the same plus n_extra f32 rows db_extra [n_extra, out] added into db before the alpha
  *     scaling, db = alpha·(Σ_rows dy + Σ_b db_extra[b]) — the generative head's bias gradient, whose position-0
- *     rows the loss kernel accumulates per subject (model_output.py:1253-1721; replaces a sum + scale + add). */
+ *     rows the loss kernel accumulates per subject (model_output.py:1253-1721; replaces a sum + scale + add).
+ *   esgpt_linear_bwd_split: esgpt_linear_bwd_ex as two launches on two streams: dx on `stream`; dw, db (and the
+ *     split-K workspace / counters, which must not be shared with work on `stream`) on `stream_dw` after it waits
+ *     for everything queued on `stream` before the call. The caller joins `stream_dw` back (an event wait) before
+ *     reading dw / db. Same tiles and split plan as the grouped launch: bitwise equal results. The weight gradient
+ *     then leaves backward's critical path (transformer.py:133-163, 378-391 Linear backward). */
 int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64_t in, int64_t out,
                      const float* bias, int act, void* pre, void* y, int64_t ldy, void* stream);
 size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx);
@@ -268,6 +273,13 @@ int esgpt_linear_bwd_ex(const void* dy, int64_t lddy, const void* x, int64_t ldx
                         int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx,
                         int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
                         int32_t* counters, const float* db_extra, int64_t n_extra, void* stream);
+int esgpt_linear_bwd_split(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T,
+                           int64_t in, int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre,
+                           void* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                           int32_t* counters, const float* db_extra, int64_t n_extra, void* stream, void* stream_dw);
+/* `waiter` waits (device-side, an event) for every piece of work queued on `signaller` before the call: the join of
+ * esgpt_linear_bwd_split's weight-gradient stream (and its fork). Both may be captured into one HIP graph. */
+int esgpt_stream_wait(void* waiter, void* signaller);
 
 /* ---- Parameter packing -------------------------------------------------------------------------------------
  * The compute-dtype copies of the f32 parameters a step reads, in ONE launch: the blocks' flat bf16 weight shadow

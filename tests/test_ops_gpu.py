@@ -206,3 +206,30 @@ def test_linear_bwd_row_sum_addend(env):
         assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
         ref = db.double() + extra.double().sum(0) * 0.75
         assert float((db2.double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max()), (T, din, dout)
+
+
+def test_linear_bwd_split_streams_equal_grouped(env):
+    """esgpt_linear_bwd_split (dX on the current stream, dW / db on the weight-gradient stream, joined by
+    esgpt::weight_grad_join) equals the grouped one-launch backward bit for bit: same tiles, same split plan — for
+    the step's projection shapes (split-K dW, the 128x128 head dW), the activation-gradient epilogue, alpha, the
+    bias-row addend and a dW-only call; the operand memory is held for the side stream while the current stream
+    allocates and overwrites in between."""
+    esgpt, _ = env
+    dev = torch.device(DEV)
+    t0, t1 = tickets(dev), tickets(dev, 1)
+    cases = [(8192, 256, 1024, 0, True), (8192, 1024, 256, -1, True), (8192, 256, 1624, -1, True),
+             (8192, 256, 768, -1, False), (256, 64, 24, 2, True)]
+    for T, din, dout, act, need_dx in cases:
+        x = torch.randn(T, din, device=DEV, generator=_g(41)).bfloat16()
+        w = (0.05 * torch.randn(dout, din, device=DEV, generator=_g(42))).bfloat16()
+        dy = torch.randn(T, dout, device=DEV, generator=_g(43)).bfloat16()
+        pre = torch.randn(T, din, device=DEV, generator=_g(44)).bfloat16() if act >= 0 else None
+        extra = torch.randn(4, dout, device=DEV, generator=_g(45))
+        alpha = torch.tensor([0.5], device=DEV)
+        want = esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, True, t0, extra)
+        got = esgpt.linear_bwd(dy.clone(), x.clone(), w, alpha, act, pre, need_dx, True, t0, extra, t1)
+        junk = [torch.full((T, max(din, dout)), 7.0, device=DEV, dtype=torch.bfloat16) for _ in range(3)]
+        esgpt.weight_grad_join(t1)
+        del junk
+        for a, b, name in zip(want, got, ("dx", "dw", "db")):
+            assert torch.equal(a, b), (T, din, dout, act, name)

@@ -190,3 +190,31 @@ def test_nested_attention_graph_replay_matches_eager_with_allocations_between_re
         assert abs(a - b) <= 1e-3 * abs(a), (le, lg)
     for k in se:
         assert (sg[k] - se[k]).abs().max().item() < 1e-4, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [True, False])
+def test_weight_grad_overlap_matches_serial_step(graph):
+    """TrainStep with the projections' weight gradients on the second stream (overlap_weight_grads) vs one stream: the same
+    losses and parameters bit for bit over several steps, captured as a HIP graph or eager (the CI model at the
+    C2 widths, reduced batch)."""
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C2"]
+    batches = [bc.batch(i, batch_size=4, device="cuda").packed() for i in range(4)]
+
+    def run(overlap):
+        cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+        torch.manual_seed(0)
+        m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
+        ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=100),
+                       torch.bfloat16, use_graph=graph, overlap_weight_grads=overlap)
+        losses = [float(ts.step(b)) for b in batches]
+        ts.check()
+        return losses, {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+    l0, s0 = run(False)
+    l1, s1 = run(True)
+    assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
