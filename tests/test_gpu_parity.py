@@ -392,7 +392,7 @@ def test_linear_bias_fn():
 
 
 GEMM_SHAPES = [(8192, 768, 256), (8192, 256, 1024), (256, 256, 8192), (1232, 256, 8192), (104, 40, 24),
-               (336, 1232, 256), (8, 8, 8), (520, 136, 72)]
+               (336, 1232, 256), (8, 8, 8), (520, 136, 72), (104, 1624, 256), (72, 136, 64), (8200, 24, 32)]
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
@@ -436,7 +436,7 @@ def _act_ref(z, act):
     return {0: F.gelu(z), 1: F.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
 
 
-@pytest.mark.parametrize("T,din,dout", [(8192, 256, 1024), (520, 136, 72), (8, 8, 8)])
+@pytest.mark.parametrize("T,din,dout", [(8192, 256, 1024), (520, 136, 72), (8, 8, 8), (300, 160, 1000)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_linear_fwd_act(T, din, dout, act):
     """c_fc epilogue: pre = x·wᵀ + b (bf16) and y = act(pre) vs f64 references."""
