@@ -17,6 +17,8 @@
 // B[k = 8h+j][col r]; C reg i = row (i&3) + 8(i>>2) + 4h, col r. An accumulator used as a B operand supplies k-step
 // s element j = row 16s + 8(j>>2) + 4h + (j&3) (permuted); the A operand is then read in that order.
 // Roofline: MFMA-bound at large L; algorithmic FLOPs 8·H·hd·T (T = allowed (q, k) pairs; recompute not counted).
+#include <cstdlib>
+
 #include "common.h"
 
 using namespace esgpt;
@@ -150,24 +152,26 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   const bool kvalid = key < Lk && (kmask == nullptr || kmask[(int64_t)b * Lk + key] != 0);
   STAMP(0);
 
-  // ---- own keys: K / V fragments (B operands of S and dP) ----
+  // ---- prologue loads, all issued before any is consumed (one memory round trip): own keys' K / V fragments (B
+  // operands of S and dP) and the K image of the whole key block (dQ = dS·K; rows clamped, zeroed when written) ----
   bf16x8 kf[HD / 16], vf[HD / 16];
+  constexpr int KIMG = KB * HD / 8 / THREADS;  // 16-B chunks of the K image per thread
+  bf16x8 kimg[KIMG];
   {
     const int kk = min(key, Lk - 1);
     const __bf16* krow = k + ((int64_t)b * Lk + kk) * ld_in + hh * HD;
     const __bf16* vrow = v + ((int64_t)b * Lk + kk) * ld_in + hh * HD;
 #pragma unroll
     for (int t = 0; t < HD / 16; ++t) {
-      kf[t] = key < Lk ? *reinterpret_cast<const bf16x8*>(krow + 16 * t + 8 * h) : zero8();
-      vf[t] = key < Lk ? *reinterpret_cast<const bf16x8*>(vrow + 16 * t + 8 * h) : zero8();
+      kf[t] = *reinterpret_cast<const bf16x8*>(krow + 16 * t + 8 * h);
+      vf[t] = *reinterpret_cast<const bf16x8*>(vrow + 16 * t + 8 * h);
     }
-  }
-  // ---- K image of the whole key block for dQ = dS·K ----
-  for (int c = tid; c < KB * HD / 8; c += THREADS) {
-    const int row = c / (HD / 8), c8 = c % (HD / 8), kr = kb0 + row;
-    bf16x8 val = zero8();
-    if (kr < Lk) val = *reinterpret_cast<const bf16x8*>(k + ((int64_t)b * Lk + kr) * ld_in + hh * HD + c8 * 8);
-    *reinterpret_cast<bf16x8*>(sK + IQ::off(row, c8 * 8)) = val;
+#pragma unroll
+    for (int i = 0; i < KIMG; ++i) {
+      const int c = tid + THREADS * i, row = c / (HD / 8), c8 = c % (HD / 8);
+      const int kr = min(kb0 + row, Lk - 1);
+      kimg[i] = *reinterpret_cast<const bf16x8*>(k + ((int64_t)b * Lk + kr) * ld_in + hh * HD + c8 * 8);
+    }
   }
 
   f32x16 dka[HD / 32], dva[HD / 32];
@@ -202,6 +206,15 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   };
   int q0 = (qlo / QT + qsplit) * QT;  // this workgroup's tiles: every nsplit-th one
   if (q0 <= qhi) prefetch(q0);
+  if (key >= Lk) {
+#pragma unroll
+    for (int t = 0; t < HD / 16; ++t) kf[t] = vf[t] = zero8();
+  }
+#pragma unroll
+  for (int i = 0; i < KIMG; ++i) {
+    const int c = tid + THREADS * i, row = c / (HD / 8), c8 = c % (HD / 8);
+    *reinterpret_cast<bf16x8*>(sK + IQ::off(row, c8 * 8)) = kb0 + row < Lk ? kimg[i] : zero8();
+  }
   STAMP(1);
   int it = 0;
 
@@ -469,7 +482,12 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   const int nkb = (int)cdiv(Lk, KB);
   float* acc = nkb > 1 ? dq32 : nullptr;
   // two workgroups per key block (even / odd query tiles) when there are at least two query tiles
-  const int nsplit = (counters && Lq > Cfg<HD>::QT) ? 2 : 1;
+  // (ESGPT_ATTN_BWD_NSPLIT=1: one workgroup per key block — tuning hook, read once)
+  static const int max_split = [] {
+    const char* e = getenv("ESGPT_ATTN_BWD_NSPLIT");
+    return (e && atoi(e) == 1) ? 1 : 2;
+  }();
+  const int nsplit = (counters && Lq > Cfg<HD>::QT && max_split > 1) ? 2 : 1;
   float* xbuf = dq32 + (nkb > 1 ? (size_t)(B * H * Lq * HD) : 0);
   if (acc && zero_async(acc, sizeof(float) * (size_t)(B * H * Lq * HD), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   const dim3 grid((unsigned)(nkb * nsplit * B * H));  // 1-D: XCD-aware order in the kernel
