@@ -144,6 +144,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the key-block halves of one (batch, head) share an XCD
   const int bh = lin / nxb, b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
+  const bool idx32 = (uint64_t)(gridDim.x / nxb) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;  // B·H = grid / nxb
   const int off = Lk - Lq;
   const int kblk = (lin % nxb) / nsplit, qsplit = (lin % nxb) % nsplit;  // key block; query-tile parity
   const int kb0 = kblk * KB;
@@ -264,7 +265,27 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
         // fully visible slice: every key of the wave valid and inside the causal / local band of every query
         const bool full = __ballot(kvalid) == ~0ull && qpos_lo >= kw0 + 31 && (window == 0 || qpos_hi - kw0 < window);
         float zk[16];  // dropout multipliers of this lane's (query row, key) elements
-        if (DROP) {
+        if (DROP && idx32) {  // 32-bit element indices (wave-uniform): the same hashes without 64-bit math
+          if ((Lk & 1) == 0 && (kw0 & 1) == 0) {
+            const int odd = key & 1;
+            const uint32_t base = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)q0) * (uint32_t)Lk + (uint32_t)(key - odd);
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+              const uint32_t e = base + (uint32_t)(32 * qs + acc_row(i + odd, h)) * (uint32_t)Lk;
+              const uint32_t mine = mix32((e >> 1) ^ dr.key);
+              const uint32_t other = (uint32_t)__shfl_xor((int)mine, 1, 64);
+              const uint32_t ha = odd ? other : mine, hb = odd ? mine : other;
+              const uint32_t ua = odd ? (ha >> 16) : (ha & 0xffffu), ub = odd ? (hb >> 16) : (hb & 0xffffu);
+              zk[i] = ua >= dr.thresh ? dr.scale : 0.f;
+              zk[i + 1] = ub >= dr.thresh ? dr.scale : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              zk[i] = dropout_mult_32(dr, ((uint32_t)bh * (uint32_t)Lq + (uint32_t)(q0 + 32 * qs + acc_row(i, h))) *
+                                              (uint32_t)Lk + (uint32_t)key);
+          }
+        } else if (DROP) {
           if ((Lk & 1) == 0 && (kw0 & 1) == 0) {
             // lanes r, r^1 hold keys 2j, 2j+1 (one hash pair) of the same query rows: for each pair of rows the
             // even lane hashes the first row, the odd lane the second, and they swap hashes (one hash per element

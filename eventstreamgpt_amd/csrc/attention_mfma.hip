@@ -140,6 +140,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the query blocks of one (batch, head) share an XCD
   const int bh = lin / nqb, b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
+  const bool idx32 = (uint64_t)(gridDim.x / nqb) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;  // B·H = grid / nqb
   const int off = Lk - Lq;
   const int qb = (lin % nqb) * ROWS;
   const int qi = qb + qh * 32 + r;
@@ -251,23 +252,43 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
       }
     if (DROP) {
       // registers (i, i+1), i even, hold consecutive keys: one hash per pair when the pair is aligned
-      const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
-      const bool aligned = (rowbase & 1) == 0;
+      if (idx32) {  // every element index of the launch fits 32 bits (wave-uniform)
+        const uint32_t rowbase = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk;
+        const bool aligned = (rowbase & 1) == 0;
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          const uint64_t e = rowbase + (uint64_t)(t0 + 32 * c + acc_row(i, h));
-          float m0, m1;
-          if (aligned) {
-            dropout_mult2(dr, e, m0, m1);
-          } else {
-            m0 = dropout_mult(dr, e);
-            m1 = dropout_mult(dr, e + 1);
+          for (int i = 0; i < 16; i += 2) {
+            const uint32_t e = rowbase + (uint32_t)(t0 + 32 * c + acc_row(i, h));
+            float m0, m1;
+            if (aligned) {
+              dropout_mult2_32(dr, e, m0, m1);
+            } else {
+              m0 = dropout_mult_32(dr, e);
+              m1 = dropout_mult_32(dr, e + 1);
+            }
+            s[c][i] *= m0;
+            s[c][i + 1] *= m1;
           }
-          s[c][i] *= m0;
-          s[c][i + 1] *= m1;
-        }
+      } else {
+        const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+        const bool aligned = (rowbase & 1) == 0;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) {
+            const uint64_t e = rowbase + (uint64_t)(t0 + 32 * c + acc_row(i, h));
+            float m0, m1;
+            if (aligned) {
+              dropout_mult2(dr, e, m0, m1);
+            } else {
+              m0 = dropout_mult(dr, e);
+              m1 = dropout_mult(dr, e + 1);
+            }
+            s[c][i] *= m0;
+            s[c][i + 1] *= m1;
+          }
+      }
     }
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;

@@ -193,6 +193,19 @@ __device__ __forceinline__ void dropout_mult2(const DropoutSpec& d, uint64_t idx
   m1 = (hh >> 16) >= d.thresh ? d.scale : 0.f;
 }
 
+// 32-bit index forms (the launch's element indices all fit 32 bits, so the high word of every pair index is 0):
+// the same bits as dropout_mult / dropout_mult2 without 64-bit index arithmetic or the high-word multiply.
+__device__ __forceinline__ float dropout_mult_32(const DropoutSpec& d, uint32_t idx) {
+  const uint32_t hh = mix32((idx >> 1) ^ d.key);
+  const uint32_t half = (idx & 1) ? (hh >> 16) : (hh & 0xffffu);
+  return half >= d.thresh ? d.scale : 0.f;
+}
+__device__ __forceinline__ void dropout_mult2_32(const DropoutSpec& d, uint32_t idx, float& m0, float& m1) {
+  const uint32_t hh = mix32((idx >> 1) ^ d.key);
+  m0 = (hh & 0xffffu) >= d.thresh ? d.scale : 0.f;
+  m1 = (hh >> 16) >= d.thresh ? d.scale : 0.f;
+}
+
 __device__ __forceinline__ DropoutSpec make_dropout(float p, const uint64_t* seed_ptr) {
   DropoutSpec d;
   d.p = p;
