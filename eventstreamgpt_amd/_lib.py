@@ -65,6 +65,11 @@ class EsgptPackSeg(ctypes.Structure):
     _fields_ = [("src", _vp), ("dst", _vp), ("n", _i64), ("n_pad", _i64), ("dst_dtype", ctypes.c_int32),
                 ("reserved", ctypes.c_int32)]
 
+class EsgptColsumJob(ctypes.Structure):
+    """``esgpt_colsum_job``: sums[c] = sum_b part[b * width + c]."""
+    _fields_ = [("part", _vp), ("n_parts", _i64), ("width", _i64), ("sums", _vp)]
+
+
 SIGNATURES = {
     "esgpt_version": (ctypes.c_char_p, []),
     "esgpt_adamw_chunk": (_i64, []),
@@ -93,6 +98,7 @@ SIGNATURES = {
     "esgpt_residual_ln_counters": (_i64, [_i64]),
     "esgpt_residual_ln_bwd": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i64, _i64, _vp, _vp, _int,
                                      _vp, _vp, _vp, _vp]),
+    "esgpt_colsum_jobs": (_int, [ctypes.POINTER(EsgptColsumJob), _i64, _vp]),
     "esgpt_bias_act_fwd": (_int, [_vp, _vp, _int, _i64, _i64, _vp, _int, _vp]),
     "esgpt_bias_act_partials": (_i64, [_i64]),
     "esgpt_bias_act_bwd": (_int, [_vp, _vp, _vp, _int, _i64, _i64, _vp, _vp, _vp, _int, _vp]),

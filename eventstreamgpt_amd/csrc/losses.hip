@@ -598,26 +598,36 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Deterministic sums of the per-row contributions: thread i sums rows i, i + 1024, ... of each term (8 loads in
-// flight), then wave sums and a fixed-order sum over the 16 waves.
+// Deterministic sums of the per-row contributions: thread i sums rows i, i + 1024, ... of each term, then wave sums
+// and a fixed-order sum over the 16 waves. The next term's loads are issued before the current term is summed (one
+// memory round trip for the whole launch instead of one per term at n_rows <= 8192).
 __global__ __launch_bounds__(1024) void reduce_kernel(const float* __restrict__ contrib, int64_t n_rows, int NT,
                                                       float* __restrict__ losses) {
   __shared__ float s[16][ESGPT_MAX_TERMS + 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int t = 0; t <= NT; ++t) {
-    const float* c = contrib + (int64_t)t * n_rows;
-    float a = 0.f;
-    int64_t i = threadIdx.x;
-    for (; i + 7 * 1024 < n_rows; i += 8 * 1024) {
-      float v[8];
+  constexpr int kU = 8;  // rows per thread and pass
+  for (int64_t i0 = 0; i0 < n_rows; i0 += kU * 1024) {
+    float cur[kU], nxt[kU];
+    auto load = [&](float (&v)[kU], int t) {
+      const float* c = contrib + (int64_t)min(t, NT) * n_rows;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = c[i + k * 1024];
+      for (int k = 0; k < kU; ++k) {
+        const int64_t i = i0 + threadIdx.x + (int64_t)k * 1024;
+        const float x = c[min(i, n_rows - 1)];
+        v[k] = i < n_rows ? x : 0.f;
+      }
+    };
+    load(cur, 0);
+    for (int t = 0; t <= NT; ++t) {
+      load(nxt, t + 1);  // clamped past the last term: a re-read, never used
+      float a = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a += v[k];
+      for (int k = 0; k < kU; ++k) a += cur[k];
+      const float w = wave_sum(a);
+      if (lane == 0) s[wave][t] = (i0 == 0 ? 0.f : s[wave][t]) + w;
+#pragma unroll
+      for (int k = 0; k < kU; ++k) cur[k] = nxt[k];
     }
-    for (; i < n_rows; i += 1024) a += c[i];
-    const float w = wave_sum(a);
-    if (lane == 0) s[wave][t] = w;
   }
   __syncthreads();
   if (threadIdx.x == 0) {

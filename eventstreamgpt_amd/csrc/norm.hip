@@ -12,6 +12,8 @@
 // (two-pass mean / variance, biased variance as torch.nn.LayerNorm).
 // HBM-bound: fwd reads x (4 B) + y (2-4 B), writes h (4 B) + out (2-4 B) per element; bwd reads dout (2-4 B), h
 // (4 B), dh_in (4 B) and writes dx (4 B) + dy (2-4 B) per element.
+#include <algorithm>
+
 #include "common.h"
 
 using namespace esgpt;
@@ -288,6 +290,49 @@ __global__ __launch_bounds__(256) void ln_colsum_kernel(const float* __restrict_
   }
 }
 
+// Many independent column sums in ONE launch (the deferred LayerNorm-backward sums of a whole backward pass):
+// block -> (job, 64-column group) through a prefix table; each block is ln_colsum_kernel's block (16 row groups in
+// a fixed order): the same sums bit for bit as one ln_colsum launch per job.
+constexpr int kMaxColsumJobs = 48;
+struct ColsumJobs {
+  esgpt_colsum_job j[kMaxColsumJobs];
+  int start[kMaxColsumJobs + 1];  // first block of each job
+  int n;
+};
+
+__global__ __launch_bounds__(256) void colsum_jobs_kernel(ColsumJobs a) {
+  __shared__ float4 s[16][16];
+  int job = 0;
+  while (job + 1 < a.n && (int)blockIdx.x >= a.start[job + 1]) ++job;  // block-uniform
+  const esgpt_colsum_job& jb = a.j[job];
+  const int c4 = threadIdx.x & 15, grp = threadIdx.x >> 4;
+  const int64_t i = (int64_t)(blockIdx.x - a.start[job]) * 64 + 4 * c4;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < jb.width) {
+#pragma unroll 8
+    for (int64_t b = grp; b < jb.n_parts; b += 16) {
+      const float4 v = *reinterpret_cast<const float4*>(jb.part + b * jb.width + i);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+  }
+  s[grp][c4] = acc;
+  __syncthreads();
+  if (grp == 0 && i < jb.width) {
+    float4 t = s[0][c4];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) {
+      t.x += s[g][c4].x;
+      t.y += s[g][c4].y;
+      t.z += s[g][c4].z;
+      t.w += s[g][c4].w;
+    }
+    *reinterpret_cast<float4*>(jb.sums + i) = t;
+  }
+}
+
 // sums[q, c] = sum_b part[b, q, c]. Block: 64 columns x 16 row groups (1024 threads); fixed order -> deterministic.
 __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int64_t nb, int64_t QD,
                                                       float* __restrict__ sums) {
@@ -414,7 +459,7 @@ void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const f
   }
 #undef LN_BWD_R
 #undef LN_BWD
-  ln_colsum_kernel<<<(unsigned)cdiv(3 * D, 64), 256, 0, st>>>(part, grid, 3 * D, sums);
+  if (sums) ln_colsum_kernel<<<(unsigned)cdiv(3 * D, 64), 256, 0, st>>>(part, grid, 3 * D, sums);
 }
 
 }  // namespace
@@ -454,12 +499,14 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
                           const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
                           float* sums, int32_t* counters, void* stream) {
   (void)counters;
-  ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && sums && D > 0 && D % 4 == 0 &&
-                D <= 256 * kMaxChunks);
+  ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && D > 0 && D % 4 == 0 && D <= 256 * kMaxChunks);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   ESGPT_REQUIRE(esgpt_residual_ln_partials(N) * 3 * D * 4 < (1ll << 31) && ((uintptr_t)sums % 16) == 0);
   hipStream_t st = as_stream(stream);
-  if (N == 0) return zero_async(sums, sizeof(float) * 3 * D, st) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+  if (N == 0) {  // no rows: zero sums (or, deferred, zero partials: one all-zero block)
+    if (sums) return zero_async(sums, sizeof(float) * 3 * D, st) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+    return zero_async(part, sizeof(float) * 3 * D, st) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+  }
   const bool yb = y_dtype == ESGPT_BF16, ob = out_dtype == ESGPT_BF16;
   if (!yb && !ob) launch_ln_bwd<float, float>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx,
                                              dy, part, sums, st);
@@ -470,6 +517,27 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
   else launch_ln_bwd<bf16, bf16>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx, dy, part,
                                  sums, st);
   ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_colsum_jobs(const esgpt_colsum_job* jobs, int64_t n_jobs, void* stream) {
+  ESGPT_REQUIRE(n_jobs >= 0 && (n_jobs == 0 || jobs != nullptr));
+  hipStream_t st = as_stream(stream);
+  for (int64_t j0 = 0; j0 < n_jobs; j0 += kMaxColsumJobs) {
+    ColsumJobs a{};
+    a.n = (int)std::min<int64_t>(kMaxColsumJobs, n_jobs - j0);
+    a.start[0] = 0;
+    for (int i = 0; i < a.n; ++i) {
+      const esgpt_colsum_job& jb = jobs[j0 + i];
+      ESGPT_REQUIRE(jb.part && jb.sums && jb.n_parts >= 1 && jb.width > 0 && jb.width % 4 == 0 &&
+                    ((uintptr_t)jb.part % 16) == 0 && ((uintptr_t)jb.sums % 16) == 0);
+      a.j[i] = jb;
+      a.start[i + 1] = a.start[i] + (int)cdiv(jb.width, 64);
+    }
+    if (a.start[a.n] == 0) continue;
+    colsum_jobs_kernel<<<(unsigned)a.start[a.n], 256, 0, st>>>(a);
+    ESGPT_LAUNCH_CHECK();
+  }
   return ESGPT_OK;
 }
 

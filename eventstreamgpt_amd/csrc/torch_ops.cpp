@@ -20,6 +20,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/esgpt_amd.h"
@@ -336,12 +337,59 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> residual_ln(const optional<Tensor>& x
 }
 
 // (dx f32 [N, D] | empty, dy y_dtype [N, D] | empty, sums f32 [3, D] = (d ln_w, d ln_b, d bias))
+std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd_impl(const optional<Tensor>& dh, const Tensor& dout_,
+                                                        const Tensor& h, const Tensor& mean, const Tensor& rstd,
+                                                        const Tensor& ln_w, const optional<Tensor>& row_mask, double p,
+                                                        const optional<Tensor>& seed, bool need_dx, bool need_dy,
+                                                        at::ScalarType y_dtype, at::ScalarType out_dtype,
+                                                        bool deferred, Tensor* part_out);
+
 std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd(const optional<Tensor>& dh, const Tensor& dout_, const Tensor& h,
                                                    const Tensor& mean, const Tensor& rstd, const Tensor& ln_w,
                                                    const optional<Tensor>& row_mask, double p,
                                                    const optional<Tensor>& seed, bool need_dx, bool need_dy,
                                                    at::ScalarType y_dtype, at::ScalarType out_dtype,
                                                    const Tensor& tickets) {
+  return residual_ln_bwd_impl(dh, dout_, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype,
+                              out_dtype, false, nullptr);
+}
+
+// The same backward with the column sums deferred: returns (dx, dy, part) — part f32 [n_parts, 3, D] holds the
+// per-block partials; esgpt::colsum_flush later sums any number of them in one launch.
+std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd_partials(const optional<Tensor>& dh, const Tensor& dout_,
+                                                            const Tensor& h, const Tensor& mean, const Tensor& rstd,
+                                                            const Tensor& ln_w, const optional<Tensor>& row_mask,
+                                                            double p, const optional<Tensor>& seed, bool need_dx,
+                                                            bool need_dy, at::ScalarType y_dtype,
+                                                            at::ScalarType out_dtype) {
+  Tensor part;
+  auto r = residual_ln_bwd_impl(dh, dout_, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype,
+                                out_dtype, true, &part);
+  return {std::get<0>(r), std::get<1>(r), part};
+}
+
+// sums[i][c] = Σ_b parts[i][b][c] for every pair, one launch (esgpt_colsum_jobs); sums[i] written in place.
+void colsum_flush(at::TensorList parts, at::TensorList sums) {
+  TORCH_CHECK(parts.size() == sums.size(), "colsum_flush: one sums tensor per partial table");
+  if (parts.empty()) return;
+  const c10::DeviceGuard guard(parts[0].device());
+  std::vector<esgpt_colsum_job> jobs(parts.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    TORCH_CHECK(parts[i].is_contiguous() && sums[i].is_contiguous() && parts[i].scalar_type() == at::kFloat &&
+                    sums[i].scalar_type() == at::kFloat && parts[i].numel() % sums[i].numel() == 0,
+                "colsum_flush: contiguous f32 [n, width] partials and [width] sums");
+    jobs[i] = esgpt_colsum_job{ptr<const float>(parts[i]), parts[i].numel() / sums[i].numel(), sums[i].numel(),
+                               ptr<float>(sums[i])};
+  }
+  check(esgpt_colsum_jobs(jobs.data(), (int64_t)jobs.size(), stream_of(parts[0])), "colsum_flush");
+}
+
+std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd_impl(const optional<Tensor>& dh, const Tensor& dout_,
+                                                        const Tensor& h, const Tensor& mean, const Tensor& rstd,
+                                                        const Tensor& ln_w, const optional<Tensor>& row_mask, double p,
+                                                        const optional<Tensor>& seed, bool need_dx, bool need_dy,
+                                                        at::ScalarType y_dtype, at::ScalarType out_dtype,
+                                                        bool deferred, Tensor* part_out) {
   const c10::DeviceGuard guard(h.device());
   const int64_t N = h.size(0), D = h.size(1);
   Tensor dout = dout_.to(out_dtype).contiguous();
@@ -349,16 +397,17 @@ std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd(const optional<Tensor>& dh, c
   auto f32 = h.options().dtype(at::kFloat);
   Tensor dx = need_dx ? at::empty({N, D}, f32) : at::empty({0}, f32);
   Tensor dy = need_dy ? at::empty({N, D}, f32.dtype(y_dtype)) : at::empty({0}, f32.dtype(y_dtype));
-  Tensor part = at::empty({esgpt_residual_ln_partials(N) * 3 * D}, f32);
-  Tensor sums = at::empty({3, D}, f32);
+  Tensor part = at::empty({std::max<int64_t>(1, esgpt_residual_ln_partials(N)), 3 * D}, f32);
+  Tensor sums = deferred ? Tensor() : at::empty({3, D}, f32);
   Tensor rm = as_opt(row_mask, at::kBool);
   check(esgpt_residual_ln_bwd(dhc.defined() ? ptr<const float>(dhc) : nullptr, dout.data_ptr(), dtype_code(out_dtype),
                               ptr<const float>(h), ptr<const float>(mean), ptr<const float>(rstd),
                               ptr<const float>(ln_w), rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p,
                               optr<const uint64_t>(seed), N, D, need_dx ? ptr<float>(dx) : nullptr,
                               need_dy ? dy.data_ptr() : nullptr, dtype_code(y_dtype), ptr<float>(part),
-                              ptr<float>(sums), ptr<int32_t>(tickets), stream_of(h)),
+                              deferred ? nullptr : ptr<float>(sums), nullptr, stream_of(h)),
         "residual_ln_bwd");
+  if (part_out) *part_out = part;
   return {dx, dy, sums};
 }
 
@@ -663,6 +712,10 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
         "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None) -> (Tensor, Tensor, Tensor)");
   m.def("weight_grad_join(Tensor like) -> ()");
+  m.def("residual_ln_bwd_partials(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, "
+        "Tensor? row_mask, float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, "
+        "ScalarType out_dtype) -> (Tensor, Tensor, Tensor)");
+  m.def("colsum_flush(Tensor[] parts, Tensor(a!)[] sums) -> ()");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
   m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, Tensor? b_pj, int act, Tensor p_fc, Tensor p_pj, "
         "Tensor tickets) -> (Tensor, Tensor, Tensor)");
@@ -695,6 +748,8 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("linear_act", &linear_act);
   m.impl("linear_bwd", &linear_bwd);
   m.impl("weight_grad_join", &weight_grad_join);
+  m.impl("residual_ln_bwd_partials", &residual_ln_bwd_partials);
+  m.impl("colsum_flush", &colsum_flush);
   m.impl("linear", &linear);
   m.impl("mlp", &mlp);
   m.impl("head_loss", &head_loss);

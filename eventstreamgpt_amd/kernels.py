@@ -210,6 +210,61 @@ class weight_grad_overlap:
         return False
 
 
+def _lib_partials(N: int) -> int:
+    """Rows of a residual_ln backward partial table (esgpt_residual_ln_partials, at least 1)."""
+    return max(1, int(L.load(require_device=False).esgpt_residual_ln_partials(N)))
+
+
+_DEFER: dict[int, list] = {}  # device index -> pending (partials, sums) of deferred LayerNorm column sums
+
+
+def _dev_idx(device: torch.device) -> int:
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def colsum_deferral_active(device: torch.device) -> bool:
+    return bool(_DEFER) and device.type == "cuda" and _dev_idx(device) in _DEFER
+
+
+def defer_colsum(device: torch.device, part: torch.Tensor, sums: torch.Tensor) -> None:
+    _DEFER[_dev_idx(device)].append((part, sums))
+
+
+def flush_colsums(device: torch.device) -> None:
+    """Sums every pending LayerNorm-backward partial table of ``device`` in ONE launch (esgpt::colsum_flush)."""
+    if device.type != "cuda":
+        return
+    pend = _DEFER.get(_dev_idx(device))
+    if pend:
+        _ops().colsum_flush([p for p, _ in pend], [s for _, s in pend])
+        pend.clear()
+
+
+class deferred_colsums:
+    """Context of one backward pass: the LayerNorm backwards (``esgpt::residual_ln``'s registered backward) write
+    only their per-block partials and hand autograd gradient tensors that one ``esgpt::colsum_flush`` launch fills
+    on exit (or at ``flush_colsums``, e.g. before a DDP bucket reads gradients) — one launch instead of one per
+    LayerNorm. Only gradients that go straight to leaf parameters are deferred (AccumulateGrad takes them without
+    reading; TrainStep's accumulate guard flushes before any accumulation). Usable under HIP-graph capture."""
+
+    def __init__(self, device: torch.device, enabled: bool = True):
+        self.device = device
+        self.enabled = enabled and device.type == "cuda"
+
+    def __enter__(self):
+        if self.enabled:
+            _DEFER.setdefault(_dev_idx(self.device), [])
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            try:
+                flush_colsums(self.device)
+            finally:
+                _DEFER.pop(_dev_idx(self.device), None)
+        return False
+
+
 def join_weight_grads(device: torch.device) -> None:
     """The current stream waits for every weight-gradient launch queued so far on ``device``."""
     _ops().weight_grad_join(tickets(device, 1))

@@ -45,7 +45,7 @@ _state = {"loaded": False}
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
-       "pack", "adamw", "weight_grad_join")
+       "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush")
 
 
 def load():
@@ -203,6 +203,20 @@ def _register():
     def _(like):
         return None
 
+    @fake(lib + "residual_ln_bwd_partials")
+    def _(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype, out_dtype):
+        N, D = h.shape
+        f = h.new_empty
+        from .kernels import _lib_partials
+
+        return (f(N, D, dtype=torch.float32) if need_dx else f(0, dtype=torch.float32),
+                f(N, D, dtype=y_dtype) if need_dy else f(0, dtype=y_dtype),
+                f(_lib_partials(N), 3 * D, dtype=torch.float32))
+
+    @fake(lib + "colsum_flush")
+    def _(parts, sums):
+        return None
+
     @fake(lib + "linear_bwd")
     def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None, dw_tickets=None):
         f32 = torch.float32
@@ -323,14 +337,24 @@ def _register():
         ctx.save_for_backward(h, mean, rstd, ln_w, row_mask, seed)
         ctx.meta = (x is not None, y is not None, bias is not None, y.dtype if y is not None else torch.float32,
                     out_dtype, p)
+        ctx.defer_ok = bias is None and _leaves(ln_w, ln_b)
 
     def _rl_bwd(ctx, dh, dout, _dm, _dr):
+        from .kernels import colsum_deferral_active, defer_colsum
+
         h, mean, rstd, ln_w, row_mask, seed = ctx.saved_tensors
         has_x, has_y, has_bias, y_dtype, out_dtype, p = ctx.meta
         if dout is None:
             dout = torch.zeros(h.shape, dtype=out_dtype, device=h.device)
-        dx, dy, sums = ops.residual_ln_bwd(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x, has_y, y_dtype,
-                                           out_dtype, _tickets(h.device))
+        if ctx.defer_ok and colsum_deferral_active(h.device):
+            # partials now, the column sums in the pass's one esgpt::colsum_flush launch
+            dx, dy, part = ops.residual_ln_bwd_partials(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x,
+                                                        has_y, y_dtype, out_dtype)
+            sums = torch.empty(3, h.shape[1], dtype=torch.float32, device=h.device)
+            defer_colsum(h.device, part, sums.view(-1))
+        else:
+            dx, dy, sums = ops.residual_ln_bwd(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x, has_y,
+                                               y_dtype, out_dtype, _tickets(h.device))
         return (dx if has_x else None, dy if has_y else None, sums[2] if has_bias else None, sums[0], sums[1],
                 None, None, None, None, None)
 

@@ -15,6 +15,7 @@
   the step as a view into one flat f32 buffer laid out last-layer-first and cut into ~25 MB buckets; a bucket is
   all-reduced (average) in place as soon as backward has produced all of its gradients (post-accumulate-grad hooks),
   so the exchange overlaps the rest of backward (SURVEY.md §8e);
+* the LayerNorm backwards' column sums (d ln_w, d ln_b) of a whole backward pass in one launch (``defer_colsums``);
 * optionally (``overlap_weight_grads``) the projections' weight / bias gradients run on a second stream (joined
   before the exchange and AdamW), off backward's critical path;
 * optional HIP-graph capture of forward+backward, one graph per batch shape signature (static shapes; batches are
@@ -29,8 +30,9 @@ import torch
 import torch.distributed as dist
 
 from .data.types import PytorchBatch
-from .kernels import (begin_dropout_step, check_errors, end_dropout_step, err_word, join_weight_grads,
-                      raise_for_error, weight_grad_overlap, weight_grad_overlap_active)
+from .kernels import (begin_dropout_step, check_errors, colsum_deferral_active, deferred_colsums,
+                      end_dropout_step, err_word, flush_colsums, join_weight_grads, raise_for_error,
+                      weight_grad_overlap, weight_grad_overlap_active)
 from .transformer.config import OptimizationConfig
 
 
@@ -210,6 +212,8 @@ class GradBuckets:
         dev = self.flat.device
         if weight_grad_overlap_active(dev):  # the bucket's weight gradients may still be in flight on their stream
             join_weight_grads(dev)
+        if colsum_deferral_active(dev):  # LayerNorm gradients whose column sums are still pending
+            flush_colsums(dev)
         with torch.no_grad():
             for i in idx:
                 p, v = self.params[i], self.views[i]
@@ -241,7 +245,7 @@ class GradBuckets:
 class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
-                 max_graphs: int = 4, overlap_weight_grads: bool = False, _force_graph: bool = False):
+                 max_graphs: int = 4, overlap_weight_grads: bool = False, defer_colsums: bool = True, _force_graph: bool = False):
         self.model = model
         self.cfg = opt_cfg
         self.dtype = compute_dtype
@@ -272,9 +276,11 @@ class TrainStep:
         # Off by default: measured on the C2 step (HIP graph) it gains nothing — the graph executor starts the side
         # chain late and every fork costs the main stream a ~4.5 us barrier gap.
         self.overlap_weight_grads = overlap_weight_grads and dev.type == "cuda"
-        if self.overlap_weight_grads:
-            # a second gradient contribution to a parameter is added on the current stream: join the weight-gradient
-            # stream first (the first contribution may still be in flight there)
+        # the LayerNorm backwards' column sums in one launch per backward pass (kernels.deferred_colsums)
+        self.defer_colsums = defer_colsums and dev.type == "cuda"
+        if dev.type == "cuda":
+            # a second gradient contribution to a parameter is added on the current stream: the first one may still
+            # be pending (a deferred LayerNorm column sum, or a weight gradient in flight on its stream) — settle it
             for p in params:
                 p.register_hook(self._make_accumulate_guard(p))
         self._pending: deque = deque()  # (event, pinned error block copy, batch) of submitted steps
@@ -284,11 +290,22 @@ class TrainStep:
         self._prefetched = None
         self._release = None
 
+    def _ones(self, loss: torch.Tensor) -> torch.Tensor:
+        """d(loss)/d(loss) = 1 as a persistent tensor (no fill launch in the step; under HIP-graph capture the graph
+        reads it in place)."""
+        one = getattr(self, "_one", None)
+        if one is None or one.shape != loss.shape or one.dtype != loss.dtype or one.device != loss.device:
+            one = self._one = torch.ones_like(loss)
+        return one
+
     @staticmethod
     def _make_accumulate_guard(p):
         def hook(grad):
-            if p.grad is not None and weight_grad_overlap_active(grad.device):
-                join_weight_grads(grad.device)
+            if p.grad is not None:
+                if colsum_deferral_active(grad.device):
+                    flush_colsums(grad.device)
+                if weight_grad_overlap_active(grad.device):
+                    join_weight_grads(grad.device)
             return None
 
         return hook
@@ -301,8 +318,9 @@ class TrainStep:
         # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
         with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32, cache_enabled=autocast_cache):
             out = self.model(batch)
-        with weight_grad_overlap(dev, enabled=self.overlap_weight_grads):
-            out.loss.backward()
+        with deferred_colsums(dev, enabled=self.defer_colsums), \
+                weight_grad_overlap(dev, enabled=self.overlap_weight_grads):
+            out.loss.backward(self._ones(out.loss))
         if dev.type == "cuda":
             end_dropout_step(dev)
         return out.loss.detach()

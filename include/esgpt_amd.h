@@ -204,12 +204,23 @@ int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const floa
                           void* stream);
 /* Backward: sums f32 [3, D] = (dgamma, dbeta, dbias) column sums (per-block partials in part, then a second
  * small launch sums them in a fixed order: deterministic). part: f32 workspace [esgpt_residual_ln_partials(N), 3,
- * D]. counters: reserved (esgpt_residual_ln_counters returns 0; may be NULL). */
+ * D]. sums == NULL: the partials only — the caller sums them later, e.g. every LayerNorm of a backward pass in
+ * ONE esgpt_colsum_jobs launch ({part, esgpt_residual_ln_partials(N) (1 when N == 0), 3·D, sums}), bit for bit the
+ * same sums. counters: reserved (esgpt_residual_ln_counters returns 0; may be NULL). */
 int64_t esgpt_residual_ln_counters(int64_t N);
 int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, const float* h, const float* mean,
                           const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
                           const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
                           float* sums, int32_t* counters, void* stream);
+/* Column sums of many partial tables in one launch: sums[c] = Σ_b part[b·width + c] (b ascending in 16 fixed-order
+ * row groups, as the residual_ln backward's own sum launch). width % 4 == 0, 16-B aligned part / sums. */
+typedef struct esgpt_colsum_job {
+  const float* part;
+  int64_t n_parts;
+  int64_t width;
+  float* sums;
+} esgpt_colsum_job;
+int esgpt_colsum_jobs(const esgpt_colsum_job* jobs, int64_t n_jobs, void* stream);
 /* g = act(f + bias) (InnerMLP c_fc bias + activation, transformer.py:378-391); act: 0 exact-erf GELU ("gelu"),
  * 1 tanh GELU ("gelu_new"), 2 ReLU. Backward: dz = dg * act'(f + bias), dbias = column sums (part workspace
  * f32 [esgpt_bias_act_partials(N), F]). Requires F % 4 == 0. */

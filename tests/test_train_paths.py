@@ -218,3 +218,37 @@ def test_weight_grad_overlap_matches_serial_step(graph):
     assert l0 == l1
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [True, False])
+@pytest.mark.parametrize("cfg_name", ["C2", "C4"])
+def test_deferred_colsums_match_per_layer_sums(graph, cfg_name):
+    """TrainStep with the LayerNorm column sums deferred to one esgpt::colsum_flush per backward (the default) vs
+    one sum launch per LayerNorm: the same losses and parameters bit for bit (CI at the C2 widths, NA at C4; HIP
+    graph and eager)."""
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS[cfg_name]
+    Model = CIPPTForGenerativeSequenceModeling if cfg_name == "C2" else NAPPTForGenerativeSequenceModeling
+    batches = [bc.batch(i, batch_size=2, device="cuda").packed() for i in range(3)]
+
+    def run(defer):
+        cfg = bc.model_config(attention_dropout=0.1, input_dropout=0.1, resid_dropout=0.1)
+        torch.manual_seed(0)
+        m = Model(cfg).cuda().train()
+        from eventstreamgpt_amd.kernels import _seed_counter
+
+        _seed_counter(torch.device("cuda")).zero_()
+        ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=100),
+                       torch.bfloat16, use_graph=graph, defer_colsums=defer)
+        losses = [float(ts.step(b)) for b in batches]
+        ts.check()
+        return losses, {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+    l0, s0 = run(False)
+    l1, s1 = run(True)
+    assert l0 == l1
+    for k in s0:
+        assert torch.equal(s0[k], s1[k]), k
