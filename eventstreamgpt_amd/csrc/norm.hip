@@ -22,7 +22,7 @@ namespace {
 
 constexpr int kWaves = 4;
 constexpr int kMaxChunks = 4;       // 4-column chunks per lane: D <= 1024
-constexpr int kBwdRowsPerWave = 4;  // backward default: rows per wave, every load issued before the row reductions
+constexpr int kBwdRowsPerWave = 2;  // backward default: rows per wave, every load issued before the row reductions
 
 // Backward rows per wave (2, 4 or 8; ESGPT_LN_BWD_ROWS tuning hook, read once).
 int bwd_rows() {
