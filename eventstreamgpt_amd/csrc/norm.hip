@@ -62,7 +62,19 @@ __device__ __forceinline__ V4 zero4() { return V4{{0.f, 0.f, 0.f, 0.f}}; }
 
 __device__ __forceinline__ uint64_t drop_idx(int64_t row, int64_t D, int64_t col) { return (uint64_t)(row * D + col); }
 
-template <typename TY, typename TO, int KC>
+// Forward rows per wave (1, 2 or 4; ESGPT_LN_FWD_ROWS tuning hook, read once): every load of the wave's rows is
+// issued before the first row reduction.
+int fwd_rows() {
+  static int r = 0;
+  if (r == 0) {
+    const char* e = getenv("ESGPT_LN_FWD_ROWS");
+    const int v = e ? atoi(e) : 1;
+    r = (v == 1 || v == 2 || v == 4) ? v : 1;
+  }
+  return r;
+}
+
+template <typename TY, typename TO, int KC, int R>
 __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __restrict__ x, const TY* __restrict__ y,
                                                               const float* __restrict__ bias,
                                                               const uint8_t* __restrict__ rmask, float drop_p,
@@ -73,64 +85,84 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
                                                               float* __restrict__ rstd_o) {
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * kWaves + wave;
-  if (row >= N) return;
-  const bool keep_row = rmask == nullptr || rmask[row] != 0;
-  V4 v[KC];
-  float s = 0.f;
+  const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * R;
+  if (row0 >= N) return;
+  // loads of every row first (rows past N clamped, results dropped)
+  V4 xv[R][KC], yv[R][KC];
+  bool keep[R];
 #pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const int64_t c = 4 * lane + 256 * k;
-    v[k] = zero4();
-    if (c < D && keep_row) {
-      if (x) v[k] = load4(x + row * D + c);
-      if (y) {
-        V4 t = load4(y + row * D + c);
-        float z[4] = {1.f, 1.f, 1.f, 1.f};
-        if (dr.p > 0.f) {  // row * D + c is even (D % 4 == 0): two element pairs
-          dropout_mult2(dr, drop_idx(row, D, c), z[0], z[1]);
-          dropout_mult2(dr, drop_idx(row, D, c + 2), z[2], z[3]);
+  for (int rr = 0; rr < R; ++rr) {
+    const int64_t row = min(row0 + rr, N - 1);
+    keep[rr] = rmask == nullptr || rmask[row] != 0;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      xv[rr][k] = yv[rr][k] = zero4();
+      if (c < D) {
+        if (x) xv[rr][k] = load4(x + row * D + c);
+        if (y) yv[rr][k] = load4(y + row * D + c);
+      }
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < R; ++rr) {
+    const int64_t row = row0 + rr;
+    if (row >= N) break;  // wave-uniform
+    V4 v[KC];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      v[k] = zero4();
+      if (c < D && keep[rr]) {
+        v[k] = xv[rr][k];
+        if (y) {
+          float z[4] = {1.f, 1.f, 1.f, 1.f};
+          if (dr.p > 0.f) {  // row * D + c is even (D % 4 == 0): two element pairs
+            dropout_mult2(dr, drop_idx(row, D, c), z[0], z[1]);
+            dropout_mult2(dr, drop_idx(row, D, c + 2), z[2], z[3]);
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float u = yv[rr][k].v[j] + (bias ? bias[c + j] : 0.f);
+            if (dr.p > 0.f) u *= z[j];
+            v[k].v[j] += u;
+          }
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) s += v[k].v[j];
+      }
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      if (c < D) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float u = t.v[j] + (bias ? bias[c + j] : 0.f);
-          if (dr.p > 0.f) u *= z[j];
-          v[k].v[j] += u;
+          const float d = v[k].v[j] - mean;
+          q += d * d;
         }
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s += v[k].v[j];
     }
-  }
-  const float mean = wave_sum(s) / (float)D;
-  float q = 0.f;
+    const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
 #pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const int64_t c = 4 * lane + 256 * k;
-    if (c < D) {
+    for (int k = 0; k < KC; ++k) {
+      const int64_t c = 4 * lane + 256 * k;
+      if (c < D) {
+        if (h) store4(h + row * D + c, v[k]);
+        const V4 wv = load4(w + c), bv = load4(b + c);
+        V4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = v[k].v[j] - mean;
-        q += d * d;
+        for (int j = 0; j < 4; ++j) o.v[j] = (v[k].v[j] - mean) * rstd * wv.v[j] + bv.v[j];
+        store4(out + row * D + c, o);
       }
     }
-  }
-  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
-#pragma unroll
-  for (int k = 0; k < KC; ++k) {
-    const int64_t c = 4 * lane + 256 * k;
-    if (c < D) {
-      if (h) store4(h + row * D + c, v[k]);
-      const V4 wv = load4(w + c), bv = load4(b + c);
-      V4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o.v[j] = (v[k].v[j] - mean) * rstd * wv.v[j] + bv.v[j];
-      store4(out + row * D + c, o);
+    if (lane == 0) {
+      mean_o[row] = mean;
+      rstd_o[row] = rstd;
     }
-  }
-  if (lane == 0) {
-    mean_o[row] = mean;
-    rstd_o[row] = rstd;
   }
 }
 
@@ -423,16 +455,24 @@ template <typename TY, typename TO>
 void launch_ln_fwd(const float* x, const void* y, const float* bias, const uint8_t* rmask, float p, const uint64_t* seed,
                    const float* w, const float* b, float eps, int64_t N, int64_t D, float* h, void* out, float* mean,
                    float* rstd, hipStream_t st) {
-  const unsigned grid = (unsigned)cdiv(N, kWaves);
-#define LN_FWD(KC)                                                                                                \
-  residual_ln_fwd_kernel<TY, TO, KC><<<grid, 256, 0, st>>>(x, (const TY*)y, bias, rmask, p, seed, w, b, eps, N, D, h, \
-                                                           (TO*)out, mean, rstd)
+  const int R = fwd_rows();
+  const unsigned grid = (unsigned)cdiv(N, kWaves * R);
+#define LN_FWD(KC, RR)                                                                                             \
+  residual_ln_fwd_kernel<TY, TO, KC, RR><<<grid, 256, 0, st>>>(x, (const TY*)y, bias, rmask, p, seed, w, b, eps, N, D, \
+                                                               h, (TO*)out, mean, rstd)
+#define LN_FWD_R(KC)                 \
+  do {                               \
+    if (R == 2) LN_FWD(KC, 2);       \
+    else if (R == 4) LN_FWD(KC, 4);  \
+    else LN_FWD(KC, 1);              \
+  } while (0)
   switch (cdiv(D, 256)) {
-    case 1: LN_FWD(1); break;
-    case 2: LN_FWD(2); break;
-    case 3: LN_FWD(3); break;
-    default: LN_FWD(4); break;
+    case 1: LN_FWD_R(1); break;
+    case 2: LN_FWD_R(2); break;
+    case 3: LN_FWD_R(3); break;
+    default: LN_FWD_R(4); break;
   }
+#undef LN_FWD_R
 #undef LN_FWD
 }
 
