@@ -509,7 +509,8 @@ constexpr int kSortCh = kSortThreads * kSortItems;  // slots per sort block
 // K1: a stable LSD radix sort of the block's (row, local slot) pairs (rocPRIM block_radix_sort: bit-stable, no
 // atomics; invalid slots carry the sentinel row V and sort last), run starts by a block max-scan of the positions
 // where the row changes, then per valid slot (row, rank within the block's run | local slot << 12) in sorted order
-// and, at every run end, the run length into counts[blk][row] (zeroed beforehand).
+// and, at every run end, the run length into counts[blk][row] (the block zeroes its counts row first; the barriers
+// of the sort order those stores before the run-end stores).
 __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs a, int64_t n_slots, int end_bit,
                                                                       int32_t* __restrict__ counts,
                                                                       int2* __restrict__ sorted,
@@ -535,6 +536,8 @@ __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs
     val[i] = (uint32_t)pos;
   }
   if (t == 0) s_nv = 0;
+  int32_t* col = counts + (int64_t)blockIdx.x * a.V;
+  for (int64_t v = t; v < a.V; v += kSortThreads) col[v] = 0;  // this block's counts row (run ends written below)
   Sort().sort(key, val, tmp.sort, 0, end_bit);
   __syncthreads();
 #pragma unroll
@@ -548,7 +551,6 @@ __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs
   }
   Scan().inclusive_scan(start, start, tmp.scan, rocprim::maximum<int>());
   int2* out = sorted + base;
-  int32_t* col = counts + (int64_t)blockIdx.x * a.V;
 #pragma unroll
   for (int i = 0; i < kSortItems; ++i) {
     const int pos = t * kSortItems + i;
@@ -568,8 +570,10 @@ __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs
 // the segment rewritten as running prefixes. Loads of a segment are issued 16 at a time.
 constexpr int kPrefWaves = 16;
 __global__ __launch_bounds__(1024) void bag_col_prefix_kernel(int32_t* __restrict__ counts, int nblk, int64_t V,
-                                                              int32_t* __restrict__ total) {
+                                                              int32_t* __restrict__ total, float* __restrict__ dtable,
+                                                              int64_t D) {
   __shared__ int32_t s_seg[kPrefWaves][64];
+  __shared__ int32_t s_tot[64];
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const int64_t v = (int64_t)blockIdx.x * 64 + lane;
   const bool ok = v < V;
@@ -587,7 +591,25 @@ __global__ __launch_bounds__(1024) void bag_col_prefix_kernel(int32_t* __restric
   __syncthreads();
   int32_t run = 0;
   for (int w = 0; w < wave; ++w) run += s_seg[w][lane];
-  if (wave == kPrefWaves - 1 && ok) total[v] = run + sum;
+  if (wave == kPrefWaves - 1) {
+    if (ok) total[v] = run + sum;
+    s_tot[lane] = ok ? run + sum : 1;
+  }
+  __syncthreads();
+  // gradient rows of this block's vocabulary rows without entries: zero (the reduce writes every other row)
+  const int64_t v0 = (int64_t)blockIdx.x * 64;
+  if ((D & 3) == 0) {
+    const int64_t q = D / 4;
+    for (int64_t i = threadIdx.x; i < 64 * q; i += 1024) {
+      const int rr = (int)(i / q);
+      if (s_tot[rr] == 0) reinterpret_cast<float4*>(dtable + (v0 + rr) * D)[i % q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < 64 * D; i += 1024) {
+      const int rr = (int)(i / D);
+      if (s_tot[rr] == 0) dtable[(v0 + rr) * D + i % D] = 0.f;
+    }
+  }
   for (int bb = b0; bb < b1; bb += 16) {
     int32_t c[16];
 #pragma unroll
@@ -1021,13 +1043,12 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
     bag_subject_sum_kernel<<<dim3((unsigned)batch->B, (unsigned)cdiv(D, 256)), 256, 0, st>>>(w.sub_part, w.n_sub, D,
                                                                                           w.sub);
   }
-  if (zero_async(w.counts, sizeof(int32_t) * w.nblk * V, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
-  if (zero_async(dtable, sizeof(float) * V * D, st) != hipSuccess) return ESGPT_ERR_LAUNCH;  // rows without entries
+  // (no zero-fill launches: the sort blocks zero their counts rows, bag_col_prefix the table rows without entries)
   int end_bit = 1;
   while (end_bit < 32 && (V >> end_bit) != 0) ++end_bit;  // keys 0 .. V (the sentinel) fit in end_bit bits
   bag_block_sort_kernel<<<(unsigned)w.nblk, kSortThreads, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
                                                                    w.n_valid);
-  bag_col_prefix_kernel<<<(unsigned)cdiv(V, 64), 1024, 0, st>>>(w.counts, (int)w.nblk, V, w.total);
+  bag_col_prefix_kernel<<<(unsigned)cdiv(V, 64), 1024, 0, st>>>(w.counts, (int)w.nblk, V, w.total, dtable, D);
   bag_row_scan_kernel<<<1, 1024, 0, st>>>(w.total, V, w.rowptr, w.multi, kChunk);
   bag_scatter_kernel<<<dim3(4, (unsigned)w.nblk), 256, 0, st>>>(a, w.sorted, w.n_valid, w.counts, w.rowptr, w.ent);
   // The number of entries is data-dependent (not known on the host without a sync): launch for the upper bound;
