@@ -115,6 +115,7 @@ SIGNATURES = {
     "esgpt_linear_bwd_split": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64,
                                       _vp, _vp, _vp, _sz, _vp, _vp, _i64, _vp, _vp]),
     "esgpt_stream_wait": (_int, [_vp, _vp]),
+    "esgpt_seed_bank": (_int, [_vp, _vp, _i64, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_collate_shape": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

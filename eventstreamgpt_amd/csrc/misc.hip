@@ -131,9 +131,26 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
   return hipGetLastError();
 }
 
+// bank[i] = counter + i (i < slots), then counter += slots: one block (every thread reads the counter before the
+// barrier; thread 0 advances it after).
+__global__ __launch_bounds__(256) void seed_bank_kernel(int64_t* __restrict__ counter, int64_t* __restrict__ bank,
+                                                        int64_t slots) {
+  const int64_t c = *counter;
+  for (int64_t i = threadIdx.x; i < slots; i += blockDim.x) bank[i] = c + i;
+  __syncthreads();
+  if (threadIdx.x == 0) *counter = c + slots;
+}
+
 }  // namespace esgpt
 
 extern "C" {
+
+int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream) {
+  ESGPT_REQUIRE(counter && bank && slots > 0);
+  esgpt::seed_bank_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counter, bank, slots);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
 
 const char* esgpt_version(void) { return "eventstreamgpt_amd 0.1.0 (gfx950)"; }
 

@@ -501,6 +501,15 @@ c10::hip::HIPStream weight_grad_stream(c10::DeviceIndex dev) {
   return *streams[dev];
 }
 
+// bank[i] = counter + i, counter += bank.numel() (one launch; both int64 device tensors, updated in place)
+void seed_bank(const Tensor& counter, const Tensor& bank) {
+  const c10::DeviceGuard guard(counter.device());
+  TORCH_CHECK(counter.scalar_type() == at::kLong && bank.scalar_type() == at::kLong && counter.numel() == 1 &&
+                  bank.is_contiguous() && counter.is_cuda() && bank.is_cuda(),
+              "seed_bank: int64 device counter [1] and contiguous int64 bank");
+  check(esgpt_seed_bank(ptr<int64_t>(counter), ptr<int64_t>(bank), bank.numel(), stream_of(counter)), "seed_bank");
+}
+
 // The current stream waits for every weight-gradient launch queued so far (before dW / db are read).
 void weight_grad_join(const Tensor& like) {
   const c10::DeviceGuard guard(like.device());
@@ -712,6 +721,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
         "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None) -> (Tensor, Tensor, Tensor)");
   m.def("weight_grad_join(Tensor like) -> ()");
+  m.def("seed_bank(Tensor(a!) counter, Tensor(b!) bank) -> ()");
   m.def("residual_ln_bwd_partials(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, "
         "Tensor? row_mask, float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, "
         "ScalarType out_dtype) -> (Tensor, Tensor, Tensor)");
@@ -748,6 +758,7 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("linear_act", &linear_act);
   m.impl("linear_bwd", &linear_bwd);
   m.impl("weight_grad_join", &weight_grad_join);
+  m.impl("seed_bank", &seed_bank);
   m.impl("residual_ln_bwd_partials", &residual_ln_bwd_partials);
   m.impl("colsum_flush", &colsum_flush);
   m.impl("linear", &linear);

@@ -389,7 +389,7 @@ def _seed_counter(device: torch.device) -> torch.Tensor:
 
 
 def begin_dropout_step(device: torch.device) -> None:
-    """Refreshes the per-step seed bank on the stream (two small kernels per training step): slot i of the bank
+    """Refreshes the per-step seed bank on the stream (one small kernel per training step): slot i of the bank
     = counter + i, then counter += slots. Until the next call, ``next_dropout_seed`` hands out slots of the bank
     (no kernel per dropout site); under HIP-graph capture the refresh is part of the graph, so every replay draws
     fresh masks. Without a bank (eager use outside a step) every call clones and advances the counter."""
@@ -397,11 +397,9 @@ def begin_dropout_step(device: torch.device) -> None:
     c = _seed_counter(device)
     bank = _BANKS.get(idx)
     if bank is None:
-        bank = {"buf": torch.empty(SEED_BANK_SLOTS, dtype=torch.int64, device=device),
-                "ar": torch.arange(SEED_BANK_SLOTS, dtype=torch.int64, device=device), "next": 0}
+        bank = {"buf": torch.empty(SEED_BANK_SLOTS, dtype=torch.int64, device=device), "next": 0}
         _BANKS[idx] = bank
-    torch.add(bank["ar"], c, out=bank["buf"])
-    c.add_(SEED_BANK_SLOTS)
+    _ops().seed_bank(c, bank["buf"])  # one launch: buf = c + arange, c += slots
     bank["next"] = 0
 
 

@@ -45,7 +45,7 @@ _state = {"loaded": False}
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
-       "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush")
+       "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank")
 
 
 def load():
@@ -201,6 +201,10 @@ def _register():
 
     @fake(lib + "weight_grad_join")
     def _(like):
+        return None
+
+    @fake(lib + "seed_bank")
+    def _(counter, bank):
         return None
 
     @fake(lib + "residual_ln_bwd_partials")
@@ -452,7 +456,7 @@ def _register():
         xc, xt, wc, wt, dzc, dzt, dbias = ctx.saved_tensors
         n_cw, n_tw = ctx.n
         rows_c, rows_t = ctx.rows
-        alpha = g.contiguous()[-1:]
+        alpha = g[-1:]  # a 1-element view (g may be a stride-0 expansion of the total's gradient)
         # the loss kernel's per-subject position-0 bias rows are summed into db inside the same launch
         dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, dbias if dbias.numel() else None,
                                     split_ok=ctx.split_ok)

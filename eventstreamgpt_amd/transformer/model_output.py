@@ -610,11 +610,11 @@ class GenerativeOutputLayerBase(torch.nn.Module):
         mods = self._content_modules()
         return torch.cat([m.weight for m in mods], 0), torch.cat([m.bias for m in mods], 0)
 
-    def _package(self, batch, losses, names):
+    def _package(self, batch, losses, names):  # noqa: D401
         cls, reg = {}, {}
         for i, (kind, m) in enumerate(names):
             (cls if kind == "classification" else reg)[m] = losses[i].detach()
-        loss = losses[-1]
+        loss = _TotalLoss.apply(losses)
         return GenerativeSequenceModelOutput(
             loss=loss,
             losses=GenerativeSequenceModelLosses(classification=cls, regression=reg,
@@ -624,6 +624,21 @@ class GenerativeOutputLayerBase(torch.nn.Module):
             event_mask=batch["event_mask"],
             dynamic_values_mask=batch["dynamic_values_mask"],
         )
+
+
+class _TotalLoss(torch.autograd.Function):
+    """``losses[-1]`` (the total of the fused losses vector) whose backward hands the incoming scalar gradient back as
+    a stride-0 view over the whole vector: the fused losses' backward reads only its last element (the per-term
+    entries are detached logging values), so backward needs no zero-fill + scatter launches."""
+
+    @staticmethod
+    def forward(ctx, losses):
+        ctx.n = losses.shape[0]
+        return losses[-1]
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.expand(ctx.n)
 
 
 def all_classification_measurements(layer: GenerativeOutputLayerBase) -> set:

@@ -291,6 +291,10 @@ int esgpt_linear_bwd_split(const void* dy, int64_t lddy, const void* x, int64_t 
 /* `waiter` waits (device-side, an event) for every piece of work queued on `signaller` before the call: the join of
  * esgpt_linear_bwd_split's weight-gradient stream (and its fork). Both may be captured into one HIP graph. */
 int esgpt_stream_wait(void* waiter, void* signaller);
+/* Dropout seed bank of one training step (the per-site keep-mask seeds, generative_modeling.py's torch RNG
+ * stream replaced by a device counter): bank[i] = *counter + i for i < slots, then *counter += slots — one launch,
+ * capturable into a HIP graph (every replay draws fresh seeds). */
+int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream);
 
 /* ---- Parameter packing -------------------------------------------------------------------------------------
  * The compute-dtype copies of the f32 parameters a step reads, in ONE launch: the blocks' flat bf16 weight shadow
