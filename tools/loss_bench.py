@@ -26,7 +26,8 @@ def main():
     dev = torch.device("cuda")
     bc = CONFIGS["C2"]
     model = CIPPTForGenerativeSequenceModeling(bc.model_config())
-    batch = bc.batch(0, batch_size=32).to(dev)
+    bsz = int(os.environ.get("LOSS_BENCH_B", "32"))  # batch size (rows = B * (L + 1): waves per resident round)
+    batch = bc.batch(0, batch_size=bsz).to(dev)
     layer = model.output_layer
     layer._layout = layer._build_layout()
     terms, _ = layer._terms_for(MO.all_classification_measurements(layer),
