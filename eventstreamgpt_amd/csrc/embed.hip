@@ -491,7 +491,7 @@ __device__ __forceinline__ bool bag_slot(const BagBwdArgs& a, int64_t slot, int6
 // reduction in slot order (every sum runs in a fixed order: table gradients are bitwise repeatable).
 //   K0 bag_subject_*    (static SUM_ALL) subject sums of dsrc over valid events and levels (16-event chunks, then
 //                       the chunks in order)
-//   K1 bag_block_sort   per block of kSortCh slots: a stable radix sort of the slots by row (slot order within a
+//   K1 bag_block_sort   per block of 1,024 or 4,096 slots: a stable radix sort of the slots by row (slot order within a
 //                       row), the block's per-row counts (counts[blk][V]) and every valid slot's (row, rank within
 //                       the block's run) in block-sorted order
 //   K2 bag_col_prefix   per row: exclusive prefix of counts over blocks (in place) and the row total
@@ -502,19 +502,25 @@ __device__ __forceinline__ bool bag_slot(const BagBwdArgs& a, int64_t slot, int6
 //   K5 bag_combine      rows spanning chunks (a compact list): tail(c0) + the heads of c0+1 .. c1 (a fixed
 //                       16-wave interleave and a fixed combine order); rows without entries stay zero-filled
 // ------------------------------------------------------------------------------------------------------------
-constexpr int kSortThreads = 256;
 constexpr int kSortItems = 4;
-constexpr int kSortCh = kSortThreads * kSortItems;  // slots per sort block
+// Slots per sort block: 256 threads x 4 (1,024) by default; 1,024 x 4 (4,096) when the per-block count rows would be
+// large (blocks x V > kBigCounts ints: 21 MB of count rows at C5 -> 5 MB), i.e. a large vocabulary over many slots.
+constexpr int64_t kBigCounts = 1 << 21;
+static int64_t sort_threads(int64_t n_slots, int64_t V) {
+  return cdiv(n_slots, 256 * kSortItems) * V > kBigCounts ? 1024 : 256;
+}
 
 // K1: a stable LSD radix sort of the block's (row, local slot) pairs (rocPRIM block_radix_sort: bit-stable, no
 // atomics; invalid slots carry the sentinel row V and sort last), run starts by a block max-scan of the positions
 // where the row changes, then per valid slot (row, rank within the block's run | local slot << 12) in sorted order
 // and, at every run end, the run length into counts[blk][row] (the block zeroes its counts row first; the barriers
 // of the sort order those stores before the run-end stores).
+template <int kSortThreads>
 __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs a, int64_t n_slots, int end_bit,
                                                                       int32_t* __restrict__ counts,
                                                                       int2* __restrict__ sorted,
                                                                       int32_t* __restrict__ n_valid) {
+  constexpr int kSortCh = kSortThreads * kSortItems;
   using Sort = rocprim::block_radix_sort<uint32_t, kSortThreads, kSortItems, uint32_t>;
   using Scan = rocprim::block_scan<int, kSortThreads>;
   __shared__ union {
@@ -672,10 +678,11 @@ __global__ __launch_bounds__(1024) void bag_row_scan_kernel(const int32_t* __res
 __global__ __launch_bounds__(256) void bag_scatter_kernel(BagBwdArgs a, const int2* __restrict__ sorted,
                                                           const int32_t* __restrict__ n_valid,
                                                           const int32_t* __restrict__ prefix,
-                                                          const int32_t* __restrict__ rowptr, int4* __restrict__ ent) {
+                                                          const int32_t* __restrict__ rowptr, int4* __restrict__ ent,
+                                                          int64_t sort_ch) {
   const int blk = blockIdx.y;
   const int nv = n_valid[blk];
-  const int64_t base = (int64_t)blk * kSortCh;
+  const int64_t base = (int64_t)blk * sort_ch;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
     const int2 e = sorted[base + i];
     const int row = e.x, rank = e.y & 4095, slot = e.y >> 12;
@@ -908,7 +915,7 @@ struct BagWs {
   float* part_tail;  // [n_chunks][D]
   float* sub;        // [B][D]
   float* sub_part;   // [B][n_sub][D]
-  int64_t nblk, n_slots, n_chunks, n_sub;
+  int64_t nblk, n_slots, n_chunks, n_sub, sort_threads, sort_ch;
   size_t bytes;
 };
 
@@ -917,7 +924,9 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 static BagWs carve(void* base, const esgpt_batch* bt, int64_t G, int64_t V, int64_t D) {
   BagWs w{};
   w.n_slots = bt->B * bt->L * G * bt->M + bt->B * bt->S;
-  w.nblk = std::max<int64_t>(1, cdiv(w.n_slots, kSortCh));
+  w.sort_threads = sort_threads(w.n_slots, V);
+  w.sort_ch = w.sort_threads * kSortItems;
+  w.nblk = std::max<int64_t>(1, cdiv(w.n_slots, w.sort_ch));
   w.n_chunks = std::max<int64_t>(1, cdiv(w.n_slots, kChunk));
   char* p = (char*)base;
   size_t off = 0;
@@ -931,7 +940,7 @@ static BagWs carve(void* base, const esgpt_batch* bt, int64_t G, int64_t V, int6
   w.rowptr = (int32_t*)take(sizeof(int32_t) * (V + 1));
   w.multi = (int32_t*)take(sizeof(int32_t) * (V + 1));
   w.n_valid = (int32_t*)take(sizeof(int32_t) * w.nblk);
-  w.sorted = (int2*)take(sizeof(int2) * w.nblk * kSortCh);
+  w.sorted = (int2*)take(sizeof(int2) * w.nblk * w.sort_ch);
   w.ent = (int4*)take(sizeof(int4) * w.n_slots);
   w.part_head = (float*)take(sizeof(float) * w.n_chunks * D);
   w.part_tail = (float*)take(sizeof(float) * w.n_chunks * D);
@@ -1046,11 +1055,16 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   // (no zero-fill launches: the sort blocks zero their counts rows, bag_col_prefix the table rows without entries)
   int end_bit = 1;
   while (end_bit < 32 && (V >> end_bit) != 0) ++end_bit;  // keys 0 .. V (the sentinel) fit in end_bit bits
-  bag_block_sort_kernel<<<(unsigned)w.nblk, kSortThreads, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
+  if (w.sort_threads == 1024)
+    bag_block_sort_kernel<1024><<<(unsigned)w.nblk, 1024, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
+                                                                   w.n_valid);
+  else
+    bag_block_sort_kernel<256><<<(unsigned)w.nblk, 256, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
                                                                    w.n_valid);
   bag_col_prefix_kernel<<<(unsigned)cdiv(V, 64), 1024, 0, st>>>(w.counts, (int)w.nblk, V, w.total, dtable, D);
   bag_row_scan_kernel<<<1, 1024, 0, st>>>(w.total, V, w.rowptr, w.multi, kChunk);
-  bag_scatter_kernel<<<dim3(4, (unsigned)w.nblk), 256, 0, st>>>(a, w.sorted, w.n_valid, w.counts, w.rowptr, w.ent);
+  bag_scatter_kernel<<<dim3(4, (unsigned)w.nblk), 256, 0, st>>>(a, w.sorted, w.n_valid, w.counts, w.rowptr, w.ent,
+                                                                 w.sort_ch);
   // The number of entries is data-dependent (not known on the host without a sync): launch for the upper bound;
   // chunks past rowptr[V] exit immediately.
   const unsigned g_red = (unsigned)cdiv(w.n_chunks, kWavesPerBlock);
