@@ -693,9 +693,11 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
             names.append(nn_)
     mods = layer._content_modules()
     if terms:
-        fused = head_losses(encoded[:, :, : G - 1, :].reshape(B * Lq * (G - 1), D),
-                            encoded[:, :, G - 1, :].reshape(B * Lq, D), batch, terms, layer._tte_spec(0), 0,
-                            max(1, G - 1), mods, [layer.TTE_layer.proj])
+        from .structured_attention import split_last_level
+
+        head, last = split_last_level(encoded)  # one cat in backward instead of two zero-filled slice gradients
+        fused = head_losses(head.reshape(B * Lq * (G - 1), D), last.reshape(B * Lq, D), batch, terms,
+                            layer._tte_spec(0), 0, max(1, G - 1), mods, [layer.TTE_layer.proj])
         if fused is not None:
             return fused, names
     if terms:

@@ -19,6 +19,50 @@ from typing import Any
 import torch
 
 
+class _SplitLast(torch.autograd.Function):
+    """x [..., G, D] -> (x[..., :G-1, :], x[..., G-1, :]) as contiguous tensors whose backward is ONE cat of the two
+    incoming gradients (autograd's slice / select backwards would zero-fill a full-size gradient for each and add
+    them). A missing incoming gradient counts as zeros."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        return x[..., :-1, :].contiguous(), x[..., -1, :].contiguous()
+
+    @staticmethod
+    def backward(ctx, d_head, d_last):
+        shape = ctx.shape
+        ref = d_head if d_head is not None else d_last
+        if d_head is None:
+            d_head = ref.new_zeros(shape[:-2] + (shape[-2] - 1, shape[-1]))
+        if d_last is None:
+            d_last = ref.new_zeros(shape[:-2] + (shape[-1],))
+        return torch.cat((d_head, d_last.unsqueeze(-2)), dim=-2)
+
+
+def split_last_level(x: torch.Tensor):
+    """(all but the last dependency-graph level, the last level) of x [..., G, D], without zero-filled backwards."""
+    return _SplitLast.apply(x)
+
+
+class _Assemble(torch.autograd.Function):
+    """The dependency-graph sequence [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i] per event (structured_attention.py:
+    125-149): history = ctx shifted by one event (zeros first), head = the graph elements but the last, ctx = the
+    contextualised event. Backward: d head = a view of the incoming gradient, d ctx = its last element plus the
+    history slot of the next event — no zero-filled slice gradients."""
+
+    @staticmethod
+    def forward(ctx_, ctx, head):
+        history = torch.nn.functional.pad(ctx[:, :-1, :], (0, 0, 1, 0))
+        return torch.cat((history.unsqueeze(2), head, ctx.unsqueeze(2)), dim=2)
+
+    @staticmethod
+    def backward(ctx_, d):
+        d_ctx = d[:, :, -1, :].clone()
+        d_ctx[:, :-1, :] += d[:, 1:, 0, :]
+        return d_ctx, d[:, :, 1:-1, :]
+
+
 class StructuredAttention(torch.nn.Module):
     def __init__(self, seq_module: torch.nn.Module, dep_graph_module: torch.nn.Module):
         super().__init__()
@@ -42,7 +86,7 @@ class StructuredAttention(torch.nn.Module):
                 kpm = seq_attention_mask.reshape(bsz, -1) == 0
             else:
                 kpm = event_mask
-            per_event = hidden_states[:, :, -1, :]
+            head, per_event = split_last_level(hidden_states)
             if m3 is not None:
                 per_event = torch.where(m3, per_event, 0.0)
             ctx = self.seq_module(per_event, key_padding_mask=kpm, **seq_module_kwargs)
@@ -51,14 +95,12 @@ class StructuredAttention(torch.nn.Module):
             if m3 is not None:
                 ctx = torch.where(m3, ctx, 0.0)
             if prepend_graph_with_history_embeddings:
-                history = torch.nn.functional.pad(ctx[:, :-1, :], (0, 0, 1, 0))  # [0, ctx_0 .. ctx_{L-2}]
-                # [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i]: the last graph element is replaced by the contextualised
-                # event (structured_attention.py:125-149).
-                dep_graph_seq = torch.cat((history.unsqueeze(2), hidden_states[:, :, :-1, :], ctx.unsqueeze(2)),
-                                          dim=2)
+                # [h_{i-1}, e_{i,1}, ..., e_{i,G-1}, ctx_i], h_{i-1} = ctx_{i-1} (zeros first): the last graph element
+                # is replaced by the contextualised event (structured_attention.py:125-149).
+                dep_graph_seq = _Assemble.apply(ctx, head)
                 static_kv_first = True
             else:
-                dep_graph_seq = torch.cat((hidden_states[:, :, :-1, :], ctx.unsqueeze(2)), dim=2)
+                dep_graph_seq = torch.cat((head, ctx.unsqueeze(2)), dim=2)
                 static_kv_first = False
         else:
             dep_graph_seq = hidden_states
