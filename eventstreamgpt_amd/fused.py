@@ -335,6 +335,23 @@ def block_fused_supported(blk, hidden: torch.Tensor) -> bool:
             and blk.attn.attention.head_dim <= 128)
 
 
+class _SkipFirst(torch.autograd.Function):
+    """hidden [Bs, T, D] -> hidden[:, 1:, :] as a contiguous [Bs·(T-1), D] tensor whose backward writes the full
+    gradient in one pass (zeros for the first position, the incoming rows after it) — not a zero-filled slice
+    gradient plus a copy."""
+
+    @staticmethod
+    def forward(ctx, hidden):
+        ctx.shape = hidden.shape
+        Bs, T, D = hidden.shape
+        return hidden[:, 1:, :].reshape(Bs * (T - 1), D).contiguous()
+
+    @staticmethod
+    def backward(ctx, d):
+        Bs, T, D = ctx.shape
+        return torch.nn.functional.pad(d.view(Bs, T - 1, D), (0, 0, 1, 0))
+
+
 def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_first: bool) -> torch.Tensor:
     """``InnerBlock.forward`` (``transformer.py:409-461``, pre-LN attention + MLP with residuals) through the HIP
     kernels: LayerNorm, one packed-QKV GEMM, attention, out_proj with its bias + residual dropout + the second
@@ -361,7 +378,8 @@ def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_fir
         o = attention(qkv, kpm, qpm, att.num_heads, window, static_kv_first, p_att)
         Tq = T - skf
         y = proj(o.reshape(Bs * Tq, D), wo, att.out_proj.bias, (att.out_proj.weight,))
-        res = hidden[:, skf:, :].reshape(Bs * Tq, D).float().contiguous()
+        # the residual rows: every row (the LayerNorm input itself) or all but the static first one
+        res = x2 if skf == 0 else _SkipFirst.apply(hidden.float())
         h1, ln2 = residual_ln(res, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt)
         y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name], with_bias=True)
         out = h1 + F.dropout(y2.float(), p=p_res, training=train)
