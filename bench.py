@@ -378,14 +378,19 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_c
         with torch.no_grad():
             emb.embed(batch, time_layer=tl)
 
-    add("embed_joint_fwd", "embed_joint_fwd_kernel<4, 1>", "hbm", embed_fwd_bytes(batch, cfg), emb_fwd)
-    eb, _keep_eb = _embed_bwd_launcher(model, batch)
-    add("embed_joint_bwd", "bag_block_sort/col_prefix/row_scan/scatter/reduce/combine/subject kernels "
-        "(esgpt_embed_bag_bwd)", "hbm",
-        embed_bwd_bytes(batch, cfg), eb, {"traffic_key": "embed_bag_bwd"})
-    lf, lbytes, _keep_lf = _loss_launcher(model, batch)
-    add("output_loss", "count + event + reduce kernels (esgpt_output_loss)", "hbm", lbytes, lf,
-        {"traffic_key": "output_loss", "shape": f"bf16 logits [{B * Lq}, {_keep_lf['zc'].shape[1]}]"})
+    # the JOINT input layer and the CI loss layout only (the NA configuration's SPLIT bags and per-level loss rows
+    # are timed inside its step)
+    ci = cfg.structured_event_processing_mode == "conditionally_independent"
+    if hasattr(emb, "embed_layer"):
+        add("embed_joint_fwd", "embed_joint_fwd_kernel<4, 1>", "hbm", embed_fwd_bytes(batch, cfg), emb_fwd)
+        eb, _keep_eb = _embed_bwd_launcher(model, batch)
+        add("embed_joint_bwd", "bag_block_sort/col_prefix/row_scan/scatter/reduce/combine/subject kernels "
+            "(esgpt_embed_bag_bwd)", "hbm",
+            embed_bwd_bytes(batch, cfg), eb, {"traffic_key": "embed_bag_bwd"})
+    if ci:
+        lf, lbytes, _keep_lf = _loss_launcher(model, batch)
+        add("output_loss", "count + event + reduce kernels (esgpt_output_loss)", "hbm", lbytes, lf,
+            {"traffic_key": "output_loss", "shape": f"bf16 logits [{B * Lq}, {_keep_lf['zc'].shape[1]}]"})
     cf, cbytes, nnz5, _keep_c5 = _c5_embed_microbench(dev)
     add("embed_c5_microbench", "embed_joint_fwd_kernel<4, 1>", "hbm", cbytes, cf,
         {"traffic_key": "embed_joint_fwd_kernel@c5",
