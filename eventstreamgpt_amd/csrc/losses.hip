@@ -66,15 +66,30 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
   const int64_t* meas = bt.dyn_meas + b * L * M;
   const uint8_t* vmask = bt.dyn_vmask + b * L * M;
   const int LM = (int)(L * M), Mi = (int)M;  // 32-bit index math (L * M < 2^31, checked on the host)
-  for (int i = threadIdx.x; i < LM; i += blockDim.x) {
-    const int64_t mi = meas[i];
-    const bool vm = vmask[i] != 0;
-    uint32_t bits = 0u;
-    for (int t = 0; t < T; ++t) {
-      const esgpt_loss_term& tm = terms.t[t];
-      if (tm.kind != ESGPT_TERM_MULTI && mi == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vm)) bits |= 1u << t;
+  // kU entries per thread and pass, loaded together at clamped indices (one memory round trip per pass instead
+  // of one per entry)
+  constexpr int kU = 4;
+  const int stride = (int)blockDim.x;
+  for (int i0 = threadIdx.x; i0 < LM; i0 += kU * stride) {
+    int64_t mi[kU];
+    uint8_t vb[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int i = min(i0 + k * stride, LM - 1);
+      mi[k] = meas[i];
+      vb[k] = vmask[i];
     }
-    if (bits) atomicOr(&s_bits[i / Mi], bits);
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int i = i0 + k * stride;
+      uint32_t bits = 0u;
+      for (int t = 0; t < T; ++t) {
+        const esgpt_loss_term& tm = terms.t[t];
+        if (tm.kind != ESGPT_TERM_MULTI && mi[k] == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vb[k] != 0))
+          bits |= 1u << t;
+      }
+      if (i < LM && bits) atomicOr(&s_bits[i / Mi], bits);
+    }
   }
   __syncthreads();
   int32_t c[ESGPT_MAX_TERMS + 1];
@@ -508,11 +523,13 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
     if (zrow) {
       constexpr int kBatch = 8;
       for (int64_t c0 = 0; c0 < nch; c0 += 64 * kBatch) {
+        // unconditional loads at clamped chunk indices: all kBatch loads in flight together, in registers
+        // (conditional loads were serialised one round trip each through scratch)
         uint4 v[kBatch];
 #pragma unroll
         for (int i = 0; i < kBatch; ++i) {
           const int64_t c = c0 + 64 * i + lane;
-          if (c < nch) v[i] = reinterpret_cast<const uint4*>(zrow)[c];
+          v[i] = reinterpret_cast<const uint4*>(zrow)[c < nch ? c : nch - 1];
         }
 #pragma unroll
         for (int i = 0; i < kBatch; ++i) {
@@ -630,16 +647,18 @@ __global__ __launch_bounds__(1024) void reduce_kernel(const float* __restrict__ 
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float total = 0.f;
-    for (int t = 0; t <= NT; ++t) {
-      float v = 0.f;
-      for (int w = 0; w < 16; ++w) v += s[w][t];
-      v = (t < NT) ? v : -v;  // last slot: -TTE_LL
-      losses[t] = v;
-      total += v;
+  // wave 0: lane t sums term t over the 16 waves (w = 0..15, the fixed order), then the total in term order from
+  // readlanes (no serial chain of LDS reads in one thread)
+  if (wave == 0) {
+    float v = 0.f;
+    if (lane <= NT) {
+      for (int w = 0; w < 16; ++w) v += s[w][lane];
+      v = (lane < NT) ? v : -v;  // last slot: -TTE_LL
+      losses[lane] = v;
     }
-    losses[NT + 1] = total;
+    float total = 0.f;
+    for (int t = 0; t <= NT; ++t) total += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), t));
+    if (lane == 0) losses[NT + 1] = total;
   }
 }
 
