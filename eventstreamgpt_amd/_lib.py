@@ -23,6 +23,7 @@ EMB_NORMALIZE, EMB_STATIC, EMB_TIME, EMB_CUMSUM, EMB_TIME_ABS = 1, 2, 4, 8, 16
 BAG_JOINT, BAG_CAT, BAG_NUM = 0, 1, 2
 TERM_SINGLE, TERM_MULTI, TERM_MVREG, TERM_UVREG = 1, 2, 3, 4
 TTE_EXP, TTE_LNM = 1, 2
+LOSS_PATH_AUTO, LOSS_PATH_STREAM, LOSS_PATH_ROW_STAGED, LOSS_PATH_GENERIC = 0, 1, 2, 3
 GEMM_K_CONTIG, GEMM_MN_CONTIG = 0, 1
 MAX_TERMS = 16
 
@@ -116,6 +117,7 @@ SIGNATURES = {
                                       _vp, _vp, _vp, _sz, _vp, _vp, _i64, _vp, _vp]),
     "esgpt_stream_wait": (_int, [_vp, _vp]),
     "esgpt_seed_bank": (_int, [_vp, _vp, _i64, _vp]),
+    "esgpt_step_begin": (_int, [_vp, _vp, _i64, _vp, _vp]),
     "esgpt_column_sum_partials": (_i64, [_i64]),
     "esgpt_column_sum": (_int, [_vp, _int, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_collate_shape": (_int, [_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -124,6 +126,9 @@ SIGNATURES = {
     "esgpt_output_loss_workspace": (_sz, [_i64, _i64, _int]),
     "esgpt_output_loss": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
                                  _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
+    "esgpt_output_loss_ex": (_int, [_PB, _vp, _i64, _i64, _int, _vp, _vp, _i64, _int, ctypes.POINTER(EsgptLossTerm),
+                                    _int, ctypes.POINTER(EsgptTTESpec), _vp, _vp, _vp, _vp, _vp, _sz, _vp, _int,
+                                    _vp]),
 }
 
 _lib = None

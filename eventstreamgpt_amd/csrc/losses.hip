@@ -5,14 +5,18 @@
 // the weighted_loss / safe_weighted_avg reductions (utils.py:134-234) behind ONE forward pass that also emits
 // d(total loss)/d(logits), so the backward of the whole output layer is two GEMMs.
 //
-//   pass 1  count_kernel   one block per subject: per-term masked event counts (weighted_loss denominators),
-//                          observed-TTE counts (ValueError if a subject has none)
-//   pass 2  event_kernel   one wave per (subject, logit row): every term's per-event loss and logit gradient,
-//                          scaled by 1 / (count[b,t] * subjects_with_events[t]); per-event contributions stored
+//   pass 1  count_kernel   one block per (subject, chunk of events): per-term masked event counts (weighted_loss
+//                          denominators) and observed-TTE counts, as per-chunk integer partials
+//   pass 2  event kernels  one wave per (subject, logit row): every term's per-event loss and logit gradient,
+//                          scaled by 1 / (count[b,t] * subjects_with_events[t]); contributions stored (per row, or
+//                          per workgroup of rows); ValueError flag for a subject without an observed TTE
 //   pass 3  reduce_kernel  one block: deterministic sums of the contributions -> per-term losses, -TTE_LL, total
 //
 // HBM traffic per logit row: read C logits + write C gradients (+ the event's M entries); HBM-bound.
 #include "common.h"
+
+#include <algorithm>
+#include <vector>
 
 using namespace esgpt;
 
@@ -48,34 +52,35 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Pass 1: one 1024-thread block per subject. The subject's L·M entries are read once, coalesced (thread = entry),
-// and each entry ORs the bit of every non-MULTI term it satisfies into its event's LDS word (SINGLE: measurement
-// present; MVREG / UVREG: measurement with a value); then thread = event: term t counts the event when it is an
-// event and (MULTI or bit t set); TTE counts events followed by an event. Integer LDS adds: exact, order-free.
-// Dynamic LDS: L words.
-__global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms, int32_t* __restrict__ counts,
-                                                     int32_t* __restrict__ err) {
+// Pass 1: one 1024-thread block per (chunk of E events, subject). The chunk's E·M entries are read once, coalesced
+// (thread = entry, up to 4 per thread, loads in flight together), and each entry ORs the bit of every non-MULTI
+// term it satisfies into its event's LDS word (SINGLE: measurement present; MVREG / UVREG: measurement with a
+// value); then thread = event: term t counts the event when it is an event and (MULTI or bit t set); TTE counts
+// events followed by an event. Integer adds: exact, order-free. partial: int32 [B][n_chunks][MAX_TERMS + 1].
+// Dynamic LDS: E words.
+__global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms, int E, int32_t* __restrict__ partial) {
   extern __shared__ uint32_t s_bits[];
   __shared__ int32_t s_cnt[ESGPT_MAX_TERMS + 1];
-  const int64_t b = blockIdx.x;
+  const int64_t b = blockIdx.y;
+  const int ch = blockIdx.x, n_ch = gridDim.x;
   const int T = terms.n;
   const int64_t L = bt.L, M = bt.M;
+  const int l0 = ch * E, ne = (int)min((int64_t)E, L - l0);
   if (threadIdx.x <= T) s_cnt[threadIdx.x] = 0;
-  for (int64_t l = threadIdx.x; l < L; l += blockDim.x) s_bits[l] = 0u;
+  for (int l = threadIdx.x; l < ne; l += blockDim.x) s_bits[l] = 0u;
   __syncthreads();
-  const int64_t* meas = bt.dyn_meas + b * L * M;
-  const uint8_t* vmask = bt.dyn_vmask + b * L * M;
-  const int LM = (int)(L * M), Mi = (int)M;  // 32-bit index math (L * M < 2^31, checked on the host)
-  // kU entries per thread and pass, loaded together at clamped indices (one memory round trip per pass instead
-  // of one per entry)
+  const int64_t base = (b * L + l0) * M;
+  const int64_t* meas = bt.dyn_meas + base;
+  const uint8_t* vmask = bt.dyn_vmask + base;
+  const int NE = ne * (int)M, Mi = (int)M;  // 32-bit index math (L * M < 2^31, checked on the host)
   constexpr int kU = 4;
   const int stride = (int)blockDim.x;
-  for (int i0 = threadIdx.x; i0 < LM; i0 += kU * stride) {
+  for (int i0 = threadIdx.x; i0 < NE; i0 += kU * stride) {
     int64_t mi[kU];
     uint8_t vb[kU];
 #pragma unroll
     for (int k = 0; k < kU; ++k) {
-      const int i = min(i0 + k * stride, LM - 1);
+      const int i = min(i0 + k * stride, NE - 1);
       mi[k] = meas[i];
       vb[k] = vmask[i];
     }
@@ -88,7 +93,7 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
         if (tm.kind != ESGPT_TERM_MULTI && mi[k] == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vb[k] != 0))
           bits |= 1u << t;
       }
-      if (i < LM && bits) atomicOr(&s_bits[i / Mi], bits);
+      if (i < NE && bits) atomicOr(&s_bits[i / Mi], bits);
     }
   }
   __syncthreads();
@@ -96,24 +101,23 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
 #pragma unroll
   for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) c[t] = 0;
   const uint8_t* em = bt.event_mask + b * L;
-  for (int64_t l = threadIdx.x; l < L; l += blockDim.x) {
-    const bool ev = em[l] != 0;
+  for (int l = threadIdx.x; l < ne; l += blockDim.x) {
+    const int64_t lg = l0 + l;
+    const bool ev = em[lg] != 0;
     const uint32_t bits = s_bits[l];
 #pragma unroll
     for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
       if (t < T && ev && (terms.t[t].kind == ESGPT_TERM_MULTI || ((bits >> t) & 1u))) ++c[t];
-    if (l + 1 < L && ev && em[l + 1]) ++c[ESGPT_MAX_TERMS];
+    if (lg + 1 < L && ev && em[lg + 1]) ++c[ESGPT_MAX_TERMS];
   }
-  // wave sums (integer: exact) -> one LDS add per wave and term
 #pragma unroll
   for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) {
-    const int v = (int)wave_sum((float)c[t]);  // < 2^24 events per subject: exact in f32
+    const int v = (int)wave_sum((float)c[t]);  // < 2^24 events per chunk: exact in f32
     const int slot = t < ESGPT_MAX_TERMS ? t : T;
     if ((t < T || t == ESGPT_MAX_TERMS) && lane_id() == 0 && v) atomicAdd(&s_cnt[slot], v);
   }
   __syncthreads();
-  if (threadIdx.x <= T) counts[b * (ESGPT_MAX_TERMS + 1) + threadIdx.x] = s_cnt[threadIdx.x];
-  if (threadIdx.x == 0 && s_cnt[T] == 0) set_err(err, ESGPT_FLAG_TTE_NO_OBS);
+  if (threadIdx.x <= T) partial[(b * n_ch + ch) * (ESGPT_MAX_TERMS + 1) + threadIdx.x] = s_cnt[threadIdx.x];
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -308,9 +312,10 @@ __device__ __forceinline__ float tte_term(const esgpt_tte_spec& tte, int lane, f
 }
 
 // Subjects-with-events per term (the outer safe_weighted_avg of weighted_loss) into s_nsub_inv; TTE averages over
-// all B. Called by wave 0: lane = subject, one ballot per term (all terms' count loads in flight together).
-__device__ __forceinline__ void subjects_with_events(const int32_t* __restrict__ counts, int64_t B, int NT, int lane,
-                                                     float* s_nsub_inv) {
+// all B. Called by wave 0: lane = subject (its chunk partials summed), one ballot per term; every load of a pass
+// in flight together.
+__device__ __forceinline__ void subjects_with_events(const int32_t* __restrict__ partial, int64_t B, int n_ch, int NT,
+                                                     int lane, float* s_nsub_inv) {
   int nsub[ESGPT_MAX_TERMS];
 #pragma unroll
   for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] = 0;
@@ -318,7 +323,12 @@ __device__ __forceinline__ void subjects_with_events(const int32_t* __restrict__
     const int64_t b = b0 + lane;
     int c[ESGPT_MAX_TERMS];
 #pragma unroll
-    for (int t = 0; t < ESGPT_MAX_TERMS; ++t) c[t] = (t < NT && b < B) ? counts[b * (ESGPT_MAX_TERMS + 1) + t] : 0;
+    for (int t = 0; t < ESGPT_MAX_TERMS; ++t) c[t] = 0;
+    for (int ch = 0; ch < n_ch; ++ch) {
+      const int32_t* row = partial + (b * n_ch + ch) * (ESGPT_MAX_TERMS + 1);
+#pragma unroll
+      for (int t = 0; t < ESGPT_MAX_TERMS; ++t) c[t] += (t < NT && b < B) ? row[t] : 0;
+    }
 #pragma unroll
     for (int t = 0; t < ESGPT_MAX_TERMS; ++t) nsub[t] += __popcll(__ballot(c[t] > 0));
   }
@@ -326,6 +336,21 @@ __device__ __forceinline__ void subjects_with_events(const int32_t* __restrict__
   for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
     if (lane == t && t < NT) s_nsub_inv[t] = nsub[t] > 0 ? 1.f / (float)nsub[t] : 0.f;
   if (lane == 0) s_nsub_inv[NT] = B > 0 ? 1.f / (float)B : 0.f;
+}
+
+// Subject b's counts: lane t (<= NT) returns term t's (lane NT: observed TTEs), summed over the chunk partials.
+__device__ __forceinline__ int32_t subject_counts(const int32_t* __restrict__ partial, int64_t b, int n_ch, int NT,
+                                                  int lane, bool active) {
+  int32_t c = 0;
+  if (active && lane <= NT)
+    for (int ch = 0; ch < n_ch; ++ch) c += partial[(b * n_ch + ch) * (ESGPT_MAX_TERMS + 1) + lane];
+  return c;
+}
+
+// The reference raises "No observed time-to-event ..." for a subject whose TTE count is 0 (model_output.py:
+// 1366-1367): flagged once per subject, by the wave of its first row.
+__device__ __forceinline__ void flag_no_tte(int32_t my_cnt, int NT, bool first_row, int32_t* err) {
+  if (first_row && __builtin_amdgcn_readlane(my_cnt, NT) == 0 && lane_id() == 0) set_err(err, ESGPT_FLAG_TTE_NO_OBS);
 }
 
 // The wave's logit-row coordinates: w -> subject b, unshifted row r (-1: the bias row in shift mode) and content
@@ -354,7 +379,7 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
                                                     const T* __restrict__ zc, int64_t ldc, int64_t n_levels, int shift,
                                                     const T* __restrict__ zc_bias, const T* __restrict__ zt,
                                                     int64_t ldt, T* __restrict__ dzc, T* __restrict__ dzt,
-                                                    float* __restrict__ dbias, const int32_t* __restrict__ counts,
+                                                    float* __restrict__ dbias, const int32_t* __restrict__ counts, int n_ch,
                                                     float* __restrict__ contrib, int64_t n_rows,
                                                     int32_t* __restrict__ err) {
   __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
@@ -362,7 +387,7 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
   const int lane = lane_id();
   const int NT = terms.n;
   const int64_t L = bt.L, M = bt.M;
-  if (wave == 0) subjects_with_events(counts, bt.B, NT, lane, s_nsub_inv);
+  if (wave == 0) subjects_with_events(counts, bt.B, n_ch, NT, lane, s_nsub_inv);
 
   const int64_t w = (int64_t)blockIdx.x * kWaves + wave;
   const RowPos q = row_pos(bt, w, n_rows, shift);
@@ -382,7 +407,8 @@ __global__ __launch_bounds__(256) void event_kernel(esgpt_batch bt, Terms terms,
   __syncthreads();  // s_nsub_inv
 
   // this subject's per-term counts: lane t holds term t's (one load per lane instead of one per term)
-  const int32_t my_cnt = lane <= NT ? counts[b * (ESGPT_MAX_TERMS + 1) + lane] : 0;
+  const int32_t my_cnt = subject_counts(counts, b, n_ch, NT, lane, q.active);
+  flag_no_tte(my_cnt, NT, q.active && q.r == -shift, err);
   float* my_contrib = contrib + w;  // contrib[t * n_rows + w]
 
   // ---------------- content terms ----------------
@@ -461,7 +487,7 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
                                                         int shift, const T* __restrict__ zc_bias,
                                                         const T* __restrict__ zt, int64_t ldt, T* __restrict__ dzc,
                                                         T* __restrict__ dzt, float* __restrict__ dbias,
-                                                        const int32_t* __restrict__ counts, float* __restrict__ contrib,
+                                                        const int32_t* __restrict__ counts, int n_ch, float* __restrict__ contrib,
                                                         int64_t n_rows, int tte_in_row, int32_t* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
   __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
@@ -476,7 +502,7 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
   T* zs = reinterpret_cast<T*>(s_dyn) + (int64_t)wave * ldp;
   float* gs = reinterpret_cast<float*>(s_dyn + (size_t)waves * ldp * sizeof(T)) + (int64_t)wave * ldp;
 
-  if (wave == 0) subjects_with_events(counts, bt.B, NT, lane, s_nsub_inv);
+  if (wave == 0) subjects_with_events(counts, bt.B, n_ch, NT, lane, s_nsub_inv);
   const int64_t w = (int64_t)blockIdx.x * waves + wave;
   const RowPos q = row_pos(bt, w, n_rows, shift);
   const int64_t b = q.b, r = q.r, p = q.p;
@@ -491,7 +517,8 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
     e_val = bt.dyn_vals[off];
     e_vm = bt.dyn_vmask[off] != 0;
   }
-  const int32_t my_cnt = (q.active && lane <= NT) ? counts[b * (ESGPT_MAX_TERMS + 1) + lane] : 0;
+  const int32_t my_cnt = subject_counts(counts, b, n_ch, NT, lane, q.active);
+  flag_no_tte(my_cnt, NT, q.active && q.r == -shift, err);
   float* my_contrib = contrib + w;
   // TTE inputs (loaded with the row)
   const bool tte_row = q.active && r >= 0;
@@ -615,6 +642,307 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Streaming event kernel (the default): one wave per logit row and no whole-row staging, so occupancy is set by
+// registers, not by the row width — the row-staged kernel holds ldc·(s + 4) B of LDS per wave, which at C5
+// (ldc = 10,640) left ONE wave per workgroup and two per CU.
+//
+// Column classes of a row (host plan, per level):
+//   dense   MULTI ranges [col, col+n): scale/n · (sigmoid(x) - y), y from the multi-hot labels (the event's entries)
+//   narrow  the 16-B chunks touching a SINGLE slice or any is-observed / regression / (in-row) TTE column: at most
+//           max_narrow<T>() chunks, staged in the wave's LDS slice (logits + f32 gradients)
+//   other   0
+// Pass 1 streams the row once in 16-B chunks (kEl elements per lane, 64·kEl columns per wave instruction, kB chunk
+// groups in flight): dense gradients, MULTI BCE sums, zeros; chunks of the narrow set go to LDS (logits, and their
+// MULTI / zero gradients) instead of HBM. Pass 2 computes the narrow terms (SINGLE softmax-CE + is-observed BCE,
+// Gaussian NLLs, TTE) from LDS — no dependent global round trips — and stores the narrow chunks. Per row: ldc·s
+// logits read + ldc·s gradients written, plus the event's entries. Same per-element formulas as content_term /
+// tte_term: gradients are bitwise those of the other two kernels; MULTI losses are summed in another order.
+constexpr int kMaxSeg = 4;       // MULTI ranges per level
+constexpr int kMaxRng = 8;       // narrow chunk ranges per level
+// narrow chunks per level: <= 4.5 KiB of LDS per wave (16 B of logits + kEl f32 gradients per chunk)
+template <typename T>
+constexpr int max_narrow() { return sizeof(T) == 4 ? 128 : 96; }
+constexpr int kMaxLevels = 8;
+
+struct StreamPlan {
+  int8_t nseg[kMaxLevels];             // MULTI terms of the level, in term order
+  int8_t seg[kMaxLevels][kMaxSeg];
+  int8_t nrng[kMaxLevels];             // narrow chunk ranges [lo, hi) of the level; slot = base + c - lo
+  int32_t lo[kMaxLevels][kMaxRng], hi[kMaxLevels][kMaxRng], base[kMaxLevels][kMaxRng];
+};
+
+template <typename T>
+__device__ __forceinline__ void unpack_chunk(const uint4& v, float (&x)[16 / sizeof(T)]) {
+  if constexpr (sizeof(T) == 4) {
+    x[0] = __uint_as_float(v.x), x[1] = __uint_as_float(v.y), x[2] = __uint_as_float(v.z), x[3] = __uint_as_float(v.w);
+  } else {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = __uint_as_float(w[i] << 16);
+      x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 pack_chunk(const float (&o)[16 / sizeof(T)]) {
+  if constexpr (sizeof(T) == 4) {
+    return make_uint4(__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3]));
+  } else {
+    uint32_t wd[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      wd[h] = (uint32_t)f32_to_bf16_bits(o[2 * h]) | ((uint32_t)f32_to_bf16_bits(o[2 * h + 1]) << 16);
+    return make_uint4(wd[0], wd[1], wd[2], wd[3]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms terms, StreamPlan plan,
+                                                           esgpt_tte_spec tte, const T* __restrict__ zc, int64_t ldc,
+                                                           int64_t n_levels, int shift, const T* __restrict__ zc_bias,
+                                                           const T* __restrict__ zt, int64_t ldt, T* __restrict__ dzc,
+                                                           T* __restrict__ dzt, float* __restrict__ dbias,
+                                                           const int32_t* __restrict__ counts, int n_ch,
+                                                           float* __restrict__ contrib, int64_t n_rows, int tte_in_row,
+                                                           int32_t* __restrict__ err) {
+  constexpr int kEl = 16 / sizeof(T);  // elements per 16-B chunk
+  constexpr int kB = 4;                // chunk groups (64 chunks each) in flight
+  __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
+  constexpr int kNarrow = max_narrow<T>();
+  __shared__ uint4 s_nz[4][kNarrow];        // narrow chunks: logits
+  __shared__ float s_ng[4][kNarrow * kEl];  // narrow chunks: f32 gradients
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = lane_id();
+  const int NT = terms.n;
+  const int64_t L = bt.L, M = bt.M;
+  const int nch = (int)(ldc / kEl);  // < 2^31 (checked on the host)
+  const T* nzT = reinterpret_cast<const T*>(s_nz[wave]);
+  float* ng = s_ng[wave];
+
+  if (wave == 0) subjects_with_events(counts, bt.B, n_ch, NT, lane, s_nsub_inv);
+  const int64_t w = (int64_t)blockIdx.x * 4 + wave;
+  const RowPos q = row_pos(bt, w, n_rows, shift);
+  const int64_t b = q.b, r = q.r, p = q.p;
+
+  int64_t e_idx = 0, e_meas = INT64_MIN;
+  float e_val = 0.f;
+  bool e_vm = false;
+  if (q.has_content && lane < M) {
+    const int64_t off = (b * L + p) * M + lane;
+    e_idx = bt.dyn_idx[off];
+    e_meas = bt.dyn_meas[off];
+    e_val = bt.dyn_vals[off];
+    e_vm = bt.dyn_vmask[off] != 0;
+  }
+  const int32_t my_cnt = subject_counts(counts, b, n_ch, NT, lane, q.active);
+  flag_no_tte(my_cnt, NT, q.active && q.r == -shift, err);
+  const bool tte_row = q.active && r >= 0;
+  const int64_t e = b * L + (r < 0 ? 0 : r);
+  const bool obs = tte_row && (r + 1 < L) && bt.event_mask[e] && bt.event_mask[e + 1];
+  const float x_tte = obs ? bt.time_delta[e] : 1.f;
+  __syncthreads();  // s_nsub_inv
+
+  float cvec = 0.f;  // lane t: term t's contribution (lane NT: the TTE log-likelihood's)
+  const int n_lv = !q.active ? 0 : shift ? 1 : (int)n_levels;
+  for (int lv = 0; lv < n_lv; ++lv) {
+    const T* zrow;
+    T* grow = nullptr;
+    float* frow = nullptr;
+    if (shift) {
+      if (r < 0) {
+        zrow = zc_bias;
+        frow = dbias + b * ldc;
+      } else {
+        zrow = zc + (b * L + r) * ldc;
+        grow = dzc + (b * L + r) * ldc;
+      }
+    } else {
+      const int64_t row = (b * L + p) * n_levels + lv;
+      zrow = zc + row * ldc;
+      grow = dzc + row * ldc;
+    }
+    const int nr = plan.nrng[lv];
+    // narrow slot of chunk c (-1: not narrow)
+    auto slot_of = [&](int c) {
+      int s = -1;
+      for (int k = 0; k < nr; ++k)
+        if (c >= plan.lo[lv][k] && c < plan.hi[lv][k]) s = plan.base[lv][k] + c - plan.lo[lv][k];
+      return s;
+    };
+
+    // ---------------- MULTI range parameters ----------------
+    const int nseg = plan.nseg[lv];
+    int labc[kMaxSeg];
+    float sn[kMaxSeg], sc[kMaxSeg], acc[kMaxSeg];
+#pragma unroll
+    for (int k = 0; k < kMaxSeg; ++k) {
+      labc[k] = -1, sn[k] = 0.f, sc[k] = 0.f, acc[k] = 0.f;
+      if (k < nseg && q.has_content) {
+        const int t = plan.seg[lv][k];
+        const esgpt_loss_term& tm = terms.t[t];
+        const int n = tm.vocab_end - tm.vocab_start;
+        const bool match = e_meas == tm.meas_idx;
+        const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
+        const float scale = (q.ev && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
+        sc[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(scale)));  // wave-uniform
+        sn[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(scale / (float)n)));
+        const int64_t my_lab = match ? e_idx - tm.vocab_start : -1;
+        labc[k] = (my_lab >= 0 && my_lab < n) ? tm.col + (int)my_lab : -1;
+      }
+    }
+
+    // ---------------- pass 1: stream the row ----------------
+    const uint4* zv = reinterpret_cast<const uint4*>(zrow);
+    for (int g0 = 0; g0 < nch; g0 += 64 * kB) {
+      uint4 v[kB];
+#pragma unroll
+      for (int i = 0; i < kB; ++i) {
+        const int c = g0 + 64 * i + lane;
+        v[i] = zv[c < nch ? c : nch - 1];  // unconditional: all kB loads in flight together
+      }
+#pragma unroll
+      for (int i = 0; i < kB; ++i) {
+        const int gb = g0 + 64 * i;  // wave-uniform
+        if (gb >= nch) break;
+        const int c = gb + lane;
+        const int glo = gb * kEl, ghi = (gb + 64) * kEl;
+        float o[kEl];
+#pragma unroll
+        for (int el = 0; el < kEl; ++el) o[el] = 0.f;
+#pragma unroll
+        for (int k = 0; k < kMaxSeg; ++k) {
+          if (k >= nseg || sn[k] == 0.f) continue;  // wave-uniform
+          const esgpt_loss_term& tm = terms.t[plan.seg[lv][k]];
+          const int lo = tm.col, hi = tm.col + tm.vocab_end - tm.vocab_start;
+          if (lo >= ghi || hi <= glo) continue;
+          float x[kEl];
+          unpack_chunk<T>(v[i], x);
+          uint32_t ym = 0;  // this lane's label bits
+          for (uint64_t bits = __ballot(labc[k] >= glo && labc[k] < ghi); bits; bits &= bits - 1) {
+            const int rel = __builtin_amdgcn_readlane(labc[k], __builtin_ctzll(bits)) - glo;
+            if (rel / kEl == lane) ym |= 1u << (rel % kEl);
+          }
+          const bool whole = lo <= glo && hi >= ghi;
+          float a = 0.f;
+#pragma unroll
+          for (int el = 0; el < kEl; ++el) {
+            const int col = c * kEl + el;
+            const float xx = x[el], yf = ((ym >> el) & 1u) ? 1.f : 0.f;
+            const float ex = __builtin_amdgcn_exp2f(-fabsf(xx) * 1.4426950408889634f);
+            const float ope = 1.f + ex;
+            const float l = fmaxf(xx, 0.f) - xx * yf + __builtin_amdgcn_logf(ope) * 0.6931471805599453f;
+            const float inv = __builtin_amdgcn_rcpf(ope);
+            const float g = sn[k] * ((xx >= 0.f ? inv : ex * inv) - yf);
+            const bool in = whole || (col >= lo && col < hi);
+            a += in ? l : 0.f;
+            o[el] = in ? g : o[el];
+          }
+          acc[k] += a;
+        }
+        int slot = -1;
+        for (int k = 0; k < nr; ++k)
+          if (plan.lo[lv][k] < gb + 64 && plan.hi[lv][k] > gb && c >= plan.lo[lv][k] && c < plan.hi[lv][k])
+            slot = plan.base[lv][k] + c - plan.lo[lv][k];
+        if (slot >= 0) {  // narrow chunk: logits and gradients so far to LDS, stored after pass 2
+          s_nz[wave][slot] = v[i];
+#pragma unroll
+          for (int el = 0; el < kEl; ++el) ng[slot * kEl + el] = o[el];
+        } else if (c < nch) {
+          if (frow) {
+#pragma unroll
+            for (int h = 0; h < kEl / 4; ++h)
+              reinterpret_cast<float4*>(frow)[c * (kEl / 4) + h] =
+                  make_float4(o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]);
+          } else {
+            reinterpret_cast<uint4*>(grow)[c] = pack_chunk<T>(o);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxSeg; ++k) {
+      if (k >= nseg) continue;
+      const int t = plan.seg[lv][k];
+      const int n = terms.t[t].vocab_end - terms.t[t].vocab_start;
+      const float ell = wave_sum(acc[k]) / (float)n;
+      if (lane == t) cvec = sc[k] * ell;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---------------- pass 2: the narrow terms, from LDS ----------------
+    auto nz = [&](int col) { return to_f32(nzT[slot_of(col / kEl) * kEl + col % kEl]); };
+    auto put = [&](int col, float g) { ng[slot_of(col / kEl) * kEl + col % kEl] = g; };
+    for (int t = 0; t < NT && q.has_content; ++t) {
+      const esgpt_loss_term& tm = terms.t[t];
+      if (tm.kind == ESGPT_TERM_MULTI) continue;
+      if (!shift && tm.level != lv) continue;  // wave-uniform
+      const bool match = e_meas == tm.meas_idx;
+      const uint64_t mm = __ballot(match), mv = __ballot(match && e_vm);
+      const bool mk = q.ev && (tm.kind == ESGPT_TERM_SINGLE ? mm != 0 : mv != 0);
+      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
+      const float scale = (mk && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
+      if (scale == 0.f) continue;  // contribution 0, gradients 0 (already in LDS)
+      const float ell =
+          content_term(tm, lane, M, match, mm, mv, e_idx, e_val, e_vm, mk, scale, err, nz, put);
+      if (lane == t) cvec = scale * ell;
+    }
+    if (tte_in_row && lv == 0 && tte_row) {
+      const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
+      const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;
+      const float ll = tte_term(
+          tte, lane, x_tte, scale, [&](int k) { return nz(tte.col + k); }, [&](int k, float g) { put(tte.col + k, g); });
+      if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
+      if (lane == NT) cvec = obs ? -scale * ll : 0.f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // ---- the narrow chunks ----
+    for (int k = 0; k < nr; ++k) {
+      const int lo = plan.lo[lv][k], n = plan.hi[lv][k] - lo, base = plan.base[lv][k];
+      for (int j = lane; j < n; j += 64) {
+        float o[kEl];
+#pragma unroll
+        for (int el = 0; el < kEl; ++el) o[el] = ng[(base + j) * kEl + el];
+        if (frow) {
+#pragma unroll
+          for (int h = 0; h < kEl / 4; ++h)
+            reinterpret_cast<float4*>(frow)[(lo + j) * (kEl / 4) + h] =
+                make_float4(o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]);
+        } else {
+          reinterpret_cast<uint4*>(grow)[lo + j] = pack_chunk<T>(o);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the LDS slice is rewritten by the next level
+  }
+
+  // ---- time-to-event into a separate dzt (NA) ----
+  if (q.active && !tte_in_row && tte_row) {
+    const T* z = zt + e * ldt + tte.col;
+    T* gz = dzt + e * ldt + tte.col;
+    const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
+    const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;
+    const float ll = tte_term(
+        tte, lane, x_tte, scale, [&](int k) { return to_f32(z[k]); },
+        [&](int k, float g) { gz[k] = from_f32<T>(g); });
+    if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
+    if (lane == NT) cvec = obs ? -scale * ll : 0.f;
+  }
+  // the workgroup's contributions: rows in order, summed in a fixed order (deterministic)
+  __shared__ float s_part[4][ESGPT_MAX_TERMS + 1];
+  if (lane <= NT) s_part[wave][lane] = cvec;
+  __syncthreads();
+  if (wave == 0 && lane <= NT)
+    contrib[(int64_t)lane * gridDim.x + blockIdx.x] =
+        ((s_part[0][lane] + s_part[1][lane]) + s_part[2][lane]) + s_part[3][lane];
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Deterministic sums of the per-row contributions: thread i sums rows i, i + 1024, ... of each term, then wave sums
 // and a fixed-order sum over the 16 waves. The next term's loads are issued before the current term is summed (one
 // memory round trip for the whole launch instead of one per term at n_rows <= 8192).
@@ -685,11 +1013,55 @@ bool disjoint_columns(const esgpt_loss_term* terms, int n_terms, int shift) {
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 constexpr int64_t kLdsBudget = 64 * 1024;  // row-staged event kernel: LDS bytes per block
+constexpr int kCountChunk = 128;           // events per count_kernel workgroup
 
-// ESGPT_LOSS_ROW_STAGE=0 forces the generic (column-by-column) event kernel (parity tests of both paths).
-bool row_stage_enabled() {
-  const char* e = getenv("ESGPT_LOSS_ROW_STAGE");
-  return !(e && e[0] == '0');
+// The streaming kernel's plan per level: MULTI terms as dense ranges (<= kMaxSeg); the 16-B chunks touching any other
+// term column (SINGLE slices, is-observed, regression, in-row TTE) as merged chunk ranges (<= kMaxRng ranges,
+// <= max_narrow<T>() chunks). False when the layout does not fit it (the caller takes another kernel).
+bool stream_plan(const esgpt_loss_term* terms, int n_terms, int64_t n_levels, int shift, int64_t ldc, int64_t kEl,
+                 const esgpt_tte_spec& tte, bool tte_in_row, StreamPlan& plan) {
+  const int64_t max_slots = kEl == 4 ? max_narrow<float>() : max_narrow<bf16>();
+  const int64_t nl = shift ? 1 : n_levels;
+  if (nl < 1 || nl > kMaxLevels || ldc / kEl >= (1ll << 30)) return false;
+  plan = StreamPlan{};
+  for (int lv = 0; lv < nl; ++lv) {
+    std::vector<std::pair<int64_t, int64_t>> cols;  // narrow column ranges [a, b)
+    for (int i = 0; i < n_terms; ++i) {
+      const esgpt_loss_term& t = terms[i];
+      if ((shift ? 0 : t.level) != lv) continue;
+      const int64_t n = t.vocab_end - t.vocab_start;
+      if (t.kind == ESGPT_TERM_MULTI) {
+        if (plan.nseg[lv] >= kMaxSeg) return false;
+        plan.seg[lv][plan.nseg[lv]++] = (int8_t)i;
+        continue;
+      }
+      const int64_t w = t.kind == ESGPT_TERM_MVREG ? 2 * n : t.kind == ESGPT_TERM_UVREG ? 2 : n;
+      cols.push_back({t.col, t.col + w});
+      if (t.kind == ESGPT_TERM_SINGLE || t.kind == ESGPT_TERM_UVREG) cols.push_back({t.obs_col, t.obs_col + 1});
+    }
+    if (tte_in_row && lv == 0) cols.push_back({tte.col, tte.col + (tte.kind == ESGPT_TTE_EXP ? 1 : 3 * tte.K)});
+    std::vector<std::pair<int64_t, int64_t>> ch;  // chunk ranges, merged
+    for (auto& c : cols) {
+      if (c.first < 0 || c.second > ldc || c.first >= c.second) return false;
+      ch.push_back({c.first / kEl, (c.second + kEl - 1) / kEl});
+    }
+    std::sort(ch.begin(), ch.end());
+    std::vector<std::pair<int64_t, int64_t>> merged;
+    for (auto& c : ch) {
+      if (!merged.empty() && c.first <= merged.back().second) merged.back().second = std::max(merged.back().second, c.second);
+      else merged.push_back(c);
+    }
+    if ((int)merged.size() > kMaxRng) return false;
+    int64_t slots = 0;
+    for (size_t k = 0; k < merged.size(); ++k) {
+      plan.lo[lv][k] = (int32_t)merged[k].first, plan.hi[lv][k] = (int32_t)merged[k].second;
+      plan.base[lv][k] = (int32_t)slots;
+      slots += merged[k].second - merged[k].first;
+    }
+    if (slots > max_slots) return false;
+    plan.nrng[lv] = (int8_t)merged.size();
+  }
+  return true;
 }
 
 }  // namespace
@@ -698,19 +1070,21 @@ extern "C" {
 
 size_t esgpt_output_loss_workspace(int64_t B, int64_t L, int n_terms) {
   const int64_t n_rows = B * (L + 1);
-  return align_up(sizeof(int32_t) * B * (ESGPT_MAX_TERMS + 1)) + align_up(sizeof(float) * n_rows * (n_terms + 1));
+  return align_up(sizeof(int32_t) * B * cdiv(L, kCountChunk) * (ESGPT_MAX_TERMS + 1)) +
+         align_up(sizeof(float) * n_rows * (n_terms + 1));
 }
 
-int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int64_t n_levels, int shift,
-                      const void* zc_bias, const void* zt, int64_t ldt, int dtype, const esgpt_loss_term* terms,
-                      int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
-                      void* workspace, size_t workspace_bytes, int32_t* err, void* stream) {
+int esgpt_output_loss_ex(const esgpt_batch* batch, const void* zc, int64_t ldc, int64_t n_levels, int shift,
+                         const void* zc_bias, const void* zt, int64_t ldt, int dtype, const esgpt_loss_term* terms,
+                         int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
+                         void* workspace, size_t workspace_bytes, int32_t* err, int path, void* stream) {
   ESGPT_REQUIRE(batch && zt && dzt && tte && losses && workspace);
   ESGPT_REQUIRE(n_terms >= 0 && n_terms <= ESGPT_MAX_TERMS);
   ESGPT_REQUIRE(n_terms == 0 || (zc && dzc));
   ESGPT_REQUIRE(!shift || (zc_bias && dbias && n_levels == 1));
   ESGPT_REQUIRE(batch->M <= kMaxM && (tte->kind == ESGPT_TTE_EXP || (tte->kind == ESGPT_TTE_LNM && tte->K <= kMaxK)));
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  ESGPT_REQUIRE(path >= ESGPT_LOSS_PATH_AUTO && path <= ESGPT_LOSS_PATH_GENERIC);
   ESGPT_REQUIRE(workspace_bytes >= esgpt_output_loss_workspace(batch->B, batch->L, n_terms));
   ESGPT_REQUIRE(batch->L <= 16384 && batch->L * batch->M < (1ll << 31));  // count_kernel: LDS word per event
   const int64_t B = batch->B, L = batch->L;
@@ -719,48 +1093,73 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
   Terms T{};
   T.n = n_terms;
   for (int i = 0; i < n_terms; ++i) T.t[i] = terms[i];
+  const int n_ch = (int)cdiv(L, kCountChunk);
   int32_t* counts = (int32_t*)workspace;
-  float* contrib = (float*)((char*)workspace + align_up(sizeof(int32_t) * B * (ESGPT_MAX_TERMS + 1)));
+  float* contrib = (float*)((char*)workspace + align_up(sizeof(int32_t) * B * n_ch * (ESGPT_MAX_TERMS + 1)));
   const size_t esz = dtype == ESGPT_F32 ? 4 : 2;
   const int64_t n_rows = B * (L + shift);
-  // Row-staged kernel when a row fits: 16-B aligned rows, LDS (logits + f32 gradients) for >= 1 wave per block
-  // within kLdsBudget; waves per block = as many as fit (<= 4).
+  // Whole-row kernels (streaming, row-staged) need 16-B aligned rows, disjoint term columns, and the TTE columns
+  // either inside the content row (CI head: handled with the row) or in a separate dzt — a dzt aliasing dzc any
+  // other way would race the full-row stores.
   const int64_t kEl = 16 / (int64_t)esz;
-  const int64_t per_wave = ldc * (int64_t)(esz + 4);
   const bool aligned = n_terms > 0 && ldc % kEl == 0 && (uintptr_t)zc % 16 == 0 && (uintptr_t)dzc % 16 == 0 &&
                        (!shift || ((uintptr_t)zc_bias % 16 == 0 && (uintptr_t)dbias % 16 == 0));
-  // TTE columns inside the content row (CI head): handled in LDS with the row. A dzt aliasing dzc any other way
-  // would race the full-row stores, so it takes the generic kernel.
   const bool same_row = zt == zc && dzt == dzc && ldt == ldc && n_levels == 1;
-  const bool staged = aligned && per_wave <= kLdsBudget && (dzt != dzc || same_row) && row_stage_enabled();
-  const bool tte_in_row = staged && same_row;
-  if (!staged) {
+  const bool whole_row = aligned && (dzt != dzc || same_row) && disjoint_columns(terms, n_terms, shift);
+  StreamPlan plan;
+  const bool can_stream = whole_row && stream_plan(terms, n_terms, n_levels, shift, ldc, kEl, *tte, same_row, plan);
+  const int64_t per_wave = ldc * (int64_t)(esz + 4);  // row-staged: logits + f32 gradients in LDS
+  const bool can_stage = aligned && per_wave <= kLdsBudget && (dzt != dzc || same_row);
+  int use = path;
+  if (use == ESGPT_LOSS_PATH_AUTO) use = can_stream ? ESGPT_LOSS_PATH_STREAM : can_stage ? ESGPT_LOSS_PATH_ROW_STAGED
+                                                                                          : ESGPT_LOSS_PATH_GENERIC;
+  if ((use == ESGPT_LOSS_PATH_STREAM && !can_stream) || (use == ESGPT_LOSS_PATH_ROW_STAGED && !can_stage))
+    return ESGPT_ERR_UNSUPPORTED;
+  const bool whole = use != ESGPT_LOSS_PATH_GENERIC;
+  const bool tte_in_row = whole && same_row;
+  if (!whole) {
     if (n_terms > 0 && zero_async(dzc, esz * B * L * n_levels * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
     if (shift && zero_async(dbias, sizeof(float) * B * ldc, st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   }
-  if (!tte_in_row && (dzt != dzc || n_terms == 0 || staged) &&
-      zero_async(dzt, esz * B * L * ldt, st) != hipSuccess)
+  if (!tte_in_row && (dzt != dzc || n_terms == 0 || whole) && zero_async(dzt, esz * B * L * ldt, st) != hipSuccess)
     return ESGPT_ERR_LAUNCH;
-  count_kernel<<<(unsigned)B, 1024, sizeof(uint32_t) * L, st>>>(*batch, T, counts, err);
-  if (staged) {
+  count_kernel<<<dim3((unsigned)n_ch, (unsigned)B), 1024, sizeof(uint32_t) * kCountChunk, st>>>(*batch, T, kCountChunk,
+                                                                                           counts);
+  int64_t n_items = n_rows;  // contributions per term (rows, or workgroups of the streaming kernel)
+  if (use == ESGPT_LOSS_PATH_STREAM) {
+    const unsigned grid = (unsigned)cdiv(n_rows, 4);
+    n_items = grid;
+    if (dtype == ESGPT_F32)
+      event_stream_kernel<float><<<grid, 256, 0, st>>>(*batch, T, plan, *tte, (const float*)zc, ldc, n_levels, shift,
+                                                       (const float*)zc_bias, (const float*)zt, ldt, (float*)dzc,
+                                                       (float*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
+                                                       err);
+    else
+      event_stream_kernel<bf16><<<grid, 256, 0, st>>>(*batch, T, plan, *tte, (const bf16*)zc, ldc, n_levels, shift,
+                                                      (const bf16*)zc_bias, (const bf16*)zt, ldt, (bf16*)dzc,
+                                                      (bf16*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
+                                                      err);
+  } else if (use == ESGPT_LOSS_PATH_ROW_STAGED) {
     const int wpb = (int)std::min<int64_t>(kWaves, kLdsBudget / per_wave);
     const unsigned grid = (unsigned)cdiv(n_rows, wpb);
     const size_t lds = (size_t)wpb * per_wave;
     if (dtype == ESGPT_F32)
       event_lds_kernel<float><<<grid, 64 * wpb, lds, st>>>(*batch, T, *tte, (const float*)zc, ldc, n_levels, shift,
                                                           (const float*)zc_bias, (const float*)zt, ldt, (float*)dzc,
-                                                          (float*)dzt, dbias, counts, contrib, n_rows, tte_in_row, err);
+                                                          (float*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
+                                                          err);
     else
       event_lds_kernel<bf16><<<grid, 64 * wpb, lds, st>>>(*batch, T, *tte, (const bf16*)zc, ldc, n_levels, shift,
                                                          (const bf16*)zc_bias, (const bf16*)zt, ldt, (bf16*)dzc,
-                                                         (bf16*)dzt, dbias, counts, contrib, n_rows, tte_in_row, err);
+                                                         (bf16*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
+                                                         err);
   } else {
     const unsigned grid = (unsigned)cdiv(n_rows, kWaves);
     const bool rmw = !disjoint_columns(terms, n_terms, shift);
 #define LAUNCH_EV(TT, RMW)                                                                                        \
   event_kernel<TT, RMW><<<grid, 256, 0, st>>>(*batch, T, *tte, (const TT*)zc, ldc, n_levels, shift,               \
                                               (const TT*)zc_bias, (const TT*)zt, ldt, (TT*)dzc, (TT*)dzt, dbias,  \
-                                              counts, contrib, n_rows, err)
+                                              counts, n_ch, contrib, n_rows, err)
     if (dtype == ESGPT_F32) {
       if (rmw) LAUNCH_EV(float, true); else LAUNCH_EV(float, false);
     } else {
@@ -768,9 +1167,17 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
     }
 #undef LAUNCH_EV
   }
-  reduce_kernel<<<1, 1024, 0, st>>>(contrib, n_rows, n_terms, losses);
+  reduce_kernel<<<1, 1024, 0, st>>>(contrib, n_items, n_terms, losses);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
+}
+
+int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int64_t n_levels, int shift,
+                      const void* zc_bias, const void* zt, int64_t ldt, int dtype, const esgpt_loss_term* terms,
+                      int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
+                      void* workspace, size_t workspace_bytes, int32_t* err, void* stream) {
+  return esgpt_output_loss_ex(batch, zc, ldc, n_levels, shift, zc_bias, zt, ldt, dtype, terms, n_terms, tte, dzc, dzt,
+                              dbias, losses, workspace, workspace_bytes, err, ESGPT_LOSS_PATH_AUTO, stream);
 }
 
 }  // extern "C"

@@ -133,10 +133,13 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
 
 // bank[i] = counter + i (i < slots), then counter += slots: one block (every thread reads the counter before the
 // barrier; thread 0 advances it after).
+// With `err` (the step's error block, 16 bytes) it is zeroed by the same launch: each training step's flags (and its
+// AdamW no-op) are its own.
 __global__ __launch_bounds__(256) void seed_bank_kernel(int64_t* __restrict__ counter, int64_t* __restrict__ bank,
-                                                        int64_t slots) {
+                                                        int64_t slots, int64_t* __restrict__ err) {
   const int64_t c = *counter;
   for (int64_t i = threadIdx.x; i < slots; i += blockDim.x) bank[i] = c + i;
+  if (err && threadIdx.x < 2) err[threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) *counter = c + slots;
 }
@@ -146,8 +149,13 @@ __global__ __launch_bounds__(256) void seed_bank_kernel(int64_t* __restrict__ co
 extern "C" {
 
 int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream) {
-  ESGPT_REQUIRE(counter && bank && slots > 0);
-  esgpt::seed_bank_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counter, bank, slots);
+  return esgpt_step_begin(counter, bank, slots, nullptr, stream);
+}
+
+int esgpt_step_begin(int64_t* counter, int64_t* bank, int64_t slots, int32_t* err, void* stream) {
+  ESGPT_REQUIRE(counter && bank && slots > 0 && (uintptr_t)err % 8 == 0);
+  esgpt::seed_bank_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counter, bank, slots,
+                                                                   reinterpret_cast<int64_t*>(err));
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

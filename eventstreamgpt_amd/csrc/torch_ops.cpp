@@ -282,7 +282,7 @@ std::vector<esgpt_loss_term> make_terms(at::IntArrayRef t) {
 std::tuple<Tensor, Tensor, Tensor, Tensor> output_loss(const Tensor& zc_, const optional<Tensor>& zt_,
                                                        const optional<Tensor>& zc_bias, BATCH_ARGS, int64_t n_levels,
                                                        int64_t shift, at::IntArrayRef terms, at::IntArrayRef tte_i,
-                                                       at::ArrayRef<double> tte_f, const Tensor& err) {
+                                                       at::ArrayRef<double> tte_f, const Tensor& err, int64_t path) {
   const c10::DeviceGuard guard(zc_.device());
   Batch bt = make_batch(BATCH_PASS);
   Tensor zc = zc_.contiguous();
@@ -300,10 +300,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> output_loss(const Tensor& zc_, const 
   Tensor losses = at::empty({n_terms + 2}, zc.options().dtype(at::kFloat));
   const size_t nb = esgpt_output_loss_workspace(bt.b.B, bt.b.L, n_terms);
   Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, zc.options().dtype(at::kByte));
-  check(esgpt_output_loss(&bt.b, zc.data_ptr(), ldc, n_levels, (int)shift, bias.defined() ? bias.data_ptr() : nullptr,
-                          zt.data_ptr(), zt.size(-1), dtype_code(zc.scalar_type()), tv.data(), n_terms, &tte,
-                          dzc.data_ptr(), same ? dzc.data_ptr() : dzt.data_ptr(), shift ? ptr<float>(dbias) : nullptr,
-                          ptr<float>(losses), ws.data_ptr(), nb, ptr<int32_t>(err), stream_of(zc)),
+  check(esgpt_output_loss_ex(&bt.b, zc.data_ptr(), ldc, n_levels, (int)shift,
+                             bias.defined() ? bias.data_ptr() : nullptr, zt.data_ptr(), zt.size(-1),
+                             dtype_code(zc.scalar_type()), tv.data(), n_terms, &tte, dzc.data_ptr(),
+                             same ? dzc.data_ptr() : dzt.data_ptr(), shift ? ptr<float>(dbias) : nullptr,
+                             ptr<float>(losses), ws.data_ptr(), nb, ptr<int32_t>(err), (int)path, stream_of(zc)),
         "output_loss");
   return {losses, dzc, dzt, dbias};
 }
@@ -502,12 +503,17 @@ c10::hip::HIPStream weight_grad_stream(c10::DeviceIndex dev) {
 }
 
 // bank[i] = counter + i, counter += bank.numel() (one launch; both int64 device tensors, updated in place)
-void seed_bank(const Tensor& counter, const Tensor& bank) {
+// With err: the step's error block is zeroed by the same launch (esgpt_step_begin).
+void seed_bank(const Tensor& counter, const Tensor& bank, const optional<Tensor>& err) {
   const c10::DeviceGuard guard(counter.device());
   TORCH_CHECK(counter.scalar_type() == at::kLong && bank.scalar_type() == at::kLong && counter.numel() == 1 &&
                   bank.is_contiguous() && counter.is_cuda() && bank.is_cuda(),
               "seed_bank: int64 device counter [1] and contiguous int64 bank");
-  check(esgpt_seed_bank(ptr<int64_t>(counter), ptr<int64_t>(bank), bank.numel(), stream_of(counter)), "seed_bank");
+  const bool has_err = err.has_value() && err->defined();
+  TORCH_CHECK(!has_err || (err->is_cuda() && err->nbytes() >= 16 && err->is_contiguous()), "seed_bank: error block");
+  check(esgpt_step_begin(ptr<int64_t>(counter), ptr<int64_t>(bank), bank.numel(),
+                         has_err ? reinterpret_cast<int32_t*>(err->data_ptr()) : nullptr, stream_of(counter)),
+        "seed_bank");
 }
 
 // The current stream waits for every weight-gradient launch queued so far (before dW / db are read).
@@ -632,7 +638,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> head_loss(const Tensor& xc, const opt
   if (wt.has_value() && wt->defined()) zt = linear(*xt, *wt, bt, {}, tickets);
   optional<Tensor> zb;  // the head bias in the logits' dtype: position 0 reads Linear(zeros) = bias
   if (shift) zb = (zb_in.has_value() && zb_in->defined()) ? *zb_in : bc.to(at::kBFloat16);
-  return output_loss(zc, zt, zb, BATCH_PASS, n_levels, shift, terms, tte_i, tte_f, err);
+  return output_loss(zc, zt, zb, BATCH_PASS, n_levels, shift, terms, tte_i, tte_f, err, ESGPT_LOSS_PATH_AUTO);
 }
 
 // ---- parameter packing -----------------------------------------------------------------------------------------
@@ -704,7 +710,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("attn_decode(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor? key_mask, Tensor? query_mask, int H, "
         "int Lk, int window) -> Tensor");
   m.def("output_loss(Tensor zc, Tensor? zt, Tensor? zc_bias, " BATCH_SCHEMA ", int n_levels, int shift, int[] terms, "
-        "int[] tte_i, float[] tte_f, Tensor err) -> (Tensor, Tensor, Tensor, Tensor)");
+        "int[] tte_i, float[] tte_f, Tensor err, int path=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("residual_ln(Tensor? x, Tensor? y, Tensor? bias, Tensor ln_w, Tensor ln_b, Tensor? row_mask, float p, "
         "Tensor? seed, float eps, ScalarType out_dtype) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("residual_ln_bwd(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, Tensor? row_mask, "
@@ -721,7 +727,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
         "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None) -> (Tensor, Tensor, Tensor)");
   m.def("weight_grad_join(Tensor like) -> ()");
-  m.def("seed_bank(Tensor(a!) counter, Tensor(b!) bank) -> ()");
+  m.def("seed_bank(Tensor(a!) counter, Tensor(b!) bank, Tensor(c!)? err=None) -> ()");
   m.def("residual_ln_bwd_partials(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, "
         "Tensor? row_mask, float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, "
         "ScalarType out_dtype) -> (Tensor, Tensor, Tensor)");

@@ -388,18 +388,19 @@ def _seed_counter(device: torch.device) -> torch.Tensor:
     return c
 
 
-def begin_dropout_step(device: torch.device) -> None:
+def begin_dropout_step(device: torch.device, reset_errors: bool = False) -> None:
     """Refreshes the per-step seed bank on the stream (one small kernel per training step): slot i of the bank
     = counter + i, then counter += slots. Until the next call, ``next_dropout_seed`` hands out slots of the bank
     (no kernel per dropout site); under HIP-graph capture the refresh is part of the graph, so every replay draws
-    fresh masks. Without a bank (eager use outside a step) every call clones and advances the counter."""
+    fresh masks. Without a bank (eager use outside a step) every call clones and advances the counter.
+    ``reset_errors``: the same launch zeroes the device error block (a training step's flags are its own)."""
     idx = device.index if device.index is not None else torch.cuda.current_device()
     c = _seed_counter(device)
     bank = _BANKS.get(idx)
     if bank is None:
         bank = {"buf": torch.empty(SEED_BANK_SLOTS, dtype=torch.int64, device=device), "next": 0}
         _BANKS[idx] = bank
-    _ops().seed_bank(c, bank["buf"])  # one launch: buf = c + arange, c += slots
+    _ops().seed_bank(c, bank["buf"], err_word(device) if reset_errors else None)  # one launch
     bank["next"] = 0
 
 

@@ -149,7 +149,7 @@ def _register():
         return zc.new_empty(n_terms + 2, dtype=f32), torch.empty_like(zc), dzt, dbias
 
     @fake(lib + "output_loss")
-    def _(zc, zt, zc_bias, em, td, tm, di, dm, dv, dvm, si, sm, n_levels, shift, terms, tte_i, tte_f, err):
+    def _(zc, zt, zc_bias, em, td, tm, di, dm, dv, dvm, si, sm, n_levels, shift, terms, tte_i, tte_f, err, path=0):
         return _loss_fake(zc, zt, shift, len(terms) // 8, di.shape[0])
 
     @fake(lib + "head_loss")
@@ -204,7 +204,7 @@ def _register():
         return None
 
     @fake(lib + "seed_bank")
-    def _(counter, bank):
+    def _(counter, bank, err=None):
         return None
 
     @fake(lib + "residual_ln_bwd_partials")
@@ -429,12 +429,12 @@ def _register():
 
     def _ol_bwd(ctx, g, *_):
         if g is None:
-            return (None,) * 18
+            return (None,) * 19
         dzc, dzt, dbias = ctx.saved_tensors
         has_zt, has_bias = ctx.meta
         gt = g[-1]
         d_bias = (dbias.sum(0) * gt).to(dzc.dtype) if (has_bias and dbias.numel()) else None
-        return ((dzc * gt.to(dzc.dtype)), (dzt * gt.to(dzt.dtype)) if has_zt else None, d_bias) + (None,) * 15
+        return ((dzc * gt.to(dzc.dtype)), (dzt * gt.to(dzt.dtype)) if has_zt else None, d_bias) + (None,) * 16
 
     reg(lib + "output_loss", _ol_bwd, setup_context=_ol_setup)
 

@@ -7,20 +7,27 @@
   hands each parameter its gradient without an accumulate-add; parameters without a gradient are skipped by
   AdamW exactly as in the reference;
 * data-dependent errors (bad embedding index, NaN TTE log-likelihood, subject without an observed TTE) are raised
-  with the reference's exception type and message. The kernels flag them in a device error block; the AdamW kernel
-  skips its update while a flag is set (the reference raises before its optimizer step, so the parameters stay at
-  their pre-error values), and ``step`` raises the error of step k at the latest when step k + 2 is submitted (the
-  host never waits for the step it just queued), ``check()`` at once;
+  with the reference's exception type and message. The kernels flag them in a device error block that the step's
+  first launch zeroes (each step's flags are its own); the AdamW kernel skips its update while a flag is set (the
+  reference raises before its optimizer step, so the parameters stay at their pre-error values), and ``step``
+  raises the error of step k at the latest when step k + 2 is submitted (the host never waits for the step it just
+  queued), ``check()`` at once. The failing step's AdamW and LR-schedule counters are rolled back when it is
+  raised; a step submitted after it (k + 1) has already run with counters one ahead;
 * data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Every ``param.grad`` ends
-  the step as a view into one flat f32 buffer laid out last-layer-first and cut into ~25 MB buckets; a bucket is
-  all-reduced (average) in place as soon as backward has produced all of its gradients (post-accumulate-grad hooks),
-  so the exchange overlaps the rest of backward (SURVEY.md §8e);
+  the step as a view into one flat f32 buffer laid out last-layer-first and cut into buckets; every step issues
+  exactly one all-reduce (average) per bucket, in bucket-index order on every rank, whichever path (eager, graph
+  capture, graph replay) the rank takes. A bucket is launched as soon as backward has produced its gradients and
+  those of every lower-index bucket, so the exchange overlaps the rest of backward. Under HIP
+  graphs the captured step is split at those points into segment graphs; each segment's buckets are exchanged
+  while the next segment replays;
 * the LayerNorm backwards' column sums (d ln_w, d ln_b) of a whole backward pass in one launch (``defer_colsums``);
 * optionally (``overlap_weight_grads``) the projections' weight / bias gradients run on a second stream (joined
   before the exchange and AdamW), off backward's critical path;
 * optional HIP-graph capture of forward+backward, one graph per batch shape signature (static shapes; batches are
   copied into the graph's static buffers). A batch whose signature matches no captured graph is captured (up to
-  ``max_graphs``) or run eagerly — never broadcast into the wrong buffers.
+  ``max_graphs``) or run eagerly — never broadcast into the wrong buffers. A signature whose warm-up pass runs any
+  ATen GEMM (a module-by-module fallback through PyTorch-ROCm BLAS, e.g. a token count the fused blocks do not
+  take) is never captured: it runs eagerly.
 """
 from __future__ import annotations
 
@@ -157,11 +164,17 @@ def graph_safe(model, compute_dtype=torch.bfloat16) -> bool:
 class GradBuckets:
     """DDP gradient exchange: one flat f32 buffer holding every trainable parameter's gradient, laid out in reverse
     registration order (the last layers' gradients are produced first in backward) and cut into buckets of
-    ~``bucket_mb``. A post-accumulate-grad hook counts each bucket's gradients; when the last one arrives the
-    bucket's gradients that are not already views of the buffer are copied in (one multi-tensor copy), ``p.grad`` is
-    re-pointed at its view, and the bucket is all-reduced in place (average) asynchronously, overlapping the rest
-    of backward. ``finish()`` zero-fills and reduces buckets whose parameters got no gradient, waits for every
-    exchange on the current stream, and leaves every ``param.grad`` a view of the buffer (what FusedAdamW reads)."""
+    ~``bucket_mb``. A post-accumulate-grad hook counts each bucket's gradients; buckets are released strictly in
+    index order — bucket b once it and every bucket below it are complete — so every rank issues the same collective
+    sequence. What a release does depends on ``mode``:
+      "launch"  the bucket's gradients that are not already views of the buffer are copied in (one multi-tensor
+                copy), ``p.grad`` is re-pointed at its view, and the bucket is all-reduced in place (average)
+                asynchronously, overlapping the rest of backward;
+      "mark"    (HIP-graph capture) ``on_boundary(buckets)`` is called instead: the capture is cut there;
+      "off"     nothing (graph warm-up passes: no collectives).
+    ``finish()`` launches the buckets not yet launched (zero-filling gradients that were never produced), in index
+    order, waits for every exchange on the current stream, and leaves every ``param.grad`` a view of the buffer
+    (what FusedAdamW reads)."""
 
     def __init__(self, params: list, world: int, bucket_mb: float = 25.0):
         self.params = params
@@ -187,9 +200,9 @@ class GradBuckets:
         for b, (idx, _, _) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
-        self._ready = [0] * len(self.buckets)
-        self._launched = [False] * len(self.buckets)
-        self._works = []
+        self.mode = "launch"
+        self.on_boundary = None
+        self.reset()
         self._hooks = [params[i].register_post_accumulate_grad_hook(self._make_hook(i)) for i in range(len(params))]
 
     def _make_hook(self, i: int):
@@ -197,13 +210,29 @@ class GradBuckets:
             b = self.bucket_of[i]
             self._ready[b] += 1
             if self._ready[b] == len(self.buckets[b][0]):
-                self._launch(b)
+                self._complete[b] = True
+                self._release()
 
         return hook
 
+    def _release(self):
+        newly = []
+        while self._next < len(self.buckets) and self._complete[self._next]:
+            newly.append(self._next)
+            self._next += 1
+        if not newly:
+            return
+        if self.mode == "launch":
+            for b in newly:
+                self._launch(b)
+        elif self.mode == "mark":
+            self.on_boundary(newly)
+
     def reset(self):
         self._ready = [0] * len(self.buckets)
+        self._complete = [False] * len(self.buckets)
         self._launched = [False] * len(self.buckets)
+        self._next = 0
         self._works = []
 
     def _launch(self, b: int):
@@ -242,6 +271,22 @@ class GradBuckets:
         self.reset()
 
 
+class _GemmSpy(torch.utils._python_dispatch.TorchDispatchMode):
+    """Records whether any ATen GEMM runs (forward or backward: the mode follows autograd into its worker threads)
+    — i.e. whether a step left the HIP kernels for a PyTorch-ROCm BLAS fallback."""
+    GEMMS = ("mm", "addmm", "bmm", "baddbmm", "matmul", "linear", "_addmm_activation", "addbmm", "_scaled_mm")
+
+    def __init__(self):
+        super().__init__()
+        self.hits = set()
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        name = func.__name__.split(".")[0]
+        if func.namespace == "aten" and name in self.GEMMS:  # torch.ops.esgpt.linear / gemm are ours
+            self.hits.add(name)
+        return func(*args, **(kwargs or {}))
+
+
 class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
@@ -270,7 +315,8 @@ class TrainStep:
         # paths (tools/na_graph_*.py).
         self.use_graph = use_graph and (_force_graph or graph_safe(model, compute_dtype))
         self.max_graphs = max_graphs
-        self.graphs: dict = {}  # shape signature -> (graph, static batch, static loss)
+        self.graphs: dict = {}  # shape signature -> (segments, static batch, static loss, grads) | None (eager)
+        self.capture_report: dict = {}  # shape signature -> ATen GEMMs seen in its warm-up pass
         self.check_errors = check_errors and dev.type == "cuda"
         # projection weight gradients on a second stream beside the rest of backward (kernels.weight_grad_overlap).
         # Off by default: measured on the C2 step (HIP graph) it gains nothing — the graph executor starts the side
@@ -314,7 +360,7 @@ class TrainStep:
     def _fwd_bwd(self, batch: PytorchBatch, autocast_cache: bool = True):
         dev = self.device
         if dev.type == "cuda":
-            begin_dropout_step(dev)
+            begin_dropout_step(dev, reset_errors=True)  # this step's error flags start clear
         # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
         with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32, cache_enabled=autocast_cache):
             out = self.model(batch)
@@ -326,45 +372,86 @@ class TrainStep:
         return out.loss.detach()
 
     def _capture(self, batch: PytorchBatch):
+        """Captures this batch signature's step (forward + backward) as HIP graph segments, or records that it
+        runs eagerly (None). Two warm-up passes on a side stream first (allocator / lazy init; no collectives); the
+        first runs under _GemmSpy: a signature whose step reaches an ATen GEMM is not captured. Under DDP the
+        capture is cut wherever GradBuckets releases buckets, so each segment's buckets can be exchanged while the
+        next segment replays."""
+        if self.check_errors:
+            self._raise_pending(keep=0)  # earlier steps' errors are theirs, not this batch's
+        sig = batch.shape_signature()
         static = batch.packed()
+        gb = self.grad_buckets
+        if gb is not None:
+            gb.mode = "off"
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):  # warm up allocator / lazy init outside the graph
-                self.opt.zero_grad(set_to_none=True)
-                self._fwd_bwd(static, autocast_cache=False)
-                if self.grad_buckets is not None:
-                    self.grad_buckets.finish()
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        check_errors(self.device, self._vocab)  # a warm-up error is this batch's error: raise it now
-        # gradients are (re)allocated inside the capture from the graph's pool and stay static across replays
-        self.opt.zero_grad(set_to_none=True)
-        hooks = None
-        if self.grad_buckets is not None:  # the exchange is not captured: it runs after each replay
-            hooks = self.grad_buckets._hooks
-            for h in hooks:
-                h.remove()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            loss = self._fwd_bwd(static, autocast_cache=False)
-        torch.cuda.synchronize()
-        if hooks is not None:
-            gb = self.grad_buckets
-            gb._hooks = [p.register_post_accumulate_grad_hook(gb._make_hook(i)) for i, p in enumerate(self.params)]
+        spy = _GemmSpy()
+        try:
+            with torch.cuda.stream(s):
+                for k in range(2):  # warm up allocator / lazy init outside the graph
+                    self.opt.zero_grad(set_to_none=True)
+                    if k == 0:
+                        with spy:
+                            self._fwd_bwd(static, autocast_cache=False)
+                    else:
+                        self._fwd_bwd(static, autocast_cache=False)
+                    if gb is not None:
+                        gb.reset()
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            check_errors(self.device, self._vocab)  # a warm-up error is this batch's error: raise it now
+            self.opt.zero_grad(set_to_none=True)
+            self.capture_report[sig] = sorted(spy.hits)
+            if spy.hits:  # a PyTorch-ROCm BLAS fallback in the step: not captured (DESIGN.md §5)
+                self.graphs[sig] = None
+                return
+            pool = torch.cuda.graph_pool_handle()
+            segs = []
+            cur = {"g": torch.cuda.CUDAGraph()}
+            if gb is not None:
+                def boundary(buckets):  # runs on the autograd worker thread, on the capturing stream
+                    dev = self.device
+                    if weight_grad_overlap_active(dev):
+                        join_weight_grads(dev)
+                    if colsum_deferral_active(dev):  # the released buckets' LayerNorm sums belong to this segment
+                        flush_colsums(dev)
+                    cur["g"].capture_end()
+                    segs.append((cur["g"], list(buckets)))
+                    cur["g"] = torch.cuda.CUDAGraph()
+                    cur["g"].capture_begin(pool=pool)
+
+                gb.mode, gb.on_boundary = "mark", boundary
+                gb.reset()
+            with torch.cuda.stream(s):
+                cur["g"].capture_begin(pool=pool)
+                loss = self._fwd_bwd(static, autocast_cache=False)
+                cur["g"].capture_end()
+                segs.append((cur["g"], []))
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+        finally:
+            if gb is not None:
+                gb.mode, gb.on_boundary = "launch", None
+                gb.reset()
         grads = [p.grad for p in self.params]
-        self.graphs[batch.shape_signature()] = (g, static, loss, grads)
+        self.graphs[sig] = (segs, static, loss, grads)
 
     def _raise_pending(self, keep: int):
         """Raises the first device error among submitted steps, waiting only for steps older than the newest
         ``keep`` (``keep = 0``: all of them)."""
         while len(self._pending) > keep or (self._pending and self._pending[0][0].query()):
-            ev, host, batch = self._pending.popleft()
+            ev, host, batch, active = self._pending.popleft()
             ev.synchronize()
             code, mx = int(host[0]), int(host[1])
             if code & 0xFFFFFFFF:
                 self._pending.clear()
                 err_word(self.device).zero_()
+                # the failing step's AdamW was a no-op on the device: take back its step counts and LR step
+                if isinstance(self.opt, FusedAdamW):
+                    for i in active:
+                        self.opt.steps[i] -= 1
+                self.sched_step -= 1
                 raise_for_error(code, mx, self._vocab, batch)
 
     def prefetch(self, batch: PytorchBatch) -> None:
@@ -410,30 +497,33 @@ class TrainStep:
         step, overlapped when ``prefetch(batch)`` was called during the previous step)."""
         if self.check_errors:
             self._raise_pending(keep=1)
+        host_batch = batch  # the caller's object (named in an error message; device staging buffers get reused)
         batch = self._to_device(batch)
         entry = None
         if self.use_graph:
             sig = batch.shape_signature()
-            entry = self.graphs.get(sig)
-            if entry is None and len(self.graphs) < self.max_graphs:
+            if sig not in self.graphs and len(self.graphs) < self.max_graphs:
                 self._capture(batch)
-                entry = self.graphs[sig]
+            entry = self.graphs.get(sig)
+        gb = self.grad_buckets
         if entry is None:
             self.opt.zero_grad(set_to_none=True)
             loss = self._fwd_bwd(batch)
         else:
-            g, static, sloss, grads = entry
+            segs, static, sloss, grads = entry
             static.copy_(batch, non_blocking=True)
             for p, gr in zip(self.params, grads):  # the graph writes its gradients into its own pool
                 p.grad = gr
-            g.replay()
+            for g, released in segs:
+                g.replay()
+                if gb is not None:  # exchanged while the next segment replays
+                    for b in released:
+                        gb._launch(b)
             # the next replay overwrites the static loss: hand back a copy, made by an elementwise kernel (x * 1 is
             # exact) rather than clone()'s D2D blit, which costs ~5 us of device time for 4 bytes
             loss = sloss.mul(1.0)
-        if self.grad_buckets is not None:
-            if entry is not None:  # graph: hooks did not run during replay; exchange every bucket now
-                self.grad_buckets.reset()
-            self.grad_buckets.finish()
+        if gb is not None:
+            gb.finish()
         if self.sched is None:
             self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step))
         else:
@@ -448,7 +538,8 @@ class TrainStep:
             host.copy_(err_word(self.device), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-            self._pending.append((ev, host, batch))
+            active = list(self.opt._active) if isinstance(self.opt, FusedAdamW) else []
+            self._pending.append((ev, host, host_batch, active))
         return loss
 
     def check(self):

@@ -188,6 +188,20 @@ int esgpt_output_loss(const esgpt_batch* batch, const void* zc, int64_t ldc, int
                       const void* zc_bias, const void* zt, int64_t ldt, int dtype, const esgpt_loss_term* terms,
                       int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
                       void* workspace, size_t workspace_bytes, int32_t* err, void* stream);
+/* The same with an explicit event-kernel path (esgpt_output_loss = ESGPT_LOSS_PATH_AUTO): STREAM (one wave per logit
+ * row, the row streamed once in 16-B chunks: dense per-range rules + sparse patches; needs disjoint term columns,
+ * <= 4 SINGLE/MULTI terms per level, <= 128 sparse gradient columns per row), ROW_STAGED (the whole row in LDS:
+ * ldc·(s + 4) B per wave <= 64 KiB), GENERIC (column by column over zero-filled gradients; any layout). AUTO takes
+ * the first that applies. A forced path that does not apply returns ESGPT_ERR_UNSUPPORTED. Every path yields the
+ * same gradients bit for bit; the MULTI per-term losses are summed in a path-dependent order. */
+#define ESGPT_LOSS_PATH_AUTO 0
+#define ESGPT_LOSS_PATH_STREAM 1
+#define ESGPT_LOSS_PATH_ROW_STAGED 2
+#define ESGPT_LOSS_PATH_GENERIC 3
+int esgpt_output_loss_ex(const esgpt_batch* batch, const void* zc, int64_t ldc, int64_t n_levels, int shift,
+                         const void* zc_bias, const void* zt, int64_t ldt, int dtype, const esgpt_loss_term* terms,
+                         int n_terms, const esgpt_tte_spec* tte, void* dzc, void* dzt, float* dbias, float* losses,
+                         void* workspace, size_t workspace_bytes, int32_t* err, int path, void* stream);
 
 /* ---- Fused block elementwise stages ---------------------------------------------------------------------
  * InnerBlock residual adds + resid_dropout + the CI encoder's per-block event mask + the following LayerNorm
@@ -295,6 +309,9 @@ int esgpt_stream_wait(void* waiter, void* signaller);
  * stream replaced by a device counter): bank[i] = *counter + i for i < slots, then *counter += slots — one launch,
  * capturable into a HIP graph (every replay draws fresh seeds). */
 int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream);
+/* The first launch of a training step: esgpt_seed_bank plus, when err != NULL, the step's error block zeroed (so the
+ * flags a step's kernels raise, and the AdamW no-op they cause, belong to that step alone). */
+int esgpt_step_begin(int64_t* counter, int64_t* bank, int64_t slots, int32_t* err, void* stream);
 
 /* ---- Parameter packing -------------------------------------------------------------------------------------
  * The compute-dtype copies of the f32 parameters a step reads, in ONE launch: the blocks' flat bf16 weight shadow

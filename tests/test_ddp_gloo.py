@@ -64,7 +64,7 @@ def _worker(rank, world, port, q):
     gb._launch = spy
     ts.step(_data(rank))
     assert launched_in_backward and all(in_bwd for _, in_bwd in launched_in_backward)
-    assert len(launched_in_backward) == len(gb.buckets)
+    assert [b for b, _ in launched_in_backward] == list(range(len(gb.buckets)))  # index order, once each
     # every gradient is a view into the one flat exchange buffer
     base = gb.flat.data_ptr()
     for p in ts.params:

@@ -1,7 +1,10 @@
 """World-size-2 data parallelism of the real training step on the GPU: both ranks on cuda:0 with the
 gloo backend (the box has one GPU; RCCL refuses two ranks on one device), the CI model through TrainStep with
-FusedAdamW and the HIP graph, each rank on its own subjects. Compared with one process that computes each rank's
-gradients (per-rank weighted_loss normalisation), averages them and takes the same optimizer steps
+FusedAdamW and the HIP graph cut into per-bucket segments, each rank on its own subjects. The ranks take different
+paths in the same step — rank 1's batches change length (the collate pads each batch to its own longest subject,
+pytorch_dataset.py:571), so it captures a new graph while rank 0 replays, and past max_graphs it runs eagerly — and
+the exchange must still pair the same buckets. Compared with one process that computes each rank's gradients
+(per-rank weighted_loss normalisation), averages them and takes the same optimizer steps
 (generative_modeling.py:434-485 under Lightning DDP)."""
 import os
 import socket
@@ -36,8 +39,12 @@ def _setup():
     return bc, m, opt
 
 
+LENGTHS = {0: [256, 256, 256], 1: [256, 200, 184]}  # rank 1: capture, capture, eager (max_graphs = 2)
+
+
 def _batches(bc, rank):
-    return [bc.batch(10 * rank + s, batch_size=8, device="cuda:0").packed() for s in range(STEPS)]
+    return [bc.batch(10 * rank + s, batch_size=8, device="cuda:0")[:, :n].packed()
+            for s, n in zip(range(STEPS), LENGTHS[rank])]
 
 
 def _worker(rank, world, port, q):
@@ -51,13 +58,26 @@ def _worker(rank, world, port, q):
         from eventstreamgpt_amd.train import TrainStep
 
         bc, m, opt = _setup()
-        ts = TrainStep(m, opt, torch.bfloat16, use_graph=True, bucket_mb=0.05)  # several buckets
+        ts = TrainStep(m, opt, torch.bfloat16, use_graph=True, bucket_mb=0.05, max_graphs=2)  # several buckets
         assert ts.use_graph and ts.distributed and len(ts.grad_buckets.buckets) > 1
+        order = []
+        orig = ts.grad_buckets._launch
+
+        def spy(b):
+            order.append(b)
+            orig(b)
+
+        ts.grad_buckets._launch = spy
         losses = []
         for i, b in enumerate(_batches(bc, rank)):
+            order.clear()
             losses.append(float(ts.step(b)))
+            nb = len(ts.grad_buckets.buckets)
+            assert order == list(range(nb)), (i, order)  # one exchange per bucket, in index order, every step
             q.put(("progress", rank, f"step {i} loss {losses[-1]:.6f}"))
         ts.check()
+        segs = [len(e[0]) for e in ts.graphs.values() if e is not None]
+        assert len(ts.graphs) == (1 if rank == 0 else 2) and all(n > 1 for n in segs), segs
         base = ts.grad_buckets.flat.data_ptr()
         in_flat = all(base <= p.grad.data_ptr() < base + 4 * ts.grad_buckets.flat.numel() for p in ts.params)
         q.put(("done", rank, (losses, in_flat, {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()})))

@@ -193,6 +193,85 @@ def test_nested_attention_graph_replay_matches_eager_with_allocations_between_re
 
 
 @pytest.mark.gpu
+def test_graph_capture_skips_signatures_with_aten_gemm_fallback():
+    """A batch whose token count the fused NA blocks do not take (B·L not a multiple of 8) runs the module path
+    through PyTorch-ROCm BLAS; its Linear backward replayed from a HIP graph returns wrong bias gradients
+    (tools/graph_blaslt_repro.py), so TrainStep does not capture that signature (warm-up under _GemmSpy) and runs it
+    eagerly: same losses and parameters as an eager TrainStep, while a fused-shape signature is still captured."""
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C4"]
+    odd = [bc.batch(i, batch_size=1, device="cuda")[:, :253].packed() for i in range(3)]  # 253 tokens
+    even = [bc.batch(10 + i, batch_size=2, device="cuda").packed() for i in range(2)]
+
+    def run(graph):
+        cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+        torch.manual_seed(0)
+        m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
+        ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=100),
+                       torch.bfloat16, use_graph=graph)
+        losses = [float(ts.step(b)) for b in odd + even]
+        ts.check()
+        return losses, {k: v.detach().float().clone() for k, v in m.state_dict().items()}, ts
+
+    le, se, _ = run(False)
+    lg, sg, ts = run(True)
+    assert ts.graphs[odd[0].shape_signature()] is None and ts.capture_report[odd[0].shape_signature()]
+    assert ts.graphs[even[0].shape_signature()] is not None, ts.capture_report
+    for a, b in zip(le, lg):
+        assert abs(a - b) <= 1e-3 * abs(a), (le, lg)
+    for k in se:
+        assert (sg[k] - se[k]).abs().max().item() < 1e-4, k
+
+
+@pytest.mark.gpu
+def test_step_error_flags_are_per_step():
+    """A step whose batch holds an out-of-range embedding index is a no-op for the parameters (its AdamW sees the
+    flag), and the step after it — on the device, the error block is zeroed by each step's first launch — updates
+    them (device semantics, TrainStep(check_errors=False)). With checking on, the error is raised as the reference's
+    AssertionError at a later submission, and the failing step's AdamW / LR-schedule counters are rolled back."""
+    from eventstreamgpt_amd.kernels import err_word
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C1"]
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+    good = [bc.batch(i, batch_size=4, device="cuda").packed() for i in range(3)]
+    bad = bc.batch(7, batch_size=4, device="cuda").packed()
+    bad.dynamic_indices[0, 0, 0] = cfg.vocab_size + 5
+    opt_cfg = OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=0, max_training_steps=100)
+
+    def snap(m):
+        return {k: v.detach().clone() for k, v in m.named_parameters()}
+
+    torch.manual_seed(0)
+    m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
+    ts = TrainStep(m, opt_cfg, torch.bfloat16, use_graph=False, check_errors=False)
+    ts.step(good[0])
+    p0 = snap(m)
+    ts.step(bad)
+    p1 = snap(m)
+    assert all(torch.equal(p0[k], p1[k]) for k in p0)  # the failing step did not update
+    ts.step(good[1])
+    p2 = snap(m)
+    assert any(not torch.equal(p1[k], p2[k]) for k in p0)  # the next step did
+    assert int(err_word(torch.device("cuda"))[0]) == 0  # and its own flags are clear
+
+    torch.manual_seed(0)
+    m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
+    ts = TrainStep(m, opt_cfg, torch.bfloat16, use_graph=False)
+    ts.step(good[0])
+    ts.step(bad)
+    torch.cuda.synchronize()
+    assert ts.sched_step == 2 and {s for s in ts.opt.steps if s} == {2}
+    with pytest.raises(AssertionError, match="Invalid embedding!"):
+        ts.step(good[1])
+    assert ts.sched_step == 1 and {s for s in ts.opt.steps if s} == {1}
+    ts.step(good[2])  # training continues from the rolled-back counters
+    ts.check()
+    assert ts.sched_step == 2 and {s for s in ts.opt.steps if s} == {2}
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("graph", [True, False])
 def test_weight_grad_overlap_matches_serial_step(graph):
     """TrainStep with the projections' weight gradients on the second stream (overlap_weight_grads) vs one stream: the same

@@ -1,0 +1,142 @@
+"""Round-1 NA graph-replay divergence, isolated: PyTorch-ROCm Linear layers (bf16 autocast, with bias) captured into a
+HIP graph the way TrainStep captured the round-1 NA blocks (two warm-up passes on a side stream, then
+torch.cuda.graph), replayed over fresh inputs with host allocations between replays, against eager gradients.
+
+Variants (one line of JSON each):
+  blas      hipblaslt (PyTorch-ROCm default for these GEMMs) | rocblas (torch.backends.cuda.preferred_blas_library)
+  churn     allocate / fill / free device memory on the host between replays (what TrainStep's callers did)
+The bias gradient of Linear backward is the reduction the round-1 diagnostics found corrupted (c_proj.bias / c_fc.bias).
+
+    python tools/graph_blaslt_repro.py
+"""
+import json
+
+import torch
+import torch.nn as nn
+
+
+def make(seed=0):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(256, 1024), nn.GELU(), nn.Linear(1024, 256)).cuda()
+
+
+def grads_of(m):
+    return [p.grad.detach().float().clone() for p in m.parameters()]
+
+
+AUTOCAST = {"on": True}
+
+
+def fwd_bwd(m, x):
+    with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False, enabled=AUTOCAST["on"]):
+        y = m(x)
+    loss = y.float().square().mean()
+    loss.backward()
+    return loss.detach()
+
+
+def run(blas: str, churn: bool, steps: int = 6, autocast: bool = True, x_grad: bool = False):
+    torch.backends.cuda.preferred_blas_library(blas)
+    AUTOCAST["on"] = autocast
+    xs = [torch.randn(8192, 256, device="cuda", generator=torch.Generator("cuda").manual_seed(100 + i))
+          .requires_grad_(x_grad) for i in range(steps)]
+    m = make()
+    want, want_loss = [], []
+    for x in xs:
+        for p in m.parameters():
+            p.grad = None
+        want_loss.append(float(fwd_bwd(m, x)))
+        want.append(grads_of(m))
+    m = make()
+    static = xs[0].detach().clone().requires_grad_(x_grad)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            for p in m.parameters():
+                p.grad = None
+            fwd_bwd(m, static)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    for p in m.parameters():
+        p.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        sloss = fwd_bwd(m, static)
+    worst, lerr = [], []
+    for i, x in enumerate(xs):
+        with torch.no_grad():
+            static.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        got = grads_of(m)
+        worst.append([float((a - b).abs().max() / (b.abs().max() + 1e-30)) for a, b in zip(got, want[i])])
+        lerr.append(abs(float(sloss) - want_loss[i]) / abs(want_loss[i]))
+        if churn:  # host-side allocations and frees between replays
+            junk = [torch.full((1 << 22,), 1e38, device="cuda") for _ in range(8)]
+            junk += [torch.empty(1 << 20, device="cuda").uniform_() for _ in range(8)]
+            del junk
+    names = [n for n, _ in m.named_parameters()]
+    return {"blas": blas, "churn": churn, "autocast": autocast, "x_requires_grad": x_grad, "loss_rel_err": [f"{e:.1e}" for e in lerr],
+            "grad_rel_err_per_param": {n: [f"{w[j]:.1e}" for w in worst] for j, n in enumerate(names)}}
+
+
+def column_sum_case(rows: int, cols: int, steps: int = 4):
+    """The bias-gradient reduction alone: y = x.sum(0) captured, replayed over fresh x."""
+    xs = [torch.randn(rows, cols, device="cuda", generator=torch.Generator("cuda").manual_seed(7 + i))
+          for i in range(steps)]
+    static = xs[0].clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            static.sum(0)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        y = static.sum(0)
+    errs = []
+    for x in xs:
+        static.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        want = x.sum(0)
+        errs.append(float((y - want).abs().max() / want.abs().max()))
+    return {"case": f"x[{rows},{cols}].sum(0) replayed", "rel_err_per_replay": [f"{e:.1e}" for e in errs]}
+
+
+def memset_node_case(replays: int = 3):
+    """hipMemsetAsync captured into a graph, followed by a kernel adding 1: after each replay the buffer holds 1 if
+    the memset node re-runs, the replay count if it does not."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    buf = torch.zeros(1 << 16, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream().cuda_stream
+        rc = hip.hipMemsetAsync(ctypes.c_void_p(buf.data_ptr()), 0, ctypes.c_size_t(buf.numel() * 4),
+                                ctypes.c_void_p(st))
+        buf.add_(1.0)
+    vals = []
+    for _ in range(replays):
+        g.replay()
+        torch.cuda.synchronize()
+        vals.append(float(buf.max()))
+    return {"case": "hipMemsetAsync node + add 1, replayed", "rc": rc, "buffer_after_each_replay": vals}
+
+
+if __name__ == "__main__":
+    for case in (lambda: column_sum_case(8192, 1024), lambda: column_sum_case(8192, 256), memset_node_case):
+        try:
+            print(json.dumps(case()), flush=True)
+        except Exception as e:
+            print(json.dumps({"error": repr(e)[:300]}), flush=True)
+    for blas, churn, ac, xg in (("hipblaslt", False, True, False), ("hipblaslt", False, False, False),
+                                ("cublas", False, False, False), ("hipblaslt", True, True, False),
+                                ("hipblaslt", False, True, True), ("hipblaslt", False, False, True)):
+        if True:
+            try:
+                print(json.dumps(run(blas, churn, autocast=ac, x_grad=xg)), flush=True)
+            except Exception as e:  # report and continue with the next variant
+                print(json.dumps({"blas": blas, "churn": churn, "error": repr(e)[:300]}), flush=True)

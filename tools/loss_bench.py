@@ -1,7 +1,7 @@
-"""esgpt_output_loss at the C2 step's head layout, per loss-term subset and per event-kernel path (row-staged /
-generic, ESGPT_LOSS_ROW_STAGE): graph-replayed launch time (count + event + reduce kernels).
+"""esgpt_output_loss_ex at a CI config's head layout (LOSS_BENCH_CFG, default C2), per loss-term subset and per
+event-kernel path (stream / row-staged / generic): graph-replayed launch time (count + event + reduce kernels).
 
-    python tools/loss_bench.py
+    python tools/loss_bench.py            LOSS_BENCH_CFG=C5 LOSS_BENCH_B=16 python tools/loss_bench.py
 """
 from __future__ import annotations
 
@@ -24,7 +24,7 @@ from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPT
 
 def main():
     dev = torch.device("cuda")
-    bc = CONFIGS["C2"]
+    bc = CONFIGS[os.environ.get("LOSS_BENCH_CFG", "C2")]
     model = CIPPTForGenerativeSequenceModeling(bc.model_config())
     bsz = int(os.environ.get("LOSS_BENCH_B", "32"))  # batch size (rows = B * (L + 1): waves per resident round)
     batch = bc.batch(0, batch_size=bsz).to(dev)
@@ -49,16 +49,16 @@ def main():
     print(json.dumps({"B": B, "L": Lq, "M": M, "C": C,
                       "terms": [(kinds[t.kind], t.vocab_end - t.vocab_start) for t in terms]}))
 
-    def launcher(sub):
+    def launcher(sub, path=L.LOSS_PATH_AUTO):
         arr = (L.EsgptLossTerm * max(1, len(sub)))(*sub)
         nb = lib.esgpt_output_loss_workspace(B, Lq, len(sub))
         ws = torch.empty(max(1, nb), dtype=torch.uint8, device=dev)
 
         def fwd():
-            L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), C, 1, 1, bias.data_ptr(), zc.data_ptr(), C, L.BF16,
-                                          arr, len(sub), ctypes.byref(tte), dzc.data_ptr(), dzc.data_ptr(),
-                                          dbias.data_ptr(), losses[: len(sub) + 2].data_ptr(), ws.data_ptr(), nb,
-                                          err.data_ptr(), L.stream()), "output_loss")
+            L.check(lib.esgpt_output_loss_ex(bv.ref, zc.data_ptr(), C, 1, 1, bias.data_ptr(), zc.data_ptr(), C,
+                                             L.BF16, arr, len(sub), ctypes.byref(tte), dzc.data_ptr(), dzc.data_ptr(),
+                                             dbias.data_ptr(), losses[: len(sub) + 2].data_ptr(), ws.data_ptr(), nb,
+                                             err.data_ptr(), path, L.stream()), "output_loss")
         return fwd, (arr, ws)
 
     if "--pmc" in sys.argv:  # eager launches of a term subset (counter collection): --pmc [all | i]
@@ -70,14 +70,26 @@ def main():
         err.zero_()
         return
     subsets = {"all": list(terms)}
-    for i, t in enumerate(terms):
-        subsets[f"only_{i}_{kinds[t.kind]}"] = [t]
-    for stage in ("1", "0"):
-        os.environ["ESGPT_LOSS_ROW_STAGE"] = stage
+    if os.environ.get("LOSS_BENCH_ONLY") != "all":
+        for i, t in enumerate(terms):
+            subsets[f"only_{i}_{kinds[t.kind]}"] = [t]
+    algo = B * Lq * C * 4 + B * Lq * M * 21
+    paths = ((L.LOSS_PATH_STREAM, "stream"), (L.LOSS_PATH_ROW_STAGED, "row_staged"), (L.LOSS_PATH_GENERIC, "generic"))
+    if os.environ.get("LOSS_BENCH_ONLY") == "all":
+        paths = paths[:1]
+    for path, pname in paths:
         for name, sub in subsets.items():
-            fn, keep = launcher(sub)
-            us = graph_time_ms(fn) * 1e3
-            print(json.dumps({"row_stage": stage, "terms": name, "us": round(us, 2)}))
+            fn, keep = launcher(sub, path)
+            try:
+                us = graph_time_ms(fn) * 1e3
+            except RuntimeError as e:  # a forced path that does not apply to this layout
+                print(json.dumps({"path": pname, "terms": name, "error": str(e)[:80]}))
+                break
+            rec = {"path": pname, "terms": name, "us": round(us, 2)}
+            if name == "all":
+                rec["algorithmic_MB"] = round(algo / 1e6, 2)
+                rec["TB_s"] = round(algo / us / 1e6, 3)
+            print(json.dumps(rec))
     err.zero_()
 
 
