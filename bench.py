@@ -13,16 +13,19 @@ synchronize on both sides); ``ms_per_step_median`` = the median step time from H
 
 Also reported (rank 0):
 * ``roofline``: the step's dominant kernel by device time, the grouped projection backward (dX + dW + db of one
-  Linear in one launch, MFMA-bound, 4·T·D·F algorithmic FLOPs) on c_fc's shape, timed in isolation (its launch
-  captured 20 times into a HIP graph, replayed between HIP events on the capturing stream), plus ``frac_in_step``:
-  the same kernel over EVERY launch shape of one step (shapes recorded from a real step, each timed likewise,
-  FLOP-weighted). ``traffic`` = HBM bytes per launch from the committed rocprofv3 PMC summary
-  (profiles/pmc_traffic.json: FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE), when present.
-* ``roofline_aux``: the same measurement for the attention forward / backward (4·H·hd·T /
-  8·H·hd·T, T = allowed (query, key) pairs of the batch), the c_fc forward, the JOINT input layer forward and its
-  table-gradient backward (HBM bytes, §8d per-occurrence accounting), the fused output-loss kernels (HBM bytes),
-  the §8d C5 embed-bag microbench (B=128, L=1024, nnz ~ 2.0 M), a long-sequence attention forward and the
-  generation decode kernel.
+  Linear in one launch, MFMA-bound, 4·T·in·out algorithmic FLOPs) over EVERY launch shape of one step (shapes
+  recorded from a real step, each launch captured 20 times into a HIP graph and replayed between HIP events on the
+  capturing stream, FLOP-weighted): ``frac`` is that step average; ``frac_isolated`` is c_fc's launch alone.
+* ``roofline_aux``: the same measurement, at the configuration's own shapes, for the attention forward / backward
+  (4·H·hd·T / 8·H·hd·T, T = allowed (query, key) pairs of the batch; the symbol is the kernel the
+  library's dispatch launches, esgpt_attn_path), the c_fc forward, the input layer (JOINT, or the NA SPLIT bags) and
+  its table-gradient backward (HBM bytes, §8d per-occurrence accounting), the fused output losses (CI, or the NA
+  per-level rows), the §8d C5 embed-bag microbench over a bf16 table larger than the Infinity Cache (C2 / C5), a
+  long-sequence attention forward and backward and the generation decode kernel.
+* ``traffic`` (every entry) = HBM bytes per launch set from this configuration's own rocprofv3 PMC passes
+  (profiles/pmc_traffic_<config>.json: FETCH_SIZE doubled per the gfx950 calibration + WRITE_SIZE; tools/pmc_traffic.py
+  --entries over ``--roofline-only --pmc-pass``), null without one; HBM-bound entries also carry the counter bytes
+  over the launch time (``achieved_counter_GBs``).
 * ``cpu_baseline``: the f32 oracle port timed on this host's cores on a bounded sample of the same workload.
 ``--roofline-only`` runs just the roofline launches (the command the PMC passes profile).
 """
@@ -72,9 +75,6 @@ def embed_fwd_bytes(batch, cfg) -> float:
     S = batch.static_indices.shape[1]
     n_ev = float(em.sum())
     return nnz * D * 4 + B * L * M * 21 + B * L * D * 4 + n_ev * S * D * 4 + B * L * 5
-
-
-PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def graph_time_ms(fn, reps: int = 20, iters: int = 5) -> float:
@@ -257,28 +257,6 @@ def _loss_launcher(model, batch):
     return fwd, float(nbytes), {"zc": zc, "dzc": dzc, "ws": ws, "arr": arr, "tte": tte}
 
 
-def _c5_embed_microbench(dev):
-    """SURVEY.md §8d embed-bag microbench: C5 vocabulary (V = 10,210), B = 128 subjects, L = 1024, M = 32
-    (nnz ~ 2.0 M), JOINT layer with static SUM_ALL and the temporal encoding, forward only."""
-    from eventstreamgpt_amd.synthetic import CONFIGS
-    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
-
-    bc = CONFIGS["C5"]
-    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
-    torch.manual_seed(0)
-    m = CIPPTForGenerativeSequenceModeling(cfg).to(dev)
-    batch = bc.batch(0, batch_size=128, device=dev)
-    emb = m.encoder.input_layer.data_embedding_layer
-    tl = m.encoder.input_layer.time_embedding_layer
-
-    def fwd():
-        with torch.no_grad():
-            emb.embed(batch, time_layer=tl)
-
-    nnz = float((batch.event_mask.unsqueeze(-1) & (batch.dynamic_indices > 0)).sum())
-    return fwd, embed_fwd_bytes(batch, cfg), nnz, (m, batch)
-
-
 def gemm_bwd_in_step(model, opt_cfg, batch, dtype) -> dict:
     """The grouped projection backward over every launch shape of one training step: the shapes are recorded from
     a real (eager) step, each distinct shape is timed in isolation (graph of 20 launches), and the in-step rate is
@@ -334,90 +312,284 @@ def gemm_bwd_in_step(model, opt_cfg, batch, dtype) -> dict:
             "ms_per_step": tot_ms, "shapes": rows}
 
 
-def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_cfg=None,
-                    dtype=torch.bfloat16) -> tuple[dict, list]:
-    """(roofline, roofline_aux): algorithmic work per launch / graph-replayed launch time, per kernel."""
-    traffic = {}
-    if os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
-            traffic = json.load(f).get("bytes_per_launch", {})
+def _attn_symbol(lib, fwd: bool, hd: int, Lq: int, Lk: int, ld_in: int, ld_o: int, drop: bool) -> str:
+    """The kernel esgpt_attn_fwd / _bwd actually launches for these arguments (the library's own dispatch rule)."""
+    from eventstreamgpt_amd import _lib as L
+
+    path = lib.esgpt_attn_path(hd, Lq, Lk, Lq, ld_in, ld_o, L.BF16)
+    d = "true" if drop else "false"
+    if path == 1:
+        return f"attn_fwd_mfma_kernel<{hd}, {d}>" if fwd else f"attn_bwd_kernel<{hd}, {d}>"
+    if path == 2:
+        return "attn_fwd_small<bf16>" if fwd else "attn_bwd_small<bf16>"
+    return "attn_fwd_generic<bf16>" if fwd else "attn_bwd_dq_generic<bf16> + attn_bwd_dkv_generic<bf16>"
+
+
+def _na_loss_launcher(model, batch):
+    """esgpt_output_loss on the NA head layout (per-level rows [B·L·(G-1), C], separate TTE rows [B·L, ldt]):
+    algorithmic bytes = the level rows' logits read + gradients written, the TTE rows likewise, the entries."""
+    import ctypes
+
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.kernels import batch_view, err_word
+    from eventstreamgpt_amd.transformer import model_output as MO
+
+    layer = model.output_layer
+    if layer._layout is None:
+        layer._layout = layer._build_layout()
+    c = model.config
+    G = len(c.measurements_per_dep_graph_level)
+    cls_all, reg_all = MO.all_classification_measurements(layer), MO.all_regression_measurements(c)
+    terms = []
+    for i in range(1, G):
+        cat, num = MO._level_sets(c.measurements_per_dep_graph_level[i])
+        terms += layer._terms_for(cat & cls_all, num & reg_all, i - 1)[0]
+    tte = layer._tte_spec(0)
+    lib = L.load()
+    bv = batch_view(batch)
+    B, Lq, M = bv.B, bv.L, bv.M
+    C = layer._layout["n_content"]
+    C += (-C) % 8
+    ldt = 1 if tte.kind == L.TTE_EXP else 3 * tte.K
+    dev = batch.device
+    g = torch.Generator(device=dev).manual_seed(5)
+    zc = torch.randn(B * Lq * (G - 1), C, device=dev, generator=g).bfloat16()
+    zt = torch.randn(B * Lq, ldt, device=dev, generator=g).bfloat16()
+    dzc, dzt = torch.empty_like(zc), torch.empty_like(zt)
+    losses = torch.empty(len(terms) + 2, device=dev)
+    nb = lib.esgpt_output_loss_workspace(B, Lq, len(terms))
+    ws = torch.empty(max(1, nb), dtype=torch.uint8, device=dev)
+    arr = (L.EsgptLossTerm * max(1, len(terms)))(*terms)
+    err = err_word(dev)
+
+    def fwd():
+        L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), C, G - 1, 0, None, zt.data_ptr(), ldt, L.BF16, arr,
+                                      len(terms), ctypes.byref(tte), dzc.data_ptr(), dzt.data_ptr(), None,
+                                      losses.data_ptr(), ws.data_ptr(), nb, err.data_ptr(), L.stream()), "na_loss")
+
+    nbytes = B * Lq * (G - 1) * C * 2 * 2 + B * Lq * ldt * 2 * 2 + B * Lq * M * 21 + B * Lq * 5
+    return fwd, float(nbytes), {"zc": zc, "zt": zt, "dzc": dzc, "dzt": dzt, "ws": ws, "arr": arr, "tte": tte}
+
+
+def _split_embed_launchers(model, batch):
+    """NA SPLIT input layer (esgpt_embed_split_bags_fwd: both tables' bags for every (event, bucket)) and its two
+    table-gradient backwards (categorical / numerical selectors)."""
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.kernels import EmbedSpec, bag_bwd, split_bags
+
+    emb = model.encoder.input_layer.data_embedding_layer
+    flags = emb._flags()
+    G = emb.n_levels
+    static = bool(flags & L.EMB_STATIC)
+    dw = emb.dynamic_weight if static else 1.0
+    cs, ns, ss = dw * emb.categorical_weight, dw * emb.numerical_weight, (emb.static_weight if static else 0.0)
+    spec = EmbedSpec(flags, emb.static_weight, emb.dynamic_weight, emb._buckets, G)
+    ct, nt = emb.categorical_embed_layer.weight, emb.numerical_embed_layer.weight
+    V, Dc, Dn = ct.shape[0], ct.shape[1], nt.shape[1]
+    B, Lq = batch.event_mask.shape
+    keep = {"dx": torch.randn(B * Lq * G, Dc + Dn, device=batch.device,
+                              generator=torch.Generator(device=batch.device).manual_seed(6))}
+
+    def fwd():
+        with torch.no_grad():
+            keep["x"] = split_bags(ct, nt, batch, spec, cs, ns, ss)
+
+    def bwd():
+        keep["dc"] = bag_bwd(batch, emb._buckets, L.BAG_CAT, flags, cs, ss, keep["dx"], Dc + Dn, Dc, V, G)
+        keep["dn"] = bag_bwd(batch, emb._buckets, L.BAG_NUM, flags & ~L.EMB_STATIC, ns, 0.0, keep["dx"][:, Dc:],
+                             Dc + Dn, Dn, V, G)
+
+    em = batch.event_mask.cpu()
+    idx = batch.dynamic_indices.cpu()
+    nnz = float((em.unsqueeze(-1) & (idx > 0)).sum())
+    M = idx.shape[2]
+    fbytes = nnz * (Dc + Dn) * 4 + B * Lq * M * 21 + B * Lq * G * (Dc + Dn) * 4 + float(em.sum()) * 2 * Dc * 4
+    bbytes = nnz * (Dc + Dn) * 4 * G + nnz * 12 * 2 + V * (Dc + Dn) * 4
+    return fwd, bwd, fbytes, bbytes, keep
+
+
+def _c5_embed_bf16_microbench(dev, V_big: int = 1 << 20):
+    """SURVEY.md §8d embed-bag microbench with a bf16 table that does not fit the 256 MiB Infinity Cache: the C5 batch
+    shape (B = 128, L = 1024, M = 32, nnz ~ 2.0 M) with its indices spread over V = 2^20 rows x D = 256 bf16
+    (512 MiB; index v -> v * 40503 mod V, padding 0 kept), JOINT layer with static SUM_ALL and the temporal
+    encoding (esgpt_embed_joint_fwd_ex). Per-occurrence bytes: every gathered row counted, 2 B per element."""
+    import ctypes
+
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.kernels import batch_view, err_word
+    from eventstreamgpt_amd.synthetic import CONFIGS
+
+    bc = CONFIGS["C5"]
+    batch = bc.batch(0, batch_size=128, device=dev)
+    big = (batch.dynamic_indices * 40503) % V_big
+    batch.dynamic_indices = torch.where(batch.dynamic_indices > 0, big.clamp_min(1), 0)
+    batch.static_indices = torch.where(batch.static_indices > 0, ((batch.static_indices * 40503) % V_big).clamp_min(1),
+                                       0)
+    D = 256
+    table = torch.randn(V_big, D, device=dev, generator=torch.Generator(device=dev).manual_seed(7)).bfloat16()
+    div = torch.exp(torch.arange(0, D, 2, device=dev).float() * (-torch.log(torch.tensor(1e4)).item() / D))
+    out = torch.empty(128, batch.event_mask.shape[1], D, device=dev)
+    lib = L.load()
+    bv = batch_view(batch)
+    err = err_word(dev)
+    flags = L.EMB_STATIC | L.EMB_TIME
+
+    def fwd():
+        L.check(lib.esgpt_embed_joint_fwd_ex(bv.ref, None, table.data_ptr(), L.BF16, V_big, D, div.data_ptr(),
+                                             div.data_ptr(), flags, 0.5, 0.5, out.data_ptr(), err.data_ptr(),
+                                             L.stream()), "embed_bf16")
+
+    em = batch.event_mask
+    B, Lq, M = batch.dynamic_indices.shape
+    nnz = float((em.unsqueeze(-1) & (batch.dynamic_indices > 0)).sum())
+    S = batch.static_indices.shape[1]
+    nbytes = nnz * D * 2 + B * Lq * M * 21 + B * Lq * D * 4 + float(em.sum()) * S * D * 2 + B * Lq * 5
+    return fwd, nbytes, nnz, (table, out, batch, div)
+
+
+def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str) -> list:
+    """The kernels measured for this configuration, at its own shapes: (name, symbol, bound, algorithmic work per
+    launch, launcher, extras). Each launcher issues exactly one launch set of the kernel."""
+    from eventstreamgpt_amd import _lib as L
+
+    lib = L.load()
     B, Lq = batch.event_mask.shape
     D, H, F = cfg.hidden_size, cfg.num_attention_heads, cfg.intermediate_size
     hd = D // H
     T_pairs = attention_flops_fwd(batch, cfg) / (4.0 * H * hd)
-    entries = []
+    ents, keep = [], []
 
-    def add(name, kernel, bound, work, fn, extra=None):
-        ms = graph_time_ms(fn)
-        if bound == "mfma":
+    def add(name, symbol, bound, work, fn, extra=None, hold=None):
+        ents.append({"kernel": name, "symbol": symbol, "bound": bound, "work": work, "fn": fn, "extra": extra or {}})
+        keep.append(hold)
+
+    drop = p_attn > 0
+    layer = f"{cfg_name} layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"
+    fa, ba, ka, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev)
+    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop), "mfma", 4.0 * H * hd * T_pairs, fa,
+        {"shape": layer + " (global)"}, ka)
+    add("attn_bwd", _attn_symbol(lib, False, hd, Lq, Lq, 3 * D, D, drop), "mfma", 8.0 * H * hd * T_pairs, ba,
+        {"shape": layer + " (global)"}, None)
+    gf, gb, kg = _gemm_launchers(B * Lq, D, F, dev)
+    add("gemm_fc_fwd", "gemm_kernel<true, true, 3, 1, 1>", "mfma", 2.0 * B * Lq * D * F, gf,
+        {"shape": f"{cfg_name} c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"}, kg)
+    add("gemm_fc_bwd", "gemm_bwd_pair_kernel", "mfma", 4.0 * B * Lq * D * F, gb,
+        {"shape": f"{cfg_name} c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"}, None)
+    emb = model.encoder.input_layer.data_embedding_layer
+    ci = cfg.structured_event_processing_mode == "conditionally_independent"
+    if hasattr(emb, "embed_layer"):
+        tl = model.encoder.input_layer.time_embedding_layer
+
+        def emb_fwd():
+            with torch.no_grad():
+                emb.embed(batch, time_layer=tl)
+
+        add("embed_joint_fwd", "embed_joint_fwd_kernel<4, 1>", "hbm", embed_fwd_bytes(batch, cfg), emb_fwd,
+            {"shape": f"{cfg_name}: JOINT, B={B} L={Lq} V={emb.embed_layer.weight.shape[0]} D={D} f32 table"})
+        eb, keb = _embed_bwd_launcher(model, batch)
+        add("embed_joint_bwd", "bag_block_sort/col_prefix/row_scan/scatter/reduce/combine/subject kernels "
+            "(esgpt_embed_bag_bwd)", "hbm", embed_bwd_bytes(batch, cfg), eb, {"shape": f"{cfg_name}: JOINT"}, keb)
+    else:
+        sf, sb, sfb, sbb, ks = _split_embed_launchers(model, batch)
+        add("embed_split_fwd", "embed_split_bags_kernel<4>", "hbm", sfb, sf,
+            {"shape": f"{cfg_name}: SPLIT cat/num bags, G={emb.n_levels} buckets, B={B} L={Lq}"}, ks)
+        add("embed_split_bwd", "esgpt_embed_bag_bwd x2 (categorical + numerical selectors)", "hbm", sbb, sb,
+            {"shape": f"{cfg_name}: SPLIT, G={emb.n_levels}"}, None)
+    if ci:
+        lf, lbytes, kl = _loss_launcher(model, batch)
+        add("output_loss", "count_kernel + event_stream_kernel<bf16> + reduce_kernel (esgpt_output_loss)", "hbm",
+            lbytes, lf, {"shape": f"{cfg_name}: bf16 logits [{B * Lq}, {kl['zc'].shape[1]}]"}, kl)
+    else:
+        nf, nbytes, kn = _na_loss_launcher(model, batch)
+        add("na_output_loss", "count_kernel + event_stream_kernel<bf16> + reduce_kernel (esgpt_output_loss, levels)",
+            "hbm", nbytes, nf, {"shape": f"{cfg_name}: bf16 level rows [{kn['zc'].shape[0]}, {kn['zc'].shape[1]}] + "
+                                         f"TTE rows [{kn['zt'].shape[0]}, {kn['zt'].shape[1]}]"}, kn)
+    if cfg_name in ("C2", "C5"):
+        cf, cbytes, nnz5, kc = _c5_embed_bf16_microbench(dev)
+        add("embed_c5_bf16_microbench", "embed_joint_fwd_kernel<4, 1, bf16>", "hbm", cbytes, cf,
+            {"shape": f"C5 batch shape B=128, L=1024, M=32, nnz={int(nnz5)}, bf16 table V=2^20 x 256 (512 MiB, "
+                      "larger than the Infinity Cache); per-occurrence bytes"}, kc)
+    # long-sequence attention: MFMA efficiency once the grid fills the chip
+    Bl, Ll, Hl = 4, 4096, 8
+    fl, bl, kll, _ = _attention_launchers(Bl, Ll, Hl * hd, Hl, torch.ones(Bl, Ll, dtype=torch.bool, device=dev), 0.0,
+                                          dev)
+    long_pairs = Bl * Ll * (Ll + 1) / 2
+    add("attn_fwd_long", _attn_symbol(lib, True, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False), "mfma",
+        4.0 * Hl * hd * long_pairs, fl, {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"}, kll)
+    add("attn_bwd_long", _attn_symbol(lib, False, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False), "mfma",
+        8.0 * Hl * hd * long_pairs, bl, {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"}, None)
+    for Bd in (B, 8 * B):
+        fd, dbytes, kd = _decode_launcher(Bd, H, hd, Lq, dev)
+        add("attn_decode" if Bd == B else "attn_decode_b8x", f"attn_decode_kernel<float, {hd}>", "hbm", dbytes, fd,
+            {"shape": f"decode: B={Bd} H={H} hd={hd}, 1 query over a {Lq}-event f32 KV cache"}, kd)
+    return ents, keep
+
+
+def pmc_file(cfg_name: str) -> str:
+    return os.path.join(REPO, "profiles", f"pmc_traffic_{cfg_name}.json")
+
+
+def pmc_pass(model, cfg, batch, dev, p_attn: float, cfg_name: str, out_json: str, reps: int = 3) -> None:
+    """The launches a rocprofv3 --pmc pass attributes (tools/pmc_traffic.py --entries): per roofline entry, one
+    seed-bank launch as a marker, then ``reps`` eager launch sets of the entry; the entry names go to out_json."""
+    from eventstreamgpt_amd.kernels import _seed_counter, begin_dropout_step
+
+    ents, keep = roofline_entries(model, cfg, batch, dev, p_attn, cfg_name)
+    _seed_counter(dev)
+    for e in ents:
+        e["fn"]()  # warm (lazy allocations, plans) before the counted launches
+    torch.cuda.synchronize()
+    for e in ents:
+        begin_dropout_step(dev)  # marker: seed_bank_kernel
+        for _ in range(reps):
+            e["fn"]()
+    begin_dropout_step(dev)
+    torch.cuda.synchronize()
+    with open(out_json, "w") as f:
+        json.dump({"config": cfg_name, "reps": reps, "entries": [e["kernel"] for e in ents]}, f)
+
+
+def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_cfg=None,
+                    dtype=torch.bfloat16, cfg_name: str = "C2") -> tuple[dict, list]:
+    """(roofline, roofline_aux): algorithmic work per launch / graph-replayed launch time, per kernel, at this
+    configuration's shapes; ``traffic`` = HBM bytes per launch set from this configuration's own PMC passes
+    (profiles/pmc_traffic_<config>.json), null when that file has no entry for the kernel."""
+    traffic = {}
+    if os.path.exists(pmc_file(cfg_name)):
+        with open(pmc_file(cfg_name)) as f:
+            traffic = json.load(f).get("bytes_per_launch", {})
+    ents, keep = roofline_entries(model, cfg, batch, dev, p_attn, cfg_name)
+    out = []
+    for e in ents:
+        ms = graph_time_ms(e["fn"])
+        work = e["work"]
+        if e["bound"] == "mfma":
             ach, peak, unit, wk = work / (ms * 1e-3) / 1e12, peak_tf, "TFLOP/s", "algorithmic_flops_per_launch"
         else:
             ach, peak, unit, wk = work / (ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s", "algorithmic_bytes_per_launch"
-        tkey = (extra or {}).pop("traffic_key", kernel)
-        e = {"kernel": name, "symbol": kernel, "bound": bound, "achieved": round(ach, 3), "peak": peak,
-             "unit": unit, "frac": round(ach / peak, 5), "traffic": traffic.get(tkey), "avg_ms": round(ms, 5),
-             wk: work, "timing": "HIP graph of 20 launches, events on the replaying stream"}
-        e.update(extra or {})
-        entries.append(e)
-
-    drop = "true" if p_attn > 0 else "false"
-    fa, ba, _keep_a, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev)
-    add("attn_fwd", f"attn_fwd_mfma_kernel<{hd}, {drop}>", "mfma", 4.0 * H * hd * T_pairs, fa,
-        {"shape": f"C2 layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"})
-    add("attn_bwd", f"attn_bwd_kernel<{hd}, {drop}>", "mfma", 8.0 * H * hd * T_pairs, ba,
-        {"shape": f"C2 layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"})
-    gf, gb, _keep_g = _gemm_launchers(B * Lq, D, F, dev)
-    add("gemm_fc_fwd", "gemm_kernel<true, true, 3, 1, 1>", "mfma", 2.0 * B * Lq * D * F, gf,
-        {"shape": f"c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"})
-    add("gemm_fc_bwd", "gemm_bwd_pair_kernel", "mfma", 4.0 * B * Lq * D * F, gb,
-        {"shape": f"c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"})
-    emb = model.encoder.input_layer.data_embedding_layer
-    tl = model.encoder.input_layer.time_embedding_layer
-
-    def emb_fwd():
-        with torch.no_grad():
-            emb.embed(batch, time_layer=tl)
-
-    # the JOINT input layer and the CI loss layout only (the NA configuration's SPLIT bags and per-level loss rows
-    # are timed inside its step)
-    ci = cfg.structured_event_processing_mode == "conditionally_independent"
-    if hasattr(emb, "embed_layer"):
-        add("embed_joint_fwd", "embed_joint_fwd_kernel<4, 1>", "hbm", embed_fwd_bytes(batch, cfg), emb_fwd)
-        eb, _keep_eb = _embed_bwd_launcher(model, batch)
-        add("embed_joint_bwd", "bag_block_sort/col_prefix/row_scan/scatter/reduce/combine/subject kernels "
-            "(esgpt_embed_bag_bwd)", "hbm",
-            embed_bwd_bytes(batch, cfg), eb, {"traffic_key": "embed_bag_bwd"})
-    if ci:
-        lf, lbytes, _keep_lf = _loss_launcher(model, batch)
-        add("output_loss", "count + event + reduce kernels (esgpt_output_loss)", "hbm", lbytes, lf,
-            {"traffic_key": "output_loss", "shape": f"bf16 logits [{B * Lq}, {_keep_lf['zc'].shape[1]}]"})
-    cf, cbytes, nnz5, _keep_c5 = _c5_embed_microbench(dev)
-    add("embed_c5_microbench", "embed_joint_fwd_kernel<4, 1>", "hbm", cbytes, cf,
-        {"traffic_key": "embed_joint_fwd_kernel@c5",
-         "shape": f"C5 vocab V=10210, B=128, L=1024, M=32, nnz={int(nnz5)}, f32 table (per-occurrence bytes)"})
-    # long-sequence attention: the forward kernel's MFMA efficiency once the grid fills the chip
-    Bl, Ll, Hl = 4, 4096, 8
-    fl, _, _keep_l, _ = _attention_launchers(Bl, Ll, Hl * hd, Hl, torch.ones(Bl, Ll, dtype=torch.bool, device=dev),
-                                             0.0, dev)
-    add("attn_fwd_long", f"attn_fwd_mfma_kernel<{hd}, false>", "mfma", 4.0 * Hl * hd * Bl * Ll * (Ll + 1) / 2, fl,
-        {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"})
-    # generation (SURVEY 8f row 3): one decode step of the C2 model over a full cache, and a larger batch
-    for Bd in (B, 8 * B):
-        fd, dbytes, _keep_d = _decode_launcher(Bd, H, hd, Lq, dev)
-        add("attn_decode" if Bd == B else "attn_decode_b256", f"attn_decode_kernel<float, {hd}>", "hbm", dbytes, fd,
-            {"shape": f"decode: B={Bd} H={H} hd={hd}, 1 query over a {Lq}-event f32 KV cache",
-             "traffic_key": f"attn_decode_kernel<float, {hd}>@grid{Bd * H * 256}"})
-    # `roofline` = the step's dominant kernel by device time: the grouped projection backward (gemm_bwd_pair_kernel,
-    # ~35 % of the C2 step in profiles/r01_c2_step_kernel_stats.csv), measured on c_fc's shape (its largest launch)
-    dom = next(i for i, e in enumerate(entries) if e["kernel"] == "gemm_fc_bwd")
-    entries[dom]["dominant"] = "largest share of the step's device time (grouped projection backward)"
+        r = {"kernel": e["kernel"], "symbol": e["symbol"], "bound": e["bound"], "achieved": round(ach, 3),
+             "peak": peak, "unit": unit, "frac": round(ach / peak, 5), "traffic": traffic.get(e["kernel"]),
+             "avg_ms": round(ms, 5), wk: work, "timing": "HIP graph of 20 launches, events on the replaying stream"}
+        if e["bound"] == "hbm" and r["traffic"]:
+            r["achieved_counter_GBs"] = round(r["traffic"] / (ms * 1e-3) / 1e9, 1)  # DRAM-side bytes / time
+        r.update(e["extra"])
+        out.append(r)
+    # `roofline` = the step's dominant kernel by device time: the grouped projection backward (gemm_bwd_pair_kernel)
+    # over EVERY launch shape of one step (frac = the step average); its c_fc launch alone is frac_isolated
+    dom = next(i for i, e in enumerate(out) if e["kernel"] == "gemm_fc_bwd")
+    d = out[dom]
+    d["dominant"] = "largest share of the step's device time (grouped projection backward)"
     if opt_cfg is not None:
         ins = gemm_bwd_in_step(model, opt_cfg, batch, dtype)
-        entries[dom]["frac_isolated"] = entries[dom]["frac"]
-        entries[dom]["achieved_in_step"] = round(ins["achieved"], 3)
-        entries[dom]["frac_in_step"] = round(ins["achieved"] / peak_tf, 5)
-        entries[dom]["in_step"] = ins
-    return entries[dom], entries[:dom] + entries[dom + 1:]
+        d["frac_isolated"], d["achieved_isolated"], d["avg_ms_isolated"] = d["frac"], d["achieved"], d["avg_ms"]
+        d["achieved"] = round(ins["achieved"], 3)
+        d["frac"] = round(ins["achieved"] / peak_tf, 5)
+        d["avg_ms"] = round(ins["ms_per_step"] / ins["launches_per_step"], 5)
+        d["algorithmic_flops_per_launch"] = round(d["achieved"] * 1e12 * d["avg_ms"] * 1e-3, 1)
+        d["in_step"] = ins
+        d["shape"] = f"{cfg_name}: every projection backward of one step ({ins['launches_per_step']} launches, " \
+                     f"{len(ins['shapes'])} shapes, FLOP-weighted); traffic = the c_fc launch's"
+    return d, out[:dom] + out[dom + 1:]
 
 
 def cpu_baseline(bc, seconds: float = 12.0) -> dict:
@@ -481,6 +653,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--roofline-only", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip the roofline launches (clean step profiles)")
+    ap.add_argument("--pmc-pass", default=None, help="with --roofline-only: the marker-separated launch sequence a "
+                    "rocprofv3 --pmc pass attributes; entry names written to this JSON file")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -508,7 +682,11 @@ def main():
 
     n_batches = 4
     if args.roofline_only:  # the launches the PMC passes profile (no training steps)
-        roofline, aux = roofline_report(model, cfg, bc.batch(0, device=dev), dev, 0.1, PEAK_BF16_TFLOPS)
+        if args.pmc_pass:
+            pmc_pass(model, cfg, bc.batch(0, device=dev), dev, 0.1, args.config, args.pmc_pass)
+            return
+        roofline, aux = roofline_report(model, cfg, bc.batch(0, device=dev), dev, 0.1, PEAK_BF16_TFLOPS,
+                                        cfg_name=args.config)
         print(json.dumps({"roofline": roofline, "roofline_aux": aux}))
         return
     # Pre-collated batches in pinned host memory, packed like the native collate's output (one buffer per batch):
@@ -560,7 +738,7 @@ def main():
     peak_tf = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
     roofline, aux = ({}, [])
     if rank == 0 and not args.no_roofline:
-        roofline, aux = roofline_report(model, cfg, host[0].to(dev), dev, 0.1, peak_tf, opt_cfg, dtype)
+        roofline, aux = roofline_report(model, cfg, host[0].to(dev), dev, 0.1, peak_tf, opt_cfg, dtype, args.config)
 
     result = {
         "metric": "train events/sec (node)",

@@ -474,7 +474,7 @@ static int g_force_generic = -1;
 
 static bool force_generic() {
   if (g_force_generic < 0) {
-    const char* e = getenv("ESGPT_ATTN_GENERIC");
+    const char* e = tuning_env("ESGPT_ATTN_GENERIC");
     g_force_generic = (e && e[0] == '1') ? 1 : 0;
   }
   return g_force_generic == 1;
@@ -506,6 +506,13 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                                      dropout_p, seed, st);
   return launch_fwd_generic<bf16>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
                                   dropout_p, seed, st);
+}
+
+int esgpt_attn_path(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o, int dtype) {
+  if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
+    return ESGPT_ATTN_PATH_MFMA;
+  if (Lk <= kSmallLk && !force_generic()) return ESGPT_ATTN_PATH_SMALL;
+  return ESGPT_ATTN_PATH_GENERIC;
 }
 
 int64_t esgpt_attn_bwd_counters(int64_t B, int64_t H, int64_t Lk) { return esgpt_attn_bwd_mfma_counters(B, H, Lk); }

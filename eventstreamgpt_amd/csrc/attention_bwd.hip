@@ -16,6 +16,8 @@
 // Fragment conventions (v_mfma_f32_32x32x16_bf16): lane l = (r = l&31, h = l>>5); A[row r][k = 8h+j],
 // B[k = 8h+j][col r]; C reg i = row (i&3) + 8(i>>2) + 4h, col r. An accumulator used as a B operand supplies k-step
 // s element j = row 16s + 8(j>>2) + 4h + (j&3) (permuted); the A operand is then read in that order.
+// hd = 16 (C1): S and dP are one K = 16 step; the Q / dO / K images are 32 columns wide with columns 16..31 zero, so
+// dVᵀ / dKᵀ / dQ run as 32-wide tiles whose rows 16..31 come out zero and are not stored.
 // Roofline: MFMA-bound at large L; algorithmic FLOPs 8·H·hd·T (T = allowed (q, k) pairs; recompute not counted).
 #include <cstdlib>
 
@@ -82,10 +84,11 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
 
 // Stores the 32 accumulator-row values of one lane's column (x[i] = row acc_row(i, h)) as bf16 into
 // dst[0 .. 31] with 16-B stores: register groups g and g+1 are joined across the half-waves with
-// v_permlane32_swap (lanes 0-31 end up with rows 8g..8g+7, lanes 32-63 with rows 8g+8..8g+15).
+// v_permlane32_swap (lanes 0-31 end up with rows 8g..8g+7, lanes 32-63 with rows 8g+8..8g+15). N = 16: rows 0..15.
+template <int N = 32>
 __device__ __forceinline__ void store_col32(__bf16* dst, const f32x16& x, int h) {
 #pragma unroll
-  for (int g = 0; g < 4; g += 2) {
+  for (int g = 0; g < N / 8; g += 2) {
     uint32_t a0 = pack2(x[4 * g], x[4 * g + 1]), a1 = pack2(x[4 * g + 2], x[4 * g + 3]);
     uint32_t b0 = pack2(x[4 * g + 4], x[4 * g + 5]), b1 = pack2(x[4 * g + 6], x[4 * g + 7]);
     const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
@@ -115,8 +118,9 @@ struct Img {
 
 template <int HD>
 struct Cfg {
+  static constexpr int HDP = HD < 32 ? 32 : HD;   // image / accumulator width (hd = 16: zero-padded to 32)
   static constexpr int QT = HD == 128 ? 32 : 64;  // queries per tile
-  static constexpr int LDS_BYTES = 2 * (KB * HD + 2 * QT * HD + KB * QT) + 8 * QT;
+  static constexpr int LDS_BYTES = 2 * (KB * HDP + 2 * QT * HDP + KB * QT) + 8 * QT;
 };
 
 template <int HD, bool DROP>
@@ -127,14 +131,14 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     __bf16* __restrict__ dq, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d,
     float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed,
     int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf) {
-  constexpr int QT = Cfg<HD>::QT;
-  using IQ = Img<HD>;  // Q, dO, K images: [row][HD]
-  using IS = Img<QT>;  // dS image: [key][QT]
+  constexpr int QT = Cfg<HD>::QT, HDP = Cfg<HD>::HDP;
+  using IQ = Img<HDP>;  // Q, dO, K images: [row][HDP]
+  using IS = Img<QT>;   // dS image: [key][QT]
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   __bf16* sK = reinterpret_cast<__bf16*>(smem_raw);
-  __bf16* sQ = sK + KB * HD;
-  __bf16* sD = sQ + QT * HD;
-  __bf16* sS = sD + QT * HD;
+  __bf16* sQ = sK + KB * HDP;
+  __bf16* sD = sQ + QT * HDP;
+  __bf16* sS = sD + QT * HDP;
   float* sL = reinterpret_cast<float*>(sS + KB * QT);
   float* sDl = sL + QT;
 
@@ -175,11 +179,19 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     }
   }
 
-  f32x16 dka[HD / 32], dva[HD / 32];
+  f32x16 dka[HDP / 32], dva[HDP / 32];
 #pragma unroll
-  for (int dt = 0; dt < HD / 32; ++dt)
+  for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) dka[dt][i] = dva[dt][i] = 0.f;
+  if (HD < HDP) {  // hd = 16: image columns 16..31 of K, Q and dO stay zero (staging writes columns 0..15 only)
+    for (int row = tid; row < KB + 2 * QT; row += THREADS) {
+      __bf16* img = row < KB ? sK : row < KB + QT ? sQ : sD;
+      const int rr = row < KB ? row : row < KB + QT ? row - KB : row - KB - QT;
+      *reinterpret_cast<bf16x8*>(img + IQ::off(rr, HD)) = zero8();
+      *reinterpret_cast<bf16x8*>(img + IQ::off(rr, HD + 8)) = zero8();
+    }
+  }
 
   const int kbend = min(Lk, kb0 + KB) - 1;  // last key of the block
   const int qlo = max(0, kb0 - off);
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
           const bf16x8 dsf = acc_frag(dp, ss);
           const int row0 = 32 * qs + 16 * ss + 4 * (g >> 1) + q4;
 #pragma unroll
-          for (int dt = 0; dt < HD / 32; ++dt) {
+          for (int dt = 0; dt < HDP / 32; ++dt) {
             const int col = 32 * dt + 16 * (g & 1) + 4 * p4;
             const bf16x8 dof = join(tr_read(sD + IQ::off(row0, col)), tr_read(sD + IQ::off(row0 + 8, col)));
             dva[dt] = mfma(dof, pf, dva[dt]);
@@ -358,7 +370,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     STAMP(5 + 6 * it);
 
     // ---- dQ[q][d] = Σ_key dS[q][key] · K[key][d] for the tile: one 32x32 output tile per wave ----
-    constexpr int NT = (QT / 32) * (HD / 32);
+    constexpr int NT = (QT / 32) * (HDP / 32);
     if (wave < NT) {
       const int qsub = wave % (QT / 32), dsub = wave / (QT / 32);
       const int qpos_max = min(q0 + QT - 1, Lq - 1) + off;
@@ -377,7 +389,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
         }
         const int qi = q0 + 32 * qsub + r;
         STAMP(6 + 6 * it);
-        if (qi < Lq) store_col32(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + 32 * dsub, acc, h);
+        if (qi < Lq) store_col32<HD < 32 ? HD : 32>(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + 32 * dsub, acc, h);
         STAMP(7 + 6 * it);
       } else {
         // dQ[q][d] = dS·K: the head dim on the lane, so that each f32 atomic instruction adds two 128-B rows
@@ -392,7 +404,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qi = q0 + 32 * qsub + acc_row(i, h);
-          if (qi < Lq) atomicAdd(dq32 + ((int64_t)bh * Lq + qi) * HD + d, acc[i]);
+          if (qi < Lq && d < HD) atomicAdd(dq32 + ((int64_t)bh * Lq + qi) * HD + d, acc[i]);
         }
       }
     }
@@ -409,7 +421,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     constexpr int kSC1 = 16;  // buffer cache policy: sc1 (write-through stores, L1-bypassing loads)
     // [dk | dv] f32 slab of this pair, [wave][dt][i/4][lane] x 16 B (coalesced per store / load instruction)
     const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(xbuf + id * (2 * KB * HD), (short)0, 2 * KB * HD * 4, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(xbuf + id * (2 * KB * HDP), (short)0, 2 * KB * HDP * 4, 0x00020000);
     int* flag = reinterpret_cast<int*>(smem_raw);
     __syncthreads();  // every wave is done with the LDS images
     if (tid == 0) *flag = __hip_atomic_fetch_add(xcnt + 2 * id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -417,16 +429,16 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     const bool first = *flag == 0;
     if (first) {
 #pragma unroll
-      for (int dt = 0; dt < HD / 32; ++dt)
+      for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
         for (int i = 0; i < 16; i += 4) {
-          const int e = 4 * (((wave * (HD / 32) + dt) * 4 + i / 4) * 64 + lane);  // float index, 16-B granules
+          const int e = 4 * (((wave * (HDP / 32) + dt) * 4 + i / 4) * 64 + lane);  // float index, 16-B granules
           const u32x4 k4 = {__float_as_uint(dka[dt][i]), __float_as_uint(dka[dt][i + 1]),
                             __float_as_uint(dka[dt][i + 2]), __float_as_uint(dka[dt][i + 3])};
           const u32x4 v4 = {__float_as_uint(dva[dt][i]), __float_as_uint(dva[dt][i + 1]),
                             __float_as_uint(dva[dt][i + 2]), __float_as_uint(dva[dt][i + 3])};
           __builtin_amdgcn_raw_buffer_store_b128(k4, xr, 4 * e, 0, kSC1);
-          __builtin_amdgcn_raw_buffer_store_b128(v4, xr, 4 * (KB * HD + e), 0, kSC1);
+          __builtin_amdgcn_raw_buffer_store_b128(v4, xr, 4 * (KB * HDP + e), 0, kSC1);
         }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -441,12 +453,12 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     }
     __syncthreads();
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
+    for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
       for (int i = 0; i < 16; i += 4) {
-        const int e = 4 * (((wave * (HD / 32) + dt) * 4 + i / 4) * 64 + lane);
+        const int e = 4 * (((wave * (HDP / 32) + dt) * 4 + i / 4) * 64 + lane);
         const u32x4 k4 = __builtin_amdgcn_raw_buffer_load_b128(xr, 4 * e, 0, kSC1);
-        const u32x4 v4 = __builtin_amdgcn_raw_buffer_load_b128(xr, 4 * (KB * HD + e), 0, kSC1);
+        const u32x4 v4 = __builtin_amdgcn_raw_buffer_load_b128(xr, 4 * (KB * HDP + e), 0, kSC1);
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           dka[dt][i + c] += __uint_as_float(k4[c]);
@@ -459,9 +471,9 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     __bf16* ko = dk + ((int64_t)b * Lk + key) * ld_d + hh * HD;
     __bf16* vo = dv + ((int64_t)b * Lk + key) * ld_d + hh * HD;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt) {
-      store_col32(ko + 32 * dt, dka[dt], h);
-      store_col32(vo + 32 * dt, dva[dt], h);
+    for (int dt = 0; dt < HDP / 32; ++dt) {
+      store_col32<HD < 32 ? HD : 32>(ko + 32 * dt, dka[dt], h);
+      store_col32<HD < 32 ? HD : 32>(vo + 32 * dt, dva[dt], h);
     }
   }
   STAMP(41);
@@ -505,7 +517,7 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   // two workgroups per key block (even / odd query tiles) when there are at least two query tiles
   // (ESGPT_ATTN_BWD_NSPLIT=1: one workgroup per key block — tuning hook, read once)
   static const int max_split = [] {
-    const char* e = getenv("ESGPT_ATTN_BWD_NSPLIT");
+    const char* e = tuning_env("ESGPT_ATTN_BWD_NSPLIT");
     return (e && atoi(e) == 1) ? 1 : 2;
   }();
   const int nsplit = (counters && Lq > Cfg<HD>::QT && max_split > 1) ? 2 : 1;
@@ -540,7 +552,8 @@ extern "C" int esgpt_debug_stamps(uint64_t* out) {
 // f32 dQ accumulator (more than one key block) + the dK / dV exchange slabs of the query-split pairs.
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
   const size_t dq = Lk > KB ? sizeof(float) * (size_t)(B * H * Lq * hd) : 0;
-  return dq + sizeof(float) * (size_t)(B * H * cdiv(Lk, KB)) * 2 * KB * hd;
+  const int64_t hdp = hd < 32 ? 32 : hd;  // exchange slabs hold the padded accumulator tiles
+  return dq + sizeof(float) * (size_t)(B * H * cdiv(Lk, KB)) * 2 * KB * hdp;
 }
 
 int64_t esgpt_attn_bwd_mfma_counters(int64_t B, int64_t H, int64_t Lk) { return 2 * B * H * cdiv(Lk, KB); }
@@ -550,6 +563,9 @@ int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
                         const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
                         int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
                         float* dq32, int32_t* counters, hipStream_t st) {
+  if (hd == 16)
+    return launch<16>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
+                      window, drop_p, seed, dq32, counters, st);
   if (hd == 32)
     return launch<32>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
                       window, drop_p, seed, dq32, counters, st);

@@ -1,5 +1,6 @@
-// bf16 MFMA flash attention forward for gfx950 (InnerSelfAttention._attn, transformer.py:171-217), hd in {32, 64,
-// 128}; the fused backward (dQ, dK, dV in one kernel) is attention_bwd.hip.
+// bf16 MFMA flash attention forward for gfx950 (InnerSelfAttention._attn, transformer.py:171-217), hd in {16, 32,
+// 64, 128}; the fused backward (dQ, dK, dV in one kernel) is attention_bwd.hip. hd = 16 (C1: hidden 64 over 4 heads)
+// is exactly one K = 16 step of S = K·Qᵀ; its P·V product runs on a 32-wide V image whose columns 16..31 stay zero.
 //
 // v_mfma_f32_32x32x16_bf16 with the query on the MFMA lane, so the per-row softmax statistics are lane-local (no
 // cross-lane row reductions beyond one xor-32 exchange):
@@ -38,11 +39,13 @@ __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
   return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
 
-// Stores one lane's 32 accumulator-row values (x[i] = row acc_row(i, h)) as bf16 into dst[0 .. 31] with 16-B
-// stores, joining register groups g, g+1 across the half-waves with v_permlane32_swap.
+// Stores one lane's 32 accumulator-row values (x[i] = row acc_row(i, h)) as bf16 into dst[0 .. N-1] (N = 32, or 16
+// for hd = 16: rows 0..15 only) with 16-B stores, joining register groups g, g+1 across the half-waves with
+// v_permlane32_swap.
+template <int N = 32>
 __device__ __forceinline__ void store_col32(__bf16* dst, const f32x16& x, int h) {
 #pragma unroll
-  for (int g = 0; g < 4; g += 2) {
+  for (int g = 0; g < N / 8; g += 2) {
     uint32_t a0 = pack2(x[4 * g], x[4 * g + 1]), a1 = pack2(x[4 * g + 2], x[4 * g + 3]);
     uint32_t b0 = pack2(x[4 * g + 4], x[4 * g + 5]), b1 = pack2(x[4 * g + 6], x[4 * g + 7]);
     const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
@@ -99,7 +102,7 @@ __device__ __forceinline__ uint64_t elem_index(int bh, int Lq, int Lk, int qi, i
 // so that a 32-lane half reading 4 rows x 32 columns touches all 64 banks once.
 template <int HD>
 struct VImg {
-  static constexpr int LD = (HD == 32) ? 32 : 160;
+  static constexpr int LD = (HD <= 32) ? 32 : 160;
 };
 
 __device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
@@ -125,14 +128,17 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
                                                                const uint8_t* __restrict__ qmask, int H, int Lq,
                                                                int Lk, int window, float drop_p,
                                                                const uint64_t* __restrict__ seed) {
+  constexpr int HDP = HD < 32 ? 32 : HD;           // output (P·V) width: hd = 16 runs one 32-wide tile
   constexpr int NP = HD + 8, VLD = VImg<HD>::LD;
   constexpr int CH = HD / 8;                        // 16-B chunks per row
   constexpr int NLD = 2 * ROWS * CH / THREADS;      // chunks per thread and tensor for a pair of tiles
   constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
   // [2 tiles][ROWS][NP] K and [2 tiles][ROWS][VLD] V images; the K image doubles as the merge buffer at the end
-  __shared__ __attribute__((aligned(16))) __bf16 sK[2 * ROWS * NP];
+  constexpr int kMergeElems = 2 * (2 * (HDP / 32) * 16 * 64 + 4 * 64);  // bf16 elements holding the f32 merge state
+  constexpr int kSK = 2 * ROWS * NP > kMergeElems ? 2 * ROWS * NP : kMergeElems;
+  __shared__ __attribute__((aligned(16))) __bf16 sK[kSK];
   __shared__ __attribute__((aligned(16))) __bf16 sV[2 * ROWS * VLD];
-  static_assert(sizeof(__bf16) * 2 * ROWS * NP >= sizeof(float) * (2 * (HD / 32) * 16 * 64 + 4 * 64), "merge");
+  static_assert(NLD >= 1, "tile pair staging");
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int qh = wave & 1, kp = wave >> 1;
@@ -158,9 +164,13 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   for (int t = 0; t < HD / 16; ++t)
     qf[t] = qin ? *reinterpret_cast<const bf16x8*>(qrow + 16 * t + 8 * h) : zero8();
 
-  f32x16 oacc[HD / 32];
+  if (HD < HDP) {  // hd = 16: V image columns 16..31 are zeros for the whole kernel (never staged over)
+    for (int i = tid; i < 2 * ROWS; i += THREADS)
+      *reinterpret_cast<bf16x8*>(sV + i * VLD + HD) = zero8(), *reinterpret_cast<bf16x8*>(sV + i * VLD + HD + 8) = zero8();
+  }
+  f32x16 oacc[HDP / 32];
 #pragma unroll
-  for (int dt = 0; dt < HD / 32; ++dt) oacc[dt] = zero16();
+  for (int dt = 0; dt < HDP / 32; ++dt) oacc[dt] = zero16();
   float m = -INFINITY, l = 0.f;  // running max (log2 domain) and normaliser
 
   const int qhi = min(Lq, qb + ROWS) - 1;
@@ -294,7 +304,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
     l = l * alpha + rs;
     m = mnew;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
+    for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
     // Vᵀ fragment by transposed reads: lane group g (16 lanes) reads keys 16ss + 4(g>>1) + {0..3} (+8) of
@@ -307,7 +317,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
         const bf16x8 pf = acc_frag(s[c], ss);
         const int row0 = 32 * c + 16 * ss + 4 * (g >> 1) + q4;
 #pragma unroll
-        for (int dt = 0; dt < HD / 32; ++dt) {
+        for (int dt = 0; dt < HDP / 32; ++dt) {
           const __bf16* vp = myV + row0 * VLD + 32 * dt + 16 * (g & 1) + 4 * p4;
           const bf16x4 lo = tr_read(vp), hi = tr_read(vp + 8 * VLD);
           bf16x8 vf;
@@ -320,14 +330,14 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
 
   // ---- merge the two key parities of each query half (the odd-parity wave hands its state over in LDS) ----
   __syncthreads();  // every wave is done with the K / V images
-  float* cO = reinterpret_cast<float*>(sK);   // [qh][HD/32][16][64]
-  float* cM = cO + 2 * (HD / 32) * 16 * 64;   // [qh][64]
+  float* cO = reinterpret_cast<float*>(sK);   // [qh][HDP/32][16][64]
+  float* cM = cO + 2 * (HDP / 32) * 16 * 64;  // [qh][64]
   float* cL = cM + 2 * 64;
   if (kp == 1) {
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
+    for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) cO[((qh * (HD / 32) + dt) * 16 + i) * 64 + lane] = oacc[dt][i];
+      for (int i = 0; i < 16; ++i) cO[((qh * (HDP / 32) + dt) * 16 + i) * 64 + lane] = oacc[dt][i];
     cM[qh * 64 + lane] = m;
     cL[qh * 64 + lane] = l;
   }
@@ -341,10 +351,10 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
     l = l * a0 + l1 * a1;
     m = mm;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt)
+    for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
       for (int i = 0; i < 16; ++i)
-        oacc[dt][i] = oacc[dt][i] * a0 + cO[((qh * (HD / 32) + dt) * 16 + i) * 64 + lane] * a1;
+        oacc[dt][i] = oacc[dt][i] * a0 + cO[((qh * (HDP / 32) + dt) * 16 + i) * 64 + lane] * a1;
   }
 
   const bool ok = qvalid && l > 0.f;
@@ -352,10 +362,10 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   if (qin) {
     __bf16* orow = o + ((int64_t)b * Lq + qi) * ld_o + hh * HD;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt) {
+    for (int dt = 0; dt < HDP / 32; ++dt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= inv;
-      store_col32(orow + 32 * dt, oacc[dt], h);
+      store_col32<HD < 32 ? HD : 32>(orow + 32 * dt, oacc[dt], h);
     }
     if (h == 0) lse[(int64_t)bh * Lq + qi] = ok ? m * kLn2 + logf(l) : 0.f;
   }
@@ -364,7 +374,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
 }  // namespace
 
 bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o) {
-  if (!(hd == 32 || hd == 64 || hd == 128)) return false;
+  if (!(hd == 16 || hd == 32 || hd == 64 || hd == 128)) return false;
   if (Lk < 16 || Lq > (1 << 30)) return false;  // short dependency-graph sequences use the generic kernel
   return (ld_in % 8 == 0) && (ld_o % 8 == 0) && (tq >= Lq);
 }
@@ -388,7 +398,9 @@ int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
                         float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
                         int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st) {
   dim3 grid((unsigned)(cdiv(Lq, ROWS) * B * H));  // 1-D: XCD-aware (query block, batch-head) order in the kernel
-  if (hd == 32)
+  if (hd == 16)
+    launch_fwd<16>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+  else if (hd == 32)
     launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
   else if (hd == 64)
     launch_fwd<64>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);

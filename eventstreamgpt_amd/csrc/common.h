@@ -242,6 +242,18 @@ __device__ __forceinline__ bool last_arrival(int32_t* counter, int expected, int
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Kernel-selection tuning hooks (ESGPT_GEMM_*, ESGPT_ATTN_*, ESGPT_LN_*): read from the environment only in a tools
+// build (`make TUNING=1`, -DESGPT_TUNING_HOOKS, used by tools/env_sweep.sh); the product library never consults the
+// caller's environment, so its kernel choices and numerics are a function of the arguments alone.
+static inline const char* tuning_env(const char* name) {
+#ifdef ESGPT_TUNING_HOOKS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // Zero-fills `bytes` bytes at `p` on `st` with a kernel (misc.hip). Used instead of hipMemsetAsync so that every

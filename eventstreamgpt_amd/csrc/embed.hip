@@ -156,8 +156,29 @@ Buckets make_buckets(const esgpt_buckets* b) {
 // ------------------------------------------------------------------------------------------------------------
 // JOINT forward: one wave per event.
 // ------------------------------------------------------------------------------------------------------------
-template <int VEC, int GMAX>
-__global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Buckets bk, const float* __restrict__ table,
+// Table row segment (VEC consecutive elements, f32 or bf16 storage) as f32.
+template <int VEC, typename TT>
+__device__ __forceinline__ void load_row(const TT* __restrict__ table, int64_t i, int64_t D, int64_t d0, float (&r)[VEC]) {
+  if constexpr (sizeof(TT) == 4) {
+    if (VEC == 4 && d0 + 3 < D) {
+      const float4 x = *reinterpret_cast<const float4*>(table + i * D + d0);
+      r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+      return;
+    }
+  } else {
+    if (VEC == 4 && d0 + 3 < D) {  // 8-B load of 4 bf16
+      const uint2 x = *reinterpret_cast<const uint2*>(table + i * D + d0);
+      r[0] = __uint_as_float(x.x << 16), r[1] = __uint_as_float(x.x & 0xffff0000u);
+      r[2] = __uint_as_float(x.y << 16), r[3] = __uint_as_float(x.y & 0xffff0000u);
+      return;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) r[v] = (d0 + v < D) ? to_f32(table[i * D + d0 + v]) : 0.f;
+}
+
+template <int VEC, int GMAX, typename TT = float>
+__global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Buckets bk, const TT* __restrict__ table,
                                                               int64_t V, int64_t D, const float* __restrict__ sin_div,
                                                               const float* __restrict__ cos_div, int flags, float sw,
                                                               float dw, float* __restrict__ out, int32_t* err) {
@@ -208,13 +229,7 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
         const int64_t i = s_idx[wave][m];
         if (i == 0) continue;  // padding_idx=0 contributes nothing
         float r[VEC];
-        if (VEC == 4 && d0 + 3 < D) {
-          const float4 x = *reinterpret_cast<const float4*>(table + i * D + d0);
-          r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
-        } else {
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) r[v] = (d0 + v < D) ? table[i * D + d0 + v] : 0.f;
-        }
+        load_row<VEC>(table, i, D, d0, r);
 #pragma unroll
         for (int g = 0; g < GMAX; ++g) {
           if (g < G) {
@@ -235,7 +250,7 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
         const float w = s_sw[wave][s];
 #pragma unroll
         for (int v = 0; v < VEC; ++v)
-          if (d0 + v < D) st[v] = fmaf(w, table[i * D + d0 + v], st[v]);
+          if (d0 + v < D) st[v] = fmaf(w, to_f32(table[i * D + d0 + v]), st[v]);
       }
     }
     double run[VEC];
@@ -958,7 +973,15 @@ extern "C" {
 int esgpt_embed_joint_fwd(const esgpt_batch* batch, const esgpt_buckets* buckets, const float* table, int64_t V,
                           int64_t D, const float* sin_div, const float* cos_div, int flags, float static_w,
                           float dynamic_w, float* out, int32_t* err, void* stream) {
+  return esgpt_embed_joint_fwd_ex(batch, buckets, table, ESGPT_F32, V, D, sin_div, cos_div, flags, static_w, dynamic_w,
+                                  out, err, stream);
+}
+
+int esgpt_embed_joint_fwd_ex(const esgpt_batch* batch, const esgpt_buckets* buckets, const void* table,
+                             int table_dtype, int64_t V, int64_t D, const float* sin_div, const float* cos_div,
+                             int flags, float static_w, float dynamic_w, float* out, int32_t* err, void* stream) {
   ESGPT_REQUIRE(batch && table && out && D > 0 && V > 0);
+  ESGPT_REQUIRE(table_dtype == ESGPT_F32 || table_dtype == ESGPT_BF16);
   ESGPT_REQUIRE(batch->M <= kMaxM && batch->S <= kMaxM);
   ESGPT_REQUIRE(!(flags & ESGPT_EMB_TIME) || (sin_div && cos_div));
   const Buckets bk = make_buckets(buckets);
@@ -968,9 +991,17 @@ int esgpt_embed_joint_fwd(const esgpt_batch* batch, const esgpt_buckets* buckets
   dim3 grid((unsigned)cdiv(n_ev, kWavesPerBlock)), block(256);
   hipStream_t st = as_stream(stream);
   const bool vec4 = (D % 4 == 0) && D >= 256;
-#define LAUNCH_J(VEC, GM)                                                                                 \
-  embed_joint_fwd_kernel<VEC, GM><<<grid, block, 0, st>>>(*batch, bk, table, V, D, sin_div, cos_div, flags, \
-                                                          static_w, dynamic_w, out, err)
+#define LAUNCH_J(VEC, GM)                                                                                    \
+  do {                                                                                                       \
+    if (table_dtype == ESGPT_F32)                                                                            \
+      embed_joint_fwd_kernel<VEC, GM, float><<<grid, block, 0, st>>>(*batch, bk, (const float*)table, V, D,   \
+                                                                     sin_div, cos_div, flags, static_w,       \
+                                                                     dynamic_w, out, err);                    \
+    else                                                                                                     \
+      embed_joint_fwd_kernel<VEC, GM, bf16><<<grid, block, 0, st>>>(*batch, bk, (const bf16*)table, V, D,     \
+                                                                    sin_div, cos_div, flags, static_w,        \
+                                                                    dynamic_w, out, err);                     \
+  } while (0)
   if (bk.G == 1) {
     if (vec4) LAUNCH_J(4, 1); else LAUNCH_J(1, 1);
   } else if (bk.G <= 4) {

@@ -578,7 +578,7 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
 int fwd_stages() {
   static int ns = 0;
   if (ns == 0) {
-    const char* e = getenv("ESGPT_GEMM_FWD_NS");
+    const char* e = tuning_env("ESGPT_GEMM_FWD_NS");
     ns = (e && atoi(e) == 2) ? 2 : 3;
   }
   return ns;
@@ -682,7 +682,7 @@ void launch_slab_reduce(const Prob& p, hipStream_t st) {
 int in_launch_splits() {
   static int v = -1;
   if (v < 0) {
-    const char* e = getenv("ESGPT_GEMM_INLAUNCH_SPLITS");
+    const char* e = tuning_env("ESGPT_GEMM_INLAUNCH_SPLITS");
     v = e ? std::max(1, atoi(e)) : 32;
   }
   return v;
@@ -699,7 +699,7 @@ struct TileCfg {
 
 // ESGPT_GEMM_TILE_FWD / _DX / _DW = "<fm><fn>" (e.g. "22"): tuning hooks, read once; only compiled shapes accepted.
 TileCfg env_tile(const char* name, TileCfg def, const int* allowed, int n_allowed) {
-  const char* e = getenv(name);
+  const char* e = tuning_env(name);
   if (!e) return def;
   const int code = atoi(e);
   for (int i = 0; i < n_allowed; ++i)
@@ -742,7 +742,7 @@ Plan plan(int64_t M, int64_t N, int64_t K, int64_t target, TileCfg c) {
   Plan p{1, (int)(cdiv(K, BK) * BK)};
   if (K == 0 || target <= 0) return p;
   int64_t splits = 1;
-  if (const char* e = getenv("ESGPT_GEMM_SPLITS")) {  // tuning hook
+  if (const char* e = tuning_env("ESGPT_GEMM_SPLITS")) {  // tuning hook
     splits = std::max<int64_t>(1, atoi(e));
   } else {
     const int64_t tiles = n_tiles(M, N, c);
@@ -810,7 +810,7 @@ bool shapes_ok(bool akc, bool bkc, const void* A, int64_t lda, const void* B, in
 int64_t dw_target(bool has_dx, int64_t T, int64_t in, int64_t out) {
   static int64_t tgt = -1;
   if (tgt < 0) {
-    const char* e = getenv("ESGPT_GEMM_DW_TARGET");  // tuning hook: fixed dW item target (0 = the default rule)
+    const char* e = tuning_env("ESGPT_GEMM_DW_TARGET");  // tuning hook: fixed dW item target (0 = the default rule)
     tgt = e ? std::max(0, atoi(e)) : 0;
   }
   if (tgt > 0) return tgt;

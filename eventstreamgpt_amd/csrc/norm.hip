@@ -28,7 +28,7 @@ constexpr int kBwdRowsPerWave = 2;  // backward default: rows per wave, every lo
 int bwd_rows() {
   static int r = 0;
   if (r == 0) {
-    const char* e = getenv("ESGPT_LN_BWD_ROWS");
+    const char* e = tuning_env("ESGPT_LN_BWD_ROWS");
     const int v = e ? atoi(e) : kBwdRowsPerWave;
     r = (v == 2 || v == 4 || v == 8) ? v : kBwdRowsPerWave;
   }
@@ -67,7 +67,7 @@ __device__ __forceinline__ uint64_t drop_idx(int64_t row, int64_t D, int64_t col
 int fwd_rows() {
   static int r = 0;
   if (r == 0) {
-    const char* e = getenv("ESGPT_LN_FWD_ROWS");
+    const char* e = tuning_env("ESGPT_LN_FWD_ROWS");
     const int v = e ? atoi(e) : 1;
     r = (v == 1 || v == 2 || v == 4) ? v : 1;
   }

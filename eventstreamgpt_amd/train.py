@@ -409,6 +409,10 @@ class TrainStep:
             pool = torch.cuda.graph_pool_handle()
             segs = []
             cur = {"g": torch.cuda.CUDAGraph()}
+            # a segment ends on the autograd worker thread that runs the bucket hook, and the next begins there:
+            # capture sequences that cross threads must be "relaxed" (HIP refuses to end a global-mode capture
+            # from another thread)
+            mode = "relaxed" if gb is not None else "global"
             if gb is not None:
                 def boundary(buckets):  # runs on the autograd worker thread, on the capturing stream
                     dev = self.device
@@ -419,12 +423,12 @@ class TrainStep:
                     cur["g"].capture_end()
                     segs.append((cur["g"], list(buckets)))
                     cur["g"] = torch.cuda.CUDAGraph()
-                    cur["g"].capture_begin(pool=pool)
+                    cur["g"].capture_begin(pool=pool, capture_error_mode=mode)
 
                 gb.mode, gb.on_boundary = "mark", boundary
                 gb.reset()
             with torch.cuda.stream(s):
-                cur["g"].capture_begin(pool=pool)
+                cur["g"].capture_begin(pool=pool, capture_error_mode=mode)
                 loss = self._fwd_bwd(static, autocast_cache=False)
                 cur["g"].capture_end()
                 segs.append((cur["g"], []))

@@ -84,6 +84,11 @@ typedef struct {
 int esgpt_embed_joint_fwd(const esgpt_batch* batch, const esgpt_buckets* buckets, const float* table,
                           int64_t V, int64_t D, const float* sin_div, const float* cos_div, int flags,
                           float static_w, float dynamic_w, float* out, int32_t* err, void* stream);
+/* The same over a table stored as table_dtype (ESGPT_F32 or ESGPT_BF16; rows are widened to f32 and accumulated in
+ * f32): the SURVEY §8(d) bf16-table gather microbench, and a bf16 embedding table kept by the caller. */
+int esgpt_embed_joint_fwd_ex(const esgpt_batch* batch, const esgpt_buckets* buckets, const void* table,
+                             int table_dtype, int64_t V, int64_t D, const float* sin_div, const float* cos_div,
+                             int flags, float static_w, float dynamic_w, float* out, int32_t* err, void* stream);
 
 /* SPLIT_CATEGORICAL_NUMERICAL mode, the gather part of _split_embed (:390-450) for every (event, bucket):
  * x[e,g] = [cat_scale * bag_cat + static_scale * static_bag_cat , num_scale * bag_num]  (f32, [B*L*G, Dc+Dn]).
@@ -126,6 +131,13 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
                    void* stream);
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
+/* The kernel family esgpt_attn_fwd / esgpt_attn_bwd launch for these arguments (labels for measurements): MFMA
+ * (attn_fwd_mfma_kernel / attn_bwd_kernel: bf16, hd in {16, 32, 64, 128}, Lk >= 16), SMALL (one wave per (sequence,
+ * head), Lk <= 16: the dependency graph) or GENERIC (lane-per-query VALU kernels: f32, other head dims). */
+#define ESGPT_ATTN_PATH_GENERIC 0
+#define ESGPT_ATTN_PATH_MFMA 1
+#define ESGPT_ATTN_PATH_SMALL 2
+int esgpt_attn_path(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o, int dtype);
 /* Backward exchange tickets: the MFMA backward runs two workgroups per key block (even / odd query tiles) that add
  * their partial dK / dV through the workspace; `counters` (esgpt_attn_bwd_counters(B, H, Lk) int32, zeroed once
  * by the caller, left zeroed; stream-ordered use) pairs them. NULL counters: one workgroup per key block. */

@@ -1,6 +1,7 @@
 #!/bin/bash
 # C2 bench under tuning-hook settings, one process each, in one GPU session: tools/env_sweep.sh "ENV=..;ENV2=.." ...
-# ("-" = defaults). Prints ms/step (mean, median) per setting.
+# ("-" = defaults). Prints ms/step (mean, median) per setting. Needs the tools build of the library: `make -C
+# eventstreamgpt_amd/csrc TUNING=1` (the product build ignores these variables; rebuild with plain make afterwards).
 for spec in "$@"; do
   envs=()
   if [ "$spec" != "-" ]; then IFS=';' read -ra envs <<< "$spec"; fi

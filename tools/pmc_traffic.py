@@ -1,80 +1,70 @@
-"""HBM traffic per launch of the roofline kernels from two rocprofv3 PMC passes (MI355X_MICROARCH.md, HBM section):
+"""HBM traffic per launch set of each roofline entry, from two rocprofv3 PMC passes over bench.py's marker-separated
+launch sequence (MI355X_MICROARCH.md, HBM section):
 
-    rocprofv3 --pmc FETCH_SIZE -d <dirF> ... -- python bench.py --roofline-only
-    rocprofv3 --pmc WRITE_SIZE -d <dirW> ... -- python bench.py --roofline-only
-    python tools/pmc_traffic.py <dirF> <dirW> [out.json]
+    python bench.py --config C2 --roofline-only --pmc-pass gpurun_out/entries_C2.json          (no profiler: names)
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d <dirF> -- python bench.py --config C2 --roofline-only \
+        --pmc-pass gpurun_out/entries_C2.json
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d <dirW> -- python bench.py ... (same)
+    python tools/pmc_traffic.py --entries gpurun_out/entries_C2.json <dirF> <dirW> profiles/pmc_traffic_C2.json
 
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. On gfx950 FETCH_SIZE reports half the bytes of wide coalesced
-streaming reads, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores. Averages over every dispatch of a
-kernel symbol; bench.py reads bytes_per_launch[symbol] into roofline.traffic.
+bench.py ``pmc_pass`` launches, per entry, one seed_bank_kernel (the marker) and then ``reps`` launch sets of the
+entry; the dispatches between marker i and marker i + 1 (Dispatch_Id order) belong to entry i, summed and divided
+by ``reps``. FETCH_SIZE / WRITE_SIZE are KiB per dispatch; on gfx950 FETCH_SIZE reports half the bytes of wide
+coalesced streaming reads, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores. bench.py reads
+bytes_per_launch[entry] into each roofline entry's ``traffic``.
 """
 import csv
 import glob
 import json
 import sys
-from collections import defaultdict
 
-SYMBOLS = ["attn_fwd_mfma_kernel<64, true>", "attn_fwd_mfma_kernel<64, false>", "attn_bwd_kernel<64, true>",
-           "gemm_kernel<true, true, 3, 1, 1>", "gemm_bwd_pair_kernel", "embed_joint_fwd_kernel<4, 1>",
-           "attn_decode_kernel<float, 64>"]
-# kernels launched at several shapes by bench.py: keyed "<symbol>@grid<work-items>"
-BY_GRID = {"attn_decode_kernel<float, 64>"}
-# the C5 embedding microbench runs the JOINT kernel on a grid far larger than C2's: its dispatches are keyed "@c5"
-C5_GRID_MIN = 4 << 20
-# multi-kernel launch sets: bytes per set = the sum over the member kernels' dispatches / the anchor's dispatches
-GROUPS = {
-    "embed_bag_bwd": (["bag_block_sort_kernel", "bag_col_prefix_kernel", "bag_row_scan_kernel", "bag_scatter_kernel",
-                       "bag_reduce_kernel", "bag_combine_kernel", "bag_subject_part_kernel", "bag_subject_sum_kernel"],
-                      "bag_block_sort_kernel"),
-    "output_loss": (["::count_kernel(", "::event_lds_kernel<", "::event_kernel<", "::reduce_kernel(float const*"],
-                    "::count_kernel("),
-}
+MARKER = "seed_bank_kernel"
 
 
-def averages(d: str, counter: str) -> dict:
-    acc = defaultdict(list)
-    group_sum = defaultdict(float)
-    group_n = defaultdict(int)
+def dispatches(d: str, counter: str) -> list:
+    rows = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] != counter:
-                continue
-            name, val = r["Kernel_Name"], float(r["Counter_Value"])
-            grid = int(r.get("Grid_Size", 0) or 0)
-            for s in SYMBOLS:
-                if s in name:
-                    if s in BY_GRID:
-                        key = f"{s}@grid{r.get('Grid_Size', '?')}"
-                    elif s.startswith("embed_joint_fwd_kernel") and grid >= C5_GRID_MIN:
-                        key = "embed_joint_fwd_kernel@c5"
-                    else:
-                        key = s
-                    acc[key].append(val)
-            for g, (members, anchor) in GROUPS.items():
-                if any(m in name for m in members):
-                    group_sum[g] += val
-                if anchor in name:
-                    group_n[g] += 1
-    out = {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
-    for g in group_sum:
-        if group_n[g]:
-            out[g] = (group_sum[g] / group_n[g], group_n[g])
-    return out
+            if r["Counter_Name"] == counter:
+                rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    rows.sort()
+    return rows
+
+
+def per_entry(rows: list, n_entries: int, reps: int) -> tuple[list, list]:
+    """Sum of the counter over each entry's segment / reps, and the kernel names seen in it."""
+    marks = [i for i, (_, name, _) in enumerate(rows) if MARKER in name]
+    if len(marks) < n_entries + 1:
+        raise SystemExit(f"expected >= {n_entries + 1} markers, found {len(marks)}")
+    marks = marks[-(n_entries + 1):]  # the pass's markers are the last ones (warm-up launches come first)
+    vals, names = [], []
+    for i in range(n_entries):
+        seg = rows[marks[i] + 1: marks[i + 1]]
+        vals.append(sum(v for _, _, v in seg) / reps)
+        names.append(sorted({n.split("(")[0][-80:] for _, n, _ in seg}))
+    return vals, names
 
 
 def main():
-    fetch, write = averages(sys.argv[1], "FETCH_SIZE"), averages(sys.argv[2], "WRITE_SIZE")
-    out = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                     "`python bench.py --roofline-only`; bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 per dispatch "
+    if sys.argv[1] != "--entries":
+        raise SystemExit(__doc__)
+    meta = json.load(open(sys.argv[2]))
+    dir_f, dir_w = sys.argv[3], sys.argv[4]
+    path = sys.argv[5] if len(sys.argv) > 5 else f"profiles/pmc_traffic_{meta['config']}.json"
+    ents, reps = meta["entries"], meta["reps"]
+    fetch, kn = per_entry(dispatches(dir_f, "FETCH_SIZE"), len(ents), reps)
+    write, _ = per_entry(dispatches(dir_w, "WRITE_SIZE"), len(ents), reps)
+    out = {"config": meta["config"],
+           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over `python bench.py "
+                     f"--config {meta['config']} --roofline-only --pmc-pass`; per entry, the dispatches between its "
+                     f"seed_bank_kernel markers / {reps} launch sets; bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 "
                      "(gfx950 FETCH_SIZE calibration)",
            "bytes_per_launch": {}, "raw_kib": {}}
-    for s in sorted(set(fetch) | set(write)):
-        if s in fetch and s in write:
-            out["bytes_per_launch"][s] = round((2 * fetch[s][0] + write[s][0]) * 1024)
-            out["raw_kib"][s] = {"FETCH_SIZE": fetch[s][0], "WRITE_SIZE": write[s][0], "dispatches": fetch[s][1]}
-    path = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
-    with open(path, "w") as f:
-        json.dump(out, f, indent=1)
+    for e, f, w, k in zip(ents, fetch, write, kn):
+        out["bytes_per_launch"][e] = round((2 * f + w) * 1024)
+        out["raw_kib"][e] = {"FETCH_SIZE": round(f, 2), "WRITE_SIZE": round(w, 2), "kernels": k}
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
 
 
