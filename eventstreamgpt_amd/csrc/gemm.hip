@@ -194,7 +194,27 @@ struct Prob {
   int fm, fn;          // tile = (64·fm) x (64·fn): each of the 4 waves holds fm x fn 32x32 fragments
   const float* rs_extra;  // optional [rs_extra_n][M] f32 rows added into rowsum before alpha
   int rs_extra_n;
+  int xmap;  // grouped backward workgroup order: 0 = xcd_remap runs; 1 (dW) / 2 (dX) = split-major (pair_lin)
+  int rps;   // xmap 2: dX row blocks per dW split chunk
 };
+
+// Split-major order of a projection backward (xmap): workgroup id -> XCD x = id % 8 (the dispatcher's round robin),
+// slot = id / 8. XCD x takes the dW splits s ≡ x (mod 8) — every tile of each — and the dX row blocks of the same
+// token chunks, so one token chunk's dY rows (and X rows) are fetched from HBM once, by one XCD, and shared in its
+// L2 by the dW split and the dX tiles that read them (the contiguous-run order had every XCD read all of X and both
+// products read dY separately: 3.6x the algorithmic bytes at C2's c_fc). Needs dW splits % 8 == 0 and equal chunks.
+__device__ __forceinline__ int pair_lin(const Prob& p, int id) {
+  const int x = id & 7, slot = id >> 3;
+  if (p.xmap == 1) {  // dW: slot -> (k, tile), split = x + 8k
+    const int ntile = p.tm * p.tn;
+    const int k = slot / ntile, t = slot - k * ntile;
+    return t * p.splits + x + 8 * k;
+  }
+  const int per = p.rps * p.tn;  // dX tiles per token chunk
+  const int k = slot / per, rem = slot - k * per;
+  const int by = (x + 8 * k) * p.rps + rem / p.tn, bx = rem % p.tn;
+  return by * p.tn + bx;  // dX is never split
+}
 
 // Σ_b extra[b][m] (fixed order) of the optional row-sum addend.
 __device__ __forceinline__ float rowsum_extra(const Prob& p, int m) {
@@ -602,9 +622,10 @@ __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1
   __shared__ __attribute__((aligned(16))) __bf16 smem[kLds];
   const int id = blockIdx.x, n1 = p0.wg0;
   if (id < n1)
-    gemm_tile<false, false, bwd_stages<WM, WN>(), WM, WN>(p1, xcd_remap(id, n1), smem);
+    gemm_tile<false, false, bwd_stages<WM, WN>(), WM, WN>(p1, p1.xmap ? pair_lin(p1, id) : xcd_remap(id, n1), smem);
   else
-    gemm_tile<true, false, bwd_stages<XM, XN>(), XM, XN>(p0, xcd_remap(id - n1, gridDim.x - n1), smem);
+    gemm_tile<true, false, bwd_stages<XM, XN>(), XM, XN>(
+        p0, p0.xmap ? pair_lin(p0, id - n1) : xcd_remap(id - n1, gridDim.x - n1), smem);
 }
 
 // Split-K reduction as its own launch (large slab sets: one last-arriving workgroup reading every slab of its tile
@@ -893,6 +914,15 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
   }
   if (has_dx && !st_dw) {
     p0.wg0 = n_wg(p1);
+    // split-major XCD order when the token chunks line up: every dW split a full chunk, splits a multiple of the 8
+    // XCDs, each chunk a whole number of dX row blocks
+    const int bm_dx = 64 * p0.fm;
+    if (p1.splits % 8 == 0 && (int64_t)p1.splits * p1.kchunk == T && p1.kchunk % bm_dx == 0 && p0.splits == 1 &&
+        p0.tm * bm_dx == T) {
+      p1.xmap = 1;
+      p0.xmap = 2;
+      p0.rps = p1.kchunk / bm_dx;
+    }
     launch_pair(p0, p1, st);
   } else {
     if (has_dx) {
