@@ -15,9 +15,13 @@ import torch
 import torch.nn as nn
 
 
+ACT = {"name": "gelu"}
+
+
 def make(seed=0):
     torch.manual_seed(seed)
-    return nn.Sequential(nn.Linear(256, 1024), nn.GELU(), nn.Linear(1024, 256)).cuda()
+    act = {"gelu": nn.GELU(), "none": nn.Identity(), "relu": nn.ReLU()}[ACT["name"]]
+    return nn.Sequential(nn.Linear(256, 1024), act, nn.Linear(1024, 256)).cuda()
 
 
 def grads_of(m):
@@ -35,8 +39,9 @@ def fwd_bwd(m, x):
     return loss.detach()
 
 
-def run(blas: str, churn: bool, steps: int = 6, autocast: bool = True, x_grad: bool = False):
+def run(blas: str, churn: bool, steps: int = 6, autocast: bool = True, x_grad: bool = False, act: str = "gelu"):
     torch.backends.cuda.preferred_blas_library(blas)
+    ACT["name"] = act
     AUTOCAST["on"] = autocast
     xs = [torch.randn(8192, 256, device="cuda", generator=torch.Generator("cuda").manual_seed(100 + i))
           .requires_grad_(x_grad) for i in range(steps)]
@@ -63,7 +68,7 @@ def run(blas: str, churn: bool, steps: int = 6, autocast: bool = True, x_grad: b
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         sloss = fwd_bwd(m, static)
-    worst, lerr = [], []
+    worst, lerr, stale = [], [], []
     for i, x in enumerate(xs):
         with torch.no_grad():
             static.copy_(x)
@@ -71,19 +76,30 @@ def run(blas: str, churn: bool, steps: int = 6, autocast: bool = True, x_grad: b
         torch.cuda.synchronize()
         got = grads_of(m)
         worst.append([float((a - b).abs().max() / (b.abs().max() + 1e-30)) for a, b in zip(got, want[i])])
+        stale.append([float((a - b).abs().max() / (b.abs().max() + 1e-30)) for a, b in zip(got, want[0])])
         lerr.append(abs(float(sloss) - want_loss[i]) / abs(want_loss[i]))
         if churn:  # host-side allocations and frees between replays
             junk = [torch.full((1 << 22,), 1e38, device="cuda") for _ in range(8)]
             junk += [torch.empty(1 << 20, device="cuda").uniform_() for _ in range(8)]
             del junk
+    # a race between captured nodes (a reader not ordered after its producer) reads the previous replay's leftovers:
+    # replaying the same input twice would then be exact the second time
+    twice = []
+    for _ in range(2):
+        with torch.no_grad():
+            static.copy_(xs[1])
+        g.replay()
+        torch.cuda.synchronize()
+        twice.append([f"{float((a - b).abs().max() / (b.abs().max() + 1e-30)):.1e}" for a, b in zip(grads_of(m), want[1])])
     names = [n for n, _ in m.named_parameters()]
-    return {"blas": blas, "churn": churn, "autocast": autocast, "x_requires_grad": x_grad, "loss_rel_err": [f"{e:.1e}" for e in lerr],
-            "grad_rel_err_per_param": {n: [f"{w[j]:.1e}" for w in worst] for j, n in enumerate(names)}}
+    return {"same_input_replayed_twice": twice, "act": ACT["name"],"blas": blas, "churn": churn, "autocast": autocast, "x_requires_grad": x_grad, "loss_rel_err": [f"{e:.1e}" for e in lerr],
+            "grad_rel_err_per_param": {n: [f"{w[j]:.1e}" for w in worst] for j, n in enumerate(names)},
+            "vs_capture_input_grads": {n: [f"{w[j]:.1e}" for w in stale] for j, n in enumerate(names)}}
 
 
-def column_sum_case(rows: int, cols: int, steps: int = 4):
+def column_sum_case(rows: int, cols: int, steps: int = 4, dtype=torch.float32):
     """The bias-gradient reduction alone: y = x.sum(0) captured, replayed over fresh x."""
-    xs = [torch.randn(rows, cols, device="cuda", generator=torch.Generator("cuda").manual_seed(7 + i))
+    xs = [torch.randn(rows, cols, device="cuda", generator=torch.Generator("cuda").manual_seed(7 + i)).to(dtype)
           for i in range(steps)]
     static = xs[0].clone()
     s = torch.cuda.Stream()
@@ -101,8 +117,52 @@ def column_sum_case(rows: int, cols: int, steps: int = 4):
         g.replay()
         torch.cuda.synchronize()
         want = x.sum(0)
-        errs.append(float((y - want).abs().max() / want.abs().max()))
-    return {"case": f"x[{rows},{cols}].sum(0) replayed", "rel_err_per_replay": [f"{e:.1e}" for e in errs]}
+        errs.append(float((y.float() - want.float()).abs().max() / want.float().abs().max()))
+    return {"case": f"x[{rows},{cols}] {dtype}.sum(0) replayed", "rel_err_per_replay": [f"{e:.1e}" for e in errs]}
+
+
+def gelu_bias_case(steps: int = 4, x_grad: bool = False):
+    """One Linear + GELU (f32, no autocast), loss = mean(y^2): which gradient goes wrong under replay, and whether
+    it equals the capture input's gradient (a stale, not re-executed node)."""
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(256, 1024).cuda()
+    xs = [torch.randn(8192, 256, device="cuda", generator=torch.Generator("cuda").manual_seed(50 + i))
+          for i in range(steps)]
+
+    def fb(x):
+        y = torch.nn.functional.gelu(lin(x))
+        loss = y.square().mean()
+        loss.backward()
+
+    want = []
+    for x in xs:
+        lin.weight.grad = lin.bias.grad = None
+        fb(x.requires_grad_(x_grad))
+        want.append((lin.weight.grad.clone(), lin.bias.grad.clone()))
+    static = xs[0].detach().clone().requires_grad_(x_grad)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            lin.weight.grad = lin.bias.grad = None
+            fb(static)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    lin.weight.grad = lin.bias.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fb(static)
+    out = []
+    for i, x in enumerate(xs):
+        with torch.no_grad():
+            static.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        r = lambda a, b: f"{float((a - b).abs().max() / b.abs().max()):.1e}"
+        out.append({"dW": r(lin.weight.grad, want[i][0]), "db": r(lin.bias.grad, want[i][1]),
+                    "db_vs_capture_input": r(lin.bias.grad, want[0][1]),
+                    "db_accumulated": r(lin.bias.grad, sum(w[1] for w in want[: i + 1]))})
+    return {"case": f"Linear+GELU f32, x.requires_grad={x_grad}", "per_replay": out}
 
 
 def memset_node_case(replays: int = 3):
@@ -127,16 +187,18 @@ def memset_node_case(replays: int = 3):
 
 
 if __name__ == "__main__":
-    for case in (lambda: column_sum_case(8192, 1024), lambda: column_sum_case(8192, 256), memset_node_case):
+    for case in (lambda: column_sum_case(8192, 1024), lambda: column_sum_case(8192, 256),
+                 lambda: column_sum_case(8192, 1024, dtype=torch.bfloat16), memset_node_case,
+                 lambda: gelu_bias_case(x_grad=False), lambda: gelu_bias_case(x_grad=True)):
         try:
             print(json.dumps(case()), flush=True)
         except Exception as e:
             print(json.dumps({"error": repr(e)[:300]}), flush=True)
-    for blas, churn, ac, xg in (("hipblaslt", False, True, False), ("hipblaslt", False, False, False),
-                                ("cublas", False, False, False), ("hipblaslt", True, True, False),
-                                ("hipblaslt", False, True, True), ("hipblaslt", False, False, True)):
+    for blas, churn, ac, xg, act in (("hipblaslt", False, True, False, "gelu"), ("hipblaslt", False, False, False, "gelu"),
+                                     ("cublas", False, False, False, "gelu"), ("hipblaslt", True, True, False, "gelu"),
+                                     ("hipblaslt", False, False, False, "none"), ("hipblaslt", False, False, False, "relu")):
         if True:
             try:
-                print(json.dumps(run(blas, churn, autocast=ac, x_grad=xg)), flush=True)
+                print(json.dumps(run(blas, churn, autocast=ac, x_grad=xg, act=act)), flush=True)
             except Exception as e:  # report and continue with the next variant
                 print(json.dumps({"blas": blas, "churn": churn, "error": repr(e)[:300]}), flush=True)
