@@ -516,6 +516,9 @@ class TrainStep:
         else:
             segs, static, sloss, grads = entry
             static.copy_(batch, non_blocking=True)
+            if self._release is not None:  # the staging buffer is consumed: the next prefetch may refill it
+                self._release.record()
+                self._release = None
             for p, gr in zip(self.params, grads):  # the graph writes its gradients into its own pool
                 p.grad = gr
             for g, released in segs:
