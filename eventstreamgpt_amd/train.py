@@ -27,7 +27,8 @@
   copied into the graph's static buffers). A batch whose signature matches no captured graph is captured (up to
   ``max_graphs``) or run eagerly — never broadcast into the wrong buffers. A signature whose warm-up pass runs any
   ATen GEMM (a module-by-module fallback through PyTorch-ROCm BLAS, e.g. a token count the fused blocks do not
-  take) is never captured: it runs eagerly.
+  take) or any ATen reduction (whose semaphore memset does not replay correctly) is never captured: it runs
+  eagerly.
 """
 from __future__ import annotations
 
@@ -272,9 +273,17 @@ class GradBuckets:
 
 
 class _GemmSpy(torch.utils._python_dispatch.TorchDispatchMode):
-    """Records whether any ATen GEMM runs (forward or backward: the mode follows autograd into its worker threads)
-    — i.e. whether a step left the HIP kernels for a PyTorch-ROCm BLAS fallback."""
+    """Records the ATen ops of a step that must not be captured into a HIP graph (forward or backward: the mode
+    follows autograd into its worker threads):
+      * GEMMs — a step that left the HIP kernels for a PyTorch-ROCm BLAS fallback (the module-by-module path);
+      * reductions — ATen's cross-block reduce kernel zeroes its semaphores with hipMemsetAsync, and a captured
+        memset node does not re-run correctly on replay on this ROCm stack (tools/graph_blaslt_repro.py: the buffer
+        holds garbage from the second replay on; fill kernels replay correctly). That is the cause of round 1's NA
+        graph divergence: the module path's bias gradients are such column sums.
+    The library's own kernels zero-fill with kernels, never hipMemsetAsync."""
     GEMMS = ("mm", "addmm", "bmm", "baddbmm", "matmul", "linear", "_addmm_activation", "addbmm", "_scaled_mm")
+    REDUCTIONS = ("sum", "mean", "amax", "amin", "max", "min", "norm", "linalg_vector_norm", "var", "std", "prod",
+                  "any", "all", "argmax", "argmin", "logsumexp", "var_mean", "std_mean", "nansum", "aminmax")
 
     def __init__(self):
         super().__init__()
@@ -282,7 +291,7 @@ class _GemmSpy(torch.utils._python_dispatch.TorchDispatchMode):
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = func.__name__.split(".")[0]
-        if func.namespace == "aten" and name in self.GEMMS:  # torch.ops.esgpt.linear / gemm are ours
+        if func.namespace == "aten" and (name in self.GEMMS or name in self.REDUCTIONS):  # torch.ops.esgpt.* are ours
             self.hits.add(name)
         return func(*args, **(kwargs or {}))
 
@@ -316,7 +325,7 @@ class TrainStep:
         self.use_graph = use_graph and (_force_graph or graph_safe(model, compute_dtype))
         self.max_graphs = max_graphs
         self.graphs: dict = {}  # shape signature -> (segments, static batch, static loss, grads) | None (eager)
-        self.capture_report: dict = {}  # shape signature -> ATen GEMMs seen in its warm-up pass
+        self.capture_report: dict = {}  # shape signature -> ATen GEMMs / reductions seen in its warm-up pass
         self.check_errors = check_errors and dev.type == "cuda"
         # projection weight gradients on a second stream beside the rest of backward (kernels.weight_grad_overlap).
         # Off by default: measured on the C2 step (HIP graph) it gains nothing — the graph executor starts the side
@@ -374,7 +383,7 @@ class TrainStep:
     def _capture(self, batch: PytorchBatch):
         """Captures this batch signature's step (forward + backward) as HIP graph segments, or records that it
         runs eagerly (None). Two warm-up passes on a side stream first (allocator / lazy init; no collectives); the
-        first runs under _GemmSpy: a signature whose step reaches an ATen GEMM is not captured. Under DDP the
+        first runs under _GemmSpy: a signature whose step reaches an ATen GEMM or reduction is not captured. Under DDP the
         capture is cut wherever GradBuckets releases buckets, so each segment's buckets can be exchanged while the
         next segment replays."""
         if self.check_errors:
@@ -403,7 +412,7 @@ class TrainStep:
             check_errors(self.device, self._vocab)  # a warm-up error is this batch's error: raise it now
             self.opt.zero_grad(set_to_none=True)
             self.capture_report[sig] = sorted(spy.hits)
-            if spy.hits:  # a PyTorch-ROCm BLAS fallback in the step: not captured
+            if spy.hits:  # a PyTorch-ROCm BLAS fallback or ATen reduction in the step: not captured
                 self.graphs[sig] = None
                 return
             pool = torch.cuda.graph_pool_handle()

@@ -331,3 +331,27 @@ def test_deferred_colsums_match_per_layer_sums(graph, cfg_name):
     assert l0 == l1
     for k in s0:
         assert torch.equal(s0[k], s1[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["C2", "C3", "C4", "C5"])
+def test_bench_configs_capture_without_aten_gemm_or_reduction(name):
+    """The bench configurations' steps are captured (one HIP graph per signature) and their warm-up pass runs no ATen
+    GEMM and no ATen reduction (a captured reduction's semaphore memset does not replay correctly: DESIGN.md §5)."""
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS[name]
+    cfg = bc.model_config(attention_dropout=0.1, input_dropout=0.1, resid_dropout=0.1)
+    Model = (CIPPTForGenerativeSequenceModeling if cfg.structured_event_processing_mode == "conditionally_independent"
+             else NAPPTForGenerativeSequenceModeling)
+    torch.manual_seed(0)
+    m = Model(cfg).cuda().train()
+    ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=100),
+                   torch.bfloat16, use_graph=True)
+    b = bc.batch(0, batch_size=2, device="cuda").packed()
+    assert torch.isfinite(ts.step(b)).all()
+    ts.check()
+    sig = b.shape_signature()
+    assert ts.capture_report[sig] == [], ts.capture_report
+    assert ts.graphs[sig] is not None

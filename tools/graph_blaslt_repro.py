@@ -165,6 +165,91 @@ def gelu_bias_case(steps: int = 4, x_grad: bool = False):
     return {"case": f"Linear+GELU f32, x.requires_grad={x_grad}", "per_replay": out}
 
 
+def memset_sweep_case(replays: int = 4):
+    """memset_node_case over sizes and byte offsets, plus the same buffer zeroed by a fill kernel (zero_())."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = {}
+    for nbytes in (64, 1024, 16384, 1 << 20):
+        for off in (0, 4, 256):
+            for how in ("memset", "fill"):
+                base = torch.zeros((off + nbytes) // 4 + 64, device="cuda")
+                buf = base[off // 4: off // 4 + nbytes // 4]
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    if how == "memset":
+                        st = torch.cuda.current_stream().cuda_stream
+                        hip.hipMemsetAsync(ctypes.c_void_p(buf.data_ptr()), 0, ctypes.c_size_t(nbytes),
+                                           ctypes.c_void_p(st))
+                    else:
+                        buf.zero_()
+                    buf.add_(1.0)
+                vals = []
+                for _ in range(replays):
+                    g.replay()
+                    torch.cuda.synchronize()
+                    vals.append(float(buf.max()))
+                out[f"{how} {nbytes}B @+{off}"] = vals
+    return {"case": "memset / fill node + add 1, max after each replay (1.0 = node re-ran)", "results": out}
+
+
+def linear_db_by_gemm_case(steps: int = 4):
+    """The failing Linear -> GELU -> Linear case with every bias gradient computed as a GEMM (dYᵀ·1) instead of
+    ATen's cross-block column-sum reduction (whose semaphores hipMemsetAsync zeroes)."""
+
+    class Lin(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w, b):
+            ctx.save_for_backward(x, w)
+            return x @ w.t() + b
+
+        @staticmethod
+        def backward(ctx, g):
+            x, w = ctx.saved_tensors
+            ones = torch.ones(g.shape[0], 1, device=g.device, dtype=g.dtype)
+            return g @ w, g.t() @ x, (g.t() @ ones).squeeze(1)
+
+    torch.manual_seed(0)
+    l0, l2 = nn.Linear(256, 1024).cuda(), nn.Linear(1024, 256).cuda()
+    ps = [l0.weight, l0.bias, l2.weight, l2.bias]
+    xs = [torch.randn(8192, 256, device="cuda", generator=torch.Generator("cuda").manual_seed(100 + i))
+          for i in range(steps)]
+
+    def fb(x):
+        h = torch.nn.functional.gelu(Lin.apply(x, l0.weight, l0.bias))
+        Lin.apply(h, l2.weight, l2.bias).square().mean().backward()
+
+    want = []
+    for x in xs:
+        for p in ps:
+            p.grad = None
+        fb(x)
+        want.append([p.grad.clone() for p in ps])
+    static = xs[0].clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            for p in ps:
+                p.grad = None
+            fb(static)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    for p in ps:
+        p.grad = None
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        fb(static)
+    errs = []
+    for i, x in enumerate(xs):
+        static.copy_(x)
+        g.replay()
+        torch.cuda.synchronize()
+        errs.append([f"{float((p.grad - w).abs().max() / w.abs().max()):.1e}" for p, w in zip(ps, want[i])])
+    return {"case": "Linear->GELU->Linear, bias gradients as GEMMs (no ATen reduction)", "per_replay_[w0,b0,w2,b2]": errs}
+
+
 def memset_node_case(replays: int = 3):
     """hipMemsetAsync captured into a graph, followed by a kernel adding 1: after each replay the buffer holds 1 if
     the memset node re-runs, the replay count if it does not."""
@@ -188,7 +273,8 @@ def memset_node_case(replays: int = 3):
 
 if __name__ == "__main__":
     for case in (lambda: column_sum_case(8192, 1024), lambda: column_sum_case(8192, 256),
-                 lambda: column_sum_case(8192, 1024, dtype=torch.bfloat16), memset_node_case,
+                 lambda: column_sum_case(8192, 1024, dtype=torch.bfloat16), memset_node_case, memset_sweep_case,
+                 linear_db_by_gemm_case,
                  lambda: gelu_bias_case(x_grad=False), lambda: gelu_bias_case(x_grad=True)):
         try:
             print(json.dumps(case()), flush=True)
