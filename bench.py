@@ -98,7 +98,8 @@ def graph_time_ms(fn, reps: int = 20, iters: int = 5) -> float:
 
 
 def _attention_launchers(B, Lq, D, H, em, p, dev):
-    """esgpt_attn_fwd / esgpt_attn_bwd launches on preallocated packed-qkv buffers (the step's layout)."""
+    """esgpt_attn_fwd_ex / esgpt_attn_bwd_ex launches on preallocated packed-qkv buffers (the step's layout and
+    path: the forward writes the dropout keep bits the backward reads, as the attention operator does)."""
     from eventstreamgpt_amd import _lib as L
     from eventstreamgpt_amd.kernels import tickets
 
@@ -114,19 +115,22 @@ def _attention_launchers(B, Lq, D, H, em, p, dev):
     bufs["dqkv"] = torch.empty_like(bufs["qkv"])
     nbytes = lib.esgpt_attn_bwd_workspace(B, H, Lq, Lq, hd)
     bufs["ws"] = torch.empty(max(1, nbytes), dtype=torch.uint8, device=dev)
+    nkeep = lib.esgpt_attn_keep_words(B, H, Lq, Lq, hd, Lq, 3 * D, D, L.BF16, p)
+    bufs["keep"] = torch.empty(max(1, nkeep), dtype=torch.int32, device=dev)
+    kp = bufs["keep"].data_ptr() if nkeep else None
     base, dbase, m, es = bufs["qkv"].data_ptr(), bufs["dqkv"].data_ptr(), bufs["em"].data_ptr(), 2
     cnt = tickets(torch.device(dev))
 
     def fwd():
-        L.check(lib.esgpt_attn_fwd(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
-                                   bufs["lse"].data_ptr(), m, m, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
-                                   L.BF16, L.stream()), "attn_fwd")
+        L.check(lib.esgpt_attn_fwd_ex(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
+                                      bufs["lse"].data_ptr(), m, m, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
+                                      L.BF16, kp, L.stream()), "attn_fwd")
 
     def bwd():
-        L.check(lib.esgpt_attn_bwd(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
-                                   bufs["do"].data_ptr(), D, bufs["lse"].data_ptr(), m, m, dbase, dbase + D * es,
-                                   dbase + 2 * D * es, 3 * D, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
-                                   L.BF16, bufs["ws"].data_ptr(), nbytes, cnt.data_ptr(), L.stream()), "attn_bwd")
+        L.check(lib.esgpt_attn_bwd_ex(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
+                                      bufs["do"].data_ptr(), D, bufs["lse"].data_ptr(), m, m, dbase, dbase + D * es,
+                                      dbase + 2 * D * es, 3 * D, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(), kp,
+                                      L.BF16, bufs["ws"].data_ptr(), nbytes, cnt.data_ptr(), L.stream()), "attn_bwd")
 
     fwd()
     return fwd, bwd, bufs, cnt
@@ -597,11 +601,13 @@ def cpu_baseline(bc, seconds: float = 12.0) -> dict:
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import esgpt_oracle as O
     from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+    from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
 
     threads = torch.get_num_threads()
     cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
     torch.manual_seed(0)
-    m = CIPPTForGenerativeSequenceModeling(cfg)
+    m = (CIPPTForGenerativeSequenceModeling if cfg.structured_event_processing_mode == "conditionally_independent"
+         else NAPPTForGenerativeSequenceModeling)(cfg)  # the parameter layout the oracle reads
     trainable = {k for k, p in m.named_parameters() if p.requires_grad}
     params = {k: v.detach().clone().requires_grad_(k in trainable) for k, v in m.state_dict().items()}
     state = {}
