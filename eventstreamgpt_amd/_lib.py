@@ -88,7 +88,18 @@ SIGNATURES = {
     "esgpt_embed_bag_bwd": (_int, [_PB, _PK, _int, _int, _f32, _f32, _vp, _i64, _i64, _i64, _vp, _vp, _sz, _vp]),
     "esgpt_attn_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
                               _i64, _f32, _vp, _int, _vp]),
+    "esgpt_attn_keep_words": (_i64, [_i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int, _f32]),
+    "esgpt_attn_fwd_ex": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                                 _i64, _f32, _vp, _int, _vp, _vp]),
+    "esgpt_attn_bwd_ex": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _vp, _int, _vp, _sz, _vp, _vp]),
     "esgpt_attn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "esgpt_residual_fwd": (_int, [_vp, _vp, _int, _vp, _i64, _i64, _f32, _vp, _i64, _i64, _vp, _vp]),
+    "esgpt_residual_bwd": (_int, [_vp, _vp, _i64, _i64, _f32, _vp, _i64, _i64, _vp, _vp, _int, _vp]),
+    "esgpt_na_split_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "esgpt_na_split_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "esgpt_na_assemble_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "esgpt_na_assemble_bwd": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp]),
     "esgpt_attn_bwd_counters": (_i64, [_i64, _i64, _i64]),
     "esgpt_attn_bwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                               _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _int, _vp, _sz, _vp, _vp]),

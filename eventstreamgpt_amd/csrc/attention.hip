@@ -460,12 +460,13 @@ int launch_bwd_generic(const void* q, const void* k, const void* v, int64_t ld_i
 // MFMA path (attention_mfma.hip).
 int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
                         float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
-                        int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st);
+                        int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, uint32_t* keep,
+                        hipStream_t st);
 int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                         int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
                         const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
                         int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
-                        float* dq32, int32_t* counters, hipStream_t st);
+                        const uint32_t* keep, float* dq32, int32_t* counters, hipStream_t st);
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
 int64_t esgpt_attn_bwd_mfma_counters(int64_t B, int64_t H, int64_t Lk);
 bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o);
@@ -486,14 +487,32 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    float* lse, const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
                    int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
                    void* stream) {
+  return esgpt_attn_fwd_ex(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window, dropout_p,
+                           seed, dtype, nullptr, stream);
+}
+
+int64_t esgpt_attn_keep_words(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int64_t tq, int64_t ld_in,
+                              int64_t ld_o, int dtype, float dropout_p) {
+  if (!(dropout_p > 0.f) || dtype != ESGPT_BF16 || force_generic() ||
+      !esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
+    return 0;
+  return B * H * Lq * cdiv(Lk, 32);
+}
+
+int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
+                      float* lse, const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
+                      int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
+                      uint32_t* keep, void* stream) {
   ESGPT_REQUIRE(q && k && v && o && lse && hd > 0 && hd <= 128 && Lq <= Lk && Lq >= 0 && window >= 0 && tq >= Lq);
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   if (B * H * Lq == 0) return ESGPT_OK;
+  if (esgpt_attn_keep_words(B, H, Lq, Lk, hd, tq, ld_in, ld_o, dtype, dropout_p) == 0) keep = nullptr;
+  ESGPT_REQUIRE(keep == nullptr || ((uintptr_t)keep % 4) == 0);
   hipStream_t st = as_stream(stream);
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return esgpt_attn_fwd_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
-                               dropout_p, seed, st);
+                               dropout_p, seed, keep, st);
   if (Lk <= kSmallLk && !force_generic()) {
     if (dtype == ESGPT_F32)
       return launch_small<float>(true, q, k, v, ld_in, tq, o, ld_o, lse, nullptr, nullptr, 0, key_mask, query_mask,
@@ -529,7 +548,20 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
                    int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
                    int dtype, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream) {
+  return esgpt_attn_bwd_ex(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv, ld_dqkv,
+                           B, H, Lq, Lk, hd, window, dropout_p, seed, nullptr, dtype, workspace, workspace_bytes,
+                           counters, stream);
+}
+
+int esgpt_attn_bwd_ex(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                      int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                      const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
+                      int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
+                      const uint32_t* keep, int dtype, void* workspace, size_t workspace_bytes, int32_t* counters,
+                      void* stream) {
   ESGPT_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv && hd > 0 && hd <= 128 && Lq <= Lk);
+  if (esgpt_attn_keep_words(B, H, Lq, Lk, hd, tq, ld_in, ld_o, dtype, dropout_p) == 0) keep = nullptr;
+  ESGPT_REQUIRE(keep == nullptr || ((uintptr_t)keep % 4) == 0);
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   ESGPT_REQUIRE(workspace && workspace_bytes >= esgpt_attn_bwd_workspace(B, H, Lq, Lk, hd));
@@ -538,8 +570,8 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
   float* delta = (float*)workspace;
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
-                               ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, (float*)workspace, counters,
-                               st);
+                               ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, keep, (float*)workspace,
+                               counters, st);
   if (Lk <= kSmallLk && !force_generic()) {
     if (dtype == ESGPT_F32)
       return launch_small<float>(false, q, k, v, ld_in, tq, o, ld_o, nullptr, lse, dout, ld_do, key_mask, query_mask,

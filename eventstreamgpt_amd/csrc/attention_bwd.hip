@@ -120,29 +120,49 @@ template <int HD>
 struct Cfg {
   static constexpr int HDP = HD < 32 ? 32 : HD;   // image / accumulator width (hd = 16: zero-padded to 32)
   static constexpr int QT = HD == 128 ? 32 : 64;  // queries per tile
-  static constexpr int LDS_BYTES = 2 * (KB * HDP + 2 * QT * HDP + KB * QT) + 8 * QT;
+  static constexpr int NKW = KB / 32;             // keep-bit words per query row of the key block
+  // K image, Q and dO images, dS image, keep words, lse and δ
+  static constexpr int LDS_BYTES = 2 * (KB * HDP + 2 * QT * HDP + KB * QT) + 4 * QT * NKW + 8 * QT;
 };
 
-template <int HD, bool DROP>
+// Dropout in the backward: none, regenerated from the counter hash, or the forward's keep bits.
+enum : int { DROP_NONE = 0, DROP_HASH = 1, DROP_BITS = 2 };
+
+// Query tile j (counted from the first tile that can see the key block) of split s out of S: S = 1 takes every
+// tile; S = 2 deals the tiles zig-zag (s = 0: 0, 3, 4, 7, 8, …; s = 1: 1, 2, 5, 6, …), so that under a causal mask
+// (tile cost growing with its index) both splits get the same dQ work.
+__device__ __forceinline__ int split_tile(int it, int s, int S) {
+  if (S == 1) return it;
+  return 4 * (it >> 1) + ((it & 1) ? 3 - s : s);
+}
+
+// nsplit > 1: the query tiles of a key block are split (zig-zag) over two workgroups that add their partial dKᵀ / dVᵀ
+// through write-through slabs (xcnt / xbuf). DM = DROP_BITS: the forward's dropout keep bits, word
+// keep[(bh*Lq + q)*nw + key/32], bit key%32, staged in LDS with each query tile; DROP_HASH: the keep mask is
+// regenerated from the counter hash (the same bits, twice the per-tile VALU work at L = 256).
+template <int HD, int DM>
 __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
     __bf16* __restrict__ dq, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d,
     float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed,
-    int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf) {
-  constexpr int QT = Cfg<HD>::QT, HDP = Cfg<HD>::HDP;
+    const uint32_t* __restrict__ keep, int nw, int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf) {
+  using C = Cfg<HD>;
+  constexpr int QT = C::QT, HDP = C::HDP, NKW = C::NKW;
+  constexpr bool DROP = DM != DROP_NONE, bits = DM == DROP_BITS;
   using IQ = Img<HDP>;  // Q, dO, K images: [row][HDP]
   using IS = Img<QT>;   // dS image: [key][QT]
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   __bf16* sK = reinterpret_cast<__bf16*>(smem_raw);
   __bf16* sQ = sK + KB * HDP;
   __bf16* sD = sQ + QT * HDP;
   __bf16* sS = sD + QT * HDP;
-  float* sL = reinterpret_cast<float*>(sS + KB * QT);
+  uint32_t* sZ = reinterpret_cast<uint32_t*>(sS + KB * QT);  // [word][query]
+  float* sL = reinterpret_cast<float*>(sZ + NKW * QT);
   float* sDl = sL + QT;
 
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;  // transposed-read lane roles
   const int nxb = ((Lk + KB - 1) / KB) * nsplit;       // workgroups per (batch, head)
   const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the key-block halves of one (batch, head) share an XCD
@@ -150,7 +170,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const bool idx32 = (uint64_t)(gridDim.x / nxb) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;  // B·H = grid / nxb
   const int off = Lk - Lq;
-  const int kblk = (lin % nxb) / nsplit, qsplit = (lin % nxb) % nsplit;  // key block; query-tile parity
+  const int kblk = (lin % nxb) / nsplit;
+  const int split = (lin % nxb) % nsplit, S = nsplit;  // this workgroup's share of the query tiles
   const int kb0 = kblk * KB;
   const int kw0 = kb0 + 32 * wave;  // this wave's first key
   const int key = kw0 + r;
@@ -160,7 +181,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   // ---- prologue loads, all issued before any is consumed (one memory round trip): own keys' K / V fragments (B
   // operands of S and dP) and the K image of the whole key block (dQ = dS·K; rows clamped, zeroed when written) ----
   bf16x8 kf[HD / 16], vf[HD / 16];
-  constexpr int KIMG = KB * HD / 8 / THREADS;  // 16-B chunks of the K image per thread
+  constexpr int KCH = KB * HD / 8;                       // 16-B chunks of the K image
+  constexpr int KIMG = (KCH + THREADS - 1) / THREADS;  // per thread
   bf16x8 kimg[KIMG];
   {
     const int kk = min(key, Lk - 1);
@@ -173,7 +195,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     }
 #pragma unroll
     for (int i = 0; i < KIMG; ++i) {
-      const int c = tid + THREADS * i, row = c / (HD / 8), c8 = c % (HD / 8);
+      const int c = min(tid + THREADS * i, KCH - 1), row = c / (HD / 8), c8 = c % (HD / 8);
       const int kr = min(kb0 + row, Lk - 1);
       kimg[i] = *reinterpret_cast<const bf16x8*>(k + ((int64_t)b * Lk + kr) * ld_in + hh * HD + c8 * 8);
     }
@@ -197,14 +219,19 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   const int qlo = max(0, kb0 - off);
   const int qhi = window ? min(Lq - 1, kbend + window - 1 - off) : Lq - 1;
   const bool direct = dq32 == nullptr;  // this workgroup holds every key of the (batch, head)
+  auto tile_q0 = [&](int it, int s) { return (qlo / QT + split_tile(it, s, S)) * QT; };
 
-  // Query-tile prefetch: one 16-B chunk of Q, dO and O per thread (QT*HD/8 <= THREADS chunks per tile), plus the
-  // row's lse / validity for the chunk-0 thread. Issued one tile ahead, written to LDS at the top of the tile.
+  // Query-tile prefetch: one 16-B chunk of Q, dO and O per thread (QT*HD/8 <= THREADS chunks per tile), the row's
+  // lse / validity for the chunk-0 thread and one keep word per thread. Issued one tile ahead, written to LDS at the
+  // top of the tile.
   constexpr int NCHUNK = QT * HD / 8;
   const bool stager = tid < NCHUNK;  // whole waves (NCHUNK is a multiple of 64)
   const int srow = tid / (HD / 8), sc8 = tid % (HD / 8);
+  const bool zstager = bits && tid < QT * NKW;
+  const int zw = tid / QT, zrow = tid % QT;  // keep word zw of query row zrow (LDS image [word][query])
   bf16x8 pq = zero8(), pd = zero8(), po = zero8();
   float pl = INFINITY;
+  uint32_t pz = 0;
   auto prefetch = [&](int q0) {
     const int qi = q0 + srow;
     const bool in = stager && qi < Lq;
@@ -216,8 +243,10 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
       po = *reinterpret_cast<const bf16x8*>(o + ((int64_t)b * Lq + qi) * ld_o + hh * HD + sc8 * 8);
       if (sc8 == 0 && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0)) pl = lse[(int64_t)bh * Lq + qi];
     }
+    const int zq = q0 + zrow, zc = (kb0 >> 5) + zw;
+    pz = (zstager && zq < Lq && zc < nw) ? keep[((int64_t)bh * Lq + zq) * nw + zc] : 0u;
   };
-  int q0 = (qlo / QT + qsplit) * QT;  // this workgroup's tiles: every nsplit-th one
+  int q0 = tile_q0(0, split);
   if (q0 <= qhi) prefetch(q0);
   if (key >= Lk) {
 #pragma unroll
@@ -226,13 +255,14 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
 #pragma unroll
   for (int i = 0; i < KIMG; ++i) {
     const int c = tid + THREADS * i, row = c / (HD / 8), c8 = c % (HD / 8);
-    *reinterpret_cast<bf16x8*>(sK + IQ::off(row, c8 * 8)) = kb0 + row < Lk ? kimg[i] : zero8();
+    if (c < KCH) *reinterpret_cast<bf16x8*>(sK + IQ::off(row, c8 * 8)) = kb0 + row < Lk ? kimg[i] : zero8();
   }
   STAMP(1);
-  int it = 0;
 
-  for (; q0 <= qhi; q0 += nsplit * QT, ++it) {
-    __syncthreads();  // the previous tile's reads of sQ / sD / sS are done
+  for (int it = 0;; ++it) {
+    q0 = tile_q0(it, split);
+    if (q0 > qhi) break;
+    __syncthreads();  // the previous tile's reads of sQ / sD / sS / sZ are done
     STAMP(2 + 6 * it);
     if (stager) {
       *reinterpret_cast<bf16x8*>(sQ + IQ::off(srow, sc8 * 8)) = pq;
@@ -248,12 +278,17 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
         sDl[srow] = pl == INFINITY ? 0.f : dl;
       }
     }
+    if (zstager) sZ[tid] = pz;
     __syncthreads();
     STAMP(3 + 6 * it);
-    if (q0 + nsplit * QT <= qhi) prefetch(q0 + nsplit * QT);  // in flight during this tile's MFMAs
+    {
+      const int qn = tile_q0(it + 1, split);
+      if (qn <= qhi) prefetch(qn);  // in flight during this tile's MFMAs
+    }
 
-    // ---- per wave: S, dP, dV, dK for its 32 keys over the tile's queries ----
-#pragma unroll
+    // ---- per wave: S, dP, dV, dK for its 32 keys over the tile's queries (slices not interleaved: register
+    // pressure) ----
+#pragma unroll 1
     for (int qs = 0; qs < QT / 32; ++qs) {
       const int qa = q0 + 32 * qs;  // first query of the slice
       const int qpos_lo = qa + off, qpos_hi = min(qa + 31, Lq - 1) + off;
@@ -276,8 +311,10 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
         constexpr float kLog2e = 1.4426950408889634f;
         // fully visible slice: every key of the wave valid and inside the causal / local band of every query
         const bool full = __ballot(kvalid) == ~0ull && qpos_lo >= kw0 + 31 && (window == 0 || qpos_hi - kw0 < window);
-        float zk[16];  // dropout multipliers of this lane's (query row, key) elements
-        if (DROP && idx32) {  // 32-bit element indices (wave-uniform): the same hashes without 64-bit math
+        float zk[16];  // dropout multipliers of this lane's (query row, key) elements (DROP_HASH)
+        const uint32_t* zrow_w = sZ + wave * QT + 32 * qs;  // DROP_BITS: this wave's keep words of the slice's rows
+        if (bits) {
+        } else if (DROP && idx32) {  // 32-bit element indices (wave-uniform): the same hashes without 64-bit math
           if ((Lk & 1) == 0 && (kw0 & 1) == 0) {
             const int odd = key & 1;
             const uint32_t base = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)q0) * (uint32_t)Lk + (uint32_t)(key - odd);
@@ -329,7 +366,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
           const bool ok = full | (kvalid & (key <= qpos) & ((window == 0) | (qpos - key < window)));
           const float p = ok ? e : 0.f;
           if (DROP) {
-            const float z = zk[i];
+            const float z = bits ? (((zrow_w[ql - 32 * qs] >> r) & 1u) ? dr.scale : 0.f) : zk[i];
             const float dl = sDl[ql];
             s[i] = p * z;                          // P∘Z (feeds dV)
             dp[i] = p * (z * (dp[i] + dl) - dl);   // dS
@@ -411,7 +448,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   }
 
   STAMP(40);
-  // ---- the key block's two query-parity workgroups hold partial dKᵀ / dVᵀ: exchange and add ----
+  // ---- the key block's two query-split workgroups hold partial dKᵀ / dVᵀ: exchange and add ----
   // The first to finish publishes its partial (write-through sc1 stores, drained, then an sc1 flag); the second
   // polls the flag (relaxed sc1 loads + s_sleep), reads the partial with sc1 loads, adds it in registers and stores
   // the bf16 result. Two-term f32 sums commute, so the result does not depend on which one finishes first.
@@ -497,24 +534,29 @@ __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict
   *reinterpret_cast<bf16x4*>(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + d) = w;
 }
 
+template <int HD, int DM>
+int set_lds_attr() {
+  return hipFuncSetAttribute((const void*)attn_bwd_kernel<HD, DM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             Cfg<HD>::LDS_BYTES) == hipSuccess
+             ? 0
+             : 1;
+}
+
 template <int HD>
 int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
            const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask, void* dq,
            void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t window,
-           float drop_p, const uint64_t* seed, float* dq32, int32_t* counters, hipStream_t st) {
+           float drop_p, const uint64_t* seed, const uint32_t* keep, float* dq32, int32_t* counters, hipStream_t st) {
   constexpr int lds = Cfg<HD>::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute((const void*)attn_bwd_kernel<HD, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds) != hipSuccess ||
-        hipFuncSetAttribute((const void*)attn_bwd_kernel<HD, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds) != hipSuccess)
+    if (set_lds_attr<HD, DROP_NONE>() || set_lds_attr<HD, DROP_HASH>() || set_lds_attr<HD, DROP_BITS>())
       return ESGPT_ERR_LAUNCH;
     attr = true;
   }
   const int nkb = (int)cdiv(Lk, KB);
   float* acc = nkb > 1 ? dq32 : nullptr;
-  // two workgroups per key block (even / odd query tiles) when there are at least two query tiles
+  // two workgroups per key block (the zig-zag query-tile split) when there are at least two query tiles
   // (ESGPT_ATTN_BWD_NSPLIT=1: one workgroup per key block — tuning hook, read once)
   static const int max_split = [] {
     const char* e = tuning_env("ESGPT_ATTN_BWD_NSPLIT");
@@ -524,16 +566,16 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   float* xbuf = dq32 + (nkb > 1 ? (size_t)(B * H * Lq * HD) : 0);
   if (acc && zero_async(acc, sizeof(float) * (size_t)(B * H * Lq * HD), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
   const dim3 grid((unsigned)(nkb * nsplit * B * H));  // 1-D: XCD-aware order in the kernel
-  if (drop_p > 0.f)
-    attn_bwd_kernel<HD, true><<<grid, THREADS, lds, st>>>(
-        (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
-        ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,
-        (int)window, drop_p, seed, nsplit, counters, xbuf);
-  else
-    attn_bwd_kernel<HD, false><<<grid, THREADS, lds, st>>>(
-        (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout,
-        ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,
-        (int)window, drop_p, seed, nsplit, counters, xbuf);
+  const int nw = (int)cdiv(Lk, 32);
+#define ESGPT_ATTN_BWD_LAUNCH(DM_)                                                                                 \
+  attn_bwd_kernel<HD, DM_><<<grid, THREADS, lds, st>>>(                                                           \
+      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout, \
+      ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,         \
+      (int)window, drop_p, seed, keep, nw, nsplit, counters, xbuf)
+  if (!(drop_p > 0.f)) ESGPT_ATTN_BWD_LAUNCH(DROP_NONE);
+  else if (keep) ESGPT_ATTN_BWD_LAUNCH(DROP_BITS);
+  else ESGPT_ATTN_BWD_LAUNCH(DROP_HASH);
+#undef ESGPT_ATTN_BWD_LAUNCH
   if (acc) {
     const int64_t n4 = B * H * Lq * HD / 4;
     dq_convert_kernel<HD><<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(acc, (__bf16*)dq, ld_d, tq, (int)H, (int)Lq, n4);
@@ -562,16 +604,16 @@ int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
                         int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
                         const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
                         int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
-                        float* dq32, int32_t* counters, hipStream_t st) {
+                        const uint32_t* keep, float* dq32, int32_t* counters, hipStream_t st) {
   if (hd == 16)
     return launch<16>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                      window, drop_p, seed, dq32, counters, st);
+                      window, drop_p, seed, keep, dq32, counters, st);
   if (hd == 32)
     return launch<32>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                      window, drop_p, seed, dq32, counters, st);
+                      window, drop_p, seed, keep, dq32, counters, st);
   if (hd == 64)
     return launch<64>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                      window, drop_p, seed, dq32, counters, st);
+                      window, drop_p, seed, keep, dq32, counters, st);
   return launch<128>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
-                     window, drop_p, seed, dq32, counters, st);
+                     window, drop_p, seed, keep, dq32, counters, st);
 }

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
                                                                const uint8_t* __restrict__ kmask,
                                                                const uint8_t* __restrict__ qmask, int H, int Lq,
                                                                int Lk, int window, float drop_p,
-                                                               const uint64_t* __restrict__ seed) {
+                                                               const uint64_t* __restrict__ seed,
+                                                               uint32_t* __restrict__ keep, int nw) {
   constexpr int HDP = HD < 32 ? 32 : HD;           // output (P·V) width: hd = 16 runs one 32-wide tile
   constexpr int NP = HD + 8, VLD = VImg<HD>::LD;
   constexpr int CH = HD / 8;                        // 16-B chunks per row
@@ -261,6 +262,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
         s[c][i] = p;
       }
     if (DROP) {
+      uint32_t kw[2] = {0u, 0u};  // keep bits of this lane's keys, at their key position within the 32-key group
       // registers (i, i+1), i even, hold consecutive keys: one hash per pair when the pair is aligned
       if (idx32) {  // every element index of the launch fits 32 bits (wave-uniform)
         const uint32_t rowbase = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk;
@@ -279,6 +281,8 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
             }
             s[c][i] *= m0;
             s[c][i + 1] *= m1;
+            kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
+            kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
           }
       } else {
         const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
@@ -297,7 +301,17 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
             }
             s[c][i] *= m0;
             s[c][i + 1] *= m1;
+            kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
+            kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
           }
+      }
+      if (keep != nullptr) {  // the backward reads these words instead of re-hashing: word (query, key / 32)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const uint32_t w = kw[c] | (uint32_t)__shfl_xor((int)kw[c], 32, 64);
+          const int wi = (t0 >> 5) + c;
+          if (h == 0 && qin && wi < nw) keep[((int64_t)bh * Lq + qi) * nw + wi] = w;
+        }
       }
     }
     rs += __shfl_xor(rs, 32, 64);
@@ -382,29 +396,32 @@ bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, i
 template <int HD>
 static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, int64_t ld_in,
                        int64_t tq, void* o, int64_t ld_o, float* lse, const uint8_t* kmask, const uint8_t* qmask,
-                       int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed) {
+                       int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed,
+                       uint32_t* keep) {
+  const int nw = (int)cdiv(Lk, 32);
   if (drop_p > 0.f)
     attn_fwd_mfma_kernel<HD, true><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k,
                                                                     (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o,
                                                                     lse, kmask, qmask, (int)H, (int)Lq, (int)Lk,
-                                                                    (int)window, drop_p, seed);
+                                                                    (int)window, drop_p, seed, keep, nw);
   else
   attn_fwd_mfma_kernel<HD, false><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                                                            ld_in, tq, (__bf16*)o, ld_o, lse, kmask, qmask, (int)H,
-                                                           (int)Lq, (int)Lk, (int)window, drop_p, seed);
+                                                           (int)Lq, (int)Lk, (int)window, drop_p, seed, nullptr, nw);
 }
 
 int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
                         float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H, int64_t Lq,
-                        int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, hipStream_t st) {
+                        int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, uint32_t* keep,
+                        hipStream_t st) {
   dim3 grid((unsigned)(cdiv(Lq, ROWS) * B * H));  // 1-D: XCD-aware (query block, batch-head) order in the kernel
   if (hd == 16)
-    launch_fwd<16>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+    launch_fwd<16>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);
   else if (hd == 32)
-    launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+    launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);
   else if (hd == 64)
-    launch_fwd<64>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+    launch_fwd<64>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);
   else
-    launch_fwd<128>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed);
+    launch_fwd<128>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);
   return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
 }

@@ -196,10 +196,87 @@ Tensor embed_bag_bwd(const Tensor& dsrc, BATCH_ARGS, at::IntArrayRef buckets, in
   return dtable;
 }
 
+// ---- nested-attention glue + residual (structured.hip) ---------------------------------------------------------
+Tensor residual(const Tensor& x_, const Tensor& y_, const optional<Tensor>& row_mask, int64_t mask_div,
+                int64_t skip_T, double dropout_p, const optional<Tensor>& seed) {
+  const c10::DeviceGuard guard(x_.device());
+  require_hip(x_, "x");
+  Tensor x = x_.contiguous(), y = y_.contiguous();
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "esgpt.residual: x must be f32");
+  const int64_t D = y.size(-1), N = y.numel() / D;
+  Tensor rm = as_opt(row_mask, at::kBool);
+  Tensor h = at::empty({N, D}, x.options());
+  check(esgpt_residual_fwd(ptr<const float>(x), y.data_ptr(), dtype_code(y.scalar_type()),
+                           rm.defined() ? ptr<const uint8_t>(rm) : nullptr, mask_div, skip_T, (float)dropout_p,
+                           optr<const uint64_t>(seed), N, D, ptr<float>(h), stream_of(x)),
+        "residual");
+  return h;
+}
+
+std::tuple<Tensor, Tensor> residual_bwd(const Tensor& dh_, const optional<Tensor>& row_mask, int64_t mask_div,
+                                        int64_t skip_T, int64_t x_rows, bool need_dx, double dropout_p,
+                                        const optional<Tensor>& seed, at::ScalarType y_dtype) {
+  const c10::DeviceGuard guard(dh_.device());
+  Tensor dh = dh_.to(at::kFloat).contiguous();
+  const int64_t D = dh.size(-1), N = dh.numel() / D;
+  Tensor rm = as_opt(row_mask, at::kBool);
+  Tensor dy = at::empty({N, D}, dh.options().dtype(y_dtype));
+  Tensor dx = need_dx ? at::empty({x_rows, D}, dh.options()) : Tensor();
+  check(esgpt_residual_bwd(ptr<const float>(dh), rm.defined() ? ptr<const uint8_t>(rm) : nullptr, mask_div, skip_T,
+                           (float)dropout_p, optr<const uint64_t>(seed), N, D, need_dx ? ptr<float>(dx) : nullptr,
+                           dy.data_ptr(), dtype_code(y_dtype), stream_of(dh)),
+        "residual_bwd");
+  return {dx, dy};
+}
+
+Tensor na_split(const Tensor& x_, const Tensor& event_mask) {
+  const c10::DeviceGuard guard(x_.device());
+  require_hip(x_, "x");
+  Tensor x = x_.to(at::kFloat).contiguous();
+  const int64_t B = x.size(0), L = x.size(1), G = x.size(2), D = x.size(3);
+  Tensor m = as_opt(event_mask, at::kBool);
+  Tensor per = at::empty({B, L, D}, x.options());
+  check(esgpt_na_split_fwd(ptr<const float>(x), ptr<const uint8_t>(m), B * L, G, D, ptr<float>(per), stream_of(x)),
+        "na_split");
+  return per;
+}
+
+void na_split_bwd_(const Tensor& dper_, const Tensor& event_mask, Tensor dx) {
+  const c10::DeviceGuard guard(dper_.device());
+  Tensor dper = dper_.to(at::kFloat).contiguous();
+  TORCH_CHECK(dx.is_contiguous() && dx.scalar_type() == at::kFloat && dx.dim() == 4, "esgpt.na_split_bwd_: dx");
+  Tensor m = as_opt(event_mask, at::kBool);
+  check(esgpt_na_split_bwd(ptr<const float>(dper), ptr<const uint8_t>(m), dx.size(0) * dx.size(1), dx.size(2),
+                           dx.size(3), ptr<float>(dx), stream_of(dper)),
+        "na_split_bwd");
+}
+
+Tensor na_assemble(const Tensor& ctx_, const Tensor& x_) {
+  const c10::DeviceGuard guard(x_.device());
+  require_hip(x_, "x");
+  Tensor ctx = ctx_.to(at::kFloat).contiguous(), x = x_.to(at::kFloat).contiguous();
+  const int64_t B = x.size(0), L = x.size(1), G = x.size(2), D = x.size(3);
+  Tensor seq = at::empty({B * L, G + 1, D}, x.options());
+  check(esgpt_na_assemble_fwd(ptr<const float>(ctx), ptr<const float>(x), B, L, G, D, ptr<float>(seq), stream_of(x)),
+        "na_assemble");
+  return seq;
+}
+
+std::tuple<Tensor, Tensor> na_assemble_bwd(const Tensor& dseq_, int64_t B, int64_t L) {
+  const c10::DeviceGuard guard(dseq_.device());
+  Tensor dseq = dseq_.to(at::kFloat).contiguous();
+  const int64_t G = dseq.size(-2) - 1, D = dseq.size(-1);
+  Tensor dctx = at::empty({B, L, D}, dseq.options());
+  Tensor dx = at::empty({B, L, G, D}, dseq.options());  // level G-1: esgpt.na_split_bwd_
+  check(esgpt_na_assemble_bwd(ptr<const float>(dseq), B, L, G, D, ptr<float>(dctx), ptr<float>(dx), stream_of(dseq)),
+        "na_assemble_bwd");
+  return {dctx, dx};
+}
+
 // ---- attention (packed qkv [Bs, T, 3D]) ------------------------------------------------------------------------
-std::tuple<Tensor, Tensor> attention(const Tensor& qkv_, const optional<Tensor>& key_mask,
-                                     const optional<Tensor>& query_mask, int64_t H, int64_t window,
-                                     bool static_kv_first, double dropout_p, const optional<Tensor>& seed) {
+std::tuple<Tensor, Tensor, Tensor> attention(const Tensor& qkv_, const optional<Tensor>& key_mask,
+                                             const optional<Tensor>& query_mask, int64_t H, int64_t window,
+                                             bool static_kv_first, double dropout_p, const optional<Tensor>& seed) {
   const c10::DeviceGuard guard(qkv_.device());
   require_hip(qkv_, "qkv");
   Tensor qkv = qkv_.contiguous();
@@ -210,17 +287,23 @@ std::tuple<Tensor, Tensor> attention(const Tensor& qkv_, const optional<Tensor>&
   Tensor km = as_opt(key_mask, at::kBool), qm = as_opt(query_mask, at::kBool);
   Tensor o = at::empty({Bs, Lq, D}, qkv.options());
   Tensor lse = at::empty({Bs, H, Lq}, qkv.options().dtype(at::kFloat));
-  check(esgpt_attn_fwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
-                       ptr<float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
-                       qm.defined() ? ptr<const uint8_t>(qm) : nullptr, Bs, H, Lq, Lk, hd, window, (float)dropout_p,
-                       optr<const uint64_t>(seed), dtype_code(qkv.scalar_type()), stream_of(qkv)),
+  // the dropout keep bits the MFMA forward draws, for the backward (empty when the path does not use them)
+  const int64_t nkeep = esgpt_attn_keep_words(Bs, H, Lq, Lk, hd, T, D3, D, dtype_code(qkv.scalar_type()),
+                                              (float)dropout_p);
+  Tensor keep = at::empty({nkeep}, qkv.options().dtype(at::kInt));
+  check(esgpt_attn_fwd_ex(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                          ptr<float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
+                          qm.defined() ? ptr<const uint8_t>(qm) : nullptr, Bs, H, Lq, Lk, hd, window,
+                          (float)dropout_p, optr<const uint64_t>(seed), dtype_code(qkv.scalar_type()),
+                          nkeep ? reinterpret_cast<uint32_t*>(keep.data_ptr()) : nullptr, stream_of(qkv)),
         "attention");
-  return {o, lse};
+  return {o, lse, keep};
 }
 
 Tensor attention_bwd(const Tensor& qkv_, const Tensor& o, const Tensor& dout_, const Tensor& lse,
                      const optional<Tensor>& key_mask, const optional<Tensor>& query_mask, int64_t H, int64_t window,
-                     bool static_kv_first, double dropout_p, const optional<Tensor>& seed, const Tensor& tickets) {
+                     bool static_kv_first, double dropout_p, const optional<Tensor>& seed,
+                     const optional<Tensor>& keep, const Tensor& tickets) {
   const c10::DeviceGuard guard(qkv_.device());
   Tensor qkv = qkv_.contiguous();
   Tensor dout = dout_.to(qkv.scalar_type()).contiguous();
@@ -234,11 +317,20 @@ Tensor attention_bwd(const Tensor& qkv_, const Tensor& o, const Tensor& dout_, c
   Tensor km = as_opt(key_mask, at::kBool), qm = as_opt(query_mask, at::kBool);
   char* base = reinterpret_cast<char*>(qkv.data_ptr());
   char* dbase = reinterpret_cast<char*>(dqkv.data_ptr());
-  check(esgpt_attn_bwd(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D, dout.data_ptr(),
-                       D, ptr<const float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
-                       qm.defined() ? ptr<const uint8_t>(qm) : nullptr, dbase + skf * D3 * es, dbase + D * es,
-                       dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd, window, (float)dropout_p, optr<const uint64_t>(seed),
-                       dtype_code(qkv.scalar_type()), ws.data_ptr(), nb, counters, stream_of(qkv)),
+  const int64_t nkeep = esgpt_attn_keep_words(Bs, H, Lq, Lk, hd, T, D3, D, dtype_code(qkv.scalar_type()),
+                                              (float)dropout_p);
+  const uint32_t* kp = nullptr;
+  if (nkeep && keep.has_value() && keep->defined() && keep->numel() == nkeep) {
+    TORCH_CHECK(keep->scalar_type() == at::kInt && keep->is_contiguous() && keep->device() == qkv.device(),
+                "esgpt.attention_bwd: keep must be the int32 tensor attention returned");
+    kp = reinterpret_cast<const uint32_t*>(keep->data_ptr());
+  }
+  check(esgpt_attn_bwd_ex(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+                          dout.data_ptr(), D, ptr<const float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
+                          qm.defined() ? ptr<const uint8_t>(qm) : nullptr, dbase + skf * D3 * es, dbase + D * es,
+                          dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd, window, (float)dropout_p,
+                          optr<const uint64_t>(seed), kp, dtype_code(qkv.scalar_type()), ws.data_ptr(), nb, counters,
+                          stream_of(qkv)),
         "attention_bwd");
   return dqkv;
 }
@@ -703,9 +795,17 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("embed_bag_bwd(Tensor dsrc, " BATCH_SCHEMA ", int[] buckets, int selector, int flags, float dyn_scale, "
         "float static_scale, int ld, int D, int V, int G) -> Tensor");
   m.def("attention(Tensor qkv, Tensor? key_mask, Tensor? query_mask, int H, int window, bool static_kv_first, "
-        "float dropout_p, Tensor? seed) -> (Tensor, Tensor)");
+        "float dropout_p, Tensor? seed) -> (Tensor, Tensor, Tensor)");
   m.def("attention_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor? key_mask, Tensor? query_mask, int H, "
-        "int window, bool static_kv_first, float dropout_p, Tensor? seed, Tensor tickets) -> Tensor");
+        "int window, bool static_kv_first, float dropout_p, Tensor? seed, Tensor? keep, Tensor tickets) -> Tensor");
+  m.def("residual(Tensor x, Tensor y, Tensor? row_mask, int mask_div, int skip_T, float dropout_p, Tensor? seed) "
+        "-> Tensor");
+  m.def("residual_bwd(Tensor dh, Tensor? row_mask, int mask_div, int skip_T, int x_rows, bool need_dx, "
+        "float dropout_p, Tensor? seed, ScalarType y_dtype) -> (Tensor, Tensor)");
+  m.def("na_split(Tensor x, Tensor event_mask) -> Tensor");
+  m.def("na_split_bwd_(Tensor dper, Tensor event_mask, Tensor(a!) dx) -> ()");
+  m.def("na_assemble(Tensor ctx, Tensor x) -> Tensor");
+  m.def("na_assemble_bwd(Tensor dseq, int B, int L) -> (Tensor, Tensor)");
   m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, int past) -> ()");
   m.def("attn_decode(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor? key_mask, Tensor? query_mask, int H, "
         "int Lk, int window) -> Tensor");
@@ -749,6 +849,12 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("embed_epilogue", &embed_epilogue);
   m.impl("embed_epilogue_bwd", &embed_epilogue_bwd);
   m.impl("embed_bag_bwd", &embed_bag_bwd);
+  m.impl("residual", &residual);
+  m.impl("residual_bwd", &residual_bwd);
+  m.impl("na_split", &na_split);
+  m.impl("na_split_bwd_", &na_split_bwd_);
+  m.impl("na_assemble", &na_assemble);
+  m.impl("na_assemble_bwd", &na_assemble_bwd);
   m.impl("attention", &attention);
   m.impl("attention_bwd", &attention_bwd);
   m.impl("kv_append", &kv_append);

@@ -35,6 +35,14 @@ def residual_ln(x, y, bias, ln_w, ln_b, row_mask, p: float, eps: float, out_dtyp
     return h, out
 
 
+def residual(x, y, row_mask, mask_div: int, skip_T: int, p: float):
+    """``esgpt::residual``: h = mask(r) ? x[xr(r)] + dropout(y[r]) : 0 (f32), mask(r) = row_mask[r // mask_div];
+    with skip_T = T the rows of x [Bs, T, D] after each first one. Differentiable in x and y."""
+    seed = next_dropout_seed(y.device) if p > 0 else None
+    with _timed("residual_fwd"):
+        return _ops().residual(x, y, row_mask, int(mask_div), int(skip_T), float(p), seed)
+
+
 class ResidualLNFn:
     """Call-compatible name of ``residual_ln``."""
 
@@ -352,12 +360,14 @@ class _SkipFirst(torch.autograd.Function):
         return torch.nn.functional.pad(d.view(Bs, T - 1, D), (0, 0, 1, 0))
 
 
-def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_first: bool) -> torch.Tensor:
+def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_first: bool, out_row_mask=None,
+                      out_mask_div: int = 1) -> torch.Tensor:
     """``InnerBlock.forward`` (``transformer.py:409-461``, pre-LN attention + MLP with residuals) through the HIP
     kernels: LayerNorm, one packed-QKV GEMM, attention, out_proj with its bias + residual dropout + the second
-    LayerNorm fused, the MLP GEMMs (bias + activation epilogue) — the same pieces as the fused CI encoder, for a
-    stand-alone block (the NA sequence and dependency-graph modules). ``hidden`` [Bs, T, D] f32; returns
-    [Bs, T - skf, D] f32."""
+    LayerNorm fused, the MLP GEMMs (bias + activation epilogue), the last residual + dropout as one kernel — the same
+    pieces as the fused CI encoder, for a stand-alone block (the NA sequence and dependency-graph modules).
+    ``hidden`` [Bs, T, D] f32; returns [Bs, T - skf, D] f32. ``out_row_mask`` (bool, one entry per ``out_mask_div``
+    output rows): rows of masked-out events are zeros (StructuredAttention's event-mask wheres, fused)."""
     att = blk.attn.attention
     Bs, T, D = hidden.shape
     skf = 1 if static_kv_first else 0
@@ -382,5 +392,5 @@ def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_fir
         res = x2 if skf == 0 else _SkipFirst.apply(hidden.float())
         h1, ln2 = residual_ln(res, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt)
         y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name], with_bias=True)
-        out = h1 + F.dropout(y2.float(), p=p_res, training=train)
+        out = residual(h1, y2, out_row_mask, out_mask_div, 0, p_res)
     return out.view(Bs, Tq, D)

@@ -439,7 +439,7 @@ def attention(qkv, key_mask, query_mask, H: int, window: int, static_kv_first: b
         raise L.HipExtensionMissing("eventstreamgpt_amd: attention needs a HIP device tensor (no CPU path)")
     seed = next_dropout_seed(qkv.device) if dropout_p > 0 else None
     with _timed("attn_fwd"):
-        o, _lse = _ops().attention(qkv, key_mask, query_mask, H, window, bool(static_kv_first), float(dropout_p),
+        o, _lse, _keep = _ops().attention(qkv, key_mask, query_mask, H, window, bool(static_kv_first), float(dropout_p),
                                    seed)
     return o
 

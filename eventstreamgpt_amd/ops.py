@@ -22,6 +22,11 @@ Differentiable operators and the reference code they replace:
 ``head_loss``         the generative heads' GEMM + ``output_loss`` (model_output.py:1253-1721)
 ====================  =====================================================================================
 
+``residual``          InnerBlock's last residual (+ the event-mask where of the NA glue; transformer.py:409-461)
+
+Used by the NA glue's autograd Functions (transformer/structured_attention.py): ``na_split`` / ``na_split_bwd_``,
+``na_assemble`` / ``na_assemble_bwd`` (structured_attention.py:63-156).
+
 Non-differentiable: ``embed_bag_bwd``, ``embed_epilogue_bwd``, ``attention_bwd``, ``residual_ln_bwd``,
 ``bias_act_bwd``, ``linear_act``, ``linear_bwd`` (+ ``weight_grad_join``: with ``dw_tickets`` the weight gradient
 runs on a second stream, joined by that op), ``gemm`` / ``gemm_``, ``column_sum``, ``kv_append``,
@@ -45,7 +50,8 @@ _state = {"loaded": False}
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
-       "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank")
+       "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank", "residual",
+       "residual_bwd", "na_split", "na_split_bwd_", "na_assemble", "na_assemble_bwd")
 
 
 def load():
@@ -128,11 +134,45 @@ def _register():
     def _(qkv, key_mask, query_mask, H, window, skf, p, seed):
         Bs, T, D3 = qkv.shape
         Lq = T - (1 if skf else 0)
-        return qkv.new_empty(Bs, Lq, D3 // 3), qkv.new_empty(Bs, H, Lq, dtype=torch.float32)
+        # keep bits: the MFMA path (bf16, hd in {16, 32, 64, 128}, Lk >= 16) with dropout (esgpt_attn_keep_words)
+        hd = D3 // 3 // H
+        nkeep = Bs * H * Lq * ((T + 31) // 32) if (p > 0 and qkv.dtype == torch.bfloat16 and hd in (16, 32, 64, 128)
+                                                    and T >= 16) else 0
+        return (qkv.new_empty(Bs, Lq, D3 // 3), qkv.new_empty(Bs, H, Lq, dtype=torch.float32),
+                qkv.new_empty(nkeep, dtype=torch.int32))
 
     @fake(lib + "attention_bwd")
-    def _(qkv, o, dout, lse, key_mask, query_mask, H, window, skf, p, seed, tickets):
+    def _(qkv, o, dout, lse, key_mask, query_mask, H, window, skf, p, seed, keep, tickets):
         return torch.empty_like(qkv)
+
+    @fake(lib + "residual")
+    def _(x, y, row_mask, mask_div, skip_T, p, seed):
+        D = y.shape[-1]
+        return x.new_empty(y.numel() // D, D, dtype=torch.float32)
+
+    @fake(lib + "residual_bwd")
+    def _(dh, row_mask, mask_div, skip_T, x_rows, need_dx, p, seed, y_dtype):
+        D = dh.shape[-1]
+        dx = dh.new_empty(x_rows, D, dtype=torch.float32) if need_dx else None
+        return dx, dh.new_empty(dh.numel() // D, D, dtype=y_dtype)
+
+    @fake(lib + "na_split")
+    def _(x, event_mask):
+        return x.new_empty(x.shape[0], x.shape[1], x.shape[3], dtype=torch.float32)
+
+    @fake(lib + "na_split_bwd_")
+    def _(dper, event_mask, dx):
+        return None
+
+    @fake(lib + "na_assemble")
+    def _(ctx, x):
+        B, L, G, D = x.shape
+        return x.new_empty(B * L, G + 1, D, dtype=torch.float32)
+
+    @fake(lib + "na_assemble_bwd")
+    def _(dseq, B, L):
+        G1, D = dseq.shape[-2], dseq.shape[-1]
+        return dseq.new_empty(B, L, D, dtype=torch.float32), dseq.new_empty(B, L, G1 - 1, D, dtype=torch.float32)
 
     @fake(lib + "kv_append")
     def _(qkv, k_cache, v_cache, past):
@@ -313,24 +353,42 @@ def _register():
 
     reg(lib + "embed_epilogue", _ee_bwd, setup_context=_ee_setup)
 
-    # attention: d qkv (one fused MFMA backward; the dropout keep-mask is regenerated from the same seed)
+    # attention: d qkv (one fused MFMA backward reading the forward's dropout keep bits; the other paths regenerate
+    # the keep mask from the same seed)
     def _at_setup(ctx, inputs, output):
         qkv, km, qm, H, window, skf, p, seed = inputs
-        o, lse = output
-        ctx.mark_non_differentiable(lse)
+        o, lse, keep = output
+        ctx.mark_non_differentiable(lse, keep)
         ctx.set_materialize_grads(False)
-        ctx.save_for_backward(qkv, o, lse, km, qm, seed)
+        ctx.save_for_backward(qkv, o, lse, km, qm, seed, keep)
         ctx.meta = (H, window, skf, p)
 
-    def _at_bwd(ctx, do, _dlse):
+    def _at_bwd(ctx, do, _dlse, _dkeep):
         if do is None:
             return (None,) * 8
-        qkv, o, lse, km, qm, seed = ctx.saved_tensors
+        qkv, o, lse, km, qm, seed, keep = ctx.saved_tensors
         H, window, skf, p = ctx.meta
-        dqkv = ops.attention_bwd(qkv, o, do, lse, km, qm, H, window, skf, p, seed, _tickets(qkv.device))
+        dqkv = ops.attention_bwd(qkv, o, do, lse, km, qm, H, window, skf, p, seed, keep, _tickets(qkv.device))
         return dqkv, None, None, None, None, None, None, None
 
     reg(lib + "attention", _at_bwd, setup_context=_at_setup)
+
+    # residual: d x (all rows of x; zeros for the rows skip_T leaves out), d y (y's dtype)
+    def _rs_setup(ctx, inputs, output):
+        x, y, row_mask, mask_div, skip_T, p, seed = inputs
+        ctx.save_for_backward(row_mask, seed)
+        ctx.meta = (mask_div, skip_T, x.numel() // x.shape[-1], p, y.dtype, tuple(x.shape), tuple(y.shape))
+        ctx.set_materialize_grads(False)
+
+    def _rs_bwd(ctx, dh):
+        if dh is None:
+            return (None,) * 7
+        row_mask, seed = ctx.saved_tensors
+        mask_div, skip_T, x_rows, p, y_dtype, xs, ys = ctx.meta
+        dx, dy = ops.residual_bwd(dh, row_mask, mask_div, skip_T, x_rows, ctx.needs_input_grad[0], p, seed, y_dtype)
+        return (None if dx is None else dx.view(xs)), dy.view(ys), None, None, None, None, None
+
+    reg(lib + "residual", _rs_bwd, setup_context=_rs_setup)
 
     # residual_ln: d x, d y, d bias, d ln_w, d ln_b (column sums in the same launch)
     def _rl_setup(ctx, inputs, output):

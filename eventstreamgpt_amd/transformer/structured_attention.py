@@ -63,6 +63,63 @@ class _Assemble(torch.autograd.Function):
         return d_ctx, d[:, :, 1:-1, :]
 
 
+class _NASplit(torch.autograd.Function):
+    """per_event = event_mask ? x[:, :, G-1] : 0 (``esgpt::na_split``). The gradient of x is assembled in ONE buffer:
+    levels 0 .. G-2 come from ``_NAAssemble``'s backward (which always runs first: the sequence module's input
+    gradient depends on it) through ``holder``; this backward writes level G-1 into it (``esgpt::na_split_bwd_``)."""
+
+    @staticmethod
+    def forward(ctx, x, event_mask, holder):
+        from ..kernels import _ops
+
+        ctx.save_for_backward(event_mask)
+        ctx.holder, ctx.shape = holder, x.shape
+        return _ops().na_split(x, event_mask)
+
+    @staticmethod
+    def backward(ctx, dper):
+        from ..kernels import _ops
+
+        (em,) = ctx.saved_tensors
+        dx = ctx.holder.pop("dx", None)
+        if dx is None:  # the dependency-graph sequence got no gradient: its levels contribute zeros
+            dx = dper.new_zeros(ctx.shape, dtype=torch.float32)
+        _ops().na_split_bwd_(dper, em, dx)
+        return dx, None, None
+
+
+class _NAAssemble(torch.autograd.Function):
+    """The dependency-graph sequence [h_{i-1}, e_{i,1} .. e_{i,G-1}, ctx_i] per event (structured_attention.py:
+    125-149) in one kernel (``esgpt::na_assemble``): ctx (the masked sequence-module output) shifted by one event
+    for the history, x's first G-1 levels, ctx. Backward (``esgpt::na_assemble_bwd``): d ctx, and levels 0 .. G-2
+    of d x handed to ``_NASplit`` through ``holder`` (x's gradient is returned there, not here)."""
+
+    @staticmethod
+    def forward(ctx, ctx_emb, x, holder):
+        from ..kernels import _ops
+
+        ctx.holder, ctx.BL = holder, (x.shape[0], x.shape[1])
+        return _ops().na_assemble(ctx_emb, x)
+
+    @staticmethod
+    def backward(ctx, dseq):
+        from ..kernels import _ops
+
+        dctx, dx = _ops().na_assemble_bwd(dseq.contiguous(), ctx.BL[0], ctx.BL[1])
+        ctx.holder["dx"] = dx
+        return dctx, None, None
+
+
+def _glue_fast_path(module, hidden_states, event_mask, seq_kwargs, dep_kwargs, prepend, update_last) -> bool:
+    """The training path (history prepended, no caches) with both modules full InnerBlocks on a HIP f32 tensor:
+    the split / assemble / mask steps run as the esgpt glue kernels."""
+    from .transformer import InnerBlock
+
+    return (prepend and update_last and event_mask is not None and not seq_kwargs and not dep_kwargs
+            and isinstance(module.seq_module, InnerBlock) and isinstance(module.dep_graph_module, InnerBlock)
+            and hidden_states.is_cuda and hidden_states.dtype == torch.float32 and hidden_states.shape[-1] % 4 == 0)
+
+
 class StructuredAttention(torch.nn.Module):
     def __init__(self, seq_module: torch.nn.Module, dep_graph_module: torch.nn.Module):
         super().__init__()
@@ -79,6 +136,20 @@ class StructuredAttention(torch.nn.Module):
         bsz, seq_len, dep_graph_len, hidden_size = hidden_states.shape
         m3 = None if event_mask is None else event_mask.unsqueeze(-1)
         seq_ret = None
+
+        if _glue_fast_path(self, hidden_states, event_mask, seq_module_kwargs, dep_graph_module_kwargs,
+                           prepend_graph_with_history_embeddings, update_last_graph_el_to_history_embedding):
+            kpm = (seq_attention_mask.reshape(bsz, -1) == 0) if seq_attention_mask is not None else event_mask
+            em = event_mask.contiguous()
+            x = hidden_states.contiguous()
+            holder: dict = {}
+            per_event = _NASplit.apply(x, em, holder)
+            ctx, seq_ret = self.seq_module(per_event, key_padding_mask=kpm, out_row_mask=em.reshape(-1))
+            dep_graph_seq = _NAAssemble.apply(ctx, x, holder)
+            out, dep_ret = self.dep_graph_module(dep_graph_seq, attention_mask=None, static_kv_first=True,
+                                                 out_row_mask=em.reshape(-1), out_mask_div=dep_graph_len)
+            return (out.reshape(bsz, seq_len, dep_graph_len, hidden_size),
+                    {"seq_module": seq_ret, "dep_graph_module": dep_ret})
 
         if prepend_graph_with_history_embeddings or update_last_graph_el_to_history_embedding:
             # key padding of the sequence module: the additive mask covers past + new events when a cache is used

@@ -189,7 +189,10 @@ class InnerBlock(nn.Module):
         self.mlp = InnerMLP(config)
 
     def forward(self, hidden_states, attention_mask=None, layer_past=None, head_mask=None, use_cache=False,
-                output_attentions=False, static_kv_first: bool = False, key_padding_mask=None):
+                output_attentions=False, static_kv_first: bool = False, key_padding_mask=None, out_row_mask=None,
+                out_mask_div: int = 1):
+        """``out_row_mask`` (this package's StructuredAttention only): output rows r with
+        ``out_row_mask[r // out_mask_div]`` False are zeros (the reference's event-mask ``where`` after the module)."""
         from ..fused import block_fused_supported, inner_block_fused
 
         if (layer_past is None and not use_cache and not output_attentions and head_mask is None
@@ -197,7 +200,7 @@ class InnerBlock(nn.Module):
             kpm = key_padding_mask
             if kpm is None and attention_mask is not None:
                 kpm = attention_mask.reshape(attention_mask.shape[0], -1) == 0
-            return inner_block_fused(self, hidden_states, kpm, static_kv_first), {}
+            return inner_block_fused(self, hidden_states, kpm, static_kv_first, out_row_mask, out_mask_div), {}
         residual = hidden_states if not static_kv_first else hidden_states[:, 1:, :]
         attn_output, outputs = self.attn(hidden_states, attention_mask=attention_mask, layer_past=layer_past,
                                          head_mask=head_mask, use_cache=use_cache,
@@ -205,6 +208,9 @@ class InnerBlock(nn.Module):
                                          key_padding_mask=key_padding_mask)
         hidden_states = attn_output + residual
         hidden_states = hidden_states + self.mlp(self.layer_norm(hidden_states))
+        if out_row_mask is not None:
+            keep = out_row_mask.reshape(-1).repeat_interleave(out_mask_div).view(hidden_states.shape[:-1] + (1,))
+            hidden_states = torch.where(keep, hidden_states, 0.0)
         if not use_cache:
             outputs.pop("present_key_value")
         return hidden_states, outputs

@@ -130,6 +130,17 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
                    int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
                    void* stream);
+/* The same, also writing the dropout keep bits the MFMA forward drew, for esgpt_attn_bwd_ex to read instead of
+ * re-hashing them: keep (uint32, esgpt_attn_keep_words(...) words, caller-owned) holds bit (key % 32) of word
+ * (bh*Lq + i)*ceil(Lk/32) + key/32 = keep(b, h, i, key) for every (query, key) pair the forward computed (pairs it
+ * skips — masked, outside the causal / local band — are left unwritten and never read as kept). keep may be NULL,
+ * and is ignored when esgpt_attn_keep_words returns 0 (no dropout, or not the MFMA path). */
+int64_t esgpt_attn_keep_words(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int64_t tq, int64_t ld_in,
+                              int64_t ld_o, int dtype, float dropout_p);
+int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
+                      float* lse, const uint8_t* key_mask, const uint8_t* query_mask, int64_t B, int64_t H, int64_t Lq,
+                      int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed, int dtype,
+                      uint32_t* keep, void* stream);
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
 /* The kernel family esgpt_attn_fwd / esgpt_attn_bwd launch for these arguments (labels for measurements): MFMA
  * (attn_fwd_mfma_kernel / attn_bwd_kernel: bf16, hd in {16, 32, 64, 128}, Lk >= 16), SMALL (one wave per (sequence,
@@ -148,6 +159,13 @@ int esgpt_attn_bwd(const void* q, const void* k, const void* v, int64_t ld_in, i
                    const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
                    int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
                    int dtype, void* workspace, size_t workspace_bytes, int32_t* counters, void* stream);
+/* The same reading the forward's keep bits (esgpt_attn_fwd_ex; NULL: regenerate them from the seed). */
+int esgpt_attn_bwd_ex(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                      int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                      const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
+                      int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
+                      const uint32_t* keep, int dtype, void* workspace, size_t workspace_bytes, int32_t* counters,
+                      void* stream);
 
 /* ---- Generation: KV-cache decode -------------------------------------------------------------------------
  * InnerSelfAttention.forward with layer_past / use_cache (transformer.py:261-268 + _attn :171-217), driven by
@@ -260,6 +278,33 @@ int esgpt_bias_act_bwd(const void* dg, const void* f, const float* bias, int act
  * (deterministic). part: f32 workspace [esgpt_column_sum_partials(N), F]. */
 int64_t esgpt_column_sum_partials(int64_t N);
 int esgpt_column_sum(const void* x, int dtype, int64_t N, int64_t F, float* part, float* out, void* stream);
+
+/* ---- Nested-attention glue (structured.hip) -----------------------------------------------------------------
+ * StructuredAttention.forward's tensor shuffles (structured_attention.py:28-219: the sequence module on each event's
+ * last graph element, the dependency-graph sequence [h_{i-1}, e_{i,1} .. e_{i,G-1}, ctx_i], the event-mask wheres) and
+ * the InnerBlock residual (transformer.py:409-461), f32 [rows, D] with D % 4 == 0, 16-B aligned.
+ * esgpt_residual_fwd: h[r] = mask(r) ? x[xr(r)] + dropout(y[r]) : 0, mask(r) = row_mask[r / mask_div] (NULL: all);
+ *   xr(r) = r, or with skip_T = T > 1 the rows of x = [N / (T-1), T, D] after each first one (static_kv_first
+ *   residual, transformer.py:437); y f32 or bf16; dropout as the other kernels (counter hash of r·D + c).
+ * esgpt_residual_bwd: dy = mask ? dropout'(dh) : 0 (y's dtype); dx (may be NULL) over all rows of x, zeros where no
+ *   output reads them.
+ * esgpt_na_split_fwd: per[e] = event_mask[e] ? x[e, G-1] : 0 (x [B·L, G, D]); _bwd writes level G-1 of dx only.
+ * esgpt_na_assemble_fwd: seq[e] = [l > 0 ? ctx[e-1] : 0, x[e, 0 .. G-2], ctx[e]] (seq [B·L, G+1, D], e = b·L + l;
+ *   ctx is the masked sequence-module output); _bwd: dctx[e] = dseq[e, G] + dseq[e+1, 0] (same subject), and levels
+ *   0 .. G-2 of dx = dseq[e, 1 .. G-1]. */
+int esgpt_residual_fwd(const float* x, const void* y, int y_dtype, const uint8_t* row_mask, int64_t mask_div,
+                       int64_t skip_T, float dropout_p, const uint64_t* seed, int64_t N, int64_t D, float* h,
+                       void* stream);
+int esgpt_residual_bwd(const float* dh, const uint8_t* row_mask, int64_t mask_div, int64_t skip_T, float dropout_p,
+                       const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, void* stream);
+int esgpt_na_split_fwd(const float* x, const uint8_t* event_mask, int64_t BL, int64_t G, int64_t D, float* per,
+                       void* stream);
+int esgpt_na_split_bwd(const float* dper, const uint8_t* event_mask, int64_t BL, int64_t G, int64_t D, float* dx,
+                       void* stream);
+int esgpt_na_assemble_fwd(const float* ctx, const float* x, int64_t B, int64_t L, int64_t G, int64_t D, float* seq,
+                          void* stream);
+int esgpt_na_assemble_bwd(const float* dseq, int64_t B, int64_t L, int64_t G, int64_t D, float* dctx, float* dx,
+                          void* stream);
 
 /* ---- Projection GEMM -------------------------------------------------------------------------------------
  * C[M, N] = alpha · (A · B) (+ bias[n]) with bf16 operands and f32 accumulation (the q/k/v/out, c_fc/c_proj and head

@@ -68,7 +68,7 @@ def test_embed_epilogue_autograd(esgpt):
 @pytest.mark.parametrize("skf", [False, True])
 def test_attention_fake_and_autograd(esgpt, skf):
     qkv = torch.empty(3, 7, 3 * 32, dtype=torch.bfloat16, device=M, requires_grad=True)
-    o, lse = esgpt.attention(qkv, None, None, 4, 0, skf, 0.0, None)
+    o, lse, keep = esgpt.attention(qkv, None, None, 4, 0, skf, 0.0, None)
     assert o.shape == (3, 7 - skf, 32) and o.dtype == torch.bfloat16 and lse.shape == (3, 4, 7 - skf)
     o.float().sum().backward()
     assert qkv.grad.shape == qkv.shape

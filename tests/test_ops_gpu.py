@@ -31,7 +31,7 @@ def test_attention_fwd_bwd_equal_c_abi(env):
     D = H * hd
     qkv = (0.5 * torch.randn(B, T, 3 * D, device=DEV, generator=_g(0))).bfloat16()
     km = torch.rand(B, T, device=DEV, generator=_g(1)) > 0.1
-    o, lse = esgpt.attention(qkv, km, km, H, 0, False, 0.0, None)
+    o, lse, keep = esgpt.attention(qkv, km, km, H, 0, False, 0.0, None)
     o2 = torch.empty_like(o)
     lse2 = torch.empty_like(lse)
     base, es = qkv.data_ptr(), 2
@@ -40,7 +40,7 @@ def test_attention_fwd_bwd_equal_c_abi(env):
     assert torch.equal(o, o2) and torch.equal(lse, lse2)
     do = torch.randn(B, T, D, device=DEV, generator=_g(2)).bfloat16()
     t = tickets(torch.device(DEV))
-    dqkv = esgpt.attention_bwd(qkv, o, do, lse, km, km, H, 0, False, 0.0, None, t)
+    dqkv = esgpt.attention_bwd(qkv, o, do, lse, km, km, H, 0, False, 0.0, None, keep, t)
     d2 = torch.empty_like(qkv)
     nb = lib.esgpt_attn_bwd_workspace(B, H, T, T, hd)
     ws = torch.empty(max(1, nb), dtype=torch.uint8, device=DEV)
@@ -50,6 +50,35 @@ def test_attention_fwd_bwd_equal_c_abi(env):
                                lse.data_ptr(), km.data_ptr(), km.data_ptr(), db, db + D * es, db + 2 * D * es, 3 * D,
                                B, H, T, T, hd, 0, 0.0, None, L.BF16, ws.data_ptr(), nb, cnt, L.stream()), "bwd")
     assert torch.equal(dqkv, d2)
+
+
+@pytest.mark.parametrize("hd,T,window", [(64, 256, 0), (64, 200, 0), (16, 256, 0), (32, 300, 32), (128, 100, 0),
+                                          (64, 600, 0)])
+def test_attention_keep_bits_equal_rehash(env, hd, T, window):
+    """With dropout, the operator's backward reads the keep bits its forward wrote (esgpt_attn_fwd_ex /
+    esgpt_attn_bwd_ex); the plain C ABI backward regenerates the mask from the seed. Both must give the same dqkv
+    bit for bit (same mask), including padded keys / queries, local windows, several key blocks and hd 16 / 128."""
+    esgpt, lib = env
+    B, H = 2, 4
+    D = H * hd
+    qkv = (0.5 * torch.randn(B, T, 3 * D, device=DEV, generator=_g(10))).bfloat16()
+    km = torch.rand(B, T, device=DEV, generator=_g(11)) > 0.1
+    seed = torch.tensor([987654321], dtype=torch.int64, device=DEV)
+    o, lse, keep = esgpt.attention(qkv, km, km, H, window, False, 0.1, seed)
+    assert keep.numel() == B * H * T * ((T + 31) // 32)
+    do = torch.randn(B, T, D, device=DEV, generator=_g(12)).bfloat16()
+    t = tickets(torch.device(DEV))
+    d_bits = esgpt.attention_bwd(qkv, o, do, lse, km, km, H, window, False, 0.1, seed, keep, t)
+    d_hash = esgpt.attention_bwd(qkv, o, do, lse, km, km, H, window, False, 0.1, seed, None, t)
+    assert torch.isfinite(d_bits.float()).all()
+    assert torch.equal(d_bits, d_hash)
+    # and the plain forward entry point draws the same output
+    o2, lse2 = torch.empty_like(o), torch.empty_like(lse)
+    base, es = qkv.data_ptr(), 2
+    L.check(lib.esgpt_attn_fwd(base, base + D * es, base + 2 * D * es, 3 * D, T, o2.data_ptr(), D, lse2.data_ptr(),
+                               km.data_ptr(), km.data_ptr(), B, H, T, T, hd, window, 0.1, seed.data_ptr(), L.BF16,
+                               L.stream()), "fwd")
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
 
 
 def test_embed_joint_and_bag_bwd_equal_c_abi(env):
@@ -233,3 +262,80 @@ def test_linear_bwd_split_streams_equal_grouped(env):
         del junk
         for a, b, name in zip(want, got, ("dx", "dw", "db")):
             assert torch.equal(a, b), (T, din, dout, act, name)
+
+
+@pytest.mark.parametrize("G", [1, 4])
+def test_na_glue_ops_match_torch(env, G):
+    """esgpt::na_split / na_assemble (+ backwards through StructuredAttention's autograd Functions) against the
+    reference's torch formulation (structured_attention.py:63-156: where on the whole-event element, history = the
+    masked ctx shifted by one event, cat), values and gradients bit for bit (pure data movement)."""
+    from eventstreamgpt_amd.transformer.structured_attention import _NAAssemble, _NASplit
+
+    B, L, D = 3, 37, 64
+    x = torch.randn(B, L, G, D, device=DEV, generator=_g(20)).requires_grad_()
+    em = torch.rand(B, L, device=DEV, generator=_g(21)) > 0.2
+    w_ctx = torch.randn(D, D, device=DEV, generator=_g(22))
+    d_out = torch.randn(B * L, G + 1, D, device=DEV, generator=_g(23))
+
+    def ours():
+        holder = {}
+        per = _NASplit.apply(x, em, holder)
+        ctx = torch.where(em[..., None], per @ w_ctx, 0.0)  # a stand-in sequence module (masked output)
+        seq = _NAAssemble.apply(ctx, x, holder)
+        return per, seq
+
+    def ref():
+        per = torch.where(em[..., None], x[:, :, -1, :], 0.0)
+        ctx = torch.where(em[..., None], per @ w_ctx, 0.0)
+        hist = torch.nn.functional.pad(ctx[:, :-1, :], (0, 0, 1, 0))
+        seq = torch.cat((hist.unsqueeze(2), x[:, :, :-1, :], ctx.unsqueeze(2)), dim=2).reshape(B * L, G + 1, D)
+        return per, seq
+
+    p1, s1 = ours()
+    (s1 * d_out).sum().backward()
+    g1 = x.grad.clone()
+    x.grad = None
+    p2, s2 = ref()
+    (s2 * d_out).sum().backward()
+    assert torch.equal(p1, p2) and torch.equal(s1, s2)
+    torch.testing.assert_close(g1, x.grad, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("skip_T,mask_div,ydt", [(0, 1, torch.bfloat16), (5, 4, torch.bfloat16), (0, 1, torch.float32)])
+def test_residual_op_matches_torch(env, skip_T, mask_div, ydt):
+    """esgpt::residual: h = mask ? x[xr] + dropout(y) : 0 (InnerBlock's last residual with the NA event-mask where):
+    exact without dropout; with dropout the kept / dropped elements scale y by 1/(1-p) or 0 and the backward applies
+    the same mask to dh; x's gradient covers every row of x (zeros for the rows skip_T leaves out)."""
+    esgpt, _ = env
+    D = 128
+    Bs, T = 6, 5
+    N = Bs * (T - 1) if skip_T else Bs * T
+    xrows = Bs * T
+    x = torch.randn(xrows, D, device=DEV, generator=_g(30)).requires_grad_()
+    y = torch.randn(N, D, device=DEV, generator=_g(31)).to(ydt).requires_grad_()
+    mask = torch.rand(N // mask_div, device=DEV, generator=_g(32)) > 0.3
+    rows = torch.arange(N, device=DEV)
+    xr = (rows // (T - 1)) * T + 1 + rows % (T - 1) if skip_T else rows
+    keep = mask.repeat_interleave(mask_div)[:, None]
+    h = esgpt.residual(x, y, mask, mask_div, skip_T, 0.0, None)
+    want = torch.where(keep, x[xr] + y.float(), 0.0)
+    assert torch.equal(h, want)
+    dh = torch.randn_like(h)
+    h.backward(dh)
+    gx = torch.zeros_like(x)
+    gx[xr] = torch.where(keep, dh, 0.0)
+    assert torch.equal(x.grad, gx)
+    assert torch.equal(y.grad, torch.where(keep, dh, 0.0).to(ydt))
+    # dropout: consistent masks forward / backward
+    seed = torch.tensor([4242], dtype=torch.int64, device=DEV)
+    x.grad = y.grad = None
+    h = esgpt.residual(x, y, None, 1, skip_T, 0.25, seed)
+    z = (h - x[xr]).detach() / y.float().detach()
+    ok = (z - 0.0).abs() < 1e-3
+    ok |= (z - 1 / 0.75).abs() < 1e-3
+    assert bool(ok[y.float().abs() > 1e-3].all())
+    h.backward(dh)
+    kept = (z > 0.5) & (y.float().abs() > 1e-3)
+    dyf = y.grad.float()
+    assert torch.allclose(dyf[kept], (dh / 0.75).to(ydt).float()[kept], rtol=1e-2, atol=1e-3)
+    assert bool((dyf[~kept & (y.float().abs() > 1e-3)] == 0).all())

@@ -18,12 +18,12 @@ def main():
     em = torch.ones(B, L, dtype=torch.bool, device="cuda")
     qkv = (0.5 * torch.randn(B, L, 3 * D, device="cuda")).bfloat16()
     seed = next_dropout_seed(qkv.device) if p > 0 else None
-    o, lse = esgpt.attention(qkv, em, em, H, 0, False, p, seed)
+    o, lse, keep = esgpt.attention(qkv, em, em, H, 0, False, p, seed)
     do = torch.randn_like(o)
     tk = tickets(qkv.device)
     for _ in range(5):
         esgpt.attention(qkv, em, em, H, 0, False, p, seed)
-        esgpt.attention_bwd(qkv, o, do, lse, em, em, H, 0, False, p, seed, tk)
+        esgpt.attention_bwd(qkv, o, do, lse, em, em, H, 0, False, p, seed, keep, tk)
     torch.cuda.synchronize()
 
 
