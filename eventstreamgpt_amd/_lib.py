@@ -110,6 +110,10 @@ SIGNATURES = {
     "esgpt_residual_ln_fwd": (_int, [_vp, _vp, _int, _vp, _vp, _f32, _vp, _vp, _vp, _f32, _i64, _i64, _vp, _vp, _int,
                                      _vp, _vp, _vp]),
     "esgpt_residual_ln_counters": (_i64, [_i64]),
+    "esgpt_residual_ln_fwd_ex": (_int, [_vp, _vp, _int, _vp, _vp, _f32, _vp, _vp, _vp, _f32, _i64, _i64, _i64, _vp,
+                                        _vp, _int, _vp, _vp, _vp]),
+    "esgpt_residual_ln_bwd_ex": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i64, _i64, _i64, _vp,
+                                        _vp, _int, _vp, _vp, _vp]),
     "esgpt_residual_ln_bwd": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _i64, _i64, _vp, _vp, _int,
                                      _vp, _vp, _vp, _vp]),
     "esgpt_colsum_jobs": (_int, [ctypes.POINTER(EsgptColsumJob), _i64, _vp]),

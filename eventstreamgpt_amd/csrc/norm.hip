@@ -62,6 +62,12 @@ __device__ __forceinline__ V4 zero4() { return V4{{0.f, 0.f, 0.f, 0.f}}; }
 
 __device__ __forceinline__ uint64_t drop_idx(int64_t row, int64_t D, int64_t col) { return (uint64_t)(row * D + col); }
 
+// Row of x under skip_T = T > 1 (static_kv_first residual, transformer.py:437): x = [N / (T-1), T, D] and output row r
+// reads the rows after each sequence's first one.
+__device__ __forceinline__ int64_t skip_row(int64_t r, int64_t skip_T) {
+  return skip_T ? (r / (skip_T - 1)) * skip_T + 1 + r % (skip_T - 1) : r;
+}
+
 // Forward rows per wave (1, 2 or 4; ESGPT_LN_FWD_ROWS tuning hook, read once): every load of the wave's rows is
 // issued before the first row reduction.
 int fwd_rows() {
@@ -82,7 +88,7 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
                                                               const float* __restrict__ w, const float* __restrict__ b,
                                                               float eps, int64_t N, int64_t D, float* __restrict__ h,
                                                               TO* __restrict__ out, float* __restrict__ mean_o,
-                                                              float* __restrict__ rstd_o) {
+                                                              float* __restrict__ rstd_o, int64_t skip_T) {
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * R;
@@ -92,14 +98,14 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
   bool keep[R];
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
-    const int64_t row = min(row0 + rr, N - 1);
+    const int64_t row = min(row0 + rr, N - 1), xrow = skip_row(row, skip_T);
     keep[rr] = rmask == nullptr || rmask[row] != 0;
 #pragma unroll
     for (int k = 0; k < KC; ++k) {
       const int64_t c = 4 * lane + 256 * k;
       xv[rr][k] = yv[rr][k] = zero4();
       if (c < D) {
-        if (x) xv[rr][k] = load4(x + row * D + c);
+        if (x) xv[rr][k] = load4(x + xrow * D + c);
         if (y) yv[rr][k] = load4(y + row * D + c);
       }
     }
@@ -176,7 +182,7 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     const float* __restrict__ dh_in, const TO* __restrict__ dout, const float* __restrict__ h,
     const float* __restrict__ mean_i, const float* __restrict__ rstd_i, const float* __restrict__ w,
     const uint8_t* __restrict__ rmask, float drop_p, const uint64_t* __restrict__ seed, int64_t N, int64_t D,
-    float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part) {
+    float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part, int64_t skip_T) {
   __shared__ float s_part[kWaves][3][4 * 64];
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -243,7 +249,12 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
           const float t = rstd[rr] * (g[k].v[j] - sg - xh[k].v[j] * sgx) + di[rr][k].v[j];
           d.v[j] = keep[rr] ? t : 0.f;
         }
-        if (dx) store4(dx + row * D + c, d);
+        if (dx) {
+          const int64_t xrow = skip_row(row, skip_T);
+          store4(dx + xrow * D + c, d);
+          // the x row before each sequence's first output row is read by no output: its gradient is zero
+          if (skip_T && row % (skip_T - 1) == 0) store4(dx + (xrow - 1) * D + c, zero4());
+        }
         if (dy) {
           V4 e;
           float z[4] = {1.f, 1.f, 1.f, 1.f};
@@ -454,12 +465,12 @@ __global__ __launch_bounds__(256) void column_partial_kernel(const T* __restrict
 template <typename TY, typename TO>
 void launch_ln_fwd(const float* x, const void* y, const float* bias, const uint8_t* rmask, float p, const uint64_t* seed,
                    const float* w, const float* b, float eps, int64_t N, int64_t D, float* h, void* out, float* mean,
-                   float* rstd, hipStream_t st) {
+                   float* rstd, int64_t skip_T, hipStream_t st) {
   const int R = fwd_rows();
   const unsigned grid = (unsigned)cdiv(N, kWaves * R);
 #define LN_FWD(KC, RR)                                                                                             \
   residual_ln_fwd_kernel<TY, TO, KC, RR><<<grid, 256, 0, st>>>(x, (const TY*)y, bias, rmask, p, seed, w, b, eps, N, D, \
-                                                               h, (TO*)out, mean, rstd)
+                                                               h, (TO*)out, mean, rstd, skip_T)
 #define LN_FWD_R(KC)                 \
   do {                               \
     if (R == 2) LN_FWD(KC, 2);       \
@@ -479,12 +490,12 @@ void launch_ln_fwd(const float* x, const void* y, const float* bias, const uint8
 template <typename TY, typename TO>
 void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const float* mean, const float* rstd,
                    const float* w, const uint8_t* rmask, float p, const uint64_t* seed, int64_t N, int64_t D, float* dx,
-                   void* dy, float* part, float* sums, hipStream_t st) {
+                   void* dy, float* part, float* sums, int64_t skip_T, hipStream_t st) {
   const int R = bwd_rows();
   const unsigned grid = (unsigned)cdiv(N, kWaves * R);
 #define LN_BWD(KC, RR)                                                                                             \
   residual_ln_bwd_kernel<TY, TO, KC, RR><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, \
-                                                               seed, N, D, dx, (TY*)dy, part)
+                                                               seed, N, D, dx, (TY*)dy, part, skip_T)
 #define LN_BWD_R(KC)              \
   do {                            \
     if (R == 2) LN_BWD(KC, 2);    \
@@ -517,19 +528,28 @@ int esgpt_residual_ln_fwd(const float* x, const void* y, int y_dtype, const floa
                           float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
                           int64_t N, int64_t D, float* h, void* out, int out_dtype, float* mean, float* rstd,
                           void* stream) {
+  return esgpt_residual_ln_fwd_ex(x, y, y_dtype, bias, row_mask, dropout_p, seed, ln_w, ln_b, eps, N, D, 0, h, out,
+                                  out_dtype, mean, rstd, stream);
+}
+
+int esgpt_residual_ln_fwd_ex(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
+                             float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
+                             int64_t N, int64_t D, int64_t skip_T, float* h, void* out, int out_dtype, float* mean,
+                             float* rstd, void* stream) {
   ESGPT_REQUIRE(ln_w && ln_b && out && mean && rstd && D > 0 && D % 4 == 0 && D <= 256 * kMaxChunks && (x || y));
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
+  ESGPT_REQUIRE(skip_T == 0 || (skip_T >= 2 && x && N % (skip_T - 1) == 0));
   if (N == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   const bool yb = y_dtype == ESGPT_BF16, ob = out_dtype == ESGPT_BF16;
   if (!yb && !ob) launch_ln_fwd<float, float>(x, y, bias, row_mask, dropout_p, seed, ln_w, ln_b, eps, N, D, h, out,
-                                             mean, rstd, st);
+                                             mean, rstd, skip_T, st);
   else if (!yb && ob) launch_ln_fwd<float, bf16>(x, y, bias, row_mask, dropout_p, seed, ln_w, ln_b, eps, N, D, h, out,
-                                                mean, rstd, st);
+                                                mean, rstd, skip_T, st);
   else if (yb && !ob) launch_ln_fwd<bf16, float>(x, y, bias, row_mask, dropout_p, seed, ln_w, ln_b, eps, N, D, h, out,
-                                                mean, rstd, st);
+                                                mean, rstd, skip_T, st);
   else launch_ln_fwd<bf16, bf16>(x, y, bias, row_mask, dropout_p, seed, ln_w, ln_b, eps, N, D, h, out, mean, rstd,
-                                 st);
+                                 skip_T, st);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
@@ -539,9 +559,18 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
                           const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
                           float* sums, int32_t* counters, void* stream) {
   (void)counters;
+  return esgpt_residual_ln_bwd_ex(dh_in, dout, out_dtype, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, 0, dx,
+                                  dy, y_dtype, part, sums, stream);
+}
+
+int esgpt_residual_ln_bwd_ex(const float* dh_in, const void* dout, int out_dtype, const float* h, const float* mean,
+                             const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
+                             const uint64_t* seed, int64_t N, int64_t D, int64_t skip_T, float* dx, void* dy,
+                             int y_dtype, float* part, float* sums, void* stream) {
   ESGPT_REQUIRE(dout && h && mean && rstd && ln_w && part && D > 0 && D % 4 == 0 && D <= 256 * kMaxChunks);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
   ESGPT_REQUIRE(esgpt_residual_ln_partials(N) * 3 * D * 4 < (1ll << 31) && ((uintptr_t)sums % 16) == 0);
+  ESGPT_REQUIRE(skip_T == 0 || (skip_T >= 2 && N % (skip_T - 1) == 0));
   hipStream_t st = as_stream(stream);
   if (N == 0) {  // no rows: zero sums (or, deferred, zero partials: one all-zero block)
     if (sums) return zero_async(sums, sizeof(float) * 3 * D, st) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
@@ -549,13 +578,13 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
   }
   const bool yb = y_dtype == ESGPT_BF16, ob = out_dtype == ESGPT_BF16;
   if (!yb && !ob) launch_ln_bwd<float, float>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx,
-                                             dy, part, sums, st);
+                                             dy, part, sums, skip_T, st);
   else if (!yb && ob) launch_ln_bwd<float, bf16>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D,
-                                                dx, dy, part, sums, st);
+                                                dx, dy, part, sums, skip_T, st);
   else if (yb && !ob) launch_ln_bwd<bf16, float>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D,
-                                                dx, dy, part, sums, st);
+                                                dx, dy, part, sums, skip_T, st);
   else launch_ln_bwd<bf16, bf16>(dh_in, dout, h, mean, rstd, ln_w, row_mask, dropout_p, seed, N, D, dx, dy, part,
-                                 sums, st);
+                                 sums, skip_T, st);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

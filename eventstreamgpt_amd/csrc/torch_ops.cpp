@@ -406,25 +406,29 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> residual_ln(const optional<Tensor>& x
                                                        const optional<Tensor>& bias, const Tensor& ln_w,
                                                        const Tensor& ln_b, const optional<Tensor>& row_mask,
                                                        double p, const optional<Tensor>& seed, double eps,
-                                                       at::ScalarType out_dtype) {
+                                                       at::ScalarType out_dtype, int64_t skip_T) {
   const c10::DeviceGuard guard(ln_w.device());
   Tensor xc = (x.has_value() && x->defined()) ? x->to(at::kFloat).contiguous() : Tensor();
   Tensor yc = (y.has_value() && y->defined()) ? y->contiguous() : Tensor();
   Tensor bc = (bias.has_value() && bias->defined()) ? bias->to(at::kFloat).contiguous() : Tensor();
   TORCH_CHECK(xc.defined() || yc.defined(), "residual_ln: x or y required");
-  const Tensor& ref = xc.defined() ? xc : yc;
+  TORCH_CHECK(skip_T == 0 || (xc.defined() && yc.defined()), "residual_ln: skip_T needs x and y");
+  const Tensor& ref = yc.defined() ? yc : xc;  // output rows (x has more under skip_T)
   const int64_t N = ref.size(0), D = ref.size(1);
+  TORCH_CHECK(skip_T == 0 || (N % (skip_T - 1) == 0 && xc.size(0) == N / (skip_T - 1) * skip_T),
+              "residual_ln: x must hold T rows per T-1 output rows under skip_T");
   const at::ScalarType y_dtype = yc.defined() ? yc.scalar_type() : at::kFloat;
   auto f32 = ln_w.options().dtype(at::kFloat);
   Tensor h = at::empty({N, D}, f32), out = at::empty({N, D}, f32.dtype(out_dtype));
   Tensor mean = at::empty({N}, f32), rstd = at::empty({N}, f32);
   Tensor rm = as_opt(row_mask, at::kBool);
-  check(esgpt_residual_ln_fwd(xc.defined() ? ptr<const float>(xc) : nullptr, yc.defined() ? yc.data_ptr() : nullptr,
-                              dtype_code(y_dtype), bc.defined() ? ptr<const float>(bc) : nullptr,
-                              rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p, optr<const uint64_t>(seed),
-                              ptr<const float>(ln_w), ptr<const float>(ln_b), (float)eps, N, D, ptr<float>(h),
-                              out.data_ptr(), dtype_code(out_dtype), ptr<float>(mean), ptr<float>(rstd),
-                              stream_of(ln_w)),
+  check(esgpt_residual_ln_fwd_ex(xc.defined() ? ptr<const float>(xc) : nullptr,
+                                 yc.defined() ? yc.data_ptr() : nullptr, dtype_code(y_dtype),
+                                 bc.defined() ? ptr<const float>(bc) : nullptr,
+                                 rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p, optr<const uint64_t>(seed),
+                                 ptr<const float>(ln_w), ptr<const float>(ln_b), (float)eps, N, D, skip_T,
+                                 ptr<float>(h), out.data_ptr(), dtype_code(out_dtype), ptr<float>(mean),
+                                 ptr<float>(rstd), stream_of(ln_w)),
         "residual_ln");
   return {h, out, mean, rstd};
 }
@@ -435,16 +439,16 @@ std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd_impl(const optional<Tensor>& 
                                                         const Tensor& ln_w, const optional<Tensor>& row_mask, double p,
                                                         const optional<Tensor>& seed, bool need_dx, bool need_dy,
                                                         at::ScalarType y_dtype, at::ScalarType out_dtype,
-                                                        bool deferred, Tensor* part_out);
+                                                        bool deferred, Tensor* part_out, int64_t skip_T);
 
 std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd(const optional<Tensor>& dh, const Tensor& dout_, const Tensor& h,
                                                    const Tensor& mean, const Tensor& rstd, const Tensor& ln_w,
                                                    const optional<Tensor>& row_mask, double p,
                                                    const optional<Tensor>& seed, bool need_dx, bool need_dy,
                                                    at::ScalarType y_dtype, at::ScalarType out_dtype,
-                                                   const Tensor& tickets) {
+                                                   const Tensor& tickets, int64_t skip_T) {
   return residual_ln_bwd_impl(dh, dout_, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype,
-                              out_dtype, false, nullptr);
+                              out_dtype, false, nullptr, skip_T);
 }
 
 // The same backward with the column sums deferred: returns (dx, dy, part) — part f32 [n_parts, 3, D] holds the
@@ -454,10 +458,10 @@ std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd_partials(const optional<Tenso
                                                             const Tensor& ln_w, const optional<Tensor>& row_mask,
                                                             double p, const optional<Tensor>& seed, bool need_dx,
                                                             bool need_dy, at::ScalarType y_dtype,
-                                                            at::ScalarType out_dtype) {
+                                                            at::ScalarType out_dtype, int64_t skip_T) {
   Tensor part;
   auto r = residual_ln_bwd_impl(dh, dout_, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype,
-                                out_dtype, true, &part);
+                                out_dtype, true, &part, skip_T);
   return {std::get<0>(r), std::get<1>(r), part};
 }
 
@@ -482,23 +486,25 @@ std::tuple<Tensor, Tensor, Tensor> residual_ln_bwd_impl(const optional<Tensor>& 
                                                         const Tensor& ln_w, const optional<Tensor>& row_mask, double p,
                                                         const optional<Tensor>& seed, bool need_dx, bool need_dy,
                                                         at::ScalarType y_dtype, at::ScalarType out_dtype,
-                                                        bool deferred, Tensor* part_out) {
+                                                        bool deferred, Tensor* part_out, int64_t skip_T) {
   const c10::DeviceGuard guard(h.device());
   const int64_t N = h.size(0), D = h.size(1);
+  const int64_t xN = skip_T ? N / (skip_T - 1) * skip_T : N;  // rows of x (dx)
   Tensor dout = dout_.to(out_dtype).contiguous();
   Tensor dhc = (dh.has_value() && dh->defined()) ? dh->to(at::kFloat).contiguous() : Tensor();
   auto f32 = h.options().dtype(at::kFloat);
-  Tensor dx = need_dx ? at::empty({N, D}, f32) : at::empty({0}, f32);
+  Tensor dx = need_dx ? at::empty({xN, D}, f32) : at::empty({0}, f32);
   Tensor dy = need_dy ? at::empty({N, D}, f32.dtype(y_dtype)) : at::empty({0}, f32.dtype(y_dtype));
   Tensor part = at::empty({std::max<int64_t>(1, esgpt_residual_ln_partials(N)), 3 * D}, f32);
   Tensor sums = deferred ? Tensor() : at::empty({3, D}, f32);
   Tensor rm = as_opt(row_mask, at::kBool);
-  check(esgpt_residual_ln_bwd(dhc.defined() ? ptr<const float>(dhc) : nullptr, dout.data_ptr(), dtype_code(out_dtype),
-                              ptr<const float>(h), ptr<const float>(mean), ptr<const float>(rstd),
-                              ptr<const float>(ln_w), rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p,
-                              optr<const uint64_t>(seed), N, D, need_dx ? ptr<float>(dx) : nullptr,
-                              need_dy ? dy.data_ptr() : nullptr, dtype_code(y_dtype), ptr<float>(part),
-                              deferred ? nullptr : ptr<float>(sums), nullptr, stream_of(h)),
+  check(esgpt_residual_ln_bwd_ex(dhc.defined() ? ptr<const float>(dhc) : nullptr, dout.data_ptr(),
+                                 dtype_code(out_dtype), ptr<const float>(h), ptr<const float>(mean),
+                                 ptr<const float>(rstd), ptr<const float>(ln_w),
+                                 rm.defined() ? ptr<const uint8_t>(rm) : nullptr, (float)p, optr<const uint64_t>(seed),
+                                 N, D, skip_T, need_dx ? ptr<float>(dx) : nullptr, need_dy ? dy.data_ptr() : nullptr,
+                                 dtype_code(y_dtype), ptr<float>(part), deferred ? nullptr : ptr<float>(sums),
+                                 stream_of(h)),
         "residual_ln_bwd");
   if (part_out) *part_out = part;
   return {dx, dy, sums};
@@ -812,10 +818,10 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("output_loss(Tensor zc, Tensor? zt, Tensor? zc_bias, " BATCH_SCHEMA ", int n_levels, int shift, int[] terms, "
         "int[] tte_i, float[] tte_f, Tensor err, int path=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("residual_ln(Tensor? x, Tensor? y, Tensor? bias, Tensor ln_w, Tensor ln_b, Tensor? row_mask, float p, "
-        "Tensor? seed, float eps, ScalarType out_dtype) -> (Tensor, Tensor, Tensor, Tensor)");
+        "Tensor? seed, float eps, ScalarType out_dtype, int skip_T=0) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("residual_ln_bwd(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, Tensor? row_mask, "
         "float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, ScalarType out_dtype, "
-        "Tensor tickets) -> (Tensor, Tensor, Tensor)");
+        "Tensor tickets, int skip_T=0) -> (Tensor, Tensor, Tensor)");
   m.def("bias_act(Tensor f, Tensor bias, int act) -> Tensor");
   m.def("bias_act_bwd(Tensor dg, Tensor f, Tensor bias, int act) -> (Tensor, Tensor)");
   m.def("column_sum(Tensor x) -> Tensor");
@@ -830,7 +836,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("seed_bank(Tensor(a!) counter, Tensor(b!) bank, Tensor(c!)? err=None) -> ()");
   m.def("residual_ln_bwd_partials(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, "
         "Tensor? row_mask, float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, "
-        "ScalarType out_dtype) -> (Tensor, Tensor, Tensor)");
+        "ScalarType out_dtype, int skip_T=0) -> (Tensor, Tensor, Tensor)");
   m.def("colsum_flush(Tensor[] parts, Tensor(a!)[] sums) -> ()");
   m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
   m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, Tensor? b_pj, int act, Tensor p_fc, Tensor p_pj, "

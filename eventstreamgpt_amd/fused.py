@@ -24,14 +24,19 @@ from .kernels import _ops, _timed, attention, batch_args, err_word, next_dropout
 _ACTS = {"gelu": 0, "gelu_new": 1, "gelu_pytorch_tanh": 1, "gelu_fast": 1, "relu": 2}
 
 
-def residual_ln(x, y, bias, ln_w, ln_b, row_mask, p: float, eps: float, out_dtype: torch.dtype):
+def residual_ln(x, y, bias, ln_w, ln_b, row_mask, p: float, eps: float, out_dtype: torch.dtype, skip_T: int = 0):
     """``esgpt::residual_ln``: h = mask ? x + dropout(y + bias) : 0 ; out = LayerNorm(h). Returns (h f32, out
-    out_dtype); differentiable in x, y, bias, ln_w, ln_b (column sums in the backward launch)."""
+    out_dtype); differentiable in x, y, bias, ln_w, ln_b (column sums in the backward launch). ``skip_T`` = T: x holds
+    T rows per T - 1 output rows and each sequence's first x row is skipped (the static_kv_first residual)."""
     dev = ln_w.device
     seed = next_dropout_seed(dev) if (p > 0 and y is not None) else None
     with _timed("residual_ln_fwd"):
-        h, out, _mean, _rstd = _ops().residual_ln(x, y, bias, ln_w, ln_b, row_mask, float(p), seed, float(eps),
-                                                  out_dtype)
+        if skip_T:
+            h, out, _mean, _rstd = _ops().residual_ln(x, y, bias, ln_w, ln_b, row_mask, float(p), seed, float(eps),
+                                                      out_dtype, int(skip_T))
+        else:
+            h, out, _mean, _rstd = _ops().residual_ln(x, y, bias, ln_w, ln_b, row_mask, float(p), seed, float(eps),
+                                                      out_dtype)
     return h, out
 
 
@@ -343,23 +348,6 @@ def block_fused_supported(blk, hidden: torch.Tensor) -> bool:
             and blk.attn.attention.head_dim <= 128)
 
 
-class _SkipFirst(torch.autograd.Function):
-    """hidden [Bs, T, D] -> hidden[:, 1:, :] as a contiguous [Bs·(T-1), D] tensor whose backward writes the full
-    gradient in one pass (zeros for the first position, the incoming rows after it) — not a zero-filled slice
-    gradient plus a copy."""
-
-    @staticmethod
-    def forward(ctx, hidden):
-        ctx.shape = hidden.shape
-        Bs, T, D = hidden.shape
-        return hidden[:, 1:, :].reshape(Bs * (T - 1), D).contiguous()
-
-    @staticmethod
-    def backward(ctx, d):
-        Bs, T, D = ctx.shape
-        return torch.nn.functional.pad(d.view(Bs, T - 1, D), (0, 0, 1, 0))
-
-
 def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_first: bool, out_row_mask=None,
                       out_mask_div: int = 1) -> torch.Tensor:
     """``InnerBlock.forward`` (``transformer.py:409-461``, pre-LN attention + MLP with residuals) through the HIP
@@ -383,14 +371,16 @@ def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_fir
     qpm = None if (kpm is None or static_kv_first) else kpm
     window = att.window_size if att.attention_type == "local" else 0
     with torch.autocast("cuda", enabled=False):
-        _, ln = residual_ln(None, x2, None, ln1.weight, ln1.bias, None, 0.0, eps, dt)
+        # h0 (= x2) feeds the block's residual: its gradient comes back into this LayerNorm's backward as dh_in
+        # (one kernel), not as a second gradient of x2 that autograd would add
+        h0, ln = residual_ln(None, x2, None, ln1.weight, ln1.bias, None, 0.0, eps, dt)
         qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight)).view(Bs, T, 3 * D)
         o = attention(qkv, kpm, qpm, att.num_heads, window, static_kv_first, p_att)
         Tq = T - skf
         y = proj(o.reshape(Bs * Tq, D), wo, att.out_proj.bias, (att.out_proj.weight,))
-        # the residual rows: every row (the LayerNorm input itself) or all but the static first one
-        res = x2 if skf == 0 else _SkipFirst.apply(hidden.float())
-        h1, ln2 = residual_ln(res, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt)
+        # the residual rows: every row of h0, or (static_kv_first) all but each sequence's first, mapped in-kernel
+        h1, ln2 = residual_ln(h0, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt,
+                              skip_T=T if skf else 0)
         y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name], with_bias=True)
         out = residual(h1, y2, out_row_mask, out_mask_div, 0, p_res)
     return out.view(Bs, Tq, D)

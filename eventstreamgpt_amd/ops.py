@@ -200,18 +200,19 @@ def _register():
         return _loss_fake(zc, zt, shift, len(terms) // 8, di.shape[0])
 
     @fake(lib + "residual_ln")
-    def _(x, y, bias, ln_w, ln_b, row_mask, p, seed, eps, out_dtype):
-        ref = x if x is not None else y
+    def _(x, y, bias, ln_w, ln_b, row_mask, p, seed, eps, out_dtype, skip_T=0):
+        ref = y if y is not None else x  # the output rows (x holds more under skip_T)
         N, D = ref.shape
         f = ln_w.new_empty
         return f(N, D, dtype=torch.float32), f(N, D, dtype=out_dtype), f(N, dtype=torch.float32), \
             f(N, dtype=torch.float32)
 
     @fake(lib + "residual_ln_bwd")
-    def _(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype, out_dtype, tickets):
+    def _(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype, out_dtype, tickets, skip_T=0):
         N, D = h.shape
         f = h.new_empty
-        return (f(N, D, dtype=torch.float32) if need_dx else f(0, dtype=torch.float32),
+        xN = N // (skip_T - 1) * skip_T if skip_T else N
+        return (f(xN, D, dtype=torch.float32) if need_dx else f(0, dtype=torch.float32),
                 f(N, D, dtype=y_dtype) if need_dy else f(0, dtype=y_dtype), f(3, D, dtype=torch.float32))
 
     @fake(lib + "bias_act")
@@ -248,12 +249,13 @@ def _register():
         return None
 
     @fake(lib + "residual_ln_bwd_partials")
-    def _(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype, out_dtype):
+    def _(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, need_dx, need_dy, y_dtype, out_dtype, skip_T=0):
         N, D = h.shape
         f = h.new_empty
         from .kernels import _lib_partials
 
-        return (f(N, D, dtype=torch.float32) if need_dx else f(0, dtype=torch.float32),
+        xN = N // (skip_T - 1) * skip_T if skip_T else N
+        return (f(xN, D, dtype=torch.float32) if need_dx else f(0, dtype=torch.float32),
                 f(N, D, dtype=y_dtype) if need_dy else f(0, dtype=y_dtype),
                 f(_lib_partials(N), 3 * D, dtype=torch.float32))
 
@@ -392,33 +394,34 @@ def _register():
 
     # residual_ln: d x, d y, d bias, d ln_w, d ln_b (column sums in the same launch)
     def _rl_setup(ctx, inputs, output):
-        x, y, bias, ln_w, ln_b, row_mask, p, seed, eps, out_dtype = inputs
+        x, y, bias, ln_w, ln_b, row_mask, p, seed, eps, out_dtype, *rest = inputs
+        skip_T = rest[0] if rest else 0
         h, out, mean, rstd = output
         ctx.mark_non_differentiable(mean, rstd)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(h, mean, rstd, ln_w, row_mask, seed)
         ctx.meta = (x is not None, y is not None, bias is not None, y.dtype if y is not None else torch.float32,
-                    out_dtype, p)
+                    out_dtype, p, skip_T, len(inputs))
         ctx.defer_ok = bias is None and _leaves(ln_w, ln_b)
 
     def _rl_bwd(ctx, dh, dout, _dm, _dr):
         from .kernels import colsum_deferral_active, defer_colsum
 
         h, mean, rstd, ln_w, row_mask, seed = ctx.saved_tensors
-        has_x, has_y, has_bias, y_dtype, out_dtype, p = ctx.meta
+        has_x, has_y, has_bias, y_dtype, out_dtype, p, skip_T, n_in = ctx.meta
         if dout is None:
             dout = torch.zeros(h.shape, dtype=out_dtype, device=h.device)
         if ctx.defer_ok and colsum_deferral_active(h.device):
             # partials now, the column sums in the pass's one esgpt::colsum_flush launch
             dx, dy, part = ops.residual_ln_bwd_partials(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x,
-                                                        has_y, y_dtype, out_dtype)
+                                                        has_y, y_dtype, out_dtype, skip_T)
             sums = torch.empty(3, h.shape[1], dtype=torch.float32, device=h.device)
             defer_colsum(h.device, part, sums.view(-1))
         else:
             dx, dy, sums = ops.residual_ln_bwd(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x, has_y,
-                                               y_dtype, out_dtype, _tickets(h.device))
+                                               y_dtype, out_dtype, _tickets(h.device), skip_T)
         return (dx if has_x else None, dy if has_y else None, sums[2] if has_bias else None, sums[0], sums[1],
-                None, None, None, None, None)
+                None, None, None, None, None) + (None,) * (n_in - 10)
 
     reg(lib + "residual_ln", _rl_bwd, setup_context=_rl_setup)
 

@@ -256,6 +256,17 @@ int esgpt_residual_ln_bwd(const float* dh_in, const void* dout, int out_dtype, c
                           const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
                           const uint64_t* seed, int64_t N, int64_t D, float* dx, void* dy, int y_dtype, float* part,
                           float* sums, int32_t* counters, void* stream);
+/* The same with skip_T = T > 1: x = [N / (T-1), T, D] and output row r reads x's rows after each sequence's first
+ * one (the static_kv_first residual, transformer.py:437); the backward's dx covers all of x's rows (zeros for the
+ * first rows). skip_T = 0: the plain forms above. */
+int esgpt_residual_ln_fwd_ex(const float* x, const void* y, int y_dtype, const float* bias, const uint8_t* row_mask,
+                             float dropout_p, const uint64_t* seed, const float* ln_w, const float* ln_b, float eps,
+                             int64_t N, int64_t D, int64_t skip_T, float* h, void* out, int out_dtype, float* mean,
+                             float* rstd, void* stream);
+int esgpt_residual_ln_bwd_ex(const float* dh_in, const void* dout, int out_dtype, const float* h, const float* mean,
+                             const float* rstd, const float* ln_w, const uint8_t* row_mask, float dropout_p,
+                             const uint64_t* seed, int64_t N, int64_t D, int64_t skip_T, float* dx, void* dy,
+                             int y_dtype, float* part, float* sums, void* stream);
 /* Column sums of many partial tables in one launch: sums[c] = Σ_b part[b·width + c] (b ascending in 16 fixed-order
  * row groups, as the residual_ln backward's own sum launch). width % 4 == 0, 16-B aligned part / sums. */
 typedef struct esgpt_colsum_job {

@@ -339,3 +339,31 @@ def test_residual_op_matches_torch(env, skip_T, mask_div, ydt):
     dyf = y.grad.float()
     assert torch.allclose(dyf[kept], (dh / 0.75).to(ydt).float()[kept], rtol=1e-2, atol=1e-3)
     assert bool((dyf[~kept & (y.float().abs() > 1e-3)] == 0).all())
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_residual_ln_skip_rows_equal_sliced_input(env, p):
+    """esgpt::residual_ln with skip_T = T (the static_kv_first residual: x [Bs, T, D], output rows = every row but
+    each sequence's first) equals the plain op on x[:, 1:] bit for bit, forward and backward (dx of the skipped rows
+    zero)."""
+    esgpt, _ = env
+    Bs, T, D = 7, 5, 256
+    x = torch.randn(Bs * T, D, device=DEV, generator=_g(40)).requires_grad_()
+    y = torch.randn(Bs * (T - 1), D, device=DEV, generator=_g(41)).bfloat16().requires_grad_()
+    w = (1 + 0.1 * torch.randn(D, device=DEV, generator=_g(42))).requires_grad_()
+    b = (0.1 * torch.randn(D, device=DEV, generator=_g(43))).requires_grad_()
+    seed = torch.tensor([777], dtype=torch.int64, device=DEV) if p > 0 else None
+    dout = torch.randn(Bs * (T - 1), D, device=DEV, generator=_g(44)).bfloat16()
+    dh = torch.randn(Bs * (T - 1), D, device=DEV, generator=_g(45))
+    h1, o1, _, _ = esgpt.residual_ln(x, y, None, w, b, None, p, seed, 1e-5, torch.bfloat16, T)
+    torch.autograd.backward([h1, o1], [dh, dout])
+    g1 = [t.grad.clone() for t in (x, y, w, b)]
+    for t in (x, y, w, b):
+        t.grad = None
+    xs = x.view(Bs, T, D)[:, 1:].reshape(-1, D)
+    h2, o2, _, _ = esgpt.residual_ln(xs, y, None, w, b, None, p, seed, 1e-5, torch.bfloat16)
+    torch.autograd.backward([h2, o2], [dh, dout])
+    assert torch.equal(h1, h2) and torch.equal(o1, o2)
+    for a, c in zip(g1, (x.grad, y.grad, w.grad, b.grad)):
+        assert torch.equal(a, c)
+    assert bool((g1[0].view(Bs, T, D)[:, 0] == 0).all())
