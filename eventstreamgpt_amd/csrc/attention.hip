@@ -16,6 +16,8 @@
 // rows of padded queries (query_mask[i] == 0) are zeros and carry no gradient.
 #include <stdlib.h>
 
+#include <initializer_list>
+
 #include "common.h"
 
 using namespace esgpt;
@@ -382,6 +384,242 @@ __global__ __launch_bounds__(256) void attn_bwd_small(
   }
 }
 
+// ---- short sequences, four queries per wave (Lk <= 8, hd in {16, 32, 64}: the C4 dependency graph) ----------
+// One wave per (sequence, head) as above, but the wave is four 16-lane row groups, each owning one query row of the
+// current block of four (VE = hd / 16 consecutive dims per lane, one 2..16-byte vector load per row): the queries run
+// in parallel (the lane-per-dimension form walks them one after another, each behind its own row loads), scores and
+// dP are 16-lane DPP row reductions, and the backward's dK / dV partials are summed over the four groups with two
+// permlane swaps at the end. Same visibility, masking, dropout-hash and zero-row semantics.
+template <typename T, int VE>
+__device__ __forceinline__ void load_vec(const T* p, float (&o)[VE]) {
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (VE == 4) {
+      const float4 t = *reinterpret_cast<const float4*>(p);
+      o[0] = t.x, o[1] = t.y, o[2] = t.z, o[3] = t.w;
+    } else if constexpr (VE == 2) {
+      const float2 t = *reinterpret_cast<const float2*>(p);
+      o[0] = t.x, o[1] = t.y;
+    } else {
+      o[0] = *reinterpret_cast<const float*>(p);
+    }
+  } else {
+    if constexpr (VE == 4) {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      o[0] = __uint_as_float(t.x << 16), o[1] = __uint_as_float(t.x & 0xffff0000u);
+      o[2] = __uint_as_float(t.y << 16), o[3] = __uint_as_float(t.y & 0xffff0000u);
+    } else if constexpr (VE == 2) {
+      const uint32_t t = *reinterpret_cast<const uint32_t*>(p);
+      o[0] = __uint_as_float(t << 16), o[1] = __uint_as_float(t & 0xffff0000u);
+    } else {
+      o[0] = __uint_as_float((uint32_t)(*reinterpret_cast<const uint16_t*>(p)) << 16);
+    }
+  }
+}
+
+template <typename T, int VE>
+__device__ __forceinline__ void store_vec(T* p, const float (&v)[VE]) {
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (VE == 4) *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    else if constexpr (VE == 2) *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+    else *reinterpret_cast<float*>(p) = v[0];
+  } else {
+    if constexpr (VE == 4) {
+      *reinterpret_cast<uint2*>(p) =
+          make_uint2((uint32_t)f32_to_bf16_bits(v[0]) | ((uint32_t)f32_to_bf16_bits(v[1]) << 16),
+                     (uint32_t)f32_to_bf16_bits(v[2]) | ((uint32_t)f32_to_bf16_bits(v[3]) << 16));
+    } else if constexpr (VE == 2) {
+      *reinterpret_cast<uint32_t*>(p) = (uint32_t)f32_to_bf16_bits(v[0]) | ((uint32_t)f32_to_bf16_bits(v[1]) << 16);
+    } else {
+      *reinterpret_cast<uint16_t*>(p) = f32_to_bf16_bits(v[0]);
+    }
+  }
+}
+
+// Sum over the 16 lanes of each row (every lane of the row ends with it); sum over the 4 rows of the wave.
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+__device__ __forceinline__ float cross_rows(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+constexpr int kSmall4Lk = 8;
+
+template <typename T, int VE>
+__global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, const T* __restrict__ k,
+                                                       const T* __restrict__ v, int64_t ld_in, int64_t tq,
+                                                       T* __restrict__ o, int64_t ld_o, float* __restrict__ lse,
+                                                       const uint8_t* __restrict__ kmask,
+                                                       const uint8_t* __restrict__ qmask, int64_t B, int64_t H,
+                                                       int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
+                                                       const uint64_t* __restrict__ seed) {
+  constexpr int LKM = kSmall4Lk;
+  const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;  // wave-uniform
+  const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
+  const int64_t h = bh % H, b = bh / H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
+  float kr[LKM][VE], vr[LKM][VE];
+  bool kv[LKM];
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    kv[j] = j < Lk && (!kmask || kmask[b * Lk + j] != 0);
+    if (j >= Lk) break;  // wave-uniform: only the sequence's keys are loaded and walked
+    load_vec<T, VE>(k + (b * Lk + j) * ld_in + h * hd + c, kr[j]);
+    load_vec<T, VE>(v + (b * Lk + j) * ld_in + h * hd + c, vr[j]);
+  }
+  for (int64_t i0 = 0; i0 < Lq; i0 += 4) {
+    const int64_t i = i0 + g;
+    const bool qin = i < Lq;
+    const int64_t ii = qin ? i : Lq - 1;
+    const int64_t pos = ii + (Lk - Lq);
+    const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+    const bool qvalid = qin && (qmask ? (qmask[b * Lq + ii] != 0) : true);
+    float qr[VE];
+    load_vec<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, qr);
+    float s[LKM];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < LKM; ++j) {
+      s[j] = -INFINITY;
+      if (j >= Lk) break;
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) t = fmaf(qr[e], kr[j][e], t);
+      t = row_sum16(t);  // every lane of the wave takes part (DPP)
+      const bool ok = qvalid && kv[j] && j >= jlo && j <= pos;
+      s[j] = ok ? t : -INFINITY;
+      m = fmaxf(m, s[j]);
+    }
+    float l = 0.f, acc[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < LKM; ++j) {
+      if (j >= Lk) break;
+      if (s[j] == -INFINITY) continue;
+      const float p = expf(s[j] - m);
+      l += p;  // normaliser over undropped probabilities
+      const float pd = dr.p > 0.f ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, ii, j)) : p;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) acc[e] = fmaf(pd, vr[j][e], acc[e]);
+    }
+    const bool ok = qvalid && l > 0.f;
+    const float inv = ok ? 1.f / l : 0.f;
+#pragma unroll
+    for (int e = 0; e < VE; ++e) acc[e] *= inv;
+    if (qin) {
+      store_vec<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, acc);
+      if ((lane & 15) == 0) lse[bh * Lq + ii] = ok ? m + logf(l) : 0.f;
+    }
+  }
+}
+
+template <typename T, int VE>
+__global__ __launch_bounds__(256) void attn_bwd_small4(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
+    const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
+    const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, T* __restrict__ dk,
+    T* __restrict__ dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window,
+    float drop_p, const uint64_t* __restrict__ seed) {
+  constexpr int LKM = kSmall4Lk;
+  const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (bh >= B * H) return;  // wave-uniform
+  const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
+  const int64_t h = bh % H, b = bh / H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
+  float kr[LKM][VE], vr[LKM][VE], dka[LKM][VE], dva[LKM][VE];
+  bool kv[LKM];
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    kv[j] = j < Lk && (!kmask || kmask[b * Lk + j] != 0);
+#pragma unroll
+    for (int e = 0; e < VE; ++e) dka[j][e] = dva[j][e] = 0.f;
+    if (j >= Lk) break;  // wave-uniform
+    load_vec<T, VE>(k + (b * Lk + j) * ld_in + h * hd + c, kr[j]);
+    load_vec<T, VE>(v + (b * Lk + j) * ld_in + h * hd + c, vr[j]);
+  }
+  for (int64_t i0 = 0; i0 < Lq; i0 += 4) {
+    const int64_t i = i0 + g;
+    const bool qin = i < Lq;
+    const int64_t ii = qin ? i : Lq - 1;
+    const int64_t pos = ii + (Lk - Lq);
+    const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+    const bool qvalid = qin && (qmask ? (qmask[b * Lq + ii] != 0) : true);
+    float qr[VE], dor[VE], orr[VE], dqa[VE];
+    load_vec<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, qr);
+    load_vec<T, VE>(dout + (b * Lq + ii) * ld_do + h * hd + c, dor);
+    load_vec<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, orr);
+    const float ls = lse[bh * Lq + ii];
+    float dl = 0.f;
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      dl = fmaf(dor[e], orr[e], dl);
+      dqa[e] = 0.f;
+    }
+    dl = row_sum16(dl);  // delta = rowsum(dO o O)
+    if (!qvalid) dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < LKM; ++j) {
+      if (j >= Lk) break;  // wave-uniform
+      float sv = 0.f, dpv = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        sv = fmaf(qr[e], kr[j][e], sv);
+        dpv = fmaf(dor[e], vr[j][e], dpv);
+      }
+      sv = row_sum16(sv);
+      dpv = row_sum16(dpv);
+      if (!(qvalid && kv[j] && j >= jlo && j <= pos)) continue;  // row-uniform
+      const float keep = dr.p > 0.f ? dropout_mult(dr, elem_index(bh, Lq, Lk, ii, j)) : 1.f;
+      const float p = expf(sv - ls);
+      const float ds = p * (dpv * keep - dl);
+      const float pd = p * keep;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        dqa[e] = fmaf(ds, kr[j][e], dqa[e]);
+        dka[j][e] = fmaf(ds, qr[e], dka[j][e]);
+        dva[j][e] = fmaf(pd, dor[e], dva[j][e]);
+      }
+    }
+    if (qin) store_vec<T, VE>(dq + (b * tq + ii) * ld_d + h * hd + c, dqa);
+  }
+  // dK / dV: the four query groups' partials summed (every group ends with the sums); group g stores the rows
+  // j = g, g + 4
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    if (j >= Lk) break;  // wave-uniform
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      dka[j][e] = cross_rows(dka[j][e]);
+      dva[j][e] = cross_rows(dva[j][e]);
+    }
+    if (j < Lk && (j & 3) == g) {
+      store_vec<T, VE>(dk + (b * Lk + j) * ld_d + h * hd + c, dka[j]);
+      store_vec<T, VE>(dv + (b * Lk + j) * ld_d + h * hd + c, dva[j]);
+    }
+  }
+}
+
+// The four-query form applies (aligned VE-element rows).
+template <typename T>
+bool small4_ok(int64_t Lk, int64_t hd, std::initializer_list<const void*> ptrs, std::initializer_list<int64_t> lds) {
+  if (!(Lk <= kSmall4Lk && (hd == 16 || hd == 32 || hd == 64))) return false;
+  const int64_t vb = (hd / 16) * (int64_t)sizeof(T);  // bytes per lane vector
+  for (const void* p : ptrs)
+    if (p && ((uintptr_t)p % vb)) return false;
+  for (int64_t ld : lds)
+    if ((ld * (int64_t)sizeof(T)) % vb) return false;
+  return true;
+}
+
 template <typename T>
 int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
                  int64_t ld_o, float* lse_w, const float* lse_r, const void* dout, int64_t ld_do,
@@ -389,6 +627,24 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
                  int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
                  hipStream_t st) {
   const dim3 grid((unsigned)cdiv(B * H, 4)), block(256);
+  if (small4_ok<T>(Lk, hd, {q, k, v, o, dout, dq, dk, dv}, {ld_in, ld_o, ld_do, ld_d})) {
+#define SMALL4(VE)                                                                                                   \
+  do {                                                                                                               \
+    if (fwd)                                                                                                         \
+      attn_fwd_small4<T, VE><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (T*)o, ld_o,  \
+                                                     lse_w, kmask, qmask, B, H, Lq, Lk, (int)hd, window, drop_p, seed); \
+    else                                                                                                             \
+      attn_bwd_small4<T, VE><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o,  \
+                                                     ld_o, (const T*)dout, ld_do, lse_r, kmask, qmask, (T*)dq,       \
+                                                     (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p,    \
+                                                     seed);                                                          \
+  } while (0)
+    if (hd == 16) SMALL4(1);
+    else if (hd == 32) SMALL4(2);
+    else SMALL4(4);
+#undef SMALL4
+    return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+  }
 #define SMALL(DPL, LKM)                                                                                             \
   do {                                                                                                              \
     if (fwd)                                                                                                        \

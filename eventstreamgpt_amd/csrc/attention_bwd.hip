@@ -147,7 +147,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
     __bf16* __restrict__ dq, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d,
     float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed,
-    const uint32_t* __restrict__ keep, int nw, int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf) {
+    const uint32_t* __restrict__ keep, int nw, int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf,
+    int64_t dq_slab) {
   using C = Cfg<HD>;
   constexpr int QT = C::QT, HDP = C::HDP, NKW = C::NKW;
   constexpr bool DROP = DM != DROP_NONE, bits = DM == DROP_BITS;
@@ -219,6 +220,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   const int qlo = max(0, kb0 - off);
   const int qhi = window ? min(Lq - 1, kbend + window - 1 - off) : Lq - 1;
   const bool direct = dq32 == nullptr;  // this workgroup holds every key of the (batch, head)
+  // otherwise this key block's partial dQ goes to its own f32 slab (plain stores, summed in dq_convert_kernel)
+  float* dq_part = direct ? nullptr : dq32 + (int64_t)kblk * dq_slab;
   auto tile_q0 = [&](int it, int s) { return (qlo / QT + split_tile(it, s, S)) * QT; };
 
   // Query-tile prefetch: one 16-B chunk of Q, dO and O per thread (QT*HD/8 <= THREADS chunks per tile), the row's
@@ -429,7 +432,8 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
         if (qi < Lq) store_col32<HD < 32 ? HD : 32>(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + 32 * dsub, acc, h);
         STAMP(7 + 6 * it);
       } else {
-        // dQ[q][d] = dS·K: the head dim on the lane, so that each f32 atomic instruction adds two 128-B rows
+        // dQ[q][d] = dS·K: the head dim on the lane, so that each store instruction writes two 128-B rows of the
+        // key block's partial (no atomics: the slabs are summed per row in key-block order, deterministic)
         for (int t = 0; t < (nkeys + 15) / 16; ++t) {
           const int kr = 16 * t + 8 * (g >> 1) + q4;
           const int qc = 32 * qsub + 16 * (g & 1) + 4 * p4, dc = 32 * dsub + 16 * (g & 1) + 4 * p4;
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int qi = q0 + 32 * qsub + acc_row(i, h);
-          if (qi < Lq && d < HD) atomicAdd(dq32 + ((int64_t)bh * Lq + qi) * HD + d, acc[i]);
+          if (qi < Lq && d < HD) dq_part[((int64_t)bh * Lq + qi) * HD + d] = acc[i];
         }
       }
     }
@@ -516,10 +520,13 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
   STAMP(41);
 }
 
-// dq (bf16, rows strided by tq) <- dq32 (f32 [B*H, Lq, HD])
+// dq (bf16, rows strided by tq) <- Σ_kb dq32[kb] (f32 [nkb][B*H, Lq, HD]) over the key blocks whose workgroups wrote
+// the row's query tile (the tiles [qlo, qhi] of attn_bwd_kernel), in key-block order.
 template <int HD>
 __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict__ dq32, __bf16* __restrict__ dq,
-                                                         int64_t ld_d, int64_t tq, int H, int Lq, int64_t n4) {
+                                                         int64_t ld_d, int64_t tq, int H, int Lq, int Lk, int window,
+                                                         int64_t n4) {
+  constexpr int QT = Cfg<HD>::QT;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
   const int64_t e = 4 * i;
@@ -528,7 +535,15 @@ __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict
   const int qi = (int)(rowi % Lq);
   const int64_t bh = rowi / Lq;
   const int b = (int)(bh / H), hh = (int)(bh % H);
-  const float4 x = *reinterpret_cast<const float4*>(dq32 + e);
+  const int off = Lk - Lq, nkb = (Lk + KB - 1) / KB, tile = qi / QT;
+  float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int kb0 = kb * KB, kbend = min(Lk, kb0 + KB) - 1;
+    const int qlo = max(0, kb0 - off), qhi = window ? min(Lq - 1, kbend + window - 1 - off) : Lq - 1;
+    if (qlo > qhi || tile < qlo / QT || tile > qhi / QT) continue;
+    const float4 v = *reinterpret_cast<const float4*>(dq32 + (int64_t)kb * n4 * 4 + e);
+    x.x += v.x, x.y += v.y, x.z += v.z, x.w += v.w;
+  }
   bf16x4 w;
   w[0] = (__bf16)x.x; w[1] = (__bf16)x.y; w[2] = (__bf16)x.z; w[3] = (__bf16)x.w;
   *reinterpret_cast<bf16x4*>(dq + ((int64_t)b * tq + qi) * ld_d + hh * HD + d) = w;
@@ -563,22 +578,23 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
     return (e && atoi(e) == 1) ? 1 : 2;
   }();
   const int nsplit = (counters && Lq > Cfg<HD>::QT && max_split > 1) ? 2 : 1;
-  float* xbuf = dq32 + (nkb > 1 ? (size_t)(B * H * Lq * HD) : 0);
-  if (acc && zero_async(acc, sizeof(float) * (size_t)(B * H * Lq * HD), st) != hipSuccess) return ESGPT_ERR_LAUNCH;
+  const int64_t slab = B * H * Lq * HD;  // one f32 dQ partial per key block (nkb > 1)
+  float* xbuf = dq32 + (nkb > 1 ? (size_t)(nkb * slab) : 0);
   const dim3 grid((unsigned)(nkb * nsplit * B * H));  // 1-D: XCD-aware order in the kernel
   const int nw = (int)cdiv(Lk, 32);
 #define ESGPT_ATTN_BWD_LAUNCH(DM_)                                                                                 \
   attn_bwd_kernel<HD, DM_><<<grid, THREADS, lds, st>>>(                                                           \
       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout, \
       ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,         \
-      (int)window, drop_p, seed, keep, nw, nsplit, counters, xbuf)
+      (int)window, drop_p, seed, keep, nw, nsplit, counters, xbuf, slab)
   if (!(drop_p > 0.f)) ESGPT_ATTN_BWD_LAUNCH(DROP_NONE);
   else if (keep) ESGPT_ATTN_BWD_LAUNCH(DROP_BITS);
   else ESGPT_ATTN_BWD_LAUNCH(DROP_HASH);
 #undef ESGPT_ATTN_BWD_LAUNCH
   if (acc) {
     const int64_t n4 = B * H * Lq * HD / 4;
-    dq_convert_kernel<HD><<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(acc, (__bf16*)dq, ld_d, tq, (int)H, (int)Lq, n4);
+    dq_convert_kernel<HD><<<(unsigned)cdiv(n4, 256), 256, 0, st>>>(acc, (__bf16*)dq, ld_d, tq, (int)H, (int)Lq,
+                                                                   (int)Lk, (int)window, n4);
   }
   return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
 }
@@ -591,9 +607,9 @@ extern "C" int esgpt_debug_stamps(uint64_t* out) {
 }
 #endif
 
-// f32 dQ accumulator (more than one key block) + the dK / dV exchange slabs of the query-split pairs.
+// f32 dQ partials, one per key block (more than one key block) + the dK / dV exchange slabs of the query-split pairs.
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
-  const size_t dq = Lk > KB ? sizeof(float) * (size_t)(B * H * Lq * hd) : 0;
+  const size_t dq = Lk > KB ? sizeof(float) * (size_t)(cdiv(Lk, KB) * B * H * Lq * hd) : 0;
   const int64_t hdp = hd < 32 ? 32 : hd;  // exchange slabs hold the padded accumulator tiles
   return dq + sizeof(float) * (size_t)(B * H * cdiv(Lk, KB)) * 2 * KB * hdp;
 }

@@ -310,7 +310,9 @@ Tensor attention_bwd(const Tensor& qkv_, const Tensor& o, const Tensor& dout_, c
   const int64_t Bs = qkv.size(0), T = qkv.size(1), D3 = qkv.size(2), D = D3 / 3, hd = D / H;
   const int64_t skf = static_kv_first ? 1 : 0, Lk = T, Lq = T - skf;
   const int64_t es = qkv.element_size();
-  Tensor dqkv = skf ? at::zeros_like(qkv) : at::empty_like(qkv);
+  // static_kv_first: the kernels write every row of dk / dv and the dq rows after token 0; token 0's dq is zero
+  Tensor dqkv = at::empty_like(qkv);
+  if (skf) dqkv.select(1, 0).narrow(-1, 0, D).zero_();
   const size_t nb = esgpt_attn_bwd_workspace(Bs, H, Lq, Lk, hd);
   Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, qkv.options().dtype(at::kByte));
   int32_t* counters = esgpt_attn_bwd_counters(Bs, H, Lk) <= tickets.numel() ? ptr<int32_t>(tickets) : nullptr;

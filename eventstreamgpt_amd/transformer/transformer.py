@@ -216,6 +216,21 @@ class InnerBlock(nn.Module):
         return hidden_states, outputs
 
 
+def _final_layer_norm(ln: nn.LayerNorm, hidden: torch.Tensor) -> torch.Tensor:
+    """``ln_f`` (f32 output). Under bf16 autocast on a HIP tensor: the library's LayerNorm (``esgpt::residual_ln`` with
+    no residual; f32 statistics, one pass each way) instead of ATen's three LayerNorm kernels."""
+    from ..fused import compute_dtype, residual_ln
+
+    D = hidden.shape[-1]
+    if not (hidden.is_cuda and compute_dtype() == torch.bfloat16 and D % 4 == 0 and D <= 1024
+            and ln.weight is not None and ln.bias is not None):
+        return ln(hidden)
+    with torch.autocast("cuda", enabled=False):
+        _, out = residual_ln(None, hidden.reshape(-1, D).float().contiguous(), None, ln.weight, ln.bias, None, 0.0,
+                             float(ln.eps), torch.float32)
+    return out.view(hidden.shape)
+
+
 class StructuredTransformerBlock(nn.Module):
     def __init__(self, config: StructuredTransformerConfig, layer_id: int):
         super().__init__()
@@ -530,7 +545,7 @@ class NestedAttentionPointProcessTransformer(StructuredTransformerPreTrainedMode
                 presents["seq_past"] += (extra["seq_module"]["present_key_value"],)
             if update_dep:
                 presents["dep_graph_past"] += (extra["dep_graph_module"]["present_key_value"],)
-        hidden = self.ln_f(hidden)
+        hidden = _final_layer_norm(self.ln_f, hidden)
         if output_hidden_states:
             all_hidden = all_hidden + (hidden,)
         if use_cache:
