@@ -19,6 +19,7 @@
 // hd = 16 (C1): S and dP are one K = 16 step; the Q / dO / K images are 32 columns wide with columns 16..31 zero, so
 // dVᵀ / dKᵀ / dQ run as 32-wide tiles whose rows 16..31 come out zero and are not stored.
 // Roofline: MFMA-bound at large L; algorithmic FLOPs 8·H·hd·T (T = allowed (q, k) pairs; recompute not counted).
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -571,13 +572,26 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   }
   const int nkb = (int)cdiv(Lk, KB);
   float* acc = nkb > 1 ? dq32 : nullptr;
-  // two workgroups per key block (the zig-zag query-tile split) when there are at least two query tiles
-  // (ESGPT_ATTN_BWD_NSPLIT=1: one workgroup per key block — tuning hook, read once)
-  static const int max_split = [] {
+  // Two workgroups per key block (the zig-zag query-tile split, partial dKᵀ / dVᵀ exchanged through write-through
+  // slabs: 2 x 128 KB per pair at hd = 64) only where the parallelism pays for that exchange: fewer key-block
+  // workgroups than CUs, or a causal chain of more than 16 query tiles for the first key block. Measured
+  // (tools/attn_bench.py, dropout 0.1): C2 (128 key blocks) 29.5 vs 30.2 us split / not; C3 L=512 H=8 global
+  // (512 blocks) 161 vs 130 us, local-32 121 vs 81 us; C5 L=1024 (256 blocks) 134 vs 123 us; L=4096 B=4 H=8
+  // (512 blocks, 64-tile chains) 574 vs 819 us. (ESGPT_ATTN_BWD_NSPLIT=1 / 2: forced — tuning hook, read once.)
+  static const int forced_split = [] {
     const char* e = tuning_env("ESGPT_ATTN_BWD_NSPLIT");
-    return (e && atoi(e) == 1) ? 1 : 2;
+    return e ? atoi(e) : 0;
   }();
-  const int nsplit = (counters && Lq > Cfg<HD>::QT && max_split > 1) ? 2 : 1;
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  const int64_t chain = window > 0 ? std::min<int64_t>(Lq, KB + window) : Lq;  // queries seen by one key block
+  const bool want_split = forced_split ? forced_split == 2 : (nkb * B * H < n_cu || chain > 1024);
+  const int nsplit = (counters && Lq > Cfg<HD>::QT && want_split) ? 2 : 1;
   const int64_t slab = B * H * Lq * HD;  // one f32 dQ partial per key block (nkb > 1)
   float* xbuf = dq32 + (nkb > 1 ? (size_t)(nkb * slab) : 0);
   const dim3 grid((unsigned)(nkb * nsplit * B * H));  // 1-D: XCD-aware order in the kernel

@@ -228,15 +228,14 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
       }
     }
     const bool full = kbits == ~0ull && t0 + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - t0 < window);
+    // row maximum of the raw scores (the log2(e) scaling is monotonic: max(s)·log2e = max(s·log2e) bit for bit),
+    // then p = exp2(s·log2e − m) as one FMA per element (in the log2 domain: m = running max · log2e)
     float mt = -INFINITY;
     if (full) {
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          s[c][i] *= kLog2e;
-          mt = fmaxf(mt, s[c][i]);
-        }
+        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[c][i]);
     } else {
 #pragma unroll
       for (int c = 0; c < 2; ++c)
@@ -244,11 +243,11 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
         for (int i = 0; i < 16; ++i) {
           const int kr = 32 * c + acc_row(i, h);
           const bool ok = qvalid && ((kbits >> kr) & 1ull) && allowed(t0 + kr, qpos, window);
-          s[c][i] = ok ? s[c][i] * kLog2e : -INFINITY;
+          s[c][i] = ok ? s[c][i] : -INFINITY;
           mt = fmaxf(mt, s[c][i]);
         }
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * kLog2e;
     const float mnew = fmaxf(m, mt);
     const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
     const float msub = (mnew == -INFINITY) ? 0.f : mnew;
@@ -257,7 +256,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const float p = __builtin_amdgcn_exp2f(s[c][i] - msub);  // exp2(-inf) = 0
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[c][i], kLog2e, -msub));  // exp2(-inf) = 0
         rs += p;  // normaliser over undropped probabilities
         s[c][i] = p;
       }
@@ -317,10 +316,11 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
     rs += __shfl_xor(rs, 32, 64);
     l = l * alpha + rs;
     m = mnew;
+    if (__ballot(alpha != 1.f))  // no lane's maximum moved (most tiles past the first): the O rescale is a no-op
 #pragma unroll
-    for (int dt = 0; dt < HDP / 32; ++dt)
+      for (int dt = 0; dt < HDP / 32; ++dt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+        for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
     // Vᵀ fragment by transposed reads: lane group g (16 lanes) reads keys 16ss + 4(g>>1) + {0..3} (+8) of
     // columns 32dt + 16(g&1) + {0..15}; the lane receives its column r, in the accumulator's permuted key order.
     const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;

@@ -102,7 +102,9 @@ def _torch_attention(qkv, H, key_mask, window, skf):
 @pytest.mark.parametrize("shape", [(3, 37, 2, 16, 0, False), (2, 64, 4, 64, 0, False), (2, 70, 4, 64, 5, False),
                                    (5, 9, 4, 8, 0, True), (4, 5, 2, 64, 2, True), (2, 256, 4, 64, 32, False),
                                    (2, 200, 2, 32, 0, False), (1, 130, 2, 128, 0, False), (1, 1024, 4, 64, 0, False),
-                                   (3, 17, 4, 64, 0, True), (2, 300, 4, 16, 0, False), (4, 256, 4, 16, 32, False)])
+                                   (3, 17, 4, 64, 0, True), (2, 300, 4, 16, 0, False), (4, 256, 4, 16, 32, False),
+                                   # >= 256 key-block workgroups: the backward without the query-tile split
+                                   (32, 256, 8, 64, 0, False), (16, 512, 8, 64, 32, False)])
 def test_attention_kernel(shape, dtype):
     from eventstreamgpt_amd.kernels import AttentionFn
 
@@ -240,7 +242,7 @@ def _np_keep(seed: int, B: int, H: int, Lq: int, Lk: int, p: float):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 96, 4, 64, 0, False), (3, 40, 2, 16, 7, False), (4, 6, 2, 64, 0, True),
-                                   (2, 260, 4, 16, 0, False)])
+                                   (2, 260, 4, 16, 0, False), (32, 256, 8, 64, 0, False)])
 def test_attention_dropout(shape, dtype):
     """Attention-probability dropout: kernels vs softmax -> mask/(1-p) -> P.V with the same counter-hash mask."""
     from eventstreamgpt_amd import kernels as K
