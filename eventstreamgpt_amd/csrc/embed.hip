@@ -504,18 +504,18 @@ __device__ __forceinline__ bool bag_slot(const BagBwdArgs& a, int64_t slot, int6
 // ------------------------------------------------------------------------------------------------------------
 // Deterministic, atomic-free bag backward: a stable counting sort of the slots by vocabulary row, then a segmented
 // reduction in slot order (every sum runs in a fixed order: table gradients are bitwise repeatable).
-//   K0 bag_subject_*    (static SUM_ALL) subject sums of dsrc over valid events and levels (16-event chunks, then
-//                       the chunks in order)
 //   K1 bag_block_sort   per block of 1,024 or 4,096 slots: a stable radix sort of the slots by row (slot order within a
 //                       row), the block's per-row counts (counts[blk][V]) and every valid slot's (row, rank within
-//                       the block's run) in block-sorted order
-//   K2 bag_col_prefix   per row: exclusive prefix of counts over blocks (in place) and the row total
-//      bag_row_scan     exclusive scan of the row totals -> rowptr[0..V]
+//                       the block's run) in block-sorted order; extra workgroups of the same launch compute the static
+//                       SUM_ALL subject sums of dsrc (fixed order)
+//   K2 bag_col_prefix   per row: exclusive prefix of counts over blocks (in place) and the row total; the last-arriving
+//                       workgroup scans the row totals -> rowptr[0..V] and the list of rows spanning several chunks
 //   K3 bag_scatter      (row, block, rank) -> CSR position rowptr[row] + prefix[blk][row] + rank: (row, src, w)
 //   K4 bag_reduce       one wave per kChunk CSR entries: rows complete in the chunk are stored; a row continuing
 //                       into the previous / next chunk is stored as that chunk's head / tail partial
-//   K5 bag_combine      rows spanning chunks (a compact list): tail(c0) + the heads of c0+1 .. c1 (a fixed
-//                       16-wave interleave and a fixed combine order); rows without entries stay zero-filled
+//   K5 bag_combine      rows spanning chunks (compact lists): tail(c0) + the heads of c0+1 .. c1 in a fixed order —
+//                       one wave per short row, 256-head segments of the long rows on 16-wave workgroups summed by
+//                       the last-arriving segment; rows without entries stay zero-filled
 // ------------------------------------------------------------------------------------------------------------
 constexpr int kSortItems = 4;
 // Slots per sort block: 256 threads x 4 (1,024) by default; 1,024 x 4 (4,096) when the per-block count rows would be
@@ -530,11 +530,117 @@ static int64_t sort_threads(int64_t n_slots, int64_t V) {
 // where the row changes, then per valid slot (row, rank within the block's run | local slot << 12) in sorted order
 // and, at every run end, the run length into counts[blk][row] (the block zeroes its counts row first; the barriers
 // of the sort order those stores before the run-end stores).
+// Subject sums of the static SUM_ALL rows (sub[b] = Σ over valid events and levels of dsrc), in two fixed-order
+// levels that ride in the sort and prefix launches as extra workgroups (independent of the sort; only the reduce
+// reads them):
+//   part (sort launch): workgroup (b, chunk of kSubWaveEv events per wave); wave w sums its kSubWaveEv events over
+//        every level in (event, level) order, 8 row loads in flight (float4 per lane when D % 4 == 0), every
+//        256-column block in turn; wave 0 adds the wave partials in wave order -> sub_part[b][chunk][D];
+//   final (prefix launch): workgroup (b, 256-column block) adds the chunk partials in chunk order -> sub[b].
+constexpr int kSubWaveEv = 16;
+struct SubjArgs {
+  const float* dsrc;
+  int64_t ld, D, G;
+  float* sub;       // [B][D]
+  float* sub_part;  // [B][n_sub][D]
+  int64_t n_sub;    // chunks per subject
+  int64_t nblk;     // workgroups of the launch's main part (sort blocks / prefix blocks)
+  int64_t sub_jobs; // B x 256-column blocks (final level)
+};
+
+__device__ __forceinline__ bool subj_vec(const SubjArgs& s) {
+  return (s.D % 4 == 0) && (s.ld % 4 == 0) && (((uintptr_t)s.dsrc % 16) == 0);
+}
+
+__device__ __forceinline__ float4 load_cols4(const float* p, int64_t d0, int64_t D, bool vec) {
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (vec) {
+    if (d0 < D) t = *reinterpret_cast<const float4*>(p + d0);
+  } else {
+    if (d0 < D) t.x = p[d0];
+    if (d0 + 1 < D) t.y = p[d0 + 1];
+    if (d0 + 2 < D) t.z = p[d0 + 2];
+    if (d0 + 3 < D) t.w = p[d0 + 3];
+  }
+  return t;
+}
+
+__device__ __forceinline__ void store_cols4(float* p, int64_t d0, int64_t D, bool vec, float4 r) {
+  if (vec) {
+    if (d0 < D) *reinterpret_cast<float4*>(p + d0) = r;
+  } else {
+    if (d0 < D) p[d0] = r.x;
+    if (d0 + 1 < D) p[d0 + 1] = r.y;
+    if (d0 + 2 < D) p[d0 + 2] = r.z;
+    if (d0 + 3 < D) p[d0 + 3] = r.w;
+  }
+}
+
+template <int kWaves>
+__device__ __forceinline__ void subject_part_block(const esgpt_batch& bt, const SubjArgs& s, int64_t job,
+                                                   float4* __restrict__ s_part) {
+  constexpr int U = 8;
+  const int wave = threadIdx.x >> 6, lane = lane_id();
+  const int64_t b = job / s.n_sub, c = job % s.n_sub;
+  const int64_t l0 = (c * kWaves + wave) * kSubWaveEv, l1 = min<int64_t>(bt.L, l0 + kSubWaveEv);
+  const int64_t nrow = l1 > l0 ? (l1 - l0) * s.G : 0;
+  const bool vec = subj_vec(s);
+  for (int64_t db = 0; db * 256 < s.D; ++db) {
+    const int64_t d0 = db * 256 + (int64_t)lane * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t r0 = 0; r0 < nrow; r0 += U) {
+      float4 x[U];
+      bool on[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // every load issued (clamped row), the masked ones dropped after it
+        const int64_t r = min(r0 + u, nrow - 1);
+        const int64_t e = b * bt.L + l0 + r / s.G, g = r % s.G;
+        on[u] = r0 + u < nrow && bt.event_mask[e];
+        x[u] = load_cols4(s.dsrc + (e * s.G + g) * s.ld, d0, s.D, vec);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (on[u]) acc.x += x[u].x, acc.y += x[u].y, acc.z += x[u].z, acc.w += x[u].w;
+    }
+    s_part[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      float4 r = s_part[lane];
+#pragma unroll
+      for (int w = 1; w < kWaves; ++w) {
+        const float4 q = s_part[w * 64 + lane];
+        r.x += q.x, r.y += q.y, r.z += q.z, r.w += q.w;
+      }
+      store_cols4(s.sub_part + (b * s.n_sub + c) * s.D, d0, s.D, s.D % 4 == 0, r);
+    }
+    __syncthreads();  // s_part is rewritten for the next column block
+  }
+}
+
+// sub[b][cols] = Σ_c sub_part[b][c][cols] in chunk order (one wave per (b, 256-column block))
+__device__ __forceinline__ void subject_final_wave(const SubjArgs& s, int64_t job) {
+  const int lane = lane_id();
+  const int64_t ncb = (s.D + 255) / 256;
+  const int64_t b = job / ncb, d0 = (job % ncb) * 256 + (int64_t)lane * 4;
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t c0 = 0; c0 < s.n_sub; c0 += 8) {
+    float4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      x[u] = load_cols4(s.sub_part + (b * s.n_sub + min(c0 + u, s.n_sub - 1)) * s.D, d0, s.D, s.D % 4 == 0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (c0 + u < s.n_sub) r.x += x[u].x, r.y += x[u].y, r.z += x[u].z, r.w += x[u].w;
+  }
+  store_cols4(s.sub + b * s.D, d0, s.D, s.D % 4 == 0, r);
+}
+
 template <int kSortThreads>
 __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs a, int64_t n_slots, int end_bit,
                                                                       int32_t* __restrict__ counts,
                                                                       int2* __restrict__ sorted,
-                                                                      int32_t* __restrict__ n_valid) {
+                                                                      int32_t* __restrict__ n_valid, SubjArgs sj,
+                                                                      int32_t* __restrict__ ticket) {
   constexpr int kSortCh = kSortThreads * kSortItems;
   using Sort = rocprim::block_radix_sort<uint32_t, kSortThreads, kSortItems, uint32_t>;
   using Scan = rocprim::block_scan<int, kSortThreads>;
@@ -542,9 +648,15 @@ __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs
     typename Sort::storage_type sort;
     typename Scan::storage_type scan;
   } tmp;
-  __shared__ uint32_t s_row[kSortCh];
+  // the sort's row keys; in a subject-sum workgroup the wave partials (kSortThreads x 16 B: the same bytes)
+  __shared__ __attribute__((aligned(16))) uint32_t s_row[kSortCh];
   __shared__ int s_nv;
+  if (blockIdx.x >= sj.nblk) {
+    subject_part_block<kSortThreads / 64>(a.bt, sj, blockIdx.x - sj.nblk, reinterpret_cast<float4*>(s_row));
+    return;
+  }
   const int t = threadIdx.x;
+  if (blockIdx.x == 0 && t == 0) *ticket = 0;  // bag_col_prefix's last-arriver ticket (the kernel boundary orders it)
   const int64_t base = (int64_t)blockIdx.x * kSortCh;
   const uint32_t sentinel = (uint32_t)a.V;
   uint32_t key[kSortItems], val[kSortItems];
@@ -589,12 +701,26 @@ __global__ __launch_bounds__(kSortThreads) void bag_block_sort_kernel(BagBwdArgs
 // counts[blk][v] -> exclusive prefix over blocks (in place); total[v]. Workgroup = 64 rows (lanes) x 16 waves; wave
 // w owns the contiguous block segment [w*S, (w+1)*S): segment sums, their exclusive prefix over waves (LDS), then
 // the segment rewritten as running prefixes. Loads of a segment are issued 16 at a time.
+// The workgroup whose ticket add comes last then runs the row scan (bag_row_scan) over every row total: the totals
+// are stored write-through and read back with agent-scope loads (the last-arriver recipe of common.h), so the scan
+// needs no launch of its own.
 constexpr int kPrefWaves = 16;
+constexpr int kCombWaves = 16;
+__device__ __forceinline__ void row_scan_body(const int32_t* __restrict__ total, int64_t V, int32_t* __restrict__ rowptr,
+                                              int32_t* __restrict__ multi, int32_t* __restrict__ heavy, int chunk);
 __global__ __launch_bounds__(1024) void bag_col_prefix_kernel(int32_t* __restrict__ counts, int nblk, int64_t V,
                                                               int32_t* __restrict__ total, float* __restrict__ dtable,
-                                                              int64_t D) {
+                                                              int64_t D, int32_t* __restrict__ rowptr,
+                                                              int32_t* __restrict__ multi, int32_t* __restrict__ heavy,
+                                                              int chunk, int32_t* __restrict__ ticket, SubjArgs sj) {
   __shared__ int32_t s_seg[kPrefWaves][64];
   __shared__ int32_t s_tot[64];
+  __shared__ int s_last;
+  if (blockIdx.x >= sj.nblk) {  // subject sums, second level: one wave per (b, 256-column block)
+    const int64_t job = (int64_t)(blockIdx.x - sj.nblk) * kPrefWaves + (threadIdx.x >> 6);
+    if (job < sj.sub_jobs) subject_final_wave(sj, job);
+    return;
+  }
   const int wave = threadIdx.x >> 6, lane = lane_id();
   const int64_t v = (int64_t)blockIdx.x * 64 + lane;
   const bool ok = v < V;
@@ -613,7 +739,7 @@ __global__ __launch_bounds__(1024) void bag_col_prefix_kernel(int32_t* __restric
   int32_t run = 0;
   for (int w = 0; w < wave; ++w) run += s_seg[w][lane];
   if (wave == kPrefWaves - 1) {
-    if (ok) total[v] = run + sum;
+    if (ok) __hip_atomic_store(total + v, run + sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // write-through
     s_tot[lane] = ok ? run + sum : 1;
   }
   __syncthreads();
@@ -641,52 +767,65 @@ __global__ __launch_bounds__(1024) void bag_col_prefix_kernel(int32_t* __restric
       run += c[u];
     }
   }
+  if (last_arrival(ticket, (int)sj.nblk, &s_last)) row_scan_body(total, V, rowptr, multi, heavy, chunk);
 }
 
-// rowptr[0..V] = exclusive scan of total[0..V) (one workgroup; per-thread contiguous segments, fixed order), and
-// the compact list of rows whose entries span more than one reduce chunk (multi[1 + j], count in multi[0]).
-__global__ __launch_bounds__(1024) void bag_row_scan_kernel(const int32_t* __restrict__ total, int64_t V,
-                                                            int32_t* __restrict__ rowptr, int32_t* __restrict__ multi,
-                                                            int chunk) {
-  __shared__ int32_t s_part[1024];
-  __shared__ int32_t s_cnt[1024];
+// rowptr[0..V] = exclusive scan of total[0..V) (the 1,024 threads of the last bag_col_prefix workgroup; per-thread
+// contiguous segments, fixed order; block scans by rocPRIM), and the compact list of rows whose entries span more
+// than one reduce chunk (multi[1 + j], count in multi[0]) and its subset spanning more than kCombWaves + 1 chunks
+// (heavy[1 + k], count in heavy[0]). total is read with sc1 loads (written through by other workgroups of the launch).
+__device__ __forceinline__ void row_scan_body(const int32_t* __restrict__ total, int64_t V, int32_t* __restrict__ rowptr,
+                                              int32_t* __restrict__ multi, int32_t* __restrict__ heavy, int chunk) {
+  using Scan = rocprim::block_scan<int, 1024>;
+  __shared__ typename Scan::storage_type s_scan;
+  constexpr int kReg = 16;  // row totals held in registers per thread (V <= 16,384); larger V re-reads them
   const int tid = threadIdx.x;
   const int64_t per = (V + 1023) / 1024;
   const int64_t lo = tid * per, hi = min(V, lo + per);
-  int32_t sum = 0, nm = 0;
-  for (int64_t i = lo; i < hi; ++i) sum += total[i];
-  s_part[tid] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int32_t add = (tid >= o) ? s_part[tid - o] : 0;
-    __syncthreads();
-    s_part[tid] += add;
-    __syncthreads();
+  // sc1 buffer loads (write-through data of other XCDs), all issued before any is used
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(total), (short)0, 0x7fffffff, 0x00020000);
+  constexpr int kSC1 = 16;
+  auto tot = [&](int64_t i) { return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * i), 0, kSC1); };
+  int32_t t[kReg];
+  const bool in_reg = per <= kReg;
+  if (in_reg) {
+#pragma unroll
+    for (int k = 0; k < kReg; ++k) t[k] = lo + k < hi ? tot(lo + k) : 0;
   }
-  int32_t run = s_part[tid] - sum;
+  auto get = [&](int64_t i) { return in_reg ? t[i - lo] : tot(i); };
+  int32_t sum = 0, nm = 0, nh = 0;
+  if (in_reg) {
+#pragma unroll
+    for (int k = 0; k < kReg; ++k) sum += t[k];
+  } else {
+    for (int64_t i = lo; i < hi; ++i) sum += tot(i);
+  }
+  int32_t base = 0, all = 0;
+  Scan().exclusive_scan(sum, base, 0, all, s_scan);
+  int32_t run = base;
   for (int64_t i = lo; i < hi; ++i) {
     rowptr[i] = run;
-    const int32_t e = run + total[i];
+    const int32_t e = run + get(i);
     if (e > run && run / chunk != (e - 1) / chunk) ++nm;
+    if (e > run && (e - 1) / chunk - run / chunk > kCombWaves) ++nh;
     run = e;
   }
-  if (tid == 1023) rowptr[V] = s_part[1023];
-  s_cnt[tid] = nm;
+  if (tid == 1023) rowptr[V] = all;
+  __syncthreads();  // s_scan is reused
+  int32_t j = 0, n_multi = 0;
+  Scan().exclusive_scan(nm, j, 0, n_multi, s_scan);
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int32_t add = (tid >= o) ? s_cnt[tid - o] : 0;
-    __syncthreads();
-    s_cnt[tid] += add;
-    __syncthreads();
-  }
-  int32_t j = s_cnt[tid] - nm;
-  run = s_part[tid] - sum;
+  int32_t k = 0, n_heavy = 0;
+  Scan().exclusive_scan(nh, k, 0, n_heavy, s_scan);
+  run = base;
   for (int64_t i = lo; i < hi; ++i) {
-    const int32_t e = run + total[i];
+    const int32_t e = run + get(i);
     if (e > run && run / chunk != (e - 1) / chunk) multi[1 + j++] = (int32_t)i;
+    if (e > run && (e - 1) / chunk - run / chunk > kCombWaves) heavy[1 + k++] = (int32_t)i;
     run = e;
   }
-  if (tid == 1023) multi[0] = s_cnt[1023];
+  if (tid == 1023) multi[0] = n_multi, heavy[0] = n_heavy;
 }
 
 // CSR entry: (row, src, weight bits, 0); src < 0 = subject-sum row (-1 - b)
@@ -709,48 +848,6 @@ __global__ __launch_bounds__(256) void bag_scatter_kernel(BagBwdArgs a, const in
   }
 }
 
-// Subject sums of dsrc over valid events and all levels, deterministic in two levels: block (b, event chunk c,
-// column block) sums kSubEv events (16 loads in flight per thread) into sub_part[b][c][D]; then sub[b] = the chunk
-// partials in chunk order.
-constexpr int kSubEv = 16;
-__global__ __launch_bounds__(256) void bag_subject_part_kernel(esgpt_batch bt, int64_t G, const float* __restrict__ dsrc,
-                                                               int64_t ld, int64_t D, float* __restrict__ sub_part) {
-  const int64_t b = blockIdx.x, c = blockIdx.y;
-  const int64_t nch = gridDim.y;
-  const int64_t d = (int64_t)blockIdx.z * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  const int64_t l0 = c * kSubEv;
-  float acc = 0.f;
-  for (int64_t g = 0; g < G; ++g) {
-    float x[kSubEv];
-#pragma unroll
-    for (int u = 0; u < kSubEv; ++u) {
-      const int64_t l = l0 + u;
-      const int64_t e = b * bt.L + l;
-      x[u] = (l < bt.L && bt.event_mask[e]) ? dsrc[(e * G + g) * ld + d] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < kSubEv; ++u) acc += x[u];
-  }
-  sub_part[(b * nch + c) * D + d] = acc;
-}
-
-__global__ __launch_bounds__(256) void bag_subject_sum_kernel(const float* __restrict__ sub_part, int64_t nch,
-                                                              int64_t D, float* __restrict__ sub) {
-  const int64_t b = blockIdx.x;
-  const int64_t d = (int64_t)blockIdx.y * blockDim.x + threadIdx.x;
-  if (d >= D) return;
-  float acc = 0.f;
-  for (int64_t c0 = 0; c0 < nch; c0 += 16) {
-    float x[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = c0 + u < nch ? sub_part[(b * nch + c0 + u) * D + d] : 0.f;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc += x[u];
-  }
-  sub[b * D + d] = acc;
-}
-
 // One wave per chunk of kChunk = 64 CSR entries (lane l holds entry l); the wave walks them in groups of kGroup with
 // the group's gathered gradient rows in flight together (entry fields wave-uniform via readlane). A run (the entries
 // of one row) that starts before / continues after the chunk is written to the chunk's head / tail partial instead
@@ -763,13 +860,15 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
                                                          const int4* __restrict__ ent, const float* __restrict__ dsrc,
                                                          int64_t ld, const float* __restrict__ sub, int64_t D,
                                                          float* __restrict__ dtable, float* __restrict__ part_head,
-                                                         float* __restrict__ part_tail) {
+                                                         float* __restrict__ part_tail, int32_t* __restrict__ comb_ticket) {
   const int wave = threadIdx.x >> 6;
   const int lane = lane_id();
   const int64_t chunk = (int64_t)blockIdx.x * kWavesPerBlock + wave;
   const int64_t lo = chunk * kChunk;
   const int64_t n_ent = rowptr[V];
   if (lo >= n_ent) return;
+  const int64_t dblocks = (D + 255) / 256;
+  if (lane < dblocks) comb_ticket[chunk * dblocks + lane] = 0;  // bag_combine's tickets of the rows starting here
   const int n = (int)min<int64_t>(kChunk, n_ent - lo);
   int32_t my_v = -1, my_s = 0;
   float my_w = 0.f;
@@ -847,71 +946,140 @@ __global__ __launch_bounds__(256) void bag_reduce_kernel(const int32_t* __restri
 // 256-column block): wave w sums the row's head partials of chunks c0 + 1 + w, c0 + 17 + w, ... (8 independent
 // loads in flight), then wave 0 adds tail(c0) and the 16 wave sums in a fixed order (deterministic whatever the
 // row's length: a univariate measurement's row spans ~300 chunks of a C2 batch). Empty rows stay as zero-filled.
-constexpr int kCombWaves = 16;
+// Rows spanning at most kCombWaves + 1 chunks (most of them: 2-3 chunks) are summed by ONE wave each: tail(c0) then
+// head(c0 + 1) .. head(c1) in order. Longer rows ("heavy", their own list) are cut into segments of kSeg heads, one
+// workgroup per (row, segment, 256-column block) (rows of at most 2·kSeg heads: one segment): wave w sums heads
+// first + w, first + w + 16, … of the segment,
+// then wave 0 adds the 16 wave sums in wave order. A one-segment row adds them onto its tail and stores the row
+// (the same additions in the same order as a short row whose wave w holds at most one head); a longer row stores the
+// segment sum write-through over head(first), and the segment whose ticket add comes last (per row and column
+// block; tickets zeroed by bag_reduce) adds tail + the segment sums in segment order. Every order is fixed: bitwise
+// repeatable. (A C5 batch has one measurement in 31 % of all entries: 1,250 chunks.)
+constexpr int kSeg = 256;
 constexpr int kCombBlocks = 256;
 __global__ __launch_bounds__(1024) void bag_combine_kernel(const int32_t* __restrict__ rowptr,
-                                                          const int32_t* __restrict__ multi, int64_t D,
-                                                          const float* __restrict__ part_head,
+                                                          const int32_t* __restrict__ multi,
+                                                          const int32_t* __restrict__ heavy, int64_t seg_bound,
+                                                          int64_t D, float* __restrict__ part_head,
                                                           const float* __restrict__ part_tail,
-                                                          float* __restrict__ dtable) {
+                                                          int32_t* __restrict__ comb_ticket, float* __restrict__ dtable) {
   __shared__ float4 s_acc[kCombWaves][64];
   const int wave = threadIdx.x >> 6, lane = lane_id();
-  const int n_multi = multi[0];
+  const int n_multi = multi[0], n_heavy = heavy[0];
   const int64_t dblocks = (D + 255) / 256;
   const bool vec = (D % 4 == 0);
-  for (int64_t job = blockIdx.x; job < (int64_t)n_multi * dblocks; job += gridDim.x) {
-    const int64_t v = multi[1 + job / dblocks];
-    const int64_t d0 = (job % dblocks) * 256 + lane * 4;
+  auto span = [&](int64_t v, int64_t& c0, int64_t& c1) {
     const int64_t s = rowptr[v], e = rowptr[v + 1];
-    const int64_t c0 = s / kChunk, c1 = (e - 1) / kChunk;
-    auto load = [&](const float* p) {
-      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (vec) {
-        if (d0 < D) t = *reinterpret_cast<const float4*>(p + d0);
-      } else {
-        if (d0 < D) t.x = p[d0];
-        if (d0 + 1 < D) t.y = p[d0 + 1];
-        if (d0 + 2 < D) t.z = p[d0 + 2];
-        if (d0 + 3 < D) t.w = p[d0 + 3];
+    c0 = s / kChunk;
+    c1 = (e - 1) / kChunk;
+  };
+  auto add4 = [](float4& r, const float4& h) { r.x += h.x, r.y += h.y, r.z += h.z, r.w += h.w; };
+  // short rows: one wave each
+  const int64_t nwaves = (int64_t)gridDim.x * kCombWaves;
+  for (int64_t j = (int64_t)blockIdx.x * kCombWaves + wave; j < n_multi; j += nwaves) {
+    const int64_t v = multi[1 + j];
+    int64_t c0, c1;
+    span(v, c0, c1);
+    if (c1 - c0 > kCombWaves) continue;
+    for (int64_t db = 0; db < dblocks; ++db) {
+      const int64_t d0 = db * 256 + lane * 4;
+      float4 r = load_cols4(part_tail + c0 * D, d0, D, vec);
+      for (int64_t u0 = 0; u0 < c1 - c0; u0 += 4) {  // 4 heads in flight (clamped loads, ordered adds)
+        float4 h[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) h[u] = load_cols4(part_head + min(c0 + 1 + u0 + u, c1) * D, d0, D, vec);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (c0 + 1 + u0 + u <= c1) add4(r, h[u]);
       }
-      return t;
-    };
+      store_cols4(dtable + v * D, d0, D, vec, r);
+    }
+  }
+  // heavy rows: one workgroup per (row, segment, 256-column block)
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int kSC1 = 16;  // buffer cache policy sc1: write-through stores, L1-bypassing loads
+  const __amdgpu_buffer_rsrc_t rs_head = __builtin_amdgcn_make_buffer_rsrc(part_head, (short)0, 0x7fffffff, 0x00020000);
+  const int64_t per_row = seg_bound * dblocks;
+  // (dealt from the last workgroup down: the short rows of phase 1 sit on the first workgroups)
+  for (int64_t job = gridDim.x - 1 - blockIdx.x; job < (int64_t)n_heavy * per_row; job += gridDim.x) {
+    const int64_t kk = job / per_row, si = (job % per_row) / dblocks, db = job % dblocks;
+    const int64_t v = heavy[1 + kk];
+    int64_t c0, c1;
+    span(v, c0, c1);
+    // up to 2·kSeg heads in one segment (the single-job form: no hand-off), longer rows in kSeg-head segments
+    const int64_t nseg = c1 - c0 <= 2 * kSeg ? 1 : (c1 - c0 + kSeg - 1) / kSeg;
+    if (si >= nseg) continue;  // workgroup-uniform
+    const int64_t first = c0 + 1 + si * kSeg, last = nseg == 1 ? c1 : min(c1, first + kSeg - 1);
+    const int64_t d0 = db * 256 + lane * 4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr int U = 8;
-    for (int64_t cb = c0 + 1 + wave; cb <= c1; cb += (int64_t)kCombWaves * U) {
+    for (int64_t cb = first + wave; cb <= last; cb += (int64_t)kCombWaves * U) {
       float4 t[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t c = cb + (int64_t)kCombWaves * u;
-        t[u] = c <= c1 ? load(part_head + c * D) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int64_t c = min(cb + (int64_t)kCombWaves * u, last);
+        t[u] = load_cols4(part_head + c * D, d0, D, vec);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        acc.x += t[u].x;
-        acc.y += t[u].y;
-        acc.z += t[u].z;
-        acc.w += t[u].w;
-      }
+      for (int u = 0; u < U; ++u)
+        if (cb + (int64_t)kCombWaves * u <= last) add4(acc, t[u]);
     }
     s_acc[wave][lane] = acc;
     __syncthreads();
     if (wave == 0) {
-      float4 r = load(part_tail + c0 * D);
+      if (nseg == 1) {
+        float4 r = load_cols4(part_tail + c0 * D, d0, D, vec);
 #pragma unroll
-      for (int w = 0; w < kCombWaves; ++w) {
-        r.x += s_acc[w][lane].x;
-        r.y += s_acc[w][lane].y;
-        r.z += s_acc[w][lane].z;
-        r.w += s_acc[w][lane].w;
-      }
-      float* dst = dtable + v * D;
-      if (vec) {
-        if (d0 < D) *reinterpret_cast<float4*>(dst + d0) = r;
+        for (int w = 0; w < kCombWaves; ++w) add4(r, s_acc[w][lane]);
+        store_cols4(dtable + v * D, d0, D, vec, r);
       } else {
-        if (d0 < D) dst[d0] = r.x;
-        if (d0 + 1 < D) dst[d0 + 1] = r.y;
-        if (d0 + 2 < D) dst[d0 + 2] = r.z;
-        if (d0 + 3 < D) dst[d0 + 3] = r.w;
+        float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int w = 0; w < kCombWaves; ++w) add4(p, s_acc[w][lane]);
+        // segment sum over head(first) (this workgroup's read of it is behind the barrier), write-through
+        const int64_t off = first * D + d0;
+        if (d0 < D) {
+          if (vec) {
+            const u32x4 w4 = {__float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(p.z), __float_as_uint(p.w)};
+            __builtin_amdgcn_raw_buffer_store_b128(w4, rs_head, (int)(4 * off), 0, kSC1);
+          } else {
+            const float pv[4] = {p.x, p.y, p.z, p.w};
+            for (int q = 0; q < 4 && d0 + q < D; ++q)
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(pv[q]), rs_head, (int)(4 * (off + q)), 0, kSC1);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int t = 0;
+        if (lane == 0)
+          t = __hip_atomic_fetch_add(comb_ticket + c0 * dblocks + db, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = __shfl(t, 0, 64);
+        if (t == nseg - 1) {  // last segment of this row and column block: tail + segment sums in segment order
+          float4 r = load_cols4(part_tail + c0 * D, d0, D, vec);
+          for (int64_t s0 = 0; s0 < nseg; s0 += 4) {
+            float4 h[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int64_t o = (c0 + 1 + min(s0 + u, nseg - 1) * kSeg) * D + d0;
+              h[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (d0 < D) {
+                if (vec) {
+                  const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs_head, (int)(4 * o), 0, kSC1);
+                  h[u] = make_float4(__uint_as_float(x[0]), __uint_as_float(x[1]), __uint_as_float(x[2]),
+                                     __uint_as_float(x[3]));
+                } else {
+                  float hv[4] = {0.f, 0.f, 0.f, 0.f};
+                  for (int q = 0; q < 4 && d0 + q < D; ++q)
+                    hv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_head, (int)(4 * (o + q)), 0, kSC1));
+                  h[u] = make_float4(hv[0], hv[1], hv[2], hv[3]);
+                }
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (s0 + u < nseg) add4(r, h[u]);
+          }
+          store_cols4(dtable + v * D, d0, D, vec, r);
+        }
       }
     }
     __syncthreads();  // s_acc is rewritten by the next job
@@ -923,6 +1091,8 @@ struct BagWs {
   int32_t* total;    // [V]
   int32_t* rowptr;   // [V + 1]
   int32_t* multi;    // [1 + V]: count, then the rows spanning several reduce chunks
+  int32_t* heavy;    // [1 + V]: count, then the rows spanning more than kCombWaves + 1 chunks
+  int32_t* comb_ticket;  // [n_chunks][D / 256]: bag_combine's per-(row, column block) tickets (zeroed by bag_reduce)
   int32_t* n_valid;  // [nblk]
   int2* sorted;      // [nblk * kSortCh]
   int4* ent;         // [n_slots]
@@ -930,7 +1100,8 @@ struct BagWs {
   float* part_tail;  // [n_chunks][D]
   float* sub;        // [B][D]
   float* sub_part;   // [B][n_sub][D]
-  int64_t nblk, n_slots, n_chunks, n_sub, sort_threads, sort_ch;
+  int32_t* ticket;   // bag_col_prefix's last-arriver ticket (zeroed by the sort launch)
+  int64_t nblk, n_slots, n_chunks, sort_threads, sort_ch;
   size_t bytes;
 };
 
@@ -954,14 +1125,16 @@ static BagWs carve(void* base, const esgpt_batch* bt, int64_t G, int64_t V, int6
   w.total = (int32_t*)take(sizeof(int32_t) * V);
   w.rowptr = (int32_t*)take(sizeof(int32_t) * (V + 1));
   w.multi = (int32_t*)take(sizeof(int32_t) * (V + 1));
+  w.heavy = (int32_t*)take(sizeof(int32_t) * (V + 1));
   w.n_valid = (int32_t*)take(sizeof(int32_t) * w.nblk);
   w.sorted = (int2*)take(sizeof(int2) * w.nblk * w.sort_ch);
   w.ent = (int4*)take(sizeof(int4) * w.n_slots);
   w.part_head = (float*)take(sizeof(float) * w.n_chunks * D);
   w.part_tail = (float*)take(sizeof(float) * w.n_chunks * D);
+  w.comb_ticket = (int32_t*)take(sizeof(int32_t) * w.n_chunks * cdiv(D, 256));
   w.sub = (float*)take(sizeof(float) * bt->B * D);
-  w.n_sub = std::max<int64_t>(1, cdiv(bt->L, kSubEv));
-  w.sub_part = (float*)take(sizeof(float) * bt->B * w.n_sub * D);
+  w.sub_part = (float*)take(sizeof(float) * bt->B * cdiv(bt->L, (w.sort_threads / 64) * kSubWaveEv) * D);
+  w.ticket = (int32_t*)take(sizeof(int32_t));
   w.bytes = off;
   return w;
 }
@@ -1077,23 +1250,27 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   ESGPT_REQUIRE(w.n_slots < (1ll << 31) && batch->B * batch->L * bk.G < (1ll << 31));  // int32 CSR fields
   hipStream_t st = as_stream(stream);
   BagBwdArgs a{*batch, bk, selector, flags, dyn_scale, static_scale, V};
-  if ((flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM && batch->B > 0) {
-    bag_subject_part_kernel<<<dim3((unsigned)batch->B, (unsigned)w.n_sub, (unsigned)cdiv(D, 256)), 256, 0, st>>>(
-        *batch, bk.G, dsrc, ld, D, w.sub_part);
-    bag_subject_sum_kernel<<<dim3((unsigned)batch->B, (unsigned)cdiv(D, 256)), 256, 0, st>>>(w.sub_part, w.n_sub, D,
-                                                                                          w.sub);
-  }
+  // the subject sums (static SUM_ALL) ride in the sort and prefix launches as extra workgroups
+  const bool subj = (flags & ESGPT_EMB_STATIC) && batch->S > 0 && selector != ESGPT_BAG_NUM && batch->B > 0;
+  const int64_t n_sub = cdiv(batch->L, (w.sort_threads / 64) * kSubWaveEv);
+  SubjArgs sj{dsrc, ld, D, bk.G, w.sub, w.sub_part, n_sub, w.nblk, batch->B * cdiv(D, 256)};
+  const int64_t n_part = subj ? batch->B * n_sub : 0;
   // (no zero-fill launches: the sort blocks zero their counts rows, bag_col_prefix the table rows without entries)
   int end_bit = 1;
   while (end_bit < 32 && (V >> end_bit) != 0) ++end_bit;  // keys 0 .. V (the sentinel) fit in end_bit bits
+  const unsigned g_sort = (unsigned)(w.nblk + n_part);
   if (w.sort_threads == 1024)
-    bag_block_sort_kernel<1024><<<(unsigned)w.nblk, 1024, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
-                                                                   w.n_valid);
+    bag_block_sort_kernel<1024><<<g_sort, 1024, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted, w.n_valid, sj,
+                                                         w.ticket);
   else
-    bag_block_sort_kernel<256><<<(unsigned)w.nblk, 256, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted,
-                                                                   w.n_valid);
-  bag_col_prefix_kernel<<<(unsigned)cdiv(V, 64), 1024, 0, st>>>(w.counts, (int)w.nblk, V, w.total, dtable, D);
-  bag_row_scan_kernel<<<1, 1024, 0, st>>>(w.total, V, w.rowptr, w.multi, kChunk);
+    bag_block_sort_kernel<256><<<g_sort, 256, 0, st>>>(a, w.n_slots, end_bit, w.counts, w.sorted, w.n_valid, sj,
+                                                       w.ticket);
+  // column prefixes, then (last-arriving workgroup) the row scan; extra workgroups finish the subject sums
+  SubjArgs sp = sj;
+  sp.nblk = cdiv(V, 64);
+  const int64_t n_fin = subj ? cdiv(sj.sub_jobs, kPrefWaves) : 0;
+  bag_col_prefix_kernel<<<(unsigned)(sp.nblk + n_fin), 1024, 0, st>>>(w.counts, (int)w.nblk, V, w.total, dtable, D,
+                                                                      w.rowptr, w.multi, w.heavy, kChunk, w.ticket, sp);
   bag_scatter_kernel<<<dim3(4, (unsigned)w.nblk), 256, 0, st>>>(a, w.sorted, w.n_valid, w.counts, w.rowptr, w.ent,
                                                                  w.sort_ch);
   // The number of entries is data-dependent (not known on the host without a sync): launch for the upper bound;
@@ -1101,11 +1278,12 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
   const unsigned g_red = (unsigned)cdiv(w.n_chunks, kWavesPerBlock);
   if (D % 4 == 0 && D >= 256 && ld % 4 == 0 && ((uintptr_t)dsrc % 16) == 0 && ((uintptr_t)dtable % 16) == 0)
     bag_reduce_kernel<4><<<g_red, 256, 0, st>>>(w.rowptr, V, w.ent, dsrc, ld, w.sub, D, dtable, w.part_head,
-                                                w.part_tail);
+                                                w.part_tail, w.comb_ticket);
   else
     bag_reduce_kernel<1><<<g_red, 256, 0, st>>>(w.rowptr, V, w.ent, dsrc, ld, w.sub, D, dtable, w.part_head,
-                                                w.part_tail);
-  bag_combine_kernel<<<kCombBlocks, 1024, 0, st>>>(w.rowptr, w.multi, D, w.part_head, w.part_tail, dtable);
+                                                w.part_tail, w.comb_ticket);
+  bag_combine_kernel<<<kCombBlocks, 1024, 0, st>>>(w.rowptr, w.multi, w.heavy, cdiv(w.n_chunks, kSeg) + 1, D,
+                                                   w.part_head, w.part_tail, w.comb_ticket, dtable);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
