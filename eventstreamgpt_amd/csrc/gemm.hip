@@ -196,6 +196,7 @@ struct Prob {
   int rs_extra_n;
   int xmap;  // grouped backward workgroup order: 0 = xcd_remap runs; 1 (dW) / 2 (dX) = split-major (pair_lin)
   int rps;   // xmap 2: dX row blocks per dW split chunk
+  int dbg;   // tools build only (ESGPT_GEMM_DBG): bit 0 = skip the bf16 output stores (timing experiments)
 };
 
 // Split-major order of a projection backward (xmap): workgroup id -> XCD x = id % 8 (the dispatcher's round robin),
@@ -234,14 +235,16 @@ __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w 
 // B image), sized for the operand layouts (the K-contig images are smaller: the 64x64 forward kernel fits 4
 // workgroups per CU instead of 3). Also holds the epilogue's C tile (f32: BM x (BN + 4) floats) and the split-K
 // reducer flag.
-template <bool AKC, bool BKC, int FM, int FN>
+template <bool AKC, bool BKC, int FM, int FN, int NB = 2>
 constexpr int lds_elems() {
-  constexpr int st = 2 * (Tile<AKC, 64 * FM>::kElems + Tile<BKC, 64 * FN>::kElems);
+  constexpr int st = NB * (Tile<AKC, 64 * FM>::kElems + Tile<BKC, 64 * FN>::kElems);
   constexpr int epi = 64 * FM * (64 * FN + 4) * 2;  // f32 C tile in bf16 elements
   return st > epi ? st : epi;
 }
 
-template <bool AKC, bool BKC, int NS_, int FM, int FN>
+// NB = LDS staging buffers: 2 (one barrier per k-tile) or 1 (two barriers per k-tile, half the LDS: the 64x64
+// forward then keeps 8 workgroups per CU resident instead of 4 — every tile of a C2 projection in flight at once).
+template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2>
 __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) {
   constexpr int NS = NS_, BM = 64 * FM, BN = 64 * FN, F = FM * FN;
   constexpr bool kRowSum = !(AKC && BKC);  // compiled out of the forward (K-contig x K-contig) instantiation
@@ -299,7 +302,10 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
       }
     };
     auto consume = [&](int st, int i) {
-      __bf16* sA = smem + (i & 1) * (TA::kElems + TB::kElems);
+      if constexpr (NB == 1) {
+        if (i > 0) __syncthreads();  // every wave is done reading the previous k-tile
+      }
+      __bf16* sA = smem + (NB == 2 ? (i & 1) : 0) * (TA::kElems + TB::kElems);
       __bf16* sB = sA + TA::kElems;
       if constexpr (FAST) {
         TA::store_fast(sA, ra[st]);
@@ -552,7 +558,7 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     for (int q = 0; q < BM * BN / 8 / THREADS; ++q) {
       const int ch = threadIdx.x + THREADS * q, tr = ch / (BN / 8), tc = (ch % (BN / 8)) * 8;
       const int gr = m0 + tr, gc = n0 + tc;
-      if (gr < M && gc < N)
+      if (gr < M && gc < N && !(p.dbg & 1))
         *reinterpret_cast<uint4*>(dst + (int64_t)gr * ld + gc) = *reinterpret_cast<const uint4*>(tb + tr * kLdB + tc);
     }
   };
@@ -587,11 +593,21 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   store_tile(d, reinterpret_cast<__bf16*>(p.C), p.ldc);
 }
 
-template <bool AKC, bool BKC, int NS_, int FM, int FN>
+template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2>
 __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC, FM, FN>()];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC, FM, FN, NB>()];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile<AKC, BKC, NS_, FM, FN>(p, lin, smem);
+  gemm_tile<AKC, BKC, NS_, FM, FN, NB>(p, lin, smem);
+}
+
+// Forward LDS staging buffers (1 or 2; ESGPT_GEMM_FWD_NB tuning hook, read once).
+int fwd_buffers() {
+  static int nb = 0;
+  if (nb == 0) {
+    const char* e = tuning_env("ESGPT_GEMM_FWD_NB");
+    nb = (e && atoi(e) == 2) ? 2 : 1;
+  }
+  return nb;
 }
 
 // Forward register-stage depth (2 or 3; ESGPT_GEMM_FWD_NS tuning hook, read once).
@@ -842,6 +858,7 @@ template <int FM, int FN>
 void launch_fwd(const Prob& p, hipStream_t st) {
   const dim3 grid((unsigned)n_wg(p));
   if (fwd_stages() == 2) gemm_kernel<true, true, 2, FM, FN><<<grid, THREADS, 0, st>>>(p);
+  else if (fwd_buffers() == 1) gemm_kernel<true, true, 3, FM, FN, 1><<<grid, THREADS, 0, st>>>(p);
   else gemm_kernel<true, true, 3, FM, FN><<<grid, THREADS, 0, st>>>(p);
 }
 
@@ -998,6 +1015,7 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
     p.aux_out = reinterpret_cast<__bf16*>(pre);
     p.ld_aux = ldy;
   }
+  if (const char* e = tuning_env("ESGPT_GEMM_DBG")) p.dbg = atoi(e);
   hipStream_t st = as_stream(stream);
   switch (tc.fm * 10 + tc.fn) {
     case 21: launch_fwd<2, 1>(p, st); break;
