@@ -600,6 +600,18 @@ __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
   gemm_tile<AKC, BKC, NS_, FM, FN, NB>(p, lin, smem);
 }
 
+// The same tiles walked by a persistent grid (gridDim.x a multiple of 8 and at most the tile count): workgroup b
+// takes ids b, b + grid, … — all on b's XCD — mapped by xcd_remap over the whole tile range, so each XCD still walks
+// a contiguous run of tiles. (Tools-build experiment, ESGPT_GEMM_PERSIST = workgroups per CU.)
+template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2>
+__global__ __launch_bounds__(THREADS) void gemm_persist_kernel(Prob p, int ntiles) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC, FM, FN, NB>()];
+  for (int id = blockIdx.x; id < ntiles; id += gridDim.x) {
+    gemm_tile<AKC, BKC, NS_, FM, FN, NB>(p, xcd_remap(id, ntiles), smem);
+    __syncthreads();  // the LDS images / epilogue tile are rewritten by the next tile
+  }
+}
+
 // Forward LDS staging buffers (1 or 2; ESGPT_GEMM_FWD_NB tuning hook, read once).
 int fwd_buffers() {
   static int nb = 0;
@@ -857,6 +869,18 @@ int64_t dw_target(bool has_dx, int64_t T, int64_t in, int64_t out) {
 template <int FM, int FN>
 void launch_fwd(const Prob& p, hipStream_t st) {
   const dim3 grid((unsigned)n_wg(p));
+  static const int persist = [] {
+    const char* e = tuning_env("ESGPT_GEMM_PERSIST");
+    return e ? atoi(e) : 0;
+  }();
+  if (persist > 0 && FM == 1 && FN == 1) {
+    const int nt = n_wg(p);
+    const int g = std::min(nt, 256 * persist) & ~7;
+    if (g >= 8 && nt % 8 == 0) {
+      gemm_persist_kernel<true, true, 3, FM, FN, 1><<<dim3((unsigned)g), THREADS, 0, st>>>(p, nt);
+      return;
+    }
+  }
   if (fwd_stages() == 2) gemm_kernel<true, true, 2, FM, FN><<<grid, THREADS, 0, st>>>(p);
   else if (fwd_buffers() == 1) gemm_kernel<true, true, 3, FM, FN, 1><<<grid, THREADS, 0, st>>>(p);
   else gemm_kernel<true, true, 3, FM, FN><<<grid, THREADS, 0, st>>>(p);
