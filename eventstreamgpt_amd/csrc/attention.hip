@@ -452,7 +452,17 @@ __device__ __forceinline__ float cross_rows(float v) {
 
 constexpr int kSmall4Lk = 8;
 
-template <typename T, int VE>
+// Dropout multiplier of element (bh, qi, kj): the 32-bit index form when every element index of the launch fits 32
+// bits (the same bits as dropout_mult; no 64-bit index products or high-word multiply).
+template <bool I32>
+__device__ __forceinline__ float small_keep(const DropoutSpec& dr, int64_t bh, int64_t Lq, int64_t Lk, int64_t qi,
+                                            int64_t kj) {
+  if constexpr (I32)
+    return dropout_mult_32(dr, ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk + (uint32_t)kj);
+  return dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kj));
+}
+
+template <typename T, int VE, int LKM, bool I32>
 __global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, const T* __restrict__ k,
                                                        const T* __restrict__ v, int64_t ld_in, int64_t tq,
                                                        T* __restrict__ o, int64_t ld_o, float* __restrict__ lse,
@@ -460,7 +470,6 @@ __global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, 
                                                        const uint8_t* __restrict__ qmask, int64_t B, int64_t H,
                                                        int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
                                                        const uint64_t* __restrict__ seed) {
-  constexpr int LKM = kSmall4Lk;
   const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bh >= B * H) return;  // wave-uniform
   const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
@@ -507,7 +516,7 @@ __global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, 
       if (s[j] == -INFINITY) continue;
       const float p = expf(s[j] - m);
       l += p;  // normaliser over undropped probabilities
-      const float pd = dr.p > 0.f ? p * dropout_mult(dr, elem_index(bh, Lq, Lk, ii, j)) : p;
+      const float pd = dr.p > 0.f ? p * small_keep<I32>(dr, bh, Lq, Lk, ii, j) : p;
 #pragma unroll
       for (int e = 0; e < VE; ++e) acc[e] = fmaf(pd, vr[j][e], acc[e]);
     }
@@ -522,14 +531,13 @@ __global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, 
   }
 }
 
-template <typename T, int VE>
+template <typename T, int VE, int LKM, bool I32>
 __global__ __launch_bounds__(256) void attn_bwd_small4(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
     const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, T* __restrict__ dk,
     T* __restrict__ dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window,
     float drop_p, const uint64_t* __restrict__ seed) {
-  constexpr int LKM = kSmall4Lk;
   const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bh >= B * H) return;  // wave-uniform
   const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
@@ -578,7 +586,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small4(
       sv = row_sum16(sv);
       dpv = row_sum16(dpv);
       if (!(qvalid && kv[j] && j >= jlo && j <= pos)) continue;  // row-uniform
-      const float keep = dr.p > 0.f ? dropout_mult(dr, elem_index(bh, Lq, Lk, ii, j)) : 1.f;
+      const float keep = dr.p > 0.f ? small_keep<I32>(dr, bh, Lq, Lk, ii, j) : 1.f;
       const float p = expf(sv - ls);
       const float ds = p * (dpv * keep - dl);
       const float pd = p * keep;
@@ -628,21 +636,34 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
                  hipStream_t st) {
   const dim3 grid((unsigned)cdiv(B * H, 4)), block(256);
   if (small4_ok<T>(Lk, hd, {q, k, v, o, dout, dq, dk, dv}, {ld_in, ld_o, ld_do, ld_d})) {
-#define SMALL4(VE)                                                                                                   \
+// key registers sized to the sequence (LKM = 4, 6 or 8 keys): the C4 dependency graph (5 keys) holds 3/4 of the
+// 8-key form's K / V / dK / dV registers
+#define SMALL4_L(VE, LKM, I32)                                                                                       \
   do {                                                                                                               \
     if (fwd)                                                                                                         \
-      attn_fwd_small4<T, VE><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (T*)o, ld_o,  \
-                                                     lse_w, kmask, qmask, B, H, Lq, Lk, (int)hd, window, drop_p, seed); \
+      attn_fwd_small4<T, VE, LKM, I32><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq,     \
+                                                               (T*)o, ld_o, lse_w, kmask, qmask, B, H, Lq, Lk,      \
+                                                               (int)hd, window, drop_p, seed);                      \
     else                                                                                                             \
-      attn_bwd_small4<T, VE><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o,  \
-                                                     ld_o, (const T*)dout, ld_do, lse_r, kmask, qmask, (T*)dq,       \
-                                                     (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p,    \
-                                                     seed);                                                          \
+      attn_bwd_small4<T, VE, LKM, I32><<<grid, block, 0, st>>>(                                                      \
+          (const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o, ld_o, (const T*)dout, ld_do, lse_r, kmask,  \
+          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed);                         \
+  } while (0)
+  // 32-bit dropout element indices whenever the launch's indices fit (the same keep bits); the 64-bit form only for
+  // launches past 2^32 elements
+  const bool idx32 = (uint64_t)(B * H) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;
+#define SMALL4(VE)                                     \
+  do {                                                 \
+    if (!idx32) SMALL4_L(VE, 8, false);                \
+    else if (Lk <= 4) SMALL4_L(VE, 4, true);           \
+    else if (Lk <= 6) SMALL4_L(VE, 6, true);           \
+    else SMALL4_L(VE, 8, true);                        \
   } while (0)
     if (hd == 16) SMALL4(1);
     else if (hd == 32) SMALL4(2);
     else SMALL4(4);
 #undef SMALL4
+#undef SMALL4_L
     return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
   }
 #define SMALL(DPL, LKM)                                                                                             \
