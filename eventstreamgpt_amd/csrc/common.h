@@ -206,6 +206,14 @@ __device__ __forceinline__ void dropout_mult2_32(const DropoutSpec& d, uint32_t 
   m1 = (hh >> 16) >= d.thresh ? d.scale : 0.f;
 }
 
+// Both multipliers of the element pair at the EVEN index row·D + col, in the 32-bit form when every element index of
+// the launch fits 32 bits (`i32`, wave-uniform): the same bits as dropout_mult2 without 64-bit index products.
+__device__ __forceinline__ void dropout_pair_rc(const DropoutSpec& d, bool i32, int64_t row, int64_t D, int64_t col,
+                                                float& m0, float& m1) {
+  if (i32) dropout_mult2_32(d, (uint32_t)row * (uint32_t)D + (uint32_t)col, m0, m1);
+  else dropout_mult2(d, (uint64_t)(row * D + col), m0, m1);
+}
+
 __device__ __forceinline__ DropoutSpec make_dropout(float p, const uint64_t* seed_ptr) {
   DropoutSpec d;
   d.p = p;

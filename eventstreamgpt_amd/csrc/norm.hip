@@ -60,7 +60,6 @@ __device__ __forceinline__ void store4(bf16* p, const V4& a) {
 
 __device__ __forceinline__ V4 zero4() { return V4{{0.f, 0.f, 0.f, 0.f}}; }
 
-__device__ __forceinline__ uint64_t drop_idx(int64_t row, int64_t D, int64_t col) { return (uint64_t)(row * D + col); }
 
 // Row of x under skip_T = T > 1 (static_kv_first residual, transformer.py:437): x = [N / (T-1), T, D] and output row r
 // reads the rows after each sequence's first one.
@@ -90,6 +89,7 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
                                                               TO* __restrict__ out, float* __restrict__ mean_o,
                                                               float* __restrict__ rstd_o, int64_t skip_T) {
   const DropoutSpec dr = make_dropout(drop_p, seed);
+  const bool i32 = (uint64_t)N * (uint64_t)D <= 0xffffffffull;  // 32-bit dropout element indices
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * R;
   if (row0 >= N) return;
@@ -125,8 +125,8 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
         if (y) {
           float z[4] = {1.f, 1.f, 1.f, 1.f};
           if (dr.p > 0.f) {  // row * D + c is even (D % 4 == 0): two element pairs
-            dropout_mult2(dr, drop_idx(row, D, c), z[0], z[1]);
-            dropout_mult2(dr, drop_idx(row, D, c + 2), z[2], z[3]);
+            dropout_pair_rc(dr, i32, row, D, c, z[0], z[1]);
+            dropout_pair_rc(dr, i32, row, D, c + 2, z[2], z[3]);
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -185,6 +185,7 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
     float* __restrict__ dx, TY* __restrict__ dy, float* __restrict__ part, int64_t skip_T) {
   __shared__ float s_part[kWaves][3][4 * 64];
   const DropoutSpec dr = make_dropout(drop_p, seed);
+  const bool i32 = (uint64_t)N * (uint64_t)D <= 0xffffffffull;  // 32-bit dropout element indices
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   V4 pg[KC], pb[KC], py[KC], wv[KC];
 #pragma unroll
@@ -259,8 +260,8 @@ __global__ __launch_bounds__(256) void residual_ln_bwd_kernel(
           V4 e;
           float z[4] = {1.f, 1.f, 1.f, 1.f};
           if (dr.p > 0.f) {
-            dropout_mult2(dr, drop_idx(row, D, c), z[0], z[1]);
-            dropout_mult2(dr, drop_idx(row, D, c + 2), z[2], z[3]);
+            dropout_pair_rc(dr, i32, row, D, c, z[0], z[1]);
+            dropout_pair_rc(dr, i32, row, D, c + 2, z[2], z[3]);
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {

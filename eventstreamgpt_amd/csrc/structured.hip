@@ -59,6 +59,7 @@ __global__ __launch_bounds__(kThreads) void residual_fwd_kernel(const float* __r
                                                                int64_t skip_T, float p, const uint64_t* seed,
                                                                int64_t N, int64_t D, float* __restrict__ h) {
   const DropoutSpec dr = make_dropout(p, seed);
+  const bool i32 = (uint64_t)N * (uint64_t)D <= 0xffffffffull;  // 32-bit dropout element indices
   const int64_t n4 = N * D / 4, D4 = D / 4;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
     const int64_t r = i / D4, c = (i - r * D4) * 4;
@@ -68,8 +69,8 @@ __global__ __launch_bounds__(kThreads) void residual_fwd_kernel(const float* __r
       float4 yv = ld4y(y + r * D + c);
       if (p > 0.f) {
         float z0, z1, z2, z3;
-        dropout_mult2(dr, (uint64_t)(r * D + c), z0, z1);
-        dropout_mult2(dr, (uint64_t)(r * D + c + 2), z2, z3);
+        dropout_pair_rc(dr, i32, r, D, c, z0, z1);
+        dropout_pair_rc(dr, i32, r, D, c + 2, z2, z3);
         yv.x *= z0, yv.y *= z1, yv.z *= z2, yv.w *= z3;
       }
       o = make_float4(xv.x + yv.x, xv.y + yv.y, xv.z + yv.z, xv.w + yv.w);
@@ -87,6 +88,7 @@ __global__ __launch_bounds__(kThreads) void residual_bwd_kernel(const float* __r
                                                                int64_t N, int64_t D, float* __restrict__ dx,
                                                                TY* __restrict__ dy) {
   const DropoutSpec dr = make_dropout(p, seed);
+  const bool i32 = (uint64_t)N * (uint64_t)D <= 0xffffffffull;  // 32-bit dropout element indices
   const int64_t D4 = D / 4, n4 = N * D4;
   const int64_t xN = skip_T ? N / (skip_T - 1) * skip_T : N;
   const int64_t total = n4 + (dx ? xN * D4 : 0);
@@ -98,8 +100,8 @@ __global__ __launch_bounds__(kThreads) void residual_bwd_kernel(const float* __r
         g = ld4(dh + r * D + c);
         if (p > 0.f) {
           float z0, z1, z2, z3;
-          dropout_mult2(dr, (uint64_t)(r * D + c), z0, z1);
-          dropout_mult2(dr, (uint64_t)(r * D + c + 2), z2, z3);
+          dropout_pair_rc(dr, i32, r, D, c, z0, z1);
+          dropout_pair_rc(dr, i32, r, D, c + 2, z2, z3);
           g.x *= z0, g.y *= z1, g.z *= z2, g.w *= z3;
         }
       }
