@@ -196,7 +196,7 @@ struct Prob {
   int rs_extra_n;
   int xmap;  // grouped backward workgroup order: 0 = xcd_remap runs; 1 (dW) / 2 (dX) = split-major (pair_lin)
   int rps;   // xmap 2: dX row blocks per dW split chunk
-  int dbg;   // tools build only (ESGPT_GEMM_DBG): bit 0 = skip the bf16 output stores (timing experiments)
+  int dbg;   // tools build only (ESGPT_GEMM_DBG): bit 0 = skip the bf16 output stores, bit 1 = skip the MFMA k-steps
 };
 
 // Split-major order of a projection backward (xmap): workgroup id -> XCD x = id % 8 (the dispatcher's round robin),
@@ -315,6 +315,7 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
         TB::store(sB, rb[st], n0, N, kb + i * BK, ke);
       }
       __syncthreads();
+      if (p.dbg & 2) return;  // tools build (ESGPT_GEMM_DBG bit 1): operand staging only, no fragment reads / MFMAs
 #pragma unroll
       for (int t = 0; t < BK / 16; ++t) {
         bf16x8 af[FM], bfr[FN];
@@ -627,7 +628,7 @@ int fwd_stages() {
   static int ns = 0;
   if (ns == 0) {
     const char* e = tuning_env("ESGPT_GEMM_FWD_NS");
-    ns = (e && atoi(e) == 2) ? 2 : 3;
+    ns = e ? std::min(5, std::max(2, atoi(e))) : 3;
   }
   return ns;
 }
@@ -759,9 +760,13 @@ constexpr int kFwdTiles[] = {11, 21, 12, 22};
 constexpr int kDxTiles[] = {11, 21, 22};
 constexpr int kDwTiles[] = {11, 22};
 
-TileCfg fwd_tile(int64_t /*M*/, int64_t /*N*/, int64_t /*K*/) {
-  static const TileCfg t = env_tile("ESGPT_GEMM_TILE_FWD", TileCfg{1, 1}, kFwdTiles, 4);
-  return t;
+// Forward tiles: 128x64 for the plain-store products with K <= 256 and at least 512 output columns (tools/fwd_sweep.sh,
+// C2 shapes: qkv 11.2 -> 10.2 us, head 20.3 -> 19.2 us), 64x64 otherwise (out_proj and c_fc with its activation
+// epilogue are 5-13 % slower at 128x64, c_proj at K = 1024 equal).
+TileCfg fwd_tile(int64_t M, int64_t N, int64_t K, bool act) {
+  static const TileCfg forced = env_tile("ESGPT_GEMM_TILE_FWD", TileCfg{0, 0}, kFwdTiles, 4);
+  if (forced.fm) return forced;
+  return (!act && K <= 256 && N >= 512 && M >= 128) ? TileCfg{2, 1} : TileCfg{1, 1};
 }
 TileCfg dx_tile(int64_t /*T*/, int64_t /*in*/, int64_t /*out*/) {
   static const TileCfg t = env_tile("ESGPT_GEMM_TILE_DX", TileCfg{1, 1}, kDxTiles, 3);
@@ -882,6 +887,10 @@ void launch_fwd(const Prob& p, hipStream_t st) {
     }
   }
   if (fwd_stages() == 2) gemm_kernel<true, true, 2, FM, FN><<<grid, THREADS, 0, st>>>(p);
+#ifdef ESGPT_TUNING_HOOKS
+  else if (fwd_stages() == 4) gemm_kernel<true, true, 4, FM, FN, 1><<<grid, THREADS, 0, st>>>(p);
+  else if (fwd_stages() == 5) gemm_kernel<true, true, 5, FM, FN, 1><<<grid, THREADS, 0, st>>>(p);
+#endif
   else if (fwd_buffers() == 1) gemm_kernel<true, true, 3, FM, FN, 1><<<grid, THREADS, 0, st>>>(p);
   else gemm_kernel<true, true, 3, FM, FN><<<grid, THREADS, 0, st>>>(p);
 }
@@ -1004,8 +1013,25 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   ESGPT_REQUIRE(shapes_ok(akc, bkc, A, lda, B, ldb, M, N, K, C, ldc, f32));
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   if (M == 0 || N == 0) return ESGPT_OK;
-  const TileCfg tc{1, 1};
+  // the forward projections (K-contig x K-contig, bf16 out, no split): the forward kernel configuration of
+  // esgpt_linear_fwd (tile / stages / LDS buffers)
+  const bool fwd_form = akc && bkc && !f32 && !accumulate && alpha == nullptr;
+  const TileCfg tc = fwd_form ? fwd_tile(M, N, K, false) : TileCfg{1, 1};
   Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget, tc);
+  if (fwd_form && p.splits == 1) {
+    if (const char* e = tuning_env("ESGPT_GEMM_DBG")) p.dbg = atoi(e);
+    hipStream_t st = as_stream(stream);
+    switch (tc.fm * 10 + tc.fn) {
+      case 21: launch_fwd<2, 1>(p, st); break;
+      case 12: launch_fwd<1, 2>(p, st); break;
+      case 22: launch_fwd<2, 2>(p, st); break;
+      default: launch_fwd<1, 1>(p, st); break;
+    }
+    ESGPT_LAUNCH_CHECK();
+    return ESGPT_OK;
+  }
+  if (tc.fm != 1 || tc.fn != 1) p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, 0, accumulate, bias, alpha, kTarget,
+                                                TileCfg{1, 1});
   if (p.splits > 1) {
     p.ext_reduce = f32 && p.splits > in_launch_splits();
     ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N, tc) && (p.ext_reduce || counters));
@@ -1031,7 +1057,7 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
   if (T == 0 || out == 0) return ESGPT_OK;
-  const TileCfg tc = fwd_tile(T, out, in);
+  const TileCfg tc = fwd_tile(T, out, in, act >= 0);
   Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 0, 0, bias, nullptr, 0, tc);  // never split
   if (act >= 0) {
     p.epi = EPI_BIAS_ACT;
