@@ -196,7 +196,8 @@ struct Prob {
   int rs_extra_n;
   int xmap;  // grouped backward workgroup order: 0 = xcd_remap runs; 1 (dW) / 2 (dX) = split-major (pair_lin)
   int rps;   // xmap 2: dX row blocks per dW split chunk
-  int dbg;   // tools build only (ESGPT_GEMM_DBG): bit 0 = skip the bf16 output stores, bit 1 = skip the MFMA k-steps
+  int dbg;   // tools build only (ESGPT_GEMM_DBG): bit 0 = skip the bf16 output stores, bit 1 = skip the MFMA k-steps,
+             // bit 2 / 3 = grouped backward without its dW / dX workgroups
 };
 
 // Split-major order of a projection backward (xmap): workgroup id -> XCD x = id % 8 (the dispatcher's round robin),
@@ -650,11 +651,14 @@ __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1
                            : lds_elems<true, false, XM, XN>();
   __shared__ __attribute__((aligned(16))) __bf16 smem[kLds];
   const int id = blockIdx.x, n1 = p0.wg0;
-  if (id < n1)
+  if (id < n1) {
+    if (p1.dbg & 4) return;  // tools build: the dX product alone
     gemm_tile<false, false, bwd_stages<WM, WN>(), WM, WN>(p1, p1.xmap ? pair_lin(p1, id) : xcd_remap(id, n1), smem);
-  else
+  } else {
+    if (p0.dbg & 8) return;  // tools build: the dW product alone
     gemm_tile<true, false, bwd_stages<XM, XN>(), XM, XN>(
         p0, p0.xmap ? pair_lin(p0, id - n1) : xcd_remap(id - n1, gridDim.x - n1), smem);
+  }
 }
 
 // Split-K reduction as its own launch (large slab sets: one last-arriving workgroup reading every slab of its tile
@@ -962,6 +966,7 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
     p1.slab = reinterpret_cast<float*>(workspace);
     p1.counters = counters;
   }
+  if (const char* e = tuning_env("ESGPT_GEMM_DBG")) p0.dbg = p1.dbg = atoi(e);
   if (has_dx && !st_dw) {
     p0.wg0 = n_wg(p1);
     // split-major XCD order when the token chunks line up: every dW split a full chunk, splits a multiple of the 8
