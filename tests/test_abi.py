@@ -68,3 +68,22 @@ def test_product_path_fails_loudly_without_gpu():
 
     with pytest.raises(HipExtensionMissing):
         BatchView(CONFIGS["C1"].batch(0, batch_size=2))
+
+
+def test_product_libraries_carry_no_tuning_hooks():
+    """Kernel selection and numerics depend on the call's arguments alone: the in-tree product libraries contain none
+    of the tools build's environment switches (make TUNING=1 builds them into eventstreamgpt_amd/tuning/)."""
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "eventstreamgpt_amd")
+    names = [b"ESGPT_GEMM_", b"ESGPT_ATTN_BWD_NSPLIT", b"ESGPT_LN_FWD_ROWS", b"ESGPT_LN_BWD_ROWS",
+             b"ESGPT_LOSS_ROW_STAGE", b"ESGPT_ATTN_GENERIC"]
+    checked = 0
+    for lib in ("libesgpt_amd.so", "libesgpt_torch.so"):
+        path = os.path.join(here, lib)
+        if not os.path.exists(path):
+            continue
+        data = open(path, "rb").read()
+        for n in names:
+            assert n not in data, (lib, n)
+        checked += 1
+    if not checked:
+        pytest.skip("libraries not built")
