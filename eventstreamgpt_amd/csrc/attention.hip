@@ -773,7 +773,13 @@ int64_t esgpt_attn_keep_words(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int6
   if (!(dropout_p > 0.f) || dtype != ESGPT_BF16 || force_generic() ||
       !esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return 0;
-  return B * H * Lq * cdiv(Lk, 32);
+  // The keep bits are O(Lq·Lk) activation memory per layer (Lq·⌈Lk/32⌉·4 B per (batch, head): 8 KiB at L = 256,
+  // 2 MiB at L = 4096). Above kKeepMaxLk keys, or kKeepMaxBytes per launch, the backward re-hashes the mask instead
+  // (the same bits; attention memory stays O(L)).
+  constexpr int64_t kKeepMaxLk = 2048, kKeepMaxBytes = 256ll << 20;
+  const int64_t words = B * H * Lq * cdiv(Lk, 32);
+  if (Lk > kKeepMaxLk || 4 * words > kKeepMaxBytes) return 0;
+  return words;
 }
 
 int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,

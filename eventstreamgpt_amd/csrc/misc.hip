@@ -27,8 +27,10 @@ __global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __r
                                                     float bc2_sqrt_all, const float* __restrict__ per_tensor,
                                                     const int32_t* __restrict__ err) {
   // A data-dependent error raised by this step's forward (bad embedding index, NaN TTE log-likelihood, subject
-  // without an observed TTE) leaves the parameters untouched: the reference raises before its optimizer step.
-  if (err != nullptr && err[0] != 0) return;
+  // without an observed TTE) leaves the parameters untouched: the reference raises before its optimizer step. The
+  // gate also holds while an EARLIER step's flags are pending in the sticky word (err[1], set by the next step's
+  // first launch until the host has read and cleared the block): a step queued behind a failed one is discarded.
+  if (err != nullptr && (err[0] | err[1]) != 0) return;
   const int64_t e = blocks[blockIdx.x];
   const int64_t ti = e >> 40;
   const esgpt_adam_tensor t = table[ti];
@@ -133,13 +135,19 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
 
 // bank[i] = counter + i (i < slots), then counter += slots: one block (every thread reads the counter before the
 // barrier; thread 0 advances it after).
-// With `err` (the step's error block, 16 bytes) it is zeroed by the same launch: each training step's flags (and its
-// AdamW no-op) are its own.
+// With `err` (the step's error block, 16 bytes: int32 flags, int32 sticky word, int64 max bad index) the same launch
+// starts the step's own flags: the previous step's flags are OR-ed into the sticky word (which keeps every later
+// AdamW a no-op until the host has read and cleared the block), then the flags and the max index are zeroed.
 __global__ __launch_bounds__(256) void seed_bank_kernel(int64_t* __restrict__ counter, int64_t* __restrict__ bank,
-                                                        int64_t slots, int64_t* __restrict__ err) {
+                                                        int64_t slots, int32_t* __restrict__ err) {
   const int64_t c = *counter;
   for (int64_t i = threadIdx.x; i < slots; i += blockDim.x) bank[i] = c + i;
-  if (err && threadIdx.x < 2) err[threadIdx.x] = 0;
+  if (err && threadIdx.x == 0) {
+    const int32_t f = err[0];
+    err[1] |= f;
+    err[0] = 0;
+    *reinterpret_cast<int64_t*>(err + 2) = 0;
+  }
   __syncthreads();
   if (threadIdx.x == 0) *counter = c + slots;
 }
@@ -154,8 +162,7 @@ int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream
 
 int esgpt_step_begin(int64_t* counter, int64_t* bank, int64_t slots, int32_t* err, void* stream) {
   ESGPT_REQUIRE(counter && bank && slots > 0 && (uintptr_t)err % 8 == 0);
-  esgpt::seed_bank_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counter, bank, slots,
-                                                                   reinterpret_cast<int64_t*>(err));
+  esgpt::seed_bank_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counter, bank, slots, err);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

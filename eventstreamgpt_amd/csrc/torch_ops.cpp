@@ -204,7 +204,11 @@ Tensor residual(const Tensor& x_, const Tensor& y_, const optional<Tensor>& row_
   Tensor x = x_.contiguous(), y = y_.contiguous();
   TORCH_CHECK(x.scalar_type() == at::kFloat, "esgpt.residual: x must be f32");
   const int64_t D = y.size(-1), N = y.numel() / D;
+  TORCH_CHECK(x.size(-1) == D && mask_div >= 1 && skip_T >= 0, "esgpt.residual: x / y widths or mask_div / skip_T");
+  TORCH_CHECK(skip_T <= 1 ? x.numel() / D == N : (N % (skip_T - 1) == 0 && x.numel() / D == N / (skip_T - 1) * skip_T),
+              "esgpt.residual: x rows must be N (or N / (T-1) * T with skip_T = T)");
   Tensor rm = as_opt(row_mask, at::kBool);
+  TORCH_CHECK(!rm.defined() || rm.numel() * mask_div == N, "esgpt.residual: row_mask must hold N / mask_div rows");
   Tensor h = at::empty({N, D}, x.options());
   check(esgpt_residual_fwd(ptr<const float>(x), y.data_ptr(), dtype_code(y.scalar_type()),
                            rm.defined() ? ptr<const uint8_t>(rm) : nullptr, mask_div, skip_T, (float)dropout_p,
@@ -219,7 +223,11 @@ std::tuple<Tensor, Tensor> residual_bwd(const Tensor& dh_, const optional<Tensor
   const c10::DeviceGuard guard(dh_.device());
   Tensor dh = dh_.to(at::kFloat).contiguous();
   const int64_t D = dh.size(-1), N = dh.numel() / D;
+  TORCH_CHECK(mask_div >= 1 && skip_T >= 0, "esgpt.residual_bwd: mask_div / skip_T");
+  TORCH_CHECK(!need_dx || (skip_T <= 1 ? x_rows == N : (N % (skip_T - 1) == 0 && x_rows == N / (skip_T - 1) * skip_T)),
+              "esgpt.residual_bwd: x_rows must be N (or N / (T-1) * T with skip_T = T)");
   Tensor rm = as_opt(row_mask, at::kBool);
+  TORCH_CHECK(!rm.defined() || rm.numel() * mask_div == N, "esgpt.residual_bwd: row_mask must hold N / mask_div rows");
   Tensor dy = at::empty({N, D}, dh.options().dtype(y_dtype));
   Tensor dx = need_dx ? at::empty({x_rows, D}, dh.options()) : Tensor();
   check(esgpt_residual_bwd(ptr<const float>(dh), rm.defined() ? ptr<const uint8_t>(rm) : nullptr, mask_div, skip_T,
@@ -233,8 +241,10 @@ Tensor na_split(const Tensor& x_, const Tensor& event_mask) {
   const c10::DeviceGuard guard(x_.device());
   require_hip(x_, "x");
   Tensor x = x_.to(at::kFloat).contiguous();
+  TORCH_CHECK(x.dim() == 4, "esgpt.na_split: x must be [B, L, G, D]");
   const int64_t B = x.size(0), L = x.size(1), G = x.size(2), D = x.size(3);
   Tensor m = as_opt(event_mask, at::kBool);
+  TORCH_CHECK(m.defined() && m.numel() == B * L, "esgpt.na_split: event_mask must hold B * L events");
   Tensor per = at::empty({B, L, D}, x.options());
   check(esgpt_na_split_fwd(ptr<const float>(x), ptr<const uint8_t>(m), B * L, G, D, ptr<float>(per), stream_of(x)),
         "na_split");
@@ -246,6 +256,8 @@ void na_split_bwd_(const Tensor& dper_, const Tensor& event_mask, Tensor dx) {
   Tensor dper = dper_.to(at::kFloat).contiguous();
   TORCH_CHECK(dx.is_contiguous() && dx.scalar_type() == at::kFloat && dx.dim() == 4, "esgpt.na_split_bwd_: dx");
   Tensor m = as_opt(event_mask, at::kBool);
+  TORCH_CHECK(m.defined() && m.numel() == dx.size(0) * dx.size(1) && dper.numel() == m.numel() * dx.size(3),
+              "esgpt.na_split_bwd_: event_mask must hold B * L events and dper B * L rows of D");
   check(esgpt_na_split_bwd(ptr<const float>(dper), ptr<const uint8_t>(m), dx.size(0) * dx.size(1), dx.size(2),
                            dx.size(3), ptr<float>(dx), stream_of(dper)),
         "na_split_bwd");
@@ -255,7 +267,9 @@ Tensor na_assemble(const Tensor& ctx_, const Tensor& x_) {
   const c10::DeviceGuard guard(x_.device());
   require_hip(x_, "x");
   Tensor ctx = ctx_.to(at::kFloat).contiguous(), x = x_.to(at::kFloat).contiguous();
+  TORCH_CHECK(x.dim() == 4, "esgpt.na_assemble: x must be [B, L, G, D]");
   const int64_t B = x.size(0), L = x.size(1), G = x.size(2), D = x.size(3);
+  TORCH_CHECK(ctx.numel() == B * L * D, "esgpt.na_assemble: ctx must hold B * L rows of D");
   Tensor seq = at::empty({B * L, G + 1, D}, x.options());
   check(esgpt_na_assemble_fwd(ptr<const float>(ctx), ptr<const float>(x), B, L, G, D, ptr<float>(seq), stream_of(x)),
         "na_assemble");
@@ -266,6 +280,7 @@ std::tuple<Tensor, Tensor> na_assemble_bwd(const Tensor& dseq_, int64_t B, int64
   const c10::DeviceGuard guard(dseq_.device());
   Tensor dseq = dseq_.to(at::kFloat).contiguous();
   const int64_t G = dseq.size(-2) - 1, D = dseq.size(-1);
+  TORCH_CHECK(G >= 1 && dseq.numel() == B * L * (G + 1) * D, "esgpt.na_assemble_bwd: dseq must be [B * L, G + 1, D]");
   Tensor dctx = at::empty({B, L, D}, dseq.options());
   Tensor dx = at::empty({B, L, G, D}, dseq.options());  // level G-1: esgpt.na_split_bwd_
   check(esgpt_na_assemble_bwd(ptr<const float>(dseq), B, L, G, D, ptr<float>(dctx), ptr<float>(dx), stream_of(dseq)),

@@ -7,12 +7,14 @@
   hands each parameter its gradient without an accumulate-add; parameters without a gradient are skipped by
   AdamW exactly as in the reference;
 * data-dependent errors (bad embedding index, NaN TTE log-likelihood, subject without an observed TTE) are raised
-  with the reference's exception type and message. The kernels flag them in a device error block that the step's
-  first launch zeroes (each step's flags are its own); the AdamW kernel skips its update while a flag is set (the
-  reference raises before its optimizer step, so the parameters stay at their pre-error values), and ``step``
-  raises the error of step k at the latest when step k + 2 is submitted (the host never waits for the step it just
-  queued), ``check()`` at once. The failing step's AdamW and LR-schedule counters are rolled back when it is
-  raised; a step submitted after it (k + 1) has already run with counters one ahead;
+  with the reference's exception type and message. The kernels flag them in a device error block whose flag word
+  each step's first launch starts afresh (each step's flags are its own), moving the previous step's flags into a
+  sticky word; the AdamW kernel skips its update while either is set. So the failing step k AND every step
+  already queued behind it leave the parameters untouched (the reference raises before its optimizer step and
+  never runs k + 1: the parameters stay at their pre-error values). ``step`` raises the error of step k at the
+  latest when step k + 2 is submitted (the host never waits for the step it just queued), ``check()`` at once; the
+  AdamW and LR-schedule counters of step k and of the discarded later steps are rolled back, and the block
+  (sticky word included) is cleared, before the raise;
 * data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Every ``param.grad`` ends
   the step as a view into one flat f32 buffer laid out last-layer-first and cut into buckets; every step issues
   exactly one all-reduce (average) per bucket, in bucket-index order on every rank, whichever path (eager, graph
@@ -289,10 +291,13 @@ class _GemmSpy(torch.utils._python_dispatch.TorchDispatchMode):
         super().__init__()
         self.hits = set()
 
+    BINARY = ("other", "out")  # aten.max.other / min.other (and their out= forms) are elementwise, not reductions
+
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = func.__name__.split(".")[0]
         if func.namespace == "aten" and (name in self.GEMMS or name in self.REDUCTIONS):  # torch.ops.esgpt.* are ours
-            self.hits.add(name)
+            if not (name in ("max", "min") and func._overloadname in self.BINARY):
+                self.hits.add(name)
         return func(*args, **(kwargs or {}))
 
 
@@ -458,13 +463,17 @@ class TrainStep:
             ev.synchronize()
             code, mx = int(host[0]), int(host[1])
             if code & 0xFFFFFFFF:
+                # the failing step's AdamW was a no-op on the device, and so is every step queued behind it (the
+                # sticky word): take back their step counts and LR steps. The block is cleared after them in
+                # stream order.
+                discarded = [active] + [e[3] for e in self._pending]
                 self._pending.clear()
                 err_word(self.device).zero_()
-                # the failing step's AdamW was a no-op on the device: take back its step counts and LR step
-                if isinstance(self.opt, FusedAdamW):
-                    for i in active:
-                        self.opt.steps[i] -= 1
-                self.sched_step -= 1
+                for act in discarded:
+                    if isinstance(self.opt, FusedAdamW):
+                        for i in act:
+                            self.opt.steps[i] -= 1
+                    self.sched_step -= 1
                 raise_for_error(code, mx, self._vocab, batch)
 
     def prefetch(self, batch: PytorchBatch) -> None:
@@ -515,7 +524,8 @@ class TrainStep:
         entry = None
         if self.use_graph:
             sig = batch.shape_signature()
-            if sig not in self.graphs and len(self.graphs) < self.max_graphs:
+            # only real graphs count against max_graphs (a signature recorded as eager holds no graph memory)
+            if sig not in self.graphs and sum(g is not None for g in self.graphs.values()) < self.max_graphs:
                 self._capture(batch)
             entry = self.graphs.get(sig)
         gb = self.grad_buckets

@@ -112,10 +112,12 @@ class _NAAssemble(torch.autograd.Function):
 
 def _glue_fast_path(module, hidden_states, event_mask, seq_kwargs, dep_kwargs, prepend, update_last) -> bool:
     """The training path (history prepended, no caches) with both modules full InnerBlocks on a HIP f32 tensor:
-    the split / assemble / mask steps run as the esgpt glue kernels."""
+    the split / assemble / mask steps run as the esgpt glue kernels (not when ``fused.ENABLED`` is off: that is the
+    plain-PyTorch module path the fused-block tests compare against)."""
+    from .. import fused
     from .transformer import InnerBlock
 
-    return (prepend and update_last and event_mask is not None and not seq_kwargs and not dep_kwargs
+    return (fused.ENABLED and prepend and update_last and event_mask is not None and not seq_kwargs and not dep_kwargs
             and isinstance(module.seq_module, InnerBlock) and isinstance(module.dep_graph_module, InnerBlock)
             and hidden_states.is_cuda and hidden_states.dtype == torch.float32 and hidden_states.shape[-1] % 4 == 0)
 

@@ -219,10 +219,11 @@ class InnerBlock(nn.Module):
 def _final_layer_norm(ln: nn.LayerNorm, hidden: torch.Tensor) -> torch.Tensor:
     """``ln_f`` (f32 output). Under bf16 autocast on a HIP tensor: the library's LayerNorm (``esgpt::residual_ln`` with
     no residual; f32 statistics, one pass each way) instead of ATen's three LayerNorm kernels."""
+    from .. import fused
     from ..fused import compute_dtype, residual_ln
 
     D = hidden.shape[-1]
-    if not (hidden.is_cuda and compute_dtype() == torch.bfloat16 and D % 4 == 0 and D <= 1024
+    if not (fused.ENABLED and hidden.is_cuda and compute_dtype() == torch.bfloat16 and D % 4 == 0 and D <= 1024
             and ln.weight is not None and ln.bias is not None):
         return ln(hidden)
     with torch.autocast("cuda", enabled=False):

@@ -13,8 +13,10 @@
  *   - Return value: ESGPT_OK or an ESGPT_ERR_* code for invalid arguments / launch failures. Data-dependent
  *     errors (out-of-range embedding index, NaN TTE log-likelihood, subject without observed TTE) are OR-ed
  *     into the caller-provided device error block `err` (16 bytes, 8-B aligned, zeroed by the caller: int32
- *     ESGPT_FLAG_* bits at byte 0, and at bytes 8..15 the int64 maximum of every out-of-range embedding index).
- *     esgpt_adamw skips its update while the flags are non-zero (the reference raises before its optimizer step);
+ *     ESGPT_FLAG_* bits at byte 0, an int32 sticky word at byte 4 (esgpt_step_begin), and at bytes 8..15 the
+ *     int64 maximum of every out-of-range embedding index).
+ *     esgpt_adamw skips its update while the flags or the sticky word are non-zero (the reference raises before
+ *     its optimizer step);
  *     the Python wrapper reads the block once per step and raises the reference's exception type and message.
  *   - dtype codes: ESGPT_F32 (float) or ESGPT_BF16 (bfloat16) for activation tensors; masters are f32.
  */
@@ -134,7 +136,9 @@ int esgpt_attn_fwd(const void* q, const void* k, const void* v, int64_t ld_in, i
  * re-hashing them: keep (uint32, esgpt_attn_keep_words(...) words, caller-owned) holds bit (key % 32) of word
  * (bh*Lq + i)*ceil(Lk/32) + key/32 = keep(b, h, i, key) for every (query, key) pair the forward computed (pairs it
  * skips — masked, outside the causal / local band — are left unwritten and never read as kept). keep may be NULL,
- * and is ignored when esgpt_attn_keep_words returns 0 (no dropout, or not the MFMA path). */
+ * and is ignored when esgpt_attn_keep_words returns 0 (no dropout, not the MFMA path, or the bits would exceed the
+ * cap: Lk > 2048 or more than 256 MiB per launch — the keep bits cost Lq·ceil(Lk/32)·4 bytes per (batch, head), so
+ * above the cap the backward re-hashes the same mask and attention memory stays O(L)). */
 int64_t esgpt_attn_keep_words(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int64_t tq, int64_t ld_in,
                               int64_t ld_o, int dtype, float dropout_p);
 int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
@@ -377,8 +381,11 @@ int esgpt_stream_wait(void* waiter, void* signaller);
  * stream replaced by a device counter): bank[i] = *counter + i for i < slots, then *counter += slots — one launch,
  * capturable into a HIP graph (every replay draws fresh seeds). */
 int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream);
-/* The first launch of a training step: esgpt_seed_bank plus, when err != NULL, the step's error block zeroed (so the
- * flags a step's kernels raise, and the AdamW no-op they cause, belong to that step alone). */
+/* The first launch of a training step: esgpt_seed_bank plus, when err != NULL, the step's own flags started: the
+ * previous step's flags (int32 word 0) are OR-ed into the sticky word (int32 word 1), then word 0 and the max bad
+ * index (int64 at byte 8) are zeroed. The flags a step's kernels raise belong to that step alone; the sticky word
+ * keeps every later AdamW a no-op until the host has read the block and cleared it (a step queued behind a failed
+ * one is discarded, as the reference never runs it). */
 int esgpt_step_begin(int64_t* counter, int64_t* bank, int64_t slots, int32_t* err, void* stream);
 
 /* ---- Parameter packing -------------------------------------------------------------------------------------
@@ -403,7 +410,7 @@ int esgpt_pack(const esgpt_pack_seg* segs, int64_t n_segs, void* stream);
  * entry per esgpt_adamw_chunk() elements of each tensor. step = the 1-based optimizer step (bias corrections) shared
  * by every tensor, or per_tensor (device f32 [n_tensors][2] = (lr / (1 - beta1^step_t), sqrt(1 - beta2^step_t)) with
  * tensor t's own step count, as torch keeps one `step` per parameter; NULL = use `step`). err: the error block of
- * the step's forward (NULL = none); a non-zero flag word makes the launch a no-op. */
+ * the step's forward (NULL = none); a non-zero flag word or sticky word makes the launch a no-op. */
 typedef struct esgpt_adam_tensor {
   float* p;
   const float* g;

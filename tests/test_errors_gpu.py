@@ -126,6 +126,44 @@ def test_trainstep_raises_without_explicit_check():
             ts.step(g)
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainstep_error_discards_queued_steps(graph):
+    """A good step queued behind a bad one (submitted before the bad step's flags were read) is discarded too: after
+    the raise the parameters are the pre-error values, the AdamW / LR counters are those of the last good step, and
+    training resumes exactly like a run that never saw the bad batch and its follower."""
+    bc = CONFIGS["C1"]
+    good = [bc.batch(i, batch_size=8, device=DEV).packed() for i in (0, 2, 3)]
+
+    def fresh():
+        m, cfg = _ci_model()
+        return m, cfg, TrainStep(m, _opt(), torch.bfloat16, use_graph=graph)
+
+    m, cfg, ts = fresh()
+    bad = bc.batch(1, batch_size=8)
+    bad.dynamic_indices[1, 1, 0] = cfg.vocab_size + 3
+    ts.step(good[0])
+    ts.check()
+    before = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    steps_before, sched_before = list(ts.opt.steps), ts.sched_step
+    with pytest.raises(AssertionError, match="Invalid embedding!"):
+        ts.step(bad.to(DEV).packed())
+        ts.step(good[1])  # queued behind the bad step: discarded with it
+        ts.check()
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+    assert ts.opt.steps == steps_before and ts.sched_step == sched_before
+    ts.step(good[2])
+    ts.check()
+    after = {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+    m2, _, ts2 = fresh()  # the same run without the bad batch and its follower
+    ts2.step(good[0])
+    ts2.step(good[2])
+    ts2.check()
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, after[k]), k
+
+
 def test_graph_per_shape_signature_matches_eager():
     """Batches of different shapes (B, L, M, S including a size-1 S) under use_graph: one graph per signature, no
     broadcasting into a captured buffer; losses and parameters equal the eager run's."""
