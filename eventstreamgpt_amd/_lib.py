@@ -132,6 +132,12 @@ SIGNATURES = {
                                    _vp, _vp, _sz, _vp, _vp, _i64, _vp]),
     "esgpt_linear_bwd_split": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64,
                                       _vp, _vp, _vp, _sz, _vp, _vp, _i64, _vp, _vp]),
+    "esgpt_gemm_f32": (_int, [_int, _vp, _i64, _int, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _i64, _int, _vp,
+                              _sz, _vp, _vp]),
+    "esgpt_linear_fwd_f32": (_int, [_vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _vp, _i64, _vp]),
+    "esgpt_linear_bwd_f32_workspace": (_sz, [_i64, _i64, _i64, _int]),
+    "esgpt_linear_bwd_f32": (_int, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _int, _vp, _i64, _vp, _i64,
+                                    _vp, _vp, _vp, _sz, _vp, _vp, _i64, _vp]),
     "esgpt_stream_wait": (_int, [_vp, _vp]),
     "esgpt_seed_bank": (_int, [_vp, _vp, _i64, _vp]),
     "esgpt_step_begin": (_int, [_vp, _vp, _i64, _vp, _vp]),

@@ -158,6 +158,180 @@ struct Tile {
   }
 };
 
+typedef __attribute__((address_space(3))) void lds_void;
+
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt left at their maxima), N < 64
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// LDS-DMA operand staging of whole tiles (buffer_load … lds): one 1-KiB wave-instruction writes its 64 lanes' 16-B
+// pieces lane-linearly into LDS, so the images carry no padding; their 16-B chunks are XOR-swizzled per image row to
+// keep the fragment reads bank-conflict free, the swizzle applied to each lane's SOURCE address (the destination
+// stays linear: cdna_hip_programming.md rule 21). No VGPR round trip, no ds_write pass, no per-chunk address math in
+// the k-loop (one uniform soffset per k-tile).
+//   K-contig image  [R rows][64 k] (128-B rows):     chunk ^ ((row >> 1) & 7)   — ds_read_b128 fragments: each
+//                                                    16-lane group reads 16 distinct rows ≡ (row & 15) → 16 bank quads
+//   M/N-contig image [64 k-rows][R columns]:  R = 64:  chunk ^ ((((row >> 1) & 1) << 2) | ((row >> 2) & 3))
+//                                             R = 128: chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))
+//                                            — ds_read_b64_tr_b16 fragments: a 32-lane half reads 4 consecutive
+//                                              k-rows x 32 columns, spread over all 64 banks
+template <bool KC, int R>
+struct GTile {
+  static constexpr int kElems = R * BK;                 // bf16 elements of one k-tile image
+  static constexpr int CPR = KC ? BK / 8 : R / 8;       // 16-B chunks per image row
+  static constexpr int RPI = 64 / CPR;                  // image rows per 1-KiB instruction
+  static constexpr int kInstr = kElems * 2 / 1024 / 4;  // instructions per wave and k-tile (4 waves)
+  static_assert(kInstr >= 1 && kInstr * 4 * 512 == kElems, "tile rows");
+
+  __device__ __forceinline__ static int sw(int row) {
+    if (KC) return (row >> 1) & 7;
+    if (R == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+    return ((row & 3) << 2) | ((row >> 2) & 3);
+  }
+  __device__ __forceinline__ static int off(int row, int col) {  // element offset, col % 4 == 0
+    return row * (KC ? BK : R) + (((col >> 3) ^ sw(row)) << 3) + (col & 7);
+  }
+  // Out-of-range pieces (rows / columns past the operand's m or n extent, k past the split's end) read zeros: their
+  // voffset is set beyond the buffer's num_records (buffer loads return 0 out of range), so edge tiles take the same
+  // loop — no register-staged fallback, no clamps. Every piece is a whole 16-B chunk (K, and M / N of an M/N-contig
+  // operand, are multiples of 8).
+  static constexpr int kOOB = (int)0x80000000u;
+  __device__ __forceinline__ static void coords(int i, int& row, int& lg) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    row = (wave + 4 * i) * RPI + lane / CPR;
+    lg = (lane % CPR) ^ sw(row);
+  }
+  // per-lane source byte offsets of this wave's instructions (row0 = the tile's first m / n, nrows its extent)
+  __device__ __forceinline__ static void lane_src(int (&vo)[kInstr], int64_t ld, int row0, int nrows) {
+#pragma unroll
+    for (int i = 0; i < kInstr; ++i) {
+      int row, lg;
+      coords(i, row, lg);
+      if (KC) vo[i] = row0 + row < nrows ? (int)(((int64_t)(row0 + row) * ld + lg * 8) * 2) : kOOB;
+      else vo[i] = row0 + lg * 8 < nrows ? (int)(((int64_t)row * ld + row0 + lg * 8) * 2) : kOOB;
+    }
+  }
+  __device__ __forceinline__ static int k_soff(int k0, int64_t ld) { return KC ? k0 * 2 : (int)(k0 * ld * 2); }
+  // one k-tile into `img`; kvalid < BK: the split's last, partial k-tile (its pieces past kvalid read zeros)
+  __device__ __forceinline__ static void issue(__amdgpu_buffer_rsrc_t rs, const int (&vo)[kInstr], int so,
+                                               __bf16* img, int kvalid) {
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < kInstr; ++i) {
+      int v = vo[i];
+      if (kvalid < BK) {
+        int row, lg;
+        coords(i, row, lg);
+        if ((KC ? lg * 8 : row) >= kvalid) v = kOOB;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave + 4 * i) * 512), 16, v, so, 0, 0);
+    }
+  }
+  // the same fragment as Tile<KC, R>::frag, from the swizzled image. The transposed reads are inline asm: hipcc
+  // (ROCm 7.2) cannot tell the ds_read_tr16_b64 builtin apart from the LDS-DMA writes in flight and drains every
+  // one of them (vmcnt(0)) before it, which serialises the k-loop; the asm form is ordered by the loop's own counted
+  // vmcnt + barrier, and its results are waited for explicitly (frag_wait) before the MFMAs read them.
+  __device__ __forceinline__ static bf16x8 frag(const __bf16* s, int sub0, int t) {
+    const int l = threadIdx.x & 63;
+    if (KC) {
+      const int r = l & 31, h = l >> 5;
+      return *reinterpret_cast<const bf16x8*>(s + off(sub0 + r, 16 * t + 8 * h));
+    } else {
+      const int g = l >> 4, w = l & 15, q = w >> 2, p = w & 3;
+      const int col = sub0 + (g & 1) * 16 + 4 * p;
+      const int kr = 16 * t + 8 * (g >> 1) + q;
+      bf16x4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"((uint32_t)(uintptr_t)(lds_bf16x4*)(s + off(kr, col)))
+                   : "memory");
+      asm volatile("ds_read_b64_tr_b16 %0, %1"
+                   : "=v"(hi) : "v"((uint32_t)(uintptr_t)(lds_bf16x4*)(s + off(kr + 4, col))) : "memory");
+      bf16x8 f;
+      f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+      f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+      return f;
+    }
+  }
+};
+
+// Waits for the inline-asm fragment reads (the compiler does not count them) before their registers are used; the
+// sched_barrier keeps hipcc from hoisting an MFMA above the wait (cdna_hip_programming.md rule 18).
+__device__ __forceinline__ void frag_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// ---- f32 operands (the reference-precision step: scripts/pretrain.py trains in f32) ----
+// v_mfma_f32_32x32x2_f32: lane l supplies A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]; the product is exact f32
+// (bitwise a k-ordered fmaf chain, one rounding per product: cdna_hip_programming.md §3), at the f32 vector rate.
+// k-stage BKF = 32; each image row holds its k in the order (0, 2, …, 30, 1, 3, …, 31), so a lane half h (k ≡ h mod 2)
+// reads its next four k-steps as one 16-B read. Register-staged (the images are permuted / transposed on the LDS
+// write); loads branch-free with clamped addresses, out-of-range chunks zeroed on the LDS write.
+constexpr int BKF = 32;
+constexpr int FLD = BKF + 4;  // image row pitch (floats): the 16-lane groups of a 16-B fragment read hit 16 bank quads
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool KC, int R>
+struct FTile {
+  static constexpr int kFloats = R * FLD;
+  static constexpr int kChunks = R * BKF / 4 / THREADS;  // 16-B chunks per thread and k-stage
+  static_assert(kChunks >= 1 && kChunks * 4 * THREADS == R * BKF, "f32 tile rows");
+  __device__ __forceinline__ static int pos(int k) { return (k & 1) * (BKF / 2) + (k >> 1); }
+  __device__ __forceinline__ static void coords(int i, int& a, int& b) {
+    const int c = threadIdx.x + THREADS * i;
+    if (KC) {
+      a = c / (BKF / 4);       // row
+      b = (c % (BKF / 4)) * 4;  // k
+    } else {
+      a = c % BKF;             // k-row (consecutive lanes walk k: the transposing LDS writes are conflict-free)
+      b = (c / BKF) * 4;       // column
+    }
+  }
+  __device__ __forceinline__ static void load(float4 (&reg)[kChunks], const float* __restrict__ g, int64_t ld,
+                                              int row0, int rows, int k0, int kend) {
+#pragma unroll
+    for (int i = 0; i < kChunks; ++i) {
+      int a, b;
+      coords(i, a, b);
+      if (KC) {
+        const int row = min(row0 + a, rows - 1), k = min(k0 + b, kend - 4);
+        reg[i] = *reinterpret_cast<const float4*>(g + (int64_t)row * ld + k);
+      } else {
+        const int k = min(k0 + a, kend - 1), col = min(row0 + b, rows - 4);
+        reg[i] = *reinterpret_cast<const float4*>(g + (int64_t)k * ld + col);
+      }
+    }
+  }
+  __device__ __forceinline__ static void store(float* s, const float4 (&reg)[kChunks], int row0, int rows, int k0,
+                                               int kend) {
+#pragma unroll
+    for (int i = 0; i < kChunks; ++i) {
+      int a, b;
+      coords(i, a, b);
+      float4 v = reg[i];
+      if (KC) {
+        if (!(row0 + a < rows && k0 + b < kend)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float2*>(s + a * FLD + (b >> 1)) = make_float2(v.x, v.z);
+        *reinterpret_cast<float2*>(s + a * FLD + BKF / 2 + (b >> 1)) = make_float2(v.y, v.w);
+      } else {
+        if (!(k0 + a < kend && row0 + b < rows)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+        const int q = pos(a);
+        s[(b + 0) * FLD + q] = v.x;
+        s[(b + 1) * FLD + q] = v.y;
+        s[(b + 2) * FLD + q] = v.z;
+        s[(b + 3) * FLD + q] = v.w;
+      }
+    }
+  }
+  // k-steps 4q .. 4q+3 of rows sub0 .. sub0+31: element j = A[sub0 + (l&31)][2(4q + j) + (l>>5)]
+  __device__ __forceinline__ static f32x4 frag(const float* s, int sub0, int q) {
+    const int l = threadIdx.x & 63;
+    return *reinterpret_cast<const f32x4*>(s + (sub0 + (l & 31)) * FLD + (l >> 5) * (BKF / 2) + 4 * q);
+  }
+};
+
 // XCD-aware order: the hardware deals consecutive workgroup ids round-robin over the 8 XCDs (each with its own
 // L2), so id -> (xcd = id % 8, slot = id / 8) is remapped (bijectively) to a linear index that gives every XCD a
 // contiguous run. The split index runs fastest (the slabs of a tile are written and reduced on one XCD), then
@@ -236,16 +410,21 @@ __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w 
 // B image), sized for the operand layouts (the K-contig images are smaller: the 64x64 forward kernel fits 4
 // workgroups per CU instead of 3). Also holds the epilogue's C tile (f32: BM x (BN + 4) floats) and the split-K
 // reducer flag.
-template <bool AKC, bool BKC, int FM, int FN, int NB = 2>
+template <bool AKC, bool BKC, int FM, int FN, int NB = 2, int NBG = 0, bool F32 = false>
 constexpr int lds_elems() {
-  constexpr int st = NB * (Tile<AKC, 64 * FM>::kElems + Tile<BKC, 64 * FN>::kElems);
+  constexpr int st = (NBG > 0 || F32) ? 0 : NB * (Tile<AKC, 64 * FM>::kElems + Tile<BKC, 64 * FN>::kElems);
+  constexpr int gl = NBG * (GTile<AKC, 64 * FM>::kElems + GTile<BKC, 64 * FN>::kElems);
+  constexpr int f32 = F32 ? 2 * 2 * (FTile<AKC, 64 * FM>::kFloats + FTile<BKC, 64 * FN>::kFloats) : 0;
   constexpr int epi = 64 * FM * (64 * FN + 4) * 2;  // f32 C tile in bf16 elements
-  return st > epi ? st : epi;
+  return std::max(std::max(std::max(st, gl), f32), epi);
 }
 
 // NB = LDS staging buffers: 2 (one barrier per k-tile) or 1 (two barriers per k-tile, half the LDS: the 64x64
 // forward then keeps 8 workgroups per CU resident instead of 4 — every tile of a C2 projection in flight at once).
-template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2>
+// NBG > 0: whole tiles are staged by LDS-DMA (GTile) through NBG buffers instead — NBG - 1 k-tiles in flight while
+// one is consumed, one raw barrier per k-tile; edge tiles keep the register-staged loop.
+// F32: f32 operands through v_mfma_f32_32x32x2_f32 (FTile), f32 outputs.
+template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2, int NBG = 0, bool F32 = false>
 __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) {
   constexpr int NS = NS_, BM = 64 * FM, BN = 64 * FN, F = FM * FN;
   constexpr bool kRowSum = !(AKC && BKC);  // compiled out of the forward (K-contig x K-contig) instantiation
@@ -346,15 +525,126 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     for (int st = 0; st < NS - 1; ++st)
       if (i0 + st < nk) consume(st, i0 + st);
   };
+  // LDS-DMA form of the whole-tile k loop: NBG buffers, k-tile i+NBG-1 issued right after the barrier that retires
+  // k-tile i (every wave is then done reading buffer (i-1) % NBG, which it overwrites), so NBG-1 k-tiles stream in
+  // while one is consumed. The counted vmcnt before each barrier leaves the younger k-tiles in flight (an LDS-DMA is
+  // ordered for a ds_read only by its issuing wave's vmcnt plus a barrier: MI355X_MICROARCH.md item 7); raw
+  // s_barrier, as __syncthreads() would drain every DMA in flight (vmcnt(0)).
+  auto mainloop_glds = [&](auto rs_c) {
+    constexpr bool RS = decltype(rs_c)::value;
+    using GA = GTile<AKC, BM>;
+    using GB = GTile<BKC, BN>;
+    constexpr int P = GA::kInstr + GB::kInstr, STAGE = GA::kElems + GB::kElems;
+    constexpr int NBq = NBG > 1 ? NBG : 2;
+    int voA[GA::kInstr], voB[GB::kInstr];
+    GA::lane_src(voA, p.lda, m0, M);
+    GB::lane_src(voB, p.ldb, n0, N);
+    const __amdgpu_buffer_rsrc_t rsA =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
+    auto issue = [&](int i, int buf) {
+      const int k0 = kb + i * BK, kv = ke - k0;
+      __bf16* sA = smem + buf * STAGE;
+      GA::issue(rsA, voA, GA::k_soff(k0, p.lda), sA, kv);
+      GB::issue(rsB, voB, GB::k_soff(k0, p.ldb), sA + GA::kElems, kv);
+    };
+#pragma unroll
+    for (int st = 0; st < NBq - 1; ++st)
+      if (st < nk) issue(st, st);
+    for (int i = 0; i < nk; ++i) {
+      const int ahead = min(NBq - 2, nk - 1 - i);  // k-tiles allowed in flight once k-tile i has landed
+      if (NBq >= 4 && ahead >= 2) vm_wait<(NBq >= 4 ? 2 * P : 0)>();
+      else if (NBq >= 3 && ahead >= 1) vm_wait<(NBq >= 3 ? P : 0)>();
+      else vm_wait<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (i + NBq - 1 < nk) issue(i + NBq - 1, (i + NBq - 1) % NBq);
+      const __bf16* sA = smem + (i % NBq) * STAGE;
+      const __bf16* sB = sA + GA::kElems;
+      // fragments of k-step t + 1 are read while the MFMAs of k-step t run
+      bf16x8 af[2][FM], bfr[2][FN];
+      auto read = [&](int t, int b) {
+#pragma unroll
+        for (int ii = 0; ii < FM; ++ii) af[b][ii] = GA::frag(sA, wm * 32 * FM + 32 * ii, t);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[b][j] = GB::frag(sB, wn * 32 * FN + 32 * j, t);
+      };
+      read(0, 0);
+#pragma unroll
+      for (int t = 0; t < BK / 16; ++t) {
+        if constexpr (!(AKC && BKC)) frag_wait();
+        if (t + 1 < BK / 16) read(t + 1, (t + 1) & 1);
+#pragma unroll
+        for (int ii = 0; ii < FM; ++ii) {
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[ii][j] = mfma(bfr[t & 1][j], af[t & 1][ii], acc[ii][j]);
+          if constexpr (RS) racc[ii] = mfma(ones, af[t & 1][ii], racc[ii]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // f32 operands: two LDS buffers (one barrier per k-stage), the next stage's loads in flight during the MFMAs
+  auto mainloop_f32 = [&](auto rs_c) {
+    constexpr bool RS = decltype(rs_c)::value;
+    using FA = FTile<AKC, BM>;
+    using FB = FTile<BKC, BN>;
+    float* sm = reinterpret_cast<float*>(smem);
+    const float* Af = reinterpret_cast<const float*>(A);
+    const float* Bf = reinterpret_cast<const float*>(B);
+    const int nkf = ke > kb ? (ke - kb + BKF - 1) / BKF : 0;
+    float4 ra[FA::kChunks], rb[FB::kChunks];
+    if (nkf > 0) {
+      FA::load(ra, Af, p.lda, m0, M, kb, ke);
+      FB::load(rb, Bf, p.ldb, n0, N, kb, ke);
+    }
+    for (int i = 0; i < nkf; ++i) {
+      float* sA = sm + (i & 1) * (FA::kFloats + FB::kFloats);
+      float* sB = sA + FA::kFloats;
+      FA::store(sA, ra, m0, M, kb + i * BKF, ke);
+      FB::store(sB, rb, n0, N, kb + i * BKF, ke);
+      __syncthreads();
+      if (i + 1 < nkf) {
+        FA::load(ra, Af, p.lda, m0, M, kb + (i + 1) * BKF, ke);
+        FB::load(rb, Bf, p.ldb, n0, N, kb + (i + 1) * BKF, ke);
+      }
+#pragma unroll
+      for (int q = 0; q < BKF / 8; ++q) {
+        f32x4 af[FM], bfr[FN];
+#pragma unroll
+        for (int ii = 0; ii < FM; ++ii) af[ii] = FA::frag(sA, wm * 32 * FM + 32 * ii, q);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = FB::frag(sB, wn * 32 * FN + 32 * j, q);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int ii = 0; ii < FM; ++ii) {
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[ii][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(bfr[j][t], af[ii][t], acc[ii][j], 0, 0, 0);
+            if constexpr (RS) racc[ii] = __builtin_amdgcn_mfma_f32_32x32x2f32(1.f, af[ii][t], racc[ii], 0, 0, 0);
+          }
+      }
+    }
+  };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  const bool fast = p.fast && m0 + BM <= M && n0 + BN <= N && nk > 0 && (ke - kb) % BK == 0;
-  if (fast) {
-    if (want_rs) mainloop(T_{}, T_{});
-    else mainloop(T_{}, F_{});
+  if constexpr (F32) {
+    if (want_rs) mainloop_f32(T_{});
+    else mainloop_f32(F_{});
+  } else if constexpr (NBG > 0) {  // every tile (the host takes this form only for operands below 2 GiB: p.fast)
+    if (want_rs) mainloop_glds(T_{});
+    else mainloop_glds(F_{});
   } else {
-    if (want_rs) mainloop(F_{}, T_{});
-    else mainloop(F_{}, F_{});
+    const bool fast = p.fast && m0 + BM <= M && n0 + BN <= N && nk > 0 && (ke - kb) % BK == 0;
+    if (fast) {
+      if (want_rs) mainloop(T_{}, T_{});
+      else mainloop(T_{}, F_{});
+    } else {
+      if (want_rs) mainloop(F_{}, T_{});
+      else mainloop(F_{}, F_{});
+    }
   }
 
   // this lane's output row of fragment row i, and the first column of fragment column j (within the tile)
@@ -496,33 +786,68 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   // instead of 32-B pieces of 32 rows.
   __syncthreads();
   if (p.out_f32) {
+    // f32 operands (F32): the activation-gradient epilogue reads an f32 pre-activation
+    if (F32 && p.epi == EPI_ACT_GRAD) {
+      const float* aux = reinterpret_cast<const float*>(p.aux);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = m0 + lrow(i);
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int c = n0 + lcol(j) + 8 * g + 4 * h;
+            if (row < M && c < N) {
+              const float4 f = *reinterpret_cast<const float4*>(aux + (int64_t)row * p.ld_aux + c);
+              acc[i][j][4 * g + 0] *= act_grad(f.x, p.act);
+              acc[i][j][4 * g + 1] *= act_grad(f.y, p.act);
+              acc[i][j][4 * g + 2] *= act_grad(f.z, p.act);
+              acc[i][j][4 * g + 3] *= act_grad(f.w, p.act);
+            }
+          }
+      }
+    }
     constexpr int kLd = BN + 4;  // f32 row pitch (floats): 16-B aligned, conflict-free fragment writes
     float* t = reinterpret_cast<float*>(smem);
+    // one f32 tile out: fragment-order LDS writes, barrier, row-major 16-B chunk stores (+= when accumulating)
+    auto store_f32 = [&](float* dst, int64_t ld, bool accum) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<float4*>(t + lrow(i) * kLd + lcol(j) + 8 * g + 4 * h) =
-              make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
-    __syncthreads();
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(t + lrow(i) * kLd + lcol(j) + 8 * g + 4 * h) =
+                make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+      __syncthreads();
 #pragma unroll
-    for (int q = 0; q < BM * BN / 4 / THREADS; ++q) {
-      const int ch = threadIdx.x + THREADS * q, tr = ch / (BN / 4), tc = (ch % (BN / 4)) * 4;
-      const int gr = m0 + tr, gc = n0 + tc;
-      if (gr >= M || gc >= N) continue;
-      float4 w = *reinterpret_cast<const float4*>(t + tr * kLd + tc);
-      float4* o4 = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + (int64_t)gr * p.ldc + gc);
-      if (p.accumulate) {
-        const float4 o = *o4;
-        w.x += o.x;
-        w.y += o.y;
-        w.z += o.z;
-        w.w += o.w;
+      for (int q = 0; q < BM * BN / 4 / THREADS; ++q) {
+        const int ch = threadIdx.x + THREADS * q, tr = ch / (BN / 4), tc = (ch % (BN / 4)) * 4;
+        const int gr = m0 + tr, gc = n0 + tc;
+        if (gr >= M || gc >= N) continue;
+        float4 w = *reinterpret_cast<const float4*>(t + tr * kLd + tc);
+        float4* o4 = reinterpret_cast<float4*>(dst + (int64_t)gr * ld + gc);
+        if (accum) {
+          const float4 o = *o4;
+          w.x += o.x;
+          w.y += o.y;
+          w.z += o.z;
+          w.w += o.w;
+        }
+        *o4 = w;
       }
-      *o4 = w;
+    };
+    if (F32 && p.epi == EPI_BIAS_ACT) {  // the f32 pre-activation, then its activation
+      store_f32(reinterpret_cast<float*>(p.aux_out), p.ld_aux, false);
+      __syncthreads();  // the LDS tile is rewritten below
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = act_fwd(acc[i][j][e], p.act);
     }
+    store_f32(reinterpret_cast<float*>(p.C), p.ldc, p.accumulate != 0);
     return;
   }
   if (p.epi == EPI_ACT_GRAD) {
@@ -595,11 +920,11 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   store_tile(d, reinterpret_cast<__bf16*>(p.C), p.ldc);
 }
 
-template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2>
+template <bool AKC, bool BKC, int NS_, int FM, int FN, int NB = 2, int NBG = 0, bool F32 = false>
 __global__ __launch_bounds__(THREADS) void gemm_kernel(Prob p) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC, FM, FN, NB>()];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[lds_elems<AKC, BKC, FM, FN, NB, NBG, F32>()];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  gemm_tile<AKC, BKC, NS_, FM, FN, NB>(p, lin, smem);
+  gemm_tile<AKC, BKC, NS_, FM, FN, NB, NBG, F32>(p, lin, smem);
 }
 
 // The same tiles walked by a persistent grid (gridDim.x a multiple of 8 and at most the tile count): workgroup b
@@ -624,6 +949,30 @@ int fwd_buffers() {
   return nb;
 }
 
+// LDS-DMA staging buffers of the whole-tile k loops (0 = register staging; ESGPT_GEMM_FWD_GLDS /
+// ESGPT_GEMM_BWD_GLDS tuning hooks, read once). Measured at the C2 shapes (tools/glds_check.sh,
+// tools/glds_bwd_sweep.sh, profiles/r04_glds_*.log): the forward projections gain 3-12 % from two LDS-DMA buffers
+// (qkv 10.3 -> 9.1-9.4 us, head 20.0 -> 17.7-19.0 us; three buffers lose); the grouped backward loses 4-6 % with
+// either depth (627 -> 659 / 671 us per step's set) and at every dX / dW tile size, so it keeps register staging.
+int fwd_glds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = tuning_env("ESGPT_GEMM_FWD_GLDS");
+    v = e ? std::min(3, std::max(0, atoi(e))) : 2;
+    if (v == 1) v = 2;
+  }
+  return v;
+}
+int bwd_glds() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = tuning_env("ESGPT_GEMM_BWD_GLDS");
+    v = e ? std::min(3, std::max(0, atoi(e))) : 0;
+    if (v == 1) v = 2;
+  }
+  return v;
+}
+
 // Forward register-stage depth (2 or 3; ESGPT_GEMM_FWD_NS tuning hook, read once).
 int fwd_stages() {
   static int ns = 0;
@@ -644,19 +993,19 @@ constexpr int bwd_stages() {
   return FM * FN >= 4 ? 2 : NS;
 }
 
-template <int XM, int XN, int WM, int WN>
+template <int XM, int XN, int WM, int WN, int NBG = 0, bool F32 = false>
 __global__ __launch_bounds__(THREADS) void gemm_bwd_pair_kernel(Prob p0, Prob p1) {
-  constexpr int kLds = lds_elems<false, false, WM, WN>() > lds_elems<true, false, XM, XN>()
-                           ? lds_elems<false, false, WM, WN>()
-                           : lds_elems<true, false, XM, XN>();
+  constexpr int kLds =
+      std::max(lds_elems<false, false, WM, WN, 2, NBG, F32>(), lds_elems<true, false, XM, XN, 2, NBG, F32>());
   __shared__ __attribute__((aligned(16))) __bf16 smem[kLds];
   const int id = blockIdx.x, n1 = p0.wg0;
   if (id < n1) {
     if (p1.dbg & 4) return;  // tools build: the dX product alone
-    gemm_tile<false, false, bwd_stages<WM, WN>(), WM, WN>(p1, p1.xmap ? pair_lin(p1, id) : xcd_remap(id, n1), smem);
+    gemm_tile<false, false, bwd_stages<WM, WN>(), WM, WN, 2, NBG, F32>(
+        p1, p1.xmap ? pair_lin(p1, id) : xcd_remap(id, n1), smem);
   } else {
     if (p0.dbg & 8) return;  // tools build: the dW product alone
-    gemm_tile<true, false, bwd_stages<XM, XN>(), XM, XN>(
+    gemm_tile<true, false, bwd_stages<XM, XN>(), XM, XN, 2, NBG, F32>(
         p0, p0.xmap ? pair_lin(p0, id - n1) : xcd_remap(id - n1, gridDim.x - n1), smem);
   }
 }
@@ -857,22 +1206,35 @@ bool shapes_ok(bool akc, bool bkc, const void* A, int64_t lda, const void* B, in
                int64_t K, const void* C, int64_t ldc, bool f32) {
   if (!(A && B && C && M >= 0 && N >= 0 && K > 0)) return false;
   if (!(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31))) return false;
-  if (!(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0)) return false;
+  // K is the chunked (16-B) dimension only of a K-contig operand; an M/N-contig operand takes any K (k = its row)
+  if (!((K % 8 == 0 || !(akc || bkc)) && lda % 8 == 0 && ldb % 8 == 0)) return false;
   if (!((akc || M % 8 == 0) && (bkc || N % 8 == 0))) return false;
   if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16)) return false;
   const int cgrp = f32 ? 4 : 8;
   return N % cgrp == 0 && ldc % cgrp == 0;
 }
 
+// The same checks for f32 operands and an f32 output (16-B chunks of 4 elements).
+bool shapes_ok_f32(bool akc, bool bkc, const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N,
+                   int64_t K, const void* C, int64_t ldc) {
+  if (!(A && B && C && M >= 0 && N >= 0 && K > 0)) return false;
+  if (!(M < (1ll << 31) && N < (1ll << 31) && K < (1ll << 31))) return false;
+  if (!((K % 4 == 0 || !(akc || bkc)) && lda % 4 == 0 && ldb % 4 == 0)) return false;
+  if (!((akc || M % 4 == 0) && (bkc || N % 4 == 0))) return false;
+  if (((uintptr_t)A % 16) || ((uintptr_t)B % 16) || ((uintptr_t)C % 16)) return false;
+  return N % 4 == 0 && ldc % 4 == 0;
+}
+
 // Workgroups of the dX product (what the grouped launch already puts on the chip): the dW split targets the rest.
-int64_t dw_target(bool has_dx, int64_t T, int64_t in, int64_t out) {
+int64_t dw_target(bool has_dx, int64_t T, int64_t in, int64_t out, bool f32 = false) {
   static int64_t tgt = -1;
   if (tgt < 0) {
     const char* e = tuning_env("ESGPT_GEMM_DW_TARGET");  // tuning hook: fixed dW item target (0 = the default rule)
     tgt = e ? std::max(0, atoi(e)) : 0;
   }
   if (tgt > 0) return tgt;
-  return has_dx ? std::max<int64_t>(64, kTarget - n_tiles(T, in, dx_tile(T, in, out))) : kTarget;
+  const TileCfg xt = f32 ? TileCfg{1, 1} : dx_tile(T, in, out);
+  return has_dx ? std::max<int64_t>(64, kTarget - n_tiles(T, in, xt)) : kTarget;
 }
 
 template <int FM, int FN>
@@ -890,6 +1252,16 @@ void launch_fwd(const Prob& p, hipStream_t st) {
       return;
     }
   }
+  if (fwd_glds() == 2 && p.fast) {
+    gemm_kernel<true, true, 3, FM, FN, 1, 2><<<grid, THREADS, 0, st>>>(p);
+    return;
+  }
+#ifdef ESGPT_TUNING_HOOKS
+  if (fwd_glds() == 3 && p.fast) {
+    gemm_kernel<true, true, 3, FM, FN, 1, 3><<<grid, THREADS, 0, st>>>(p);
+    return;
+  }
+#endif
   if (fwd_stages() == 2) gemm_kernel<true, true, 2, FM, FN><<<grid, THREADS, 0, st>>>(p);
 #ifdef ESGPT_TUNING_HOOKS
   else if (fwd_stages() == 4) gemm_kernel<true, true, 4, FM, FN, 1><<<grid, THREADS, 0, st>>>(p);
@@ -899,11 +1271,21 @@ void launch_fwd(const Prob& p, hipStream_t st) {
   else gemm_kernel<true, true, 3, FM, FN><<<grid, THREADS, 0, st>>>(p);
 }
 
+template <int XM, int XN, int NBG>
+void launch_pair_g(const Prob& p0, const Prob& p1, hipStream_t st) {
+  const dim3 grid((unsigned)(n_wg(p0) + n_wg(p1)));
+  if (p1.fm == 2) gemm_bwd_pair_kernel<XM, XN, 2, 2, NBG><<<grid, THREADS, 0, st>>>(p0, p1);
+  else gemm_bwd_pair_kernel<XM, XN, 1, 1, NBG><<<grid, THREADS, 0, st>>>(p0, p1);
+}
 template <int XM, int XN>
 void launch_pair_x(const Prob& p0, const Prob& p1, hipStream_t st) {
-  const dim3 grid((unsigned)(n_wg(p0) + n_wg(p1)));
-  if (p1.fm == 2) gemm_bwd_pair_kernel<XM, XN, 2, 2><<<grid, THREADS, 0, st>>>(p0, p1);
-  else gemm_bwd_pair_kernel<XM, XN, 1, 1><<<grid, THREADS, 0, st>>>(p0, p1);
+  switch (p0.fast && p1.fast ? bwd_glds() : 0) {
+#ifdef ESGPT_TUNING_HOOKS
+    case 2: launch_pair_g<XM, XN, 2>(p0, p1, st); break;
+    case 3: launch_pair_g<XM, XN, 3>(p0, p1, st); break;
+#endif
+    default: launch_pair_g<XM, XN, 0>(p0, p1, st); break;
+  }
 }
 
 void launch_pair(const Prob& p0, const Prob& p1, hipStream_t st) {
@@ -923,10 +1305,11 @@ void launch_dx_only(const Prob& p0, hipStream_t st) {
 // split: dX on st, dW (+ db, its split-K workspace and counters) on st_dw after it waits for the work queued on st
 // so far — the weight gradient leaves the critical path of backward and runs beside the next layers' kernels. Both
 // forms use the same tiles and split plan (the dW target counts the dX tiles either way): bitwise equal results.
+// f32: every operand and dx in f32 (the reference-precision step), 64x64 f32-MFMA tiles.
 int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
                     int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre, void* dx, int64_t lddx,
                     float* dw, float* db, void* workspace, size_t workspace_bytes, int32_t* counters,
-                    const float* db_extra, int64_t n_extra, hipStream_t st, hipStream_t st_dw) {
+                    const float* db_extra, int64_t n_extra, hipStream_t st, hipStream_t st_dw, bool f32 = false) {
   ESGPT_REQUIRE(T >= 0 && in >= 0 && out >= 0);
   ESGPT_REQUIRE(n_extra >= 0 && n_extra < (1 << 20) &&
                 (n_extra == 0 || (db_extra != nullptr && db != nullptr && T > 0)));
@@ -940,12 +1323,19 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
     if (db && zero_async(db, sizeof(float) * out, sw) != hipSuccess) return ESGPT_ERR_LAUNCH;
     return ESGPT_OK;
   }
-  ESGPT_REQUIRE(shapes_ok(false, false, dy, lddy, x, ldx, out, in, T, dw, in, true));
-  if (has_dx) ESGPT_REQUIRE(shapes_ok(true, false, dy, lddy, w, in, T, in, out, dx, lddx, false));
-  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
+  if (f32) {
+    ESGPT_REQUIRE(shapes_ok_f32(false, false, dy, lddy, x, ldx, out, in, T, dw, in));
+    if (has_dx) ESGPT_REQUIRE(shapes_ok_f32(true, false, dy, lddy, w, in, T, in, out, dx, lddx));
+    ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 16) == 0));
+  } else {
+    ESGPT_REQUIRE(shapes_ok(false, false, dy, lddy, x, ldx, out, in, T, dw, in, true));
+    if (has_dx) ESGPT_REQUIRE(shapes_ok(true, false, dy, lddy, w, in, T, in, out, dx, lddx, false));
+    ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
+  }
   Prob p0{};
   if (has_dx) {
-    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0, dx_tile(T, in, out));
+    p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, f32 ? 1 : 0, 0, nullptr, alpha, 0,
+                   f32 ? TileCfg{1, 1} : dx_tile(T, in, out));
     if (act >= 0) {
       p0.epi = EPI_ACT_GRAD;
       p0.act = act;
@@ -953,8 +1343,9 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
       p0.ld_aux = ldpre;
     }
   }
-  const TileCfg wc = dw_tile(T, in, out);
-  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in, out), wc);
+  const TileCfg wc = f32 ? TileCfg{1, 1} : dw_tile(T, in, out);
+  Prob p1 = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, dw_target(has_dx, T, in, out, f32),
+                      wc);
   p1.rowsum = db;
   p1.rs_extra = n_extra ? db_extra : nullptr;
   p1.rs_extra_n = (int)n_extra;
@@ -978,7 +1369,13 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
       p0.xmap = 2;
       p0.rps = p1.kchunk / bm_dx;
     }
-    launch_pair(p0, p1, st);
+    if (f32)
+      gemm_bwd_pair_kernel<1, 1, 1, 1, 0, true><<<dim3((unsigned)(n_wg(p0) + n_wg(p1))), THREADS, 0, st>>>(p0, p1);
+    else
+      launch_pair(p0, p1, st);
+  } else if (f32) {
+    if (has_dx) gemm_kernel<true, false, NS, 1, 1, 2, 0, true><<<dim3((unsigned)n_wg(p0)), THREADS, 0, st>>>(p0);
+    gemm_kernel<false, false, NS, 1, 1, 2, 0, true><<<dim3((unsigned)n_wg(p1)), THREADS, 0, sw>>>(p1);
   } else {
     if (has_dx) {
       switch (p0.fm * 10 + p0.fn) {
@@ -1101,6 +1498,67 @@ int esgpt_linear_bwd_ex(const void* dy, int64_t lddy, const void* x, int64_t ldx
                         int32_t* counters, const float* db_extra, int64_t n_extra, void* stream) {
   return linear_bwd_impl(dy, lddy, x, ldx, w, T, in, out, alpha, act, pre, ldpre, dx, lddx, dw, db, workspace,
                          workspace_bytes, counters, db_extra, n_extra, as_stream(stream), nullptr);
+}
+
+size_t esgpt_linear_bwd_f32_workspace(int64_t T, int64_t in, int64_t out, int has_dx) {
+  return slab_bytes(plan(out, in, T, dw_target(has_dx != 0, T, in, out, true), TileCfg{1, 1}).splits, out, in,
+                    TileCfg{1, 1});
+}
+
+int esgpt_linear_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* w, int64_t T,
+                         int64_t in, int64_t out, const float* alpha, int act, const float* pre, int64_t ldpre,
+                         float* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                         int32_t* counters, const float* db_extra, int64_t n_extra, void* stream) {
+  return linear_bwd_impl(dy, lddy, x, ldx, w, T, in, out, alpha, act, pre, ldpre, dx, lddx, dw, db, workspace,
+                         workspace_bytes, counters, db_extra, n_extra, as_stream(stream), nullptr, true);
+}
+
+int esgpt_linear_fwd_f32(const float* x, int64_t ldx, const float* w, int64_t T, int64_t in, int64_t out,
+                         const float* bias, int act, float* pre, float* y, int64_t ldy, void* stream) {
+  ESGPT_REQUIRE(shapes_ok_f32(true, true, x, ldx, w, in, T, out, in, y, ldy));
+  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2));
+  ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
+  ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
+  if (T == 0 || out == 0) return ESGPT_OK;
+  Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 1, 0, bias, nullptr, 0, TileCfg{1, 1});  // never split
+  if (act >= 0) {
+    p.epi = EPI_BIAS_ACT;
+    p.act = act;
+    p.aux_out = reinterpret_cast<__bf16*>(pre);
+    p.ld_aux = ldy;
+  }
+  gemm_kernel<true, true, NS, 1, 1, 2, 0, true><<<dim3((unsigned)n_wg(p)), THREADS, 0, as_stream(stream)>>>(p);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_gemm_f32(int a_layout, const float* A, int64_t lda, int b_layout, const float* B, int64_t ldb, int64_t M,
+                   int64_t N, int64_t K, const float* bias, const float* alpha, float* C, int64_t ldc, int accumulate,
+                   void* workspace, size_t workspace_bytes, int32_t* counters, void* stream) {
+  const bool akc = a_layout == ESGPT_GEMM_K_CONTIG, bkc = b_layout == ESGPT_GEMM_K_CONTIG;
+  ESGPT_REQUIRE(akc || a_layout == ESGPT_GEMM_MN_CONTIG);
+  ESGPT_REQUIRE(bkc || b_layout == ESGPT_GEMM_MN_CONTIG);
+  ESGPT_REQUIRE(shapes_ok_f32(akc, bkc, A, lda, B, ldb, M, N, K, C, ldc));
+  ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
+  if (M == 0 || N == 0) return ESGPT_OK;
+  Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, 1, accumulate, bias, alpha, kTarget, TileCfg{1, 1});
+  if (p.splits > 1) {
+    p.ext_reduce = p.splits > in_launch_splits();
+    ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N, TileCfg{1, 1}) &&
+                  (p.ext_reduce || counters));
+    ESGPT_REQUIRE(slab_bytes(p.splits, M, N, TileCfg{1, 1}) < (1ull << 31));
+    p.slab = reinterpret_cast<float*>(workspace);
+    p.counters = counters;
+  }
+  hipStream_t st = as_stream(stream);
+  const dim3 grid((unsigned)n_wg(p));
+  if (akc && bkc) gemm_kernel<true, true, NS, 1, 1, 2, 0, true><<<grid, THREADS, 0, st>>>(p);
+  else if (akc) gemm_kernel<true, false, NS, 1, 1, 2, 0, true><<<grid, THREADS, 0, st>>>(p);
+  else if (bkc) gemm_kernel<false, true, NS, 1, 1, 2, 0, true><<<grid, THREADS, 0, st>>>(p);
+  else gemm_kernel<false, false, NS, 1, 1, 2, 0, true><<<grid, THREADS, 0, st>>>(p);
+  if (p.ext_reduce) launch_slab_reduce(p, st);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
 }
 
 int esgpt_linear_bwd_split(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T,

@@ -137,16 +137,17 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
 // barrier; thread 0 advances it after).
 // With `err` (the step's error block, 16 bytes: int32 flags, int32 sticky word, int64 max bad index) the same launch
 // starts the step's own flags: the previous step's flags are OR-ed into the sticky word (which keeps every later
-// AdamW a no-op until the host has read and cleared the block), then the flags and the max index are zeroed.
+// AdamW a no-op until the host has read and cleared the block), then the flags are zeroed (and the max bad index,
+// unless an error is pending: it belongs to that error's message).
 __global__ __launch_bounds__(256) void seed_bank_kernel(int64_t* __restrict__ counter, int64_t* __restrict__ bank,
                                                         int64_t slots, int32_t* __restrict__ err) {
   const int64_t c = *counter;
   for (int64_t i = threadIdx.x; i < slots; i += blockDim.x) bank[i] = c + i;
   if (err && threadIdx.x == 0) {
-    const int32_t f = err[0];
-    err[1] |= f;
+    const int32_t sticky = err[1] | err[0];
+    err[1] = sticky;
     err[0] = 0;
-    *reinterpret_cast<int64_t*>(err + 2) = 0;
+    if (sticky == 0) *reinterpret_cast<int64_t*>(err + 2) = 0;  // kept while an error is pending (its message)
   }
   __syncthreads();
   if (threadIdx.x == 0) *counter = c + slots;

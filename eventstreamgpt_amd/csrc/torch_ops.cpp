@@ -569,6 +569,15 @@ void gemm_into(int64_t a_layout, const Tensor& a, int64_t lda, int64_t b_layout,
   const size_t nb = esgpt_gemm_workspace(M, N, K);
   Tensor ws = nb ? at::empty({(int64_t)nb}, a.options().dtype(at::kByte)) : Tensor();
   TORCH_CHECK(!nb || esgpt_gemm_counters(M, N) <= tickets.numel(), "GEMM tile grid exceeds the ticket array");
+  if (a.scalar_type() == at::kFloat) {  // f32 operands (the reference precision): exact-f32 MFMA, f32 output
+    TORCH_CHECK(b.scalar_type() == at::kFloat && c.scalar_type() == at::kFloat, "gemm: f32 operands need f32 B and C");
+    check(esgpt_gemm_f32((int)a_layout, ptr<const float>(a), lda, (int)b_layout, ptr<const float>(b), ldb, M, N, K,
+                         optr<const float>(bias), optr<const float>(alpha), ptr<float>(c), c.stride(0),
+                         accumulate ? 1 : 0, ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tickets),
+                         stream_of(a)),
+          "gemm_f32");
+    return;
+  }
   check(esgpt_gemm_bf16((int)a_layout, a.data_ptr(), lda, (int)b_layout, b.data_ptr(), ldb, M, N, K,
                         optr<const float>(bias), optr<const float>(alpha), c.data_ptr(), c.stride(0),
                         dtype_code(c.scalar_type()), accumulate ? 1 : 0, ws.defined() ? ws.data_ptr() : nullptr, nb,
@@ -601,6 +610,14 @@ std::tuple<Tensor, Tensor> linear_act(const Tensor& x, const Tensor& w, const op
   const int64_t T = x.size(0), din = x.size(1), dout = w.size(0);
   Tensor y = at::empty({T, dout}, x.options());
   Tensor pre = act >= 0 ? at::empty({T, dout}, x.options()) : at::empty({0}, x.options());
+  if (x.scalar_type() == at::kFloat) {
+    TORCH_CHECK(w.scalar_type() == at::kFloat, "linear: f32 x needs an f32 w");
+    check(esgpt_linear_fwd_f32(ptr<const float>(x), x.stride(0), ptr<const float>(w), T, din, dout,
+                               optr<const float>(bias), (int)act, act >= 0 ? ptr<float>(pre) : nullptr, ptr<float>(y),
+                               dout, stream_of(x)),
+          "linear_fwd_f32");
+    return {pre, y};
+  }
   check(esgpt_linear_fwd(x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout, optr<const float>(bias), (int)act,
                          act >= 0 ? pre.data_ptr() : nullptr, y.data_ptr(), dout, stream_of(x)),
         "linear_fwd");
@@ -650,8 +667,10 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
   const c10::DeviceGuard guard(x.device());
   // dw_tickets given: split form — dX on the current stream, dW / db on the device's weight-gradient stream (with
   // their own ticket array, workspace and outputs allocated in that stream's order); weight_grad_join before use
-  const bool split = dw_tickets.has_value() && dw_tickets->defined();
-  Tensor dy = dy_.contiguous();
+  const bool f32op = x.scalar_type() == at::kFloat;
+  // the f32 (reference-precision) form runs grouped on the current stream
+  const bool split = !f32op && dw_tickets.has_value() && dw_tickets->defined();
+  Tensor dy = f32op ? dy_.to(at::kFloat).contiguous() : dy_.contiguous();
   Tensor db_extra;
   if (db_extra_.has_value() && db_extra_->defined() && db_extra_->numel()) {
     db_extra = as(*db_extra_, at::kFloat);
@@ -660,7 +679,8 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
   const int64_t T = dy.size(0), dout = dy.size(1), din = x.size(1);
   auto f32 = x.options().dtype(at::kFloat);
   Tensor dx = need_dx ? at::empty({T, din}, dy.options()) : at::empty({0}, dy.options());
-  const size_t nb = esgpt_linear_bwd_workspace(T, din, dout, need_dx ? 1 : 0);
+  const size_t nb = f32op ? esgpt_linear_bwd_f32_workspace(T, din, dout, need_dx ? 1 : 0)
+                          : esgpt_linear_bwd_workspace(T, din, dout, need_dx ? 1 : 0);
   const Tensor& tk = split ? *dw_tickets : tickets;
   TORCH_CHECK(!nb || esgpt_gemm_counters(dout, din) <= tk.numel(), "GEMM tile grid exceeds the ticket array");
   const bool has_pre = pre.has_value() && pre->defined();
@@ -678,7 +698,18 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
     ws = nb ? at::empty({(int64_t)nb}, x.options().dtype(at::kByte)) : Tensor();
   }
   const void* dxp = need_dx ? dx.data_ptr() : nullptr;
-  if (split) {
+  if (f32op) {
+    TORCH_CHECK(w.scalar_type() == at::kFloat && (!has_pre || pre->scalar_type() == at::kFloat),
+                "linear_bwd: f32 x needs f32 w and pre");
+    check(esgpt_linear_bwd_f32(ptr<const float>(dy), dy.stride(0), ptr<const float>(x), x.stride(0),
+                               ptr<const float>(w), T, din, dout, optr<const float>(alpha), (int)act,
+                               has_pre ? ptr<const float>(*pre) : nullptr, has_pre ? pre->stride(0) : 0,
+                               reinterpret_cast<float*>(const_cast<void*>(dxp)), need_dx ? din : 0, ptr<float>(dw),
+                               need_db ? ptr<float>(db) : nullptr, ws.defined() ? ws.data_ptr() : nullptr, nb,
+                               ptr<int32_t>(tickets), db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
+                               db_extra.defined() ? db_extra.size(0) : 0, s_cur),
+          "linear_bwd_f32");
+  } else if (split) {
     check(esgpt_linear_bwd_split(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
                                  optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
                                  has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0,
@@ -752,7 +783,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> head_loss(const Tensor& xc, const opt
   optional<Tensor> zt;
   if (wt.has_value() && wt->defined()) zt = linear(*xt, *wt, bt, {}, tickets);
   optional<Tensor> zb;  // the head bias in the logits' dtype: position 0 reads Linear(zeros) = bias
-  if (shift) zb = (zb_in.has_value() && zb_in->defined()) ? *zb_in : bc.to(at::kBFloat16);
+  if (shift) zb = (zb_in.has_value() && zb_in->defined()) ? *zb_in : bc.to(zc.scalar_type());
   return output_loss(zc, zt, zb, BATCH_PASS, n_levels, shift, terms, tte_i, tte_f, err, ESGPT_LOSS_PATH_AUTO);
 }
 

@@ -180,13 +180,14 @@ class DataEmbeddingLayer(torch.nn.Module):
                        cat_scale, num_scale, static_scale)
         w = torch.cat([self.cat_proj.weight, self.num_proj.weight], dim=1)
         bias = (cat_scale + static_scale) * self.cat_proj.bias + num_scale * self.num_proj.bias
-        from ..fused import compute_dtype, gemm_supported, linear_op
+        from ..fused import GEMM_DTYPES, compute_dtype, gemm_supported, linear_op
 
         x2 = x.reshape(-1, x.shape[-1])
-        if x2.is_cuda and compute_dtype() == torch.bfloat16 and gemm_supported(x2.shape[0], w.shape[1], w.shape[0]):
-            # bf16: the HIP GEMM (bias in the epilogue; dW, db in one grouped backward launch)
+        dt = compute_dtype()
+        if x2.is_cuda and dt in GEMM_DTYPES and gemm_supported(x2.shape[0], w.shape[1], w.shape[0]):
+            # the HIP GEMM, bf16 or exact f32 (bias in the epilogue; dW, db in one grouped backward launch)
             with torch.autocast("cuda", enabled=False):
-                y = linear_op(x2.to(torch.bfloat16).contiguous(), w.detach().to(torch.bfloat16),
+                y = linear_op(x2.to(dt).contiguous(), w.detach().to(dt).contiguous(),
                               bias.float().contiguous(), [w]).float().view(*x.shape[:-1], w.shape[0])
         else:
             y = torch.nn.functional.linear(x, w, bias).float()

@@ -95,8 +95,13 @@ def _gemm(a, a_layout: int, lda: int, b, b_layout: int, ldb: int, M: int, N: int
 
 
 def gemm_supported(n_tokens: int, d_in: int, d_out: int) -> bool:
-    """Shape constraints of esgpt_gemm_bf16 for the fwd / dx / dW products of one projection."""
-    return n_tokens % 8 == 0 and d_in % 8 == 0 and d_out % 8 == 0
+    """Shape constraints of the library GEMMs (esgpt_gemm_bf16 / _f32) for the fwd / dx / dW products of one
+    projection: the feature dimensions in 16-B chunks; any token count (the dW product's token dimension is a row
+    index of both operands, and edge rows are zero-filled in-kernel)."""
+    return d_in % 8 == 0 and d_out % 8 == 0
+
+
+GEMM_DTYPES = (torch.bfloat16, torch.float32)  # bf16 MFMA, or exact-f32 MFMA (the reference's precision)
 
 
 def linear_op(x, w_lp, bias, masters):
@@ -164,10 +169,10 @@ class ProjFn:
 
 
 def proj(x, w_lp, bias, params):
-    """Projection through the HIP GEMM when the shapes allow it, else ``F.linear`` on the (differentiable)
-    compute-dtype weights."""
-    if w_lp is not None and w_lp.dtype == torch.bfloat16 and gemm_supported(x.shape[0], x.shape[1], w_lp.shape[0]):
-        return linear_op(x.to(torch.bfloat16), w_lp, bias, params)
+    """Projection through the HIP GEMM (bf16 shadow, or the f32 weights themselves in the reference-precision mode)
+    when the shapes allow it, else ``F.linear`` on the (differentiable) compute-dtype weights."""
+    if w_lp is not None and w_lp.dtype in GEMM_DTYPES and gemm_supported(x.shape[0], x.shape[1], w_lp.shape[0]):
+        return linear_op(x.to(w_lp.dtype).contiguous(), w_lp, bias, params)
     w = params[0] if len(params) == 1 else torch.cat(list(params), 0)
     dt = x.dtype
     return F.linear(x, w.to(dt), None if bias is None else bias.to(dt))
@@ -194,9 +199,9 @@ class MLPFn:
 def mlp(x, w_fc, w_pj, fc, pj, act: int, with_bias: bool = False):
     """InnerMLP (c_proj's bias included only with ``with_bias``): ``mlp_op`` when the bf16 GEMM shapes allow it,
     else proj + bias_act + proj."""
-    if (w_fc is not None and w_fc.dtype == torch.bfloat16
+    if (w_fc is not None and w_fc.dtype in GEMM_DTYPES
             and gemm_supported(x.shape[0], x.shape[1], w_fc.shape[0])):
-        return mlp_op(x.to(torch.bfloat16).contiguous(), w_fc, w_pj, fc.bias, act, fc.weight, pj.weight,
+        return mlp_op(x.to(w_fc.dtype).contiguous(), w_fc, w_pj, fc.bias, act, fc.weight, pj.weight,
                       pj.bias if with_bias else None)
     f = proj(x, w_fc, None, (fc.weight,))
     g = bias_act(f, fc.bias, act)
@@ -213,8 +218,9 @@ def weight_shadow(blocks, dtype):
         a = b.attn.attention
         ws += [a.q_proj.weight, a.k_proj.weight, a.v_proj.weight, a.out_proj.weight, b.mlp.c_fc.weight,
                b.mlp.c_proj.weight]
-    if dtype == torch.bfloat16:  # one esgpt::pack launch (a cat + a cast otherwise)
-        flat = _ops().pack([w.detach() for w in ws], [len(ws)], [0], [L.BF16])[0]
+    if dtype in GEMM_DTYPES:  # one esgpt::pack launch (a cat + a cast otherwise)
+        code = L.BF16 if dtype == torch.bfloat16 else L.F32
+        flat = _ops().pack([w.detach().contiguous() for w in ws], [len(ws)], [0], [code])[0]
     else:
         flat = torch.cat([w.reshape(-1) for w in ws]).to(dtype)
     out, off = [], 0
@@ -236,9 +242,11 @@ def linear_bias(x: torch.Tensor, params, biases) -> torch.Tensor:
     dt = compute_dtype()
     b = torch.cat(list(biases), 0) if len(biases) > 1 else biases[0]
     with torch.autocast("cuda", enabled=False):
-        if dt == torch.bfloat16:
-            with torch.no_grad():
-                w_lp = torch.cat([p.detach() for p in params], 0).to(dt)
+        if dt in GEMM_DTYPES and x.is_cuda:
+            with torch.no_grad():  # one esgpt::pack launch: the row-concatenated weights in the compute dtype
+                code = L.BF16 if dt == torch.bfloat16 else L.F32
+                w_lp = _ops().pack([p.detach().float().contiguous() for p in params], [len(params)], [0], [code])[0]
+                w_lp = w_lp.view(-1, params[0].shape[1])
             return proj(x.to(dt), w_lp, b, params)
         return proj(x.to(dt), None, b, params)
 
@@ -250,25 +258,26 @@ def head_loss_op(xc, xt, batch, terms, tte, shift: int, n_levels: int, cw, cb, t
     incoming d(total) straight from device memory (the GEMM's alpha pointer) — no logits-sized scaling pass, no host
     sync. ``xt`` / ``tw`` / ``tb`` are None / empty when the TTE columns are part of the content head (CI). Returns
     f32 [n_terms + 2] like ``output_loss``."""
+    wcode = L.BF16 if xc.dtype == torch.bfloat16 else L.F32  # the logits' (and GEMM operands') dtype
     with torch.no_grad():
-        # every padded head weight / bias copy in one esgpt::pack launch: [W_c | 0] bf16, [b_c | 0] f32 and bf16
-        # (the position-0 logits when shifted), [W_t | 0] bf16, [b_t | 0] f32
+        # every padded head weight / bias copy in one esgpt::pack launch: [W_c | 0] (compute dtype), [b_c | 0] f32
+        # and in the logits' dtype (the position-0 logits when shifted), [W_t | 0], [b_t | 0] f32
         D = cw[0].shape[1]
         nc = sum(w.shape[0] for w in cw)
         pc = (-nc) % 8
         srcs = [w.detach() for w in cw] + [b.detach() for b in cb] + ([b.detach() for b in cb] if shift else [])
-        groups, tails, codes = [len(cw), len(cb)], [pc * D, pc], [L.BF16, L.F32]
+        groups, tails, codes = [len(cw), len(cb)], [pc * D, pc], [wcode, L.F32]
         if shift:
             groups.append(len(cb))
             tails.append(pc)
-            codes.append(L.BF16)
+            codes.append(wcode)
         if tw:
             nt = sum(w.shape[0] for w in tw)
             pt = (-nt) % 8
             srcs += [w.detach() for w in tw] + [b.detach() for b in tb]
             groups += [len(tw), len(tb)]
             tails += [pt * D, pt]
-            codes += [L.BF16, L.F32]
+            codes += [wcode, L.F32]
         out = _ops().pack([t.float().contiguous() for t in srcs], groups, tails, codes)
         wc, bc = out[0].view(nc + pc, D), out[1]
         zb = out[2] if shift else None
@@ -284,17 +293,18 @@ def head_loss_op(xc, xt, batch, terms, tte, shift: int, n_levels: int, cw, cb, t
 
 
 def head_losses(xc, xt, batch, terms, tte, shift, n_levels, cmods, tmods):
-    """Generative heads + losses through ``esgpt::head_loss`` (bf16 compute) — None if the shapes do not fit the
-    HIP GEMM (the caller then uses the module-by-module path)."""
+    """Generative heads + losses through ``esgpt::head_loss`` (bf16 compute, or exact f32 in the reference-precision
+    mode) — None if the shapes do not fit the HIP GEMM (the caller then uses the module-by-module path)."""
     D = xc.shape[1]
-    if compute_dtype() != torch.bfloat16 or D % 8 or xc.shape[0] % 8 or (xt is not None and xt.shape[0] % 8):
+    dt = compute_dtype()
+    if dt not in GEMM_DTYPES or D % 8 or not xc.is_cuda:
         return None
     cw = [m.weight for m in cmods]
     cb = [m.bias for m in cmods]
     tw = [m.weight for m in tmods]
     tb = [m.bias for m in tmods]
-    xc = xc.to(torch.bfloat16).contiguous()
-    xt = None if xt is None else xt.to(torch.bfloat16).contiguous()
+    xc = xc.to(dt).contiguous()
+    xt = None if xt is None else xt.to(dt).contiguous()
     with torch.autocast("cuda", enabled=False):
         return head_loss_op(xc, xt, batch, terms, tte, shift, n_levels, cw, cb, tw, tb)
 
@@ -315,7 +325,7 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
     eps = float(cfg.layer_norm_epsilon)
     act = _ACTS[cfg.activation_function]
     blocks = list(encoder.h)
-    weights = weight_shadow(blocks, dt) if dt == torch.bfloat16 else [(None,) * 4] * len(blocks)
+    weights = weight_shadow(blocks, dt) if dt in GEMM_DTYPES else [(None,) * 4] * len(blocks)
     ln0 = blocks[0].attn.layer_norm
     h, ln = residual_ln(None, input_embeds.reshape(N, D).float().contiguous(), None, ln0.weight, ln0.bias,
                         None, p_in, eps, dt)
@@ -337,15 +347,14 @@ def ci_encoder_fused(encoder, batch, input_embeds: torch.Tensor, input_dropout: 
 
 
 def block_fused_supported(blk, hidden: torch.Tensor) -> bool:
-    """An ``InnerBlock`` can run through the HIP kernels (bf16 autocast on a HIP tensor, GEMM-friendly shapes)."""
-    if not (hidden.is_cuda and compute_dtype() == torch.bfloat16 and ENABLED):
+    """An ``InnerBlock`` can run through the HIP kernels (bf16 autocast or f32 on a HIP tensor, GEMM-friendly
+    feature widths; any token count)."""
+    if not (hidden.is_cuda and compute_dtype() in GEMM_DTYPES and ENABLED):
         return False
     cfg_act = getattr(blk.mlp, "act_name", None)
     D = hidden.shape[-1]
     F_ = blk.mlp.c_fc.out_features
-    n_tok = hidden.numel() // D
-    return (cfg_act in _ACTS and D % 8 == 0 and F_ % 8 == 0 and n_tok % 8 == 0 and D <= 1024
-            and blk.attn.attention.head_dim <= 128)
+    return cfg_act in _ACTS and D % 8 == 0 and F_ % 8 == 0 and D <= 1024 and blk.attn.attention.head_dim <= 128
 
 
 def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_first: bool, out_row_mask=None,
@@ -363,7 +372,7 @@ def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_fir
     train = blk.training
     p_res = float(att.resid_dropout.p) if train else 0.0
     p_att = att.attn_dropout_p if train else 0.0
-    dt = torch.bfloat16
+    dt = compute_dtype()  # bf16, or f32 (the reference precision: exact-f32 MFMA GEMMs)
     wqkv, wo, wfc, wpj = weight_shadow([blk], dt)[0]
     ln1 = blk.attn.layer_norm
     x2 = hidden.reshape(Bs * T, D).float().contiguous()

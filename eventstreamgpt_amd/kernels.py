@@ -144,7 +144,8 @@ def raise_for_error(code: int, max_index: int, n_total_embeddings: int | None = 
 
 
 def check_errors(device: torch.device | None = None, n_total_embeddings: int | None = None, batch=None):
-    """Reads (one host sync) and clears the device error block; raises the reference's exception for it.
+    """Reads (one host sync) and clears the device error block; raises the reference's exception for its flags —
+    the latest step's own, or the pending ones of an earlier step held in the sticky word (esgpt_step_begin).
     ``n_total_embeddings`` defaults to the table size of the latest embedding launch on the device."""
     device = device or torch.device("cuda", torch.cuda.current_device())
     w = err_word(device)
@@ -153,7 +154,7 @@ def check_errors(device: torch.device | None = None, n_total_embeddings: int | N
         w.zero_()
         if n_total_embeddings is None:
             n_total_embeddings = _LAST_V.get(_dev_index(device))
-        raise_for_error(code, mx, n_total_embeddings, batch)
+        raise_for_error((code | (code >> 32)) & 0xFFFFFFFF, mx, n_total_embeddings, batch)
 
 
 _TICKETS: dict[tuple[int, int], torch.Tensor] = {}

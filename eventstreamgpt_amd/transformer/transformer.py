@@ -106,9 +106,11 @@ class InnerSelfAttention(nn.Module):
             raise NotImplementedError("eventstreamgpt_amd: head_mask is not supported")
         if key_padding_mask is None and attention_mask is not None:
             key_padding_mask = attention_mask.reshape(attention_mask.shape[0], -1) == 0
+        window = self.window_size if self.attention_type == "local" else 0
+        if layer_past is None and not use_cache and self._library_gemms(hidden_states):
+            return self._forward_library(hidden_states, key_padding_mask, static_kv_first, window)
         w = self._packed_qkv_weight()
         qkv = nn.functional.linear(hidden_states, w)
-        window = self.window_size if self.attention_type == "local" else 0
         if static_kv_first and use_cache and layer_past is None:
             # NA dependency-graph prefill (transformer.py:246-265 with static_kv_first): the graph sequences are
             # attended as in training; present = the keys / values of every graph position, history included
@@ -132,6 +134,41 @@ class InnerSelfAttention(nn.Module):
         o = attention(qkv, kpm, qpm, self.num_heads, window, static_kv_first, p)
         out = self.resid_dropout(self.out_proj(o))
         return out, {"present_key_value": None}
+
+
+    def _library_gemms(self, hidden_states) -> bool:
+        """The training projections run on the library GEMMs (bf16 autocast or f32, HIP tensor)."""
+        from .. import fused
+
+        D = self.embed_dim
+        return (fused.ENABLED and hidden_states.is_cuda and fused.compute_dtype() in fused.GEMM_DTYPES
+                and fused.gemm_supported(1, D, 3 * D))
+
+    def _forward_library(self, hidden_states, key_padding_mask, static_kv_first: bool, window: int):
+        """The training forward with the q|k|v and out projections on the library GEMMs (packed-QKV GEMM into the
+        attention kernel's layout; out_proj's bias in its epilogue; the weight gradients straight to the f32
+        parameters) — the module-by-module path of the NA attention-only modules."""
+        from .. import _lib as L
+        from .. import fused
+
+        dt = fused.compute_dtype()
+        code = L.BF16 if dt == torch.bfloat16 else L.F32
+        D = self.embed_dim
+        ws = [self.q_proj.weight, self.k_proj.weight, self.v_proj.weight, self.out_proj.weight]
+        with torch.no_grad():  # one esgpt::pack launch: the packed q|k|v and out weights in the compute dtype
+            flat = fused._ops().pack([w.detach().float().contiguous() for w in ws], [len(ws)], [0], [code])[0]
+        wqkv, wo = flat[: 3 * D * D].view(3 * D, D), flat[3 * D * D:].view(D, D)
+        lead = hidden_states.shape[:-1]
+        kpm = None if key_padding_mask is None else key_padding_mask.contiguous()
+        qpm = None if (kpm is None or static_kv_first) else kpm
+        p = self.attn_dropout_p if self.training else 0.0
+        with torch.autocast("cuda", enabled=False):
+            x2 = hidden_states.reshape(-1, D).to(dt)
+            qkv = fused.proj(x2, wqkv, None, tuple(ws[:3])).view(*lead, 3 * D)
+            o = attention(qkv, kpm, qpm, self.num_heads, window, static_kv_first, p)
+            out = fused.proj(o.reshape(-1, D), wo, self.out_proj.bias, (self.out_proj.weight,))
+        out = out.view(*o.shape[:-1], D)
+        return self.resid_dropout(out), {"present_key_value": None}
 
 
 class InnerAttention(nn.Module):
@@ -217,13 +254,13 @@ class InnerBlock(nn.Module):
 
 
 def _final_layer_norm(ln: nn.LayerNorm, hidden: torch.Tensor) -> torch.Tensor:
-    """``ln_f`` (f32 output). Under bf16 autocast on a HIP tensor: the library's LayerNorm (``esgpt::residual_ln`` with
+    """``ln_f`` (f32 output). On a HIP tensor (bf16 autocast or f32): the library's LayerNorm (``esgpt::residual_ln`` with
     no residual; f32 statistics, one pass each way) instead of ATen's three LayerNorm kernels."""
     from .. import fused
     from ..fused import compute_dtype, residual_ln
 
     D = hidden.shape[-1]
-    if not (fused.ENABLED and hidden.is_cuda and compute_dtype() == torch.bfloat16 and D % 4 == 0 and D <= 1024
+    if not (fused.ENABLED and hidden.is_cuda and compute_dtype() in fused.GEMM_DTYPES and D % 4 == 0 and D <= 1024
             and ln.weight is not None and ln.bias is not None):
         return ln(hidden)
     with torch.autocast("cuda", enabled=False):

@@ -329,7 +329,8 @@ int esgpt_na_assemble_bwd(const float* dseq, int64_t B, int64_t L, int64_t G, in
  * so y = x·Wᵀ is (K, K), dx = dy·W is (K, MN) and dW = dyᵀ·x is (MN, MN). c_dtype ESGPT_BF16 or ESGPT_F32;
  * accumulate (f32 only): C += alpha·A·B (+ bias). alpha: optional DEVICE pointer to one f32 (NULL = 1), read at
  * run time (e.g. the incoming gradient of a loss, without a host sync or a separate scaling kernel). Requires K > 0,
- * K, lda, ldb multiples of 8, the MN-contig extents multiples of 8, 16-B aligned A, B, C (and bias), and N, ldc
+ * K (when either operand is K-contig; a dW product (MN, MN) takes any token count), lda, ldb multiples of 8, the
+ * MN-contig extents multiples of 8, 16-B aligned A, B, C (and bias), and N, ldc
  * multiples of 8 (bf16 C) / 4 (f32 C). Split-K: f32 slabs in `workspace` (esgpt_gemm_workspace(M, N, K) bytes, 0 =
  * none needed) and one int32 ticket per output tile in `counters` (esgpt_gemm_counters(M, N) entries, zeroed once
  * by the caller; every launch leaves them zeroed; launches sharing a counter array must be stream-ordered). The
@@ -374,6 +375,24 @@ int esgpt_linear_bwd_split(const void* dy, int64_t lddy, const void* x, int64_t 
                            int64_t in, int64_t out, const float* alpha, int act, const void* pre, int64_t ldpre,
                            void* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
                            int32_t* counters, const float* db_extra, int64_t n_extra, void* stream, void* stream_dw);
+/* f32 forms (the reference's precision: scripts/pretrain.py:24 trains in f32; gfx950 has no TF32 / xf32): every
+ * operand, pre-activation and output f32, products on v_mfma_f32_32x32x2_f32 — exact f32, one fmaf per product in
+ * k order, at the f32 vector rate. Same semantics, workspace / counter rules and deterministic split-K as the bf16
+ * entry points above; K, lda, ldb, ldc multiples of 4, the MN-contig extents and N multiples of 4, 16-B aligned.
+ *   esgpt_gemm_f32: C (f32) [+]= alpha·A·B (+ bias); workspace esgpt_gemm_workspace(M, N, K).
+ *   esgpt_linear_fwd_f32: y = x·wᵀ + bias, or with act >= 0 pre = x·wᵀ + bias (f32) and y = act(pre).
+ *   esgpt_linear_bwd_f32: the grouped backward (dx f32 [· act'(pre)], dw, db [+ db_extra]) in one launch;
+ *     workspace esgpt_linear_bwd_f32_workspace(T, in, out, dx != NULL). */
+int esgpt_gemm_f32(int a_layout, const float* A, int64_t lda, int b_layout, const float* B, int64_t ldb, int64_t M,
+                   int64_t N, int64_t K, const float* bias, const float* alpha, float* C, int64_t ldc, int accumulate,
+                   void* workspace, size_t workspace_bytes, int32_t* counters, void* stream);
+int esgpt_linear_fwd_f32(const float* x, int64_t ldx, const float* w, int64_t T, int64_t in, int64_t out,
+                         const float* bias, int act, float* pre, float* y, int64_t ldy, void* stream);
+size_t esgpt_linear_bwd_f32_workspace(int64_t T, int64_t in, int64_t out, int has_dx);
+int esgpt_linear_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* w, int64_t T,
+                         int64_t in, int64_t out, const float* alpha, int act, const float* pre, int64_t ldpre,
+                         float* dx, int64_t lddx, float* dw, float* db, void* workspace, size_t workspace_bytes,
+                         int32_t* counters, const float* db_extra, int64_t n_extra, void* stream);
 /* `waiter` waits (device-side, an event) for every piece of work queued on `signaller` before the call: the join of
  * esgpt_linear_bwd_split's weight-gradient stream (and its fork). Both may be captured into one HIP graph. */
 int esgpt_stream_wait(void* waiter, void* signaller);
@@ -382,8 +401,8 @@ int esgpt_stream_wait(void* waiter, void* signaller);
  * capturable into a HIP graph (every replay draws fresh seeds). */
 int esgpt_seed_bank(int64_t* counter, int64_t* bank, int64_t slots, void* stream);
 /* The first launch of a training step: esgpt_seed_bank plus, when err != NULL, the step's own flags started: the
- * previous step's flags (int32 word 0) are OR-ed into the sticky word (int32 word 1), then word 0 and the max bad
- * index (int64 at byte 8) are zeroed. The flags a step's kernels raise belong to that step alone; the sticky word
+ * previous step's flags (int32 word 0) are OR-ed into the sticky word (int32 word 1), then word 0 is zeroed (and the
+ * max bad index, int64 at byte 8, when no error is pending). The flags a step's kernels raise belong to that step alone; the sticky word
  * keeps every later AdamW a no-op until the host has read the block and cleared it (a step queued behind a failed
  * one is discarded, as the reference never runs it). */
 int esgpt_step_begin(int64_t* counter, int64_t* bank, int64_t slots, int32_t* err, void* stream);

@@ -48,6 +48,8 @@ def fused_mode(request):
 def test_model_matches_reference_f32(name, fused_mode):
     if not fused_mode and name.startswith("na_"):
         pytest.skip("NA encoder has a single (module) path")
+    from eventstreamgpt_amd.train import _GemmSpy
+
     fx, cfg, batch = load_case(name)
     m = _model(cfg).to(DEV)
     m.load_state_dict(fx["state_dict"])
@@ -55,14 +57,18 @@ def test_model_matches_reference_f32(name, fused_mode):
     b = batch.to(DEV)
     enc = m.encoder(b).last_hidden_state
     assert rel_err(enc.detach().cpu(), fx["encoded"]) < 1e-5
-    out = m(b)
+    spy = _GemmSpy()
+    with spy:
+        out = m(b)
+        out.loss.backward()
+    if fused_mode:  # the reference-precision step runs on the library's own f32 MFMA GEMMs, not PyTorch-ROCm BLAS
+        assert not (spy.hits & set(_GemmSpy.GEMMS)), spy.hits
     assert abs(out.loss.item() - fx["loss"].item()) <= 1e-5 * abs(fx["loss"].item())
     for k, v in fx["classification"].items():
         assert out.losses.classification[k].item() == pytest.approx(v.item(), rel=1e-5, abs=1e-6), k
     for k, v in fx["regression"].items():
         assert out.losses.regression[k].item() == pytest.approx(v.item(), rel=1e-5, abs=1e-6), k
     assert out.losses.time_to_event.item() == pytest.approx(fx["tte_nll"].item(), rel=1e-5, abs=1e-6)
-    out.loss.backward()
     named = dict(m.named_parameters())
     for k, g in fx["grads"].items():
         got = named[k].grad
@@ -398,6 +404,40 @@ GEMM_SHAPES = [(8192, 768, 256), (8192, 256, 1024), (256, 256, 8192), (1232, 256
                (336, 1232, 256), (8, 8, 8), (520, 136, 72), (104, 1624, 256), (72, 136, 64), (8200, 24, 32)]
 
 
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES + [(336, 1232, 8193), (104, 40, 1000)])
+@pytest.mark.parametrize("a_kc", [True, False])
+@pytest.mark.parametrize("b_kc", [True, False])
+def test_gemm_kernel_f32(M, N, K, a_kc, b_kc):
+    """esgpt_gemm_f32 (exact-f32 MFMA, the reference precision) for every operand layout vs an f64 matmul of the
+    same f32 values, with bias, accumulate, split-K and ragged tails (a K-contig operand needs K % 4 == 0; the
+    (MN, MN) dW form takes any K). Error bound: f32 accumulation, |err| <= 1e-5 · max Σ_k |a·b|."""
+    from eventstreamgpt_amd.fused import _gemm
+
+    if (a_kc or b_kc) and K % 4:
+        pytest.skip("a K-contig f32 operand needs K % 4 == 0")
+    g = torch.Generator().manual_seed(M * 5 + N * 3 + K)
+    a = torch.randn(M, K, generator=g)
+    b = torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    ref = a.double() @ b.double()
+    mag = (a.double().abs() @ b.double().abs()).max().item() + 1.0
+    a_st = a.contiguous() if a_kc else a.t().contiguous()
+    b_st = b.t().contiguous() if b_kc else b.contiguous()
+    lda, ldb = (K if a_kc else M), (K if b_kc else N)
+    A, Bm = a_st.to(DEV), b_st.to(DEV)
+    from eventstreamgpt_amd import _lib as L
+
+    la = L.GEMM_K_CONTIG if a_kc else L.GEMM_MN_CONTIG
+    lb = L.GEMM_K_CONTIG if b_kc else L.GEMM_MN_CONTIG
+    c32 = torch.full((M, N), float("nan"), device=DEV)
+    _gemm(A, la, lda, Bm, lb, ldb, M, N, K, c32, bias=bias.to(DEV))
+    assert ((c32.double().cpu() - ref - bias.double()).abs().max() / mag).item() < 1e-5
+    acc = torch.randn(M, N, generator=g).to(DEV)
+    want = acc.double().cpu() + ref
+    _gemm(A, la, lda, Bm, lb, ldb, M, N, K, acc, accumulate=True)
+    assert ((acc.double().cpu() - want).abs().max() / mag).item() < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
 @pytest.mark.parametrize("a_kc", [True, False])
 @pytest.mark.parametrize("b_kc", [True, False])
@@ -492,6 +532,42 @@ def test_linear_bwd(T, din, dout, act, need_dx):
     else:
         assert dx is None
     assert int(tickets(torch.device(DEV)).abs().sum()) == 0
+
+
+@pytest.mark.parametrize("T,din,dout", [(8192, 256, 1024), (1000, 1024, 256), (333, 136, 72), (7, 8, 8)])
+@pytest.mark.parametrize("act", [-1, 0, 2])
+def test_linear_f32_fwd_bwd(T, din, dout, act):
+    """The f32 projection (esgpt_linear_fwd_f32 / _bwd_f32, exact-f32 MFMA): y = act(x·wᵀ + b) with the f32
+    pre-activation, and the grouped backward dx (· act'(pre)), dW, db — vs f64 references at the reference
+    precision's tolerance (1e-5 of the magnitude), including ragged token counts (T % 8 != 0)."""
+    from eventstreamgpt_amd.fused import linear_bwd, linear_fwd_act, linear_op
+
+    g = torch.Generator().manual_seed(T + din * 7 + dout + act)
+    x = torch.randn(T, din, generator=g)
+    w = 0.1 * torch.randn(dout, din, generator=g)
+    b = torch.randn(dout, generator=g)
+    pre_ref = x.double() @ w.double().t() + b.double()
+    if act >= 0:
+        pre, y = linear_fwd_act(x.to(DEV), w.to(DEV), b.to(DEV), act)
+        assert pre.dtype == torch.float32 and y.dtype == torch.float32
+        assert rel_err(pre.cpu(), pre_ref) < 1e-5
+        assert rel_err(y.cpu(), _act_ref(pre.double().cpu(), act)) < 1e-5
+    else:
+        y = linear_op(x.to(DEV), w.to(DEV), b.to(DEV), [])
+        assert y.dtype == torch.float32 and rel_err(y.cpu(), pre_ref) < 1e-5
+    dy = torch.randn(T, dout, generator=g)
+    prev = torch.randn(T, din, generator=g) if act >= 0 else None
+    alpha = torch.tensor([0.75])
+    dx, dw, db = linear_bwd(dy.to(DEV), x.to(DEV), w.to(DEV), alpha=alpha.to(DEV), act=act,
+                            pre=None if prev is None else prev.to(DEV), need_dx=True, need_db=True)
+    assert dx.dtype == torch.float32
+    assert rel_err(dw.cpu(), 0.75 * (dy.double().t() @ x.double())) < 1e-5
+    assert rel_err(db.cpu(), 0.75 * dy.double().sum(0)) < 1e-5
+    dxr = 0.75 * (dy.double() @ w.double())
+    if act >= 0:
+        z = prev.double().requires_grad_(True)
+        dxr = dxr * torch.autograd.grad(_act_ref(z, act).sum(), z)[0]
+    assert rel_err(dx.cpu(), dxr) < 1e-5
 
 
 @pytest.mark.parametrize("act", [0, 1])

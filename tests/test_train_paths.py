@@ -192,45 +192,72 @@ def test_nested_attention_graph_replay_matches_eager_with_allocations_between_re
         assert (sg[k] - se[k]).abs().max().item() < 1e-4, k
 
 
-@pytest.mark.gpu
-def test_graph_capture_skips_signatures_with_aten_gemm_fallback():
-    """A batch whose token count the fused NA blocks do not take (B·L not a multiple of 8) runs the module path
-    through PyTorch-ROCm BLAS; its Linear backward replayed from a HIP graph returns wrong bias gradients
-    (tools/graph_blaslt_repro.py), so TrainStep does not capture that signature (warm-up under _GemmSpy) and runs it
-    eagerly: same losses and parameters as an eager TrainStep, while a fused-shape signature is still captured."""
+def _na_graph_vs_eager(batches, fused_enabled=True):
+    from eventstreamgpt_amd import fused
     from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
 
     bc = CONFIGS["C4"]
-    odd = [bc.batch(i, batch_size=1, device="cuda")[:, :253].packed() for i in range(3)]  # 253 tokens
-    even = [bc.batch(10 + i, batch_size=2, device="cuda").packed() for i in range(2)]
 
     def run(graph):
         cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
         torch.manual_seed(0)
         m = NAPPTForGenerativeSequenceModeling(cfg).cuda().train()
         ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=100),
-                       torch.bfloat16, use_graph=graph)
-        losses = [float(ts.step(b)) for b in odd + even]
+                       torch.bfloat16, use_graph=graph, _force_graph=graph and not fused_enabled)
+        losses = [float(ts.step(b)) for b in batches]
         ts.check()
         return losses, {k: v.detach().float().clone() for k, v in m.state_dict().items()}, ts
 
-    le, se, _ = run(False)
-    lg, sg, ts = run(True)
-    assert ts.graphs[odd[0].shape_signature()] is None and ts.capture_report[odd[0].shape_signature()]
-    assert ts.graphs[even[0].shape_signature()] is not None, ts.capture_report
+    old = fused.ENABLED
+    fused.ENABLED = fused_enabled
+    try:
+        le, se, _ = run(False)
+        lg, sg, ts = run(True)
+    finally:
+        fused.ENABLED = old
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-3 * abs(a), (le, lg)
     for k in se:
         assert (sg[k] - se[k]).abs().max().item() < 1e-4, k
+    return ts
+
+
+@pytest.mark.gpu
+def test_ragged_token_counts_stay_on_library_gemms_and_capture():
+    """A batch with a token count that is not a multiple of 8 (B·L = 253; the reference pads each batch to its own
+    longest subject, pytorch_dataset.py:571) runs the fused NA blocks on the library GEMMs (the dW products take any
+    token count; edge rows are zero-filled in-kernel): its warm-up shows no ATen GEMM or reduction, so the signature is
+    captured, and graph replay equals the eager step."""
+    bc = CONFIGS["C4"]
+    odd = [bc.batch(i, batch_size=1, device="cuda")[:, :253].packed() for i in range(3)]  # 253 tokens
+    even = [bc.batch(10 + i, batch_size=2, device="cuda").packed() for i in range(2)]
+    ts = _na_graph_vs_eager(odd + even)
+    assert ts.graphs[odd[0].shape_signature()] is not None, ts.capture_report
+    assert not ts.capture_report[odd[0].shape_signature()], ts.capture_report
+    assert ts.graphs[even[0].shape_signature()] is not None, ts.capture_report
+
+
+@pytest.mark.gpu
+def test_graph_capture_skips_signatures_with_aten_gemm_fallback():
+    """The module-by-module path (fused.ENABLED off) runs its Linears through PyTorch-ROCm BLAS, whose backward
+    replayed from a HIP graph returns wrong bias gradients (tools/graph_blaslt_repro.py): TrainStep does not capture
+    such a signature (warm-up under _GemmSpy) and runs it eagerly, with eager's losses and parameters."""
+    bc = CONFIGS["C4"]
+    batches = [bc.batch(i, batch_size=1, device="cuda").packed() for i in range(3)]
+    ts = _na_graph_vs_eager(batches, fused_enabled=False)
+    sig = batches[0].shape_signature()
+    assert ts.graphs[sig] is None and ts.capture_report[sig]
 
 
 @pytest.mark.gpu
 def test_step_error_flags_are_per_step():
     """A step whose batch holds an out-of-range embedding index is a no-op for the parameters (its AdamW sees the
-    flag), and the step after it — on the device, the error block is zeroed by each step's first launch — updates
-    them (device semantics, TrainStep(check_errors=False)). With checking on, the error is raised as the reference's
-    AssertionError at a later submission, and the failing step's AdamW / LR-schedule counters are rolled back."""
-    from eventstreamgpt_amd.kernels import err_word
+    flag). On the device each step's first launch starts its own flags and moves the previous step's into the sticky
+    word, so every later step stays a no-op until the host has read and cleared the block (device semantics,
+    TrainStep(check_errors=False): kernels.check_errors raises the reference's AssertionError and clears it; then
+    steps update again, with clear flags of their own). With checking on, the error is raised at a later submission
+    and the failing step's AdamW / LR-schedule counters are rolled back."""
+    from eventstreamgpt_amd.kernels import check_errors, err_word
     from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
 
     bc = CONFIGS["C1"]
@@ -253,8 +280,15 @@ def test_step_error_flags_are_per_step():
     assert all(torch.equal(p0[k], p1[k]) for k in p0)  # the failing step did not update
     ts.step(good[1])
     p2 = snap(m)
-    assert any(not torch.equal(p1[k], p2[k]) for k in p0)  # the next step did
-    assert int(err_word(torch.device("cuda"))[0]) == 0  # and its own flags are clear
+    assert all(torch.equal(p1[k], p2[k]) for k in p0)  # nor did the step queued behind it (sticky word)
+    w = err_word(torch.device("cuda"))
+    assert int(w[0]) & 0xFFFFFFFF == 0 and int(w[0]) >> 32 != 0  # its own flags are clear, the sticky word set
+    with pytest.raises(AssertionError, match="Invalid embedding!"):
+        check_errors(torch.device("cuda"), cfg.vocab_size)  # reads and clears the block
+    ts.step(good[2])
+    p3 = snap(m)
+    assert any(not torch.equal(p2[k], p3[k]) for k in p0)  # the next step updates
+    assert int(err_word(torch.device("cuda"))[0]) == 0
 
     torch.manual_seed(0)
     m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
