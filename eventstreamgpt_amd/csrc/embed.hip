@@ -122,12 +122,26 @@ __device__ __forceinline__ void load_static(const esgpt_batch& bt, int64_t b, in
 
 // Exclusive cumsum of masked deltas up to event l of subject b, accumulated in double (the reference's CPU
 // cumsum accumulates f32 in double, so this reproduces its values) and rounded to f32.
+// Loads are issued kTU per lane at a time from clamped addresses (selected away past l), so a long prefix costs one
+// memory round trip per 64·kTU events instead of one per 64; each lane still adds its deltas in ascending order.
 __device__ __forceinline__ float event_time(const esgpt_batch& bt, int64_t b, int64_t l, int lane, bool abs_time) {
   if (abs_time) return bt.time_abs[b * bt.L + l];
+  constexpr int kTU = 4;
+  const uint8_t* em = bt.event_mask + b * bt.L;
+  const float* td = bt.time_delta + b * bt.L;
   double acc = 0.0;
-  for (int64_t j = lane; j < l; j += 64) {
-    const float d = bt.event_mask[b * bt.L + j] ? bt.time_delta[b * bt.L + j] : 0.0f;
-    acc += (double)d;
+  for (int64_t j0 = 0; j0 < l; j0 += 64 * kTU) {
+    uint8_t m[kTU];
+    float d[kTU];
+#pragma unroll
+    for (int u = 0; u < kTU; ++u) {
+      const int64_t j = min(j0 + 64 * u + lane, l > 0 ? l - 1 : 0);
+      m[u] = em[j];
+      d[u] = td[j];
+    }
+#pragma unroll
+    for (int u = 0; u < kTU; ++u)
+      if (j0 + 64 * u + lane < l) acc += (double)(m[u] ? d[u] : 0.0f);
   }
   acc = wave_sum_d(acc);
   return (float)acc;
@@ -198,25 +212,35 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
   const bool use_static = (flags & ESGPT_EMB_STATIC) && bt.S > 0;
   const bool valid = active && bt.event_mask[e] != 0;
 
+  // The event's non-padding entries are compacted to the front of the wave's LDS lists in entry order (ballot +
+  // prefix popcount), so the gathers below walk only real rows: the same f32 sums in the same order.
   const Entry en = load_entry(bt, e, lane, normalize, V, err);
-  if (lane < bt.M) {
-    s_idx[wave][lane] = en.idx;
-    for (int g = 0; g < G; ++g) s_w[wave][g][lane] = entry_weight(en, bk, g, ESGPT_BAG_JOINT);
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint64_t live = __ballot(lane < bt.M && en.idx != 0);
+  const int n_live = __popcll(live);
+  if ((live >> lane) & 1ull) {
+    const int pos = __popcll(live & below);
+    s_idx[wave][pos] = en.idx;
+    for (int g = 0; g < G; ++g) s_w[wave][g][pos] = entry_weight(en, bk, g, ESGPT_BAG_JOINT);
   }
+  int n_slive = 0;
   if (use_static) {
     int64_t sidx;
     float swt;
     load_static(bt, b, lane, normalize, V, err, sidx, swt);
-    if (lane < bt.S) {
-      s_sidx[wave][lane] = sidx;
-      s_sw[wave][lane] = swt;
+    const uint64_t slive = __ballot(lane < bt.S && sidx != 0);
+    n_slive = __popcll(slive);
+    if ((slive >> lane) & 1ull) {
+      const int pos = __popcll(slive & below);
+      s_sidx[wave][pos] = sidx;
+      s_sw[wave][pos] = swt;
     }
   }
-  float t = 0.f;
-  if (flags & ESGPT_EMB_TIME) t = event_time(bt, b, l, lane, flags & ESGPT_EMB_TIME_ABS);
   __syncthreads();
 
   const int64_t n_chunks = (D + 64 * VEC - 1) / (64 * VEC);
+  float t = 0.f;
+  bool t_done = !(flags & ESGPT_EMB_TIME);
   for (int64_t c = 0; c < n_chunks; ++c) {
     const int64_t d0 = c * 64 * VEC + lane * VEC;
     float acc[GMAX][VEC];
@@ -224,34 +248,77 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
     for (int g = 0; g < GMAX; ++g)
 #pragma unroll
       for (int v = 0; v < VEC; ++v) acc[g][v] = 0.f;
-    if (valid) {
-      for (int m = 0; m < bt.M; ++m) {
-        const int64_t i = s_idx[wave][m];
-        if (i == 0) continue;  // padding_idx=0 contributes nothing
-        float r[VEC];
-        load_row<VEC>(table, i, D, d0, r);
-#pragma unroll
-        for (int g = 0; g < GMAX; ++g) {
-          if (g < G) {
-            const float w = s_w[wave][g][m];
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) acc[g][v] = fmaf(w, r[v], acc[g][v]);
-          }
-        }
-      }
-    }
+    // Rows are gathered kGU at a time, every load of a group in flight before the first FMA (one dependent
+    // memory round trip per group instead of per row: a gather from a table beyond the caches is latency-bound
+    // otherwise). Padding entries (index 0, padding_idx) load row 0 harmlessly and are skipped in the sums, which
+    // keep the entry order (the same f32 results bit for bit).
+    constexpr int kGU = sizeof(TT) == 4 ? 4 : 8;  // bf16 (large tables beyond the caches): more rows in flight
     float st[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) st[v] = 0.f;
-    if (use_static && valid) {
-      for (int s = 0; s < bt.S; ++s) {
-        const int64_t i = s_sidx[wave][s];
-        if (i == 0) continue;
-        const float w = s_sw[wave][s];
+    // whole chunks (D a multiple of 64·VEC, every lane in range): unconditional vector loads in a branch-free loop,
+    // so the compiler keeps each group's loads in flight together (a per-lane bounds branch around each load makes
+    // it wait for every load in turn: one row per memory round trip)
+    auto gather_all = [&](auto whole_c) {
+      constexpr bool WHOLE = decltype(whole_c)::value;
+      auto gather = [&](float (&r)[VEC], int64_t i) {
+        if constexpr (WHOLE && sizeof(TT) == 4) {
+          const float4 x = *reinterpret_cast<const float4*>(table + i * D + d0);
+          r[0] = x.x; r[1] = x.y; r[2] = x.z; r[3] = x.w;
+        } else if constexpr (WHOLE) {
+          const uint2 x = *reinterpret_cast<const uint2*>(table + i * D + d0);
+          r[0] = __uint_as_float(x.x << 16), r[1] = __uint_as_float(x.x & 0xffff0000u);
+          r[2] = __uint_as_float(x.y << 16), r[3] = __uint_as_float(x.y & 0xffff0000u);
+        } else {
+          load_row<VEC>(table, i, D, d0, r);
+        }
+      };
+      if (valid) {
+        for (int m0 = 0; m0 < n_live; m0 += kGU) {
+          float r[kGU][VEC];
+          int64_t iu[kGU];
 #pragma unroll
-        for (int v = 0; v < VEC; ++v)
-          if (d0 + v < D) st[v] = fmaf(w, to_f32(table[i * D + d0 + v]), st[v]);
+          for (int u = 0; u < kGU; ++u) iu[u] = s_idx[wave][min(m0 + u, kMaxM - 1)] * (m0 + u < n_live ? 1 : 0);
+#pragma unroll
+          for (int u = 0; u < kGU; ++u) gather(r[u], iu[u]);
+#pragma unroll
+          for (int u = 0; u < kGU; ++u) {
+            if (iu[u] == 0) continue;  // padding_idx=0 contributes nothing (wave-uniform)
+#pragma unroll
+            for (int g = 0; g < GMAX; ++g) {
+              if (g < G) {
+                const float w = s_w[wave][g][m0 + u];
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) acc[g][v] = fmaf(w, r[u][v], acc[g][v]);
+              }
+            }
+          }
+        }
       }
+      if (use_static && valid) {
+        for (int s0 = 0; s0 < n_slive; s0 += kGU) {
+          float r[kGU][VEC];
+          int64_t iu[kGU];
+#pragma unroll
+          for (int u = 0; u < kGU; ++u) iu[u] = s_sidx[wave][min(s0 + u, kMaxM - 1)] * (s0 + u < n_slive ? 1 : 0);
+#pragma unroll
+          for (int u = 0; u < kGU; ++u) gather(r[u], iu[u]);
+#pragma unroll
+          for (int u = 0; u < kGU; ++u) {
+            if (iu[u] == 0) continue;
+            const float w = s_sw[wave][s0 + u];
+#pragma unroll
+            for (int v = 0; v < VEC; ++v)
+              if (d0 + v < D) st[v] = fmaf(w, r[u][v], st[v]);
+          }
+        }
+      }
+    };
+    if (VEC == 4 && D % (64 * VEC) == 0) gather_all(std::true_type{});
+    else gather_all(std::false_type{});
+    if (!t_done) {  // the event's time (a prefix sum over the subject's deltas) after the gathers are in flight
+      t = event_time(bt, b, l, lane, flags & ESGPT_EMB_TIME_ABS);
+      t_done = true;
     }
     double run[VEC];
 #pragma unroll
