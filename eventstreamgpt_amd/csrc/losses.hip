@@ -52,15 +52,19 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int l) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Pass 1: one 1024-thread block per (chunk of E events, subject). The chunk's E·M entries are read once, coalesced
-// (thread = entry, up to 4 per thread, loads in flight together), and each entry ORs the bit of every non-MULTI
+// Pass 1: one workgroup per (chunk of E events, subject). The chunk's E·M entries are read once, coalesced
+// (thread = entry, 4 per thread, loads in flight together), and each entry ORs the bit of every non-MULTI
 // term it satisfies into its event's LDS word (SINGLE: measurement present; MVREG / UVREG: measurement with a
 // value); then thread = event: term t counts the event when it is an event and (MULTI or bit t set); TTE counts
 // events followed by an event. Integer adds: exact, order-free. partial: int32 [B][n_chunks][MAX_TERMS + 1].
 // Dynamic LDS: E words.
+// The term bits an entry sets depend only on its measurement index (and its value mask): per-index masks built once
+// per workgroup in LDS (kLut indices; larger indices take the per-term scan).
+constexpr int kLut = 256;
 __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms, int E, int32_t* __restrict__ partial) {
   extern __shared__ uint32_t s_bits[];
   __shared__ int32_t s_cnt[ESGPT_MAX_TERMS + 1];
+  __shared__ uint32_t s_lut_any[kLut], s_lut_val[kLut];
   const int64_t b = blockIdx.y;
   const int ch = blockIdx.x, n_ch = gridDim.x;
   const int T = terms.n;
@@ -68,6 +72,13 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
   const int l0 = ch * E, ne = (int)min((int64_t)E, L - l0);
   if (threadIdx.x <= T) s_cnt[threadIdx.x] = 0;
   for (int l = threadIdx.x; l < ne; l += blockDim.x) s_bits[l] = 0u;
+  for (int i = threadIdx.x; i < kLut; i += blockDim.x) s_lut_any[i] = s_lut_val[i] = 0u;
+  __syncthreads();
+  if (threadIdx.x < T) {
+    const esgpt_loss_term& tm = terms.t[threadIdx.x];
+    if (tm.kind != ESGPT_TERM_MULTI && tm.meas_idx >= 0 && tm.meas_idx < kLut)
+      atomicOr(tm.kind == ESGPT_TERM_SINGLE ? &s_lut_any[tm.meas_idx] : &s_lut_val[tm.meas_idx], 1u << threadIdx.x);
+  }
   __syncthreads();
   const int64_t base = (b * L + l0) * M;
   const int64_t* meas = bt.dyn_meas + base;
@@ -88,10 +99,14 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
     for (int k = 0; k < kU; ++k) {
       const int i = i0 + k * stride;
       uint32_t bits = 0u;
-      for (int t = 0; t < T; ++t) {
-        const esgpt_loss_term& tm = terms.t[t];
-        if (tm.kind != ESGPT_TERM_MULTI && mi[k] == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vb[k] != 0))
-          bits |= 1u << t;
+      if (mi[k] >= 0 && mi[k] < kLut) {
+        bits = s_lut_any[mi[k]] | (vb[k] != 0 ? s_lut_val[mi[k]] : 0u);
+      } else {
+        for (int t = 0; t < T; ++t) {
+          const esgpt_loss_term& tm = terms.t[t];
+          if (tm.kind != ESGPT_TERM_MULTI && mi[k] == tm.meas_idx && (tm.kind == ESGPT_TERM_SINGLE || vb[k] != 0))
+            bits |= 1u << t;
+        }
       }
       if (i < NE && bits) atomicOr(&s_bits[i / Mi], bits);
     }
@@ -139,6 +154,38 @@ __device__ __forceinline__ float content_term(const esgpt_loss_term& tm, int lan
     if (mk && (lab < 0 || lab >= n)) {
       set_err(err, ESGPT_FLAG_BAD_LABEL);
       lab = 0;
+    }
+    constexpr int kR = 4;  // n <= 64·kR: the logits read once into registers (same arithmetic, same order)
+    if (n <= 64 * kR) {
+      float xs[kR], ex[kR];
+#pragma unroll
+      for (int k = 0; k < kR; ++k) xs[k] = lane + 64 * k < n ? z(tm.col + lane + 64 * k) : -INFINITY;
+      const float xl = z(tm.col + lab);
+      const float zo = z(tm.obs_col);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < kR; ++k)
+        if (lane + 64 * k < n) mx = fmaxf(mx, xs[k]);
+      mx = wave_max(mx);
+      float se = 0.f;
+#pragma unroll
+      for (int k = 0; k < kR; ++k) {
+        ex[k] = lane + 64 * k < n ? expf(xs[k] - mx) : 0.f;
+        if (lane + 64 * k < n) se += ex[k];
+      }
+      se = wave_sum(se);
+      const float lse = mx + logf(se);
+      ell = (lse - xl) + bce_logits(zo, has ? 1.f : 0.f);
+      if (scale != 0.f) {
+        const float inv = 1.f / se;
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          const int j = lane + 64 * k;
+          if (j < n) put(tm.col + j, scale * (ex[k] * inv - (j == lab ? 1.f : 0.f)));
+        }
+        if (lane == 0) put(tm.obs_col, scale * (sigmoidf_(zo) - (has ? 1.f : 0.f)));
+      }
+      return ell;
     }
     float mx = -INFINITY;
     for (int j = lane; j < n; j += 64) mx = fmaxf(mx, z(tm.col + j));
@@ -362,9 +409,11 @@ struct RowPos {
 __device__ __forceinline__ RowPos row_pos(const esgpt_batch& bt, int64_t w, int64_t n_rows, int shift) {
   RowPos q;
   q.active = w < n_rows;
-  const int64_t per_b = bt.L + shift;
-  q.b = q.active ? w / per_b : 0;
-  q.r = q.active ? (w % per_b) - shift : 0;
+  // 32-bit division: a 64-bit one is a long scalar instruction sequence per wave (n_rows < 2^31, host-checked)
+  const uint32_t per_b = (uint32_t)(bt.L + shift), wu = (uint32_t)w;
+  const uint32_t qb = wu / per_b;
+  q.b = q.active ? (int64_t)qb : 0;
+  q.r = q.active ? (int64_t)(wu - qb * per_b) - shift : 0;
   q.p = q.r + shift;
   q.has_content = q.active && q.p < bt.L;
   q.ev = q.has_content && bt.event_mask[q.b * bt.L + q.p] != 0;
@@ -642,6 +691,56 @@ __global__ __launch_bounds__(256) void event_lds_kernel(esgpt_batch bt, Terms te
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Deterministic sums of the per-row (or per-workgroup) contributions by one workgroup of NTh threads: thread i sums
+// items i, i + NTh, ... of each term, then wave sums and a fixed-order sum over the waves. The next term's loads are
+// issued before the current term is summed (one memory round trip per pass instead of one per term).
+template <int NTh>
+__device__ __forceinline__ void reduce_contrib(const float* __restrict__ contrib, int64_t n_rows, int NT,
+                                               float* __restrict__ losses) {
+  constexpr int NW = NTh / 64;
+  __shared__ float s[NW][ESGPT_MAX_TERMS + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  constexpr int kU = 8;  // items per thread and pass
+  for (int64_t i0 = 0; i0 < n_rows; i0 += kU * NTh) {
+    float cur[kU], nxt[kU];
+    auto load = [&](float (&v)[kU], int t) {
+      const float* c = contrib + (int64_t)min(t, NT) * n_rows;
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const int64_t i = i0 + threadIdx.x + (int64_t)k * NTh;
+        const float x = c[min(i, n_rows - 1)];
+        v[k] = i < n_rows ? x : 0.f;
+      }
+    };
+    load(cur, 0);
+    for (int t = 0; t <= NT; ++t) {
+      load(nxt, t + 1);  // clamped past the last term: a re-read, never used
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < kU; ++k) a += cur[k];
+      const float w = wave_sum(a);
+      if (lane == 0) s[wave][t] = (i0 == 0 ? 0.f : s[wave][t]) + w;
+#pragma unroll
+      for (int k = 0; k < kU; ++k) cur[k] = nxt[k];
+    }
+  }
+  __syncthreads();
+  // wave 0: lane t sums term t over the waves (the fixed order), then the total in term order from readlanes (no
+  // serial chain of LDS reads in one thread)
+  if (wave == 0) {
+    float v = 0.f;
+    if (lane <= NT) {
+      for (int w = 0; w < NW; ++w) v += s[w][lane];
+      v = (lane < NT) ? v : -v;  // last slot: -TTE_LL
+      losses[lane] = v;
+    }
+    float total = 0.f;
+    for (int t = 0; t <= NT; ++t) total += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), t));
+    if (lane == 0) losses[NT + 1] = total;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Streaming event kernel (the default): one wave per logit row and no whole-row staging, so occupancy is set by
 // registers, not by the row width — the row-staged kernel holds ldc·(s + 4) B of LDS per wave, which at C5
 // (ldc = 10,640) left ONE wave per workgroup and two per CU.
@@ -663,12 +762,17 @@ constexpr int kMaxRng = 8;       // narrow chunk ranges per level
 template <typename T>
 constexpr int max_narrow() { return sizeof(T) == 4 ? 128 : 96; }
 constexpr int kMaxLevels = 8;
+constexpr int kMap = 1, kSkipP1 = 2, kSkipP2 = 4, kSkipSub = 8, kSkipTte = 16, kSkipStore = 32, kTot = 64;
 
 struct StreamPlan {
   int8_t nseg[kMaxLevels];             // MULTI terms of the level, in term order
   int8_t seg[kMaxLevels][kMaxSeg];
   int8_t nrng[kMaxLevels];             // narrow chunk ranges [lo, hi) of the level; slot = base + c - lo
   int32_t lo[kMaxLevels][kMaxRng], hi[kMaxLevels][kMaxRng], base[kMaxLevels][kMaxRng];
+  int32_t max_slots;                   // narrow chunks of the widest level
+  // LDS element index of narrow column col = col + delta (a term's columns lie in one merged range): per term
+  // (its value columns, its is-observed column) and for the in-row TTE columns
+  int32_t dcol[ESGPT_MAX_TERMS], dobs[ESGPT_MAX_TERMS], dtte;
 };
 
 template <typename T>
@@ -706,50 +810,33 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
                                                            T* __restrict__ dzt, float* __restrict__ dbias,
                                                            const int32_t* __restrict__ counts, int n_ch,
                                                            float* __restrict__ contrib, int64_t n_rows, int tte_in_row,
-                                                           int32_t* __restrict__ err) {
+                                                           int32_t* __restrict__ err, int flags) {
   constexpr int kEl = 16 / sizeof(T);  // elements per 16-B chunk
   constexpr int kB = 4;                // chunk groups (64 chunks each) in flight
+  // Dynamic LDS: [narrow logits: 4 waves x S uint4][narrow f32 gradients: 4 x S x kEl][per-subject counts: B x (NT+1)
+  // int32, kTot][chunk -> narrow slot map of every level, int16 (-1: not narrow), kMap]. The map replaces a scan of
+  // the level's ranges per narrow access; the counts replace per-wave chains of loads over the count partials.
+  extern __shared__ __align__(16) unsigned char s_dyn[];
   __shared__ float s_nsub_inv[ESGPT_MAX_TERMS + 1];
-  constexpr int kNarrow = max_narrow<T>();
-  __shared__ uint4 s_nz[4][kNarrow];        // narrow chunks: logits
-  __shared__ float s_ng[4][kNarrow * kEl];  // narrow chunks: f32 gradients
+  const int S = plan.max_slots;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = lane_id();
-  const int NT = terms.n;
+  const int NT = terms.n, nt1 = NT + 1;
   const int64_t L = bt.L, M = bt.M;
   const int nch = (int)(ldc / kEl);  // < 2^31 (checked on the host)
-  const T* nzT = reinterpret_cast<const T*>(s_nz[wave]);
-  float* ng = s_ng[wave];
+  const bool use_map = flags & kMap, use_tot = flags & kTot;
+  uint4* s_nz = reinterpret_cast<uint4*>(s_dyn) + wave * S;
+  float* ng = reinterpret_cast<float*>(s_dyn + (size_t)4 * S * 16) + wave * S * kEl;
+  int32_t* s_tot = reinterpret_cast<int32_t*>(s_dyn + (size_t)4 * S * 16 + (size_t)4 * S * kEl * 4);
+  int16_t* s_slot = reinterpret_cast<int16_t*>(s_tot + (use_tot ? bt.B * nt1 : 0));
+  const T* nzT = reinterpret_cast<const T*>(s_nz);
 
-  if (wave == 0) subjects_with_events(counts, bt.B, n_ch, NT, lane, s_nsub_inv);
   const int64_t w = (int64_t)blockIdx.x * 4 + wave;
   const RowPos q = row_pos(bt, w, n_rows, shift);
   const int64_t b = q.b, r = q.r, p = q.p;
-
-  int64_t e_idx = 0, e_meas = INT64_MIN;
-  float e_val = 0.f;
-  bool e_vm = false;
-  if (q.has_content && lane < M) {
-    const int64_t off = (b * L + p) * M + lane;
-    e_idx = bt.dyn_idx[off];
-    e_meas = bt.dyn_meas[off];
-    e_val = bt.dyn_vals[off];
-    e_vm = bt.dyn_vmask[off] != 0;
-  }
-  const int32_t my_cnt = subject_counts(counts, b, n_ch, NT, lane, q.active);
-  flag_no_tte(my_cnt, NT, q.active && q.r == -shift, err);
-  const bool tte_row = q.active && r >= 0;
-  const int64_t e = b * L + (r < 0 ? 0 : r);
-  const bool obs = tte_row && (r + 1 < L) && bt.event_mask[e] && bt.event_mask[e + 1];
-  const float x_tte = obs ? bt.time_delta[e] : 1.f;
-  __syncthreads();  // s_nsub_inv
-
-  float cvec = 0.f;  // lane t: term t's contribution (lane NT: the TTE log-likelihood's)
-  const int n_lv = !q.active ? 0 : shift ? 1 : (int)n_levels;
-  for (int lv = 0; lv < n_lv; ++lv) {
-    const T* zrow;
-    T* grow = nullptr;
-    float* frow = nullptr;
+  // the logit / gradient rows of level lv
+  auto rows = [&](int lv, const T*& zrow, T*& grow, float*& frow) {
+    grow = nullptr, frow = nullptr;
     if (shift) {
       if (r < 0) {
         zrow = zc_bias;
@@ -763,14 +850,101 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
       zrow = zc + row * ldc;
       grow = dzc + row * ldc;
     }
+  };
+  // the first chunk groups of the first row, issued before the setup so their latency overlaps it
+  uint4 v[kB];
+  auto load_group = [&](const uint4* zv, int g0) {
+#pragma unroll
+    for (int i = 0; i < kB; ++i) {
+      const int c = g0 + 64 * i + lane;
+      v[i] = zv[c < nch ? c : nch - 1];  // unconditional: all kB loads in flight together
+    }
+  };
+  if (q.active) {
+    const T* z0;
+    T* g0;
+    float* f0;
+    rows(0, z0, g0, f0);
+    load_group(reinterpret_cast<const uint4*>(z0), 0);
+  }
+
+  // flags: kMap / kTot as above; bits 1..5 = sections skipped (tools build only, ESGPT_LOSS_SKIP: the per-section
+  // instruction counts; results are then wrong)
+  int64_t e_idx = 0, e_meas = INT64_MIN;
+  float e_val = 0.f;
+  bool e_vm = false;
+  if (q.has_content && lane < M) {
+    const int64_t off = (b * L + p) * M + lane;
+    e_idx = bt.dyn_idx[off];
+    e_meas = bt.dyn_meas[off];
+    e_val = bt.dyn_vals[off];
+    e_vm = bt.dyn_vmask[off] != 0;
+  }
+  const bool tte_row = q.active && r >= 0;
+  const int64_t e = b * L + (r < 0 ? 0 : r);
+  const int64_t e1 = min(e + 1, bt.B * L - 1);  // every load issued together (clamped; used only when r + 1 < L)
+  const bool em0 = bt.event_mask[e] != 0, em1 = bt.event_mask[e1] != 0;
+  const float td = bt.time_delta[e];
+  const bool obs = tte_row && (r + 1 < L) && em0 && em1;
+  const float x_tte = obs ? td : 1.f;
+
+  if (use_tot) {  // per-subject counts: thread = (subject, term), its chunk partials summed, loads in flight together
+    const int n_tot = (int)bt.B * nt1;
+    for (int i = threadIdx.x; i < n_tot; i += 256) {
+      const int bb = i / nt1, t = i - bb * nt1;
+      const int32_t* src = counts + (int64_t)bb * n_ch * (ESGPT_MAX_TERMS + 1) + t;  // slot NT: observed TTEs
+      int32_t c = 0;
+#pragma unroll 8
+      for (int ch = 0; ch < n_ch; ++ch) c += src[(int64_t)ch * (ESGPT_MAX_TERMS + 1)];
+      s_tot[i] = c;
+    }
+  } else if (wave == 0 && !(flags & kSkipSub)) {
+    subjects_with_events(counts, bt.B, n_ch, NT, lane, s_nsub_inv);
+  }
+  if (wave == 0 && (flags & kSkipSub) && lane <= NT) s_nsub_inv[lane] = 1.f;
+  if (use_map) {
+    const int n_lvm = shift ? 1 : (int)n_levels;
+    for (int lv = 0; lv < n_lvm; ++lv)
+      for (int c = threadIdx.x; c < nch; c += 256) {
+        int sl = -1;
+        for (int k = 0; k < plan.nrng[lv]; ++k)
+          if (c >= plan.lo[lv][k] && c < plan.hi[lv][k]) sl = plan.base[lv][k] + c - plan.lo[lv][k];
+        s_slot[lv * nch + c] = (int16_t)sl;
+      }
+  }
+  __syncthreads();  // s_tot / s_nsub_inv, s_slot
+
+  // lane t <= NT: 1 / subjects-with-events of term t (lane NT: 1 / B), and this subject's count of term t
+  float nsinv;
+  int32_t my_cnt = 0;
+  if (use_tot) {
+    int nsub = 0;
+    for (int64_t b0 = 0; b0 < bt.B; b0 += 64) {
+      const int64_t bb = b0 + lane;
+      for (int t = 0; t < NT; ++t) {
+        const int n = __popcll(__ballot(bb < bt.B && s_tot[bb * nt1 + t] > 0));
+        if (lane == t) nsub += n;
+      }
+    }
+    nsinv = lane < NT ? (nsub > 0 ? 1.f / (float)nsub : 0.f) : 1.f / (float)bt.B;
+    if ((flags & kSkipSub)) nsinv = 1.f;
+    if (q.active && lane <= NT) my_cnt = s_tot[b * nt1 + lane];
+  } else {
+    nsinv = lane <= NT ? s_nsub_inv[lane] : 0.f;
+    my_cnt = subject_counts(counts, b, n_ch, NT, lane, q.active);
+  }
+  auto nsub_inv = [&](int t) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(nsinv), t)); };
+  flag_no_tte(my_cnt, NT, q.active && q.r == -shift, err);
+
+  float cvec = 0.f;  // lane t: term t's contribution (lane NT: the TTE log-likelihood's)
+  const int n_lv = !q.active ? 0 : shift ? 1 : (int)n_levels;
+  for (int lv = 0; lv < n_lv; ++lv) {
+    const T* zrow;
+    T* grow;
+    float* frow;
+    rows(lv, zrow, grow, frow);
     const int nr = plan.nrng[lv];
-    // narrow slot of chunk c (-1: not narrow)
-    auto slot_of = [&](int c) {
-      int s = -1;
-      for (int k = 0; k < nr; ++k)
-        if (c >= plan.lo[lv][k] && c < plan.hi[lv][k]) s = plan.base[lv][k] + c - plan.lo[lv][k];
-      return s;
-    };
+    const int16_t* lv_slot = s_slot + lv * nch;  // narrow slot of chunk c (-1: not narrow)
 
     // ---------------- MULTI range parameters ----------------
     const int nseg = plan.nseg[lv];
@@ -785,7 +959,7 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
         const int n = tm.vocab_end - tm.vocab_start;
         const bool match = e_meas == tm.meas_idx;
         const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
-        const float scale = (q.ev && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
+        const float scale = (q.ev && cnt > 0) ? nsub_inv(t) / (float)cnt : 0.f;
         sc[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(scale)));  // wave-uniform
         sn[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(scale / (float)n)));
         const int64_t my_lab = match ? e_idx - tm.vocab_start : -1;
@@ -796,12 +970,7 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
     // ---------------- pass 1: stream the row ----------------
     const uint4* zv = reinterpret_cast<const uint4*>(zrow);
     for (int g0 = 0; g0 < nch; g0 += 64 * kB) {
-      uint4 v[kB];
-#pragma unroll
-      for (int i = 0; i < kB; ++i) {
-        const int c = g0 + 64 * i + lane;
-        v[i] = zv[c < nch ? c : nch - 1];  // unconditional: all kB loads in flight together
-      }
+      if (lv > 0 || g0 > 0) load_group(zv, g0);  // the first group was issued before the setup
 #pragma unroll
       for (int i = 0; i < kB; ++i) {
         const int gb = g0 + 64 * i;  // wave-uniform
@@ -813,7 +982,7 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
         for (int el = 0; el < kEl; ++el) o[el] = 0.f;
 #pragma unroll
         for (int k = 0; k < kMaxSeg; ++k) {
-          if (k >= nseg || sn[k] == 0.f) continue;  // wave-uniform
+          if (k >= nseg || sn[k] == 0.f || (flags & kSkipP1)) continue;  // wave-uniform
           const esgpt_loss_term& tm = terms.t[plan.seg[lv][k]];
           const int lo = tm.col, hi = tm.col + tm.vocab_end - tm.vocab_start;
           if (lo >= ghi || hi <= glo) continue;
@@ -842,11 +1011,15 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
           acc[k] += a;
         }
         int slot = -1;
-        for (int k = 0; k < nr; ++k)
-          if (plan.lo[lv][k] < gb + 64 && plan.hi[lv][k] > gb && c >= plan.lo[lv][k] && c < plan.hi[lv][k])
-            slot = plan.base[lv][k] + c - plan.lo[lv][k];
+        if (use_map) {
+          slot = c < nch ? (int)lv_slot[c] : -1;
+        } else {
+          for (int k = 0; k < nr; ++k)
+            if (plan.lo[lv][k] < gb + 64 && plan.hi[lv][k] > gb && c >= plan.lo[lv][k] && c < plan.hi[lv][k])
+              slot = plan.base[lv][k] + c - plan.lo[lv][k];
+        }
         if (slot >= 0) {  // narrow chunk: logits and gradients so far to LDS, stored after pass 2
-          s_nz[wave][slot] = v[i];
+          s_nz[slot] = v[i];
 #pragma unroll
           for (int el = 0; el < kEl; ++el) ng[slot * kEl + el] = o[el];
         } else if (c < nch) {
@@ -874,9 +1047,7 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     // ---------------- pass 2: the narrow terms, from LDS ----------------
-    auto nz = [&](int col) { return to_f32(nzT[slot_of(col / kEl) * kEl + col % kEl]); };
-    auto put = [&](int col, float g) { ng[slot_of(col / kEl) * kEl + col % kEl] = g; };
-    for (int t = 0; t < NT && q.has_content; ++t) {
+    for (int t = 0; t < NT && q.has_content && !(flags & kSkipP2); ++t) {
       const esgpt_loss_term& tm = terms.t[t];
       if (tm.kind == ESGPT_TERM_MULTI) continue;
       if (!shift && tm.level != lv) continue;  // wave-uniform
@@ -884,17 +1055,21 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
       const uint64_t mm = __ballot(match), mv = __ballot(match && e_vm);
       const bool mk = q.ev && (tm.kind == ESGPT_TERM_SINGLE ? mm != 0 : mv != 0);
       const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, t);
-      const float scale = (mk && cnt > 0) ? s_nsub_inv[t] / (float)cnt : 0.f;
+      const float scale = (mk && cnt > 0) ? nsub_inv(t) / (float)cnt : 0.f;
       if (scale == 0.f) continue;  // contribution 0, gradients 0 (already in LDS)
-      const float ell =
-          content_term(tm, lane, M, match, mm, mv, e_idx, e_val, e_vm, mk, scale, err, nz, put);
+      const int dc = plan.dcol[t], dob = plan.dobs[t], ocol = tm.obs_col;
+      const float ell = content_term(
+          tm, lane, M, match, mm, mv, e_idx, e_val, e_vm, mk, scale, err,
+          [&](int col) { return to_f32(nzT[col + (col == ocol ? dob : dc)]); },
+          [&](int col, float g) { ng[col + (col == ocol ? dob : dc)] = g; });
       if (lane == t) cvec = scale * ell;
     }
-    if (tte_in_row && lv == 0 && tte_row) {
+    if (tte_in_row && lv == 0 && tte_row && !(flags & kSkipTte)) {
       const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
-      const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;
+      const float scale = (obs && cnt > 0) ? -nsub_inv(NT) / (float)cnt : 0.f;
       const float ll = tte_term(
-          tte, lane, x_tte, scale, [&](int k) { return nz(tte.col + k); }, [&](int k, float g) { put(tte.col + k, g); });
+          tte, lane, x_tte, scale, [&](int k) { return to_f32(nzT[tte.col + k + plan.dtte]); },
+          [&](int k, float g) { ng[tte.col + k + plan.dtte] = g; });
       if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
       if (lane == NT) cvec = obs ? -scale * ll : 0.f;
     }
@@ -902,7 +1077,7 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // ---- the narrow chunks ----
-    for (int k = 0; k < nr; ++k) {
+    for (int k = 0; k < nr && !(flags & kSkipStore); ++k) {
       const int lo = plan.lo[lv][k], n = plan.hi[lv][k] - lo, base = plan.base[lv][k];
       for (int j = lane; j < n; j += 64) {
         float o[kEl];
@@ -926,14 +1101,16 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
     const T* z = zt + e * ldt + tte.col;
     T* gz = dzt + e * ldt + tte.col;
     const int32_t cnt = __builtin_amdgcn_readlane(my_cnt, NT);
-    const float scale = (obs && cnt > 0) ? -s_nsub_inv[NT] / (float)cnt : 0.f;
+    const float scale = (obs && cnt > 0) ? -nsub_inv(NT) / (float)cnt : 0.f;
     const float ll = tte_term(
         tte, lane, x_tte, scale, [&](int k) { return to_f32(z[k]); },
         [&](int k, float g) { gz[k] = from_f32<T>(g); });
     if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
     if (lane == NT) cvec = obs ? -scale * ll : 0.f;
   }
-  // the workgroup's contributions: rows in order, summed in a fixed order (deterministic)
+  // the workgroup's contributions: rows in order, summed in a fixed order (deterministic). (A last-arriver fold
+  // of reduce_kernel into this launch was measured at C2: the agent-scope release each workgroup then needs
+  // writes back its XCD's L2, full of dirty gradient rows — 56 -> 100 us.)
   __shared__ float s_part[4][ESGPT_MAX_TERMS + 1];
   if (lane <= NT) s_part[wave][lane] = cvec;
   __syncthreads();
@@ -942,52 +1119,11 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
         ((s_part[0][lane] + s_part[1][lane]) + s_part[2][lane]) + s_part[3][lane];
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// Deterministic sums of the per-row contributions: thread i sums rows i, i + 1024, ... of each term, then wave sums
-// and a fixed-order sum over the 16 waves. The next term's loads are issued before the current term is summed (one
-// memory round trip for the whole launch instead of one per term at n_rows <= 8192).
+
+// The other two event kernels' contributions (per row), summed by one workgroup.
 __global__ __launch_bounds__(1024) void reduce_kernel(const float* __restrict__ contrib, int64_t n_rows, int NT,
                                                       float* __restrict__ losses) {
-  __shared__ float s[16][ESGPT_MAX_TERMS + 1];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  constexpr int kU = 8;  // rows per thread and pass
-  for (int64_t i0 = 0; i0 < n_rows; i0 += kU * 1024) {
-    float cur[kU], nxt[kU];
-    auto load = [&](float (&v)[kU], int t) {
-      const float* c = contrib + (int64_t)min(t, NT) * n_rows;
-#pragma unroll
-      for (int k = 0; k < kU; ++k) {
-        const int64_t i = i0 + threadIdx.x + (int64_t)k * 1024;
-        const float x = c[min(i, n_rows - 1)];
-        v[k] = i < n_rows ? x : 0.f;
-      }
-    };
-    load(cur, 0);
-    for (int t = 0; t <= NT; ++t) {
-      load(nxt, t + 1);  // clamped past the last term: a re-read, never used
-      float a = 0.f;
-#pragma unroll
-      for (int k = 0; k < kU; ++k) a += cur[k];
-      const float w = wave_sum(a);
-      if (lane == 0) s[wave][t] = (i0 == 0 ? 0.f : s[wave][t]) + w;
-#pragma unroll
-      for (int k = 0; k < kU; ++k) cur[k] = nxt[k];
-    }
-  }
-  __syncthreads();
-  // wave 0: lane t sums term t over the 16 waves (w = 0..15, the fixed order), then the total in term order from
-  // readlanes (no serial chain of LDS reads in one thread)
-  if (wave == 0) {
-    float v = 0.f;
-    if (lane <= NT) {
-      for (int w = 0; w < 16; ++w) v += s[w][lane];
-      v = (lane < NT) ? v : -v;  // last slot: -TTE_LL
-      losses[lane] = v;
-    }
-    float total = 0.f;
-    for (int t = 0; t <= NT; ++t) total += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), t));
-    if (lane == 0) losses[NT + 1] = total;
-  }
+  reduce_contrib<1024>(contrib, n_rows, NT, losses);
 }
 
 // True when no two terms write the same gradient column of one logit row (the event kernel then stores instead of
@@ -1013,7 +1149,8 @@ bool disjoint_columns(const esgpt_loss_term* terms, int n_terms, int shift) {
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 constexpr int64_t kLdsBudget = 64 * 1024;  // row-staged event kernel: LDS bytes per block
-constexpr int kCountChunk = 128;           // events per count_kernel workgroup
+constexpr int kCountChunk = 32;            // events per count_kernel workgroup (C2: 256 workgroups)
+constexpr int kCountThreads = 256;
 
 // The streaming kernel's plan per level: MULTI terms as dense ranges (<= kMaxSeg); the 16-B chunks touching any other
 // term column (SINGLE slices, is-observed, regression, in-row TTE) as merged chunk ranges (<= kMaxRng ranges,
@@ -1060,6 +1197,21 @@ bool stream_plan(const esgpt_loss_term* terms, int n_terms, int64_t n_levels, in
     }
     if (slots > max_slots) return false;
     plan.nrng[lv] = (int8_t)merged.size();
+    auto delta = [&](int64_t col) -> int32_t {
+      const int64_t ck = col / kEl;
+      for (size_t k = 0; k < merged.size(); ++k)
+        if (ck >= merged[k].first && ck < merged[k].second)
+          return (int32_t)((plan.base[lv][k] - merged[k].first) * kEl);
+      return 0;  // not reached: every narrow column was inserted above
+    };
+    for (int i = 0; i < n_terms; ++i) {
+      const esgpt_loss_term& t = terms[i];
+      if ((shift ? 0 : t.level) != lv || t.kind == ESGPT_TERM_MULTI) continue;
+      plan.dcol[i] = delta(t.col);
+      if (t.kind == ESGPT_TERM_SINGLE || t.kind == ESGPT_TERM_UVREG) plan.dobs[i] = delta(t.obs_col);
+    }
+    if (tte_in_row && lv == 0) plan.dtte = delta(tte.col);
+    plan.max_slots = std::max<int32_t>(plan.max_slots, (int32_t)std::max<int64_t>(slots, 1));
   }
   return true;
 }
@@ -1087,6 +1239,7 @@ int esgpt_output_loss_ex(const esgpt_batch* batch, const void* zc, int64_t ldc, 
   ESGPT_REQUIRE(path >= ESGPT_LOSS_PATH_AUTO && path <= ESGPT_LOSS_PATH_GENERIC);
   ESGPT_REQUIRE(workspace_bytes >= esgpt_output_loss_workspace(batch->B, batch->L, n_terms));
   ESGPT_REQUIRE(batch->L <= 16384 && batch->L * batch->M < (1ll << 31));  // count_kernel: LDS word per event
+  ESGPT_REQUIRE(batch->B * (batch->L + 1) < (1ll << 31));                // row_pos: 32-bit row indices
   const int64_t B = batch->B, L = batch->L;
   if (B == 0 || L == 0) return ESGPT_ERR_INVALID_ARG;
   hipStream_t st = as_stream(stream);
@@ -1123,22 +1276,32 @@ int esgpt_output_loss_ex(const esgpt_batch* batch, const void* zc, int64_t ldc, 
   }
   if (!tte_in_row && (dzt != dzc || n_terms == 0 || whole) && zero_async(dzt, esz * B * L * ldt, st) != hipSuccess)
     return ESGPT_ERR_LAUNCH;
-  count_kernel<<<dim3((unsigned)n_ch, (unsigned)B), 1024, sizeof(uint32_t) * kCountChunk, st>>>(*batch, T, kCountChunk,
-                                                                                           counts);
+  count_kernel<<<dim3((unsigned)n_ch, (unsigned)B), kCountThreads, sizeof(uint32_t) * kCountChunk, st>>>(
+      *batch, T, kCountChunk, counts);
   int64_t n_items = n_rows;  // contributions per term (rows, or workgroups of the streaming kernel)
   if (use == ESGPT_LOSS_PATH_STREAM) {
     const unsigned grid = (unsigned)cdiv(n_rows, 4);
     n_items = grid;
+    // dynamic LDS: the narrow chunks of 4 waves, then the per-subject counts and the chunk -> slot map when they fit
+    const size_t eb = 16 + sizeof(float) * kEl;  // bytes per narrow chunk: logits + f32 gradients
+    const size_t narrow_bytes = 4 * (size_t)plan.max_slots * eb;
+    const size_t tot_bytes = sizeof(int32_t) * (size_t)B * (n_terms + 1);
+    const size_t map_bytes = sizeof(int16_t) * (size_t)(shift ? 1 : n_levels) * (size_t)(ldc / kEl);
+    const bool use_tot = tot_bytes <= 8192;
+    const bool use_map = narrow_bytes + (use_tot ? tot_bytes : 0) + map_bytes <= 32768;
+    const size_t dyn = narrow_bytes + (use_tot ? tot_bytes : 0) + (use_map ? map_bytes : 0);
+    const char* skip = tuning_env("ESGPT_LOSS_SKIP");  // tools build only
+    const int flags = (use_map ? kMap : 0) | (use_tot ? kTot : 0) | (skip ? ((atoi(skip) << 1) & 62) : 0);
     if (dtype == ESGPT_F32)
-      event_stream_kernel<float><<<grid, 256, 0, st>>>(*batch, T, plan, *tte, (const float*)zc, ldc, n_levels, shift,
-                                                       (const float*)zc_bias, (const float*)zt, ldt, (float*)dzc,
-                                                       (float*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
-                                                       err);
+      event_stream_kernel<float><<<grid, 256, dyn, st>>>(*batch, T, plan, *tte, (const float*)zc, ldc, n_levels, shift,
+                                                         (const float*)zc_bias, (const float*)zt, ldt, (float*)dzc,
+                                                         (float*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
+                                                         err, flags);
     else
-      event_stream_kernel<bf16><<<grid, 256, 0, st>>>(*batch, T, plan, *tte, (const bf16*)zc, ldc, n_levels, shift,
-                                                      (const bf16*)zc_bias, (const bf16*)zt, ldt, (bf16*)dzc,
-                                                      (bf16*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
-                                                      err);
+      event_stream_kernel<bf16><<<grid, 256, dyn, st>>>(*batch, T, plan, *tte, (const bf16*)zc, ldc, n_levels, shift,
+                                                        (const bf16*)zc_bias, (const bf16*)zt, ldt, (bf16*)dzc,
+                                                        (bf16*)dzt, dbias, counts, n_ch, contrib, n_rows, tte_in_row,
+                                                        err, flags);
   } else if (use == ESGPT_LOSS_PATH_ROW_STAGED) {
     const int wpb = (int)std::min<int64_t>(kWaves, kLdsBudget / per_wave);
     const unsigned grid = (unsigned)cdiv(n_rows, wpb);
