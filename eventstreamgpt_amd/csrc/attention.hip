@@ -3,11 +3,11 @@
 // Three implementations behind one entry point:
 //   * attn_*_generic  — one lane per query (forward, dQ) or per key (dK/dV), f32 arithmetic, any head dim up to
 //     128, f32 or bf16 I/O. Lanes of a wave hold consecutive queries of one (batch, head), so every K/V (or Q/dO)
-//     row load in the key loop is wave-uniform (a broadcast). Used for the f32 parity mode and for sequences
-//     longer than 16 without an MFMA path.
+//     row load in the key loop is wave-uniform (a broadcast). Used for head dims / layouts without an MFMA path.
 //   * attn_*_small — Lk <= 16 (the NA model's dependency-graph sequences, Lk = G + 1): one wave per (sequence,
 //     head), lane = head dimension, K / V in registers, one fused backward pass.
-//   * attn_*_mfma (attention_mfma.hip) — bf16 v_mfma_f32_32x32x16_bf16 flash kernels for hd in {32, 64, 128}.
+//   * attn_*_mfma (attention_mfma.hip) — bf16 v_mfma_f32_32x32x16_bf16 flash kernels for hd in {16, 32, 64, 128};
+//     attn_*_f32 (attention_f32.hip) — the f32 path on v_mfma_f32_32x32x2_f32 (exact f32), same head dims.
 //
 // Semantics (all): s_ij = q_i . k_j in f32 with NO 1/sqrt(hd) scaling; key j is visible to query i (at key
 // position p_i = i + Lk - Lq) iff j <= p_i, (local) p_i - j < window, and key_mask[j]; softmax in f32; the
@@ -747,6 +747,17 @@ int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
 int64_t esgpt_attn_bwd_mfma_counters(int64_t B, int64_t H, int64_t Lk);
 bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o);
+// f32 MFMA path (attention_f32.hip).
+bool esgpt_attn_f32_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t ld_in, int64_t ld_o);
+int esgpt_attn_fwd_f32_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o,
+                            int64_t ld_o, float* lse, const uint8_t* kmask, const uint8_t* qmask, int64_t B, int64_t H,
+                            int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                            hipStream_t st);
+int esgpt_attn_bwd_f32_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                            int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
+                            const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
+                            int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                            float* delta, hipStream_t st);
 
 static int g_force_generic = -1;
 
@@ -796,6 +807,11 @@ int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return esgpt_attn_fwd_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
                                dropout_p, seed, keep, st);
+  if (dtype == ESGPT_F32 && !force_generic() && esgpt_attn_f32_mfma_supported(hd, Lq, Lk, ld_in, ld_o)) {
+    const int rc = esgpt_attn_fwd_f32_mfma(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd,
+                                           window, dropout_p, seed, st);
+    if (rc != ESGPT_ERR_UNSUPPORTED) return rc;  // unaligned operands: the generic kernels
+  }
   if (Lk <= kSmallLk && !force_generic()) {
     if (dtype == ESGPT_F32)
       return launch_small<float>(true, q, k, v, ld_in, tq, o, ld_o, lse, nullptr, nullptr, 0, key_mask, query_mask,
@@ -813,6 +829,8 @@ int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
 int esgpt_attn_path(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o, int dtype) {
   if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
     return ESGPT_ATTN_PATH_MFMA;
+  if (dtype == ESGPT_F32 && !force_generic() && esgpt_attn_f32_mfma_supported(hd, Lq, Lk, ld_in, ld_o))
+    return ESGPT_ATTN_PATH_MFMA_F32;  // (16-B aligned operands; otherwise the launch takes the generic kernels)
   if (Lk <= kSmallLk && !force_generic()) return ESGPT_ATTN_PATH_SMALL;
   return ESGPT_ATTN_PATH_GENERIC;
 }
@@ -855,6 +873,11 @@ int esgpt_attn_bwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
     return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
                                ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, keep, (float*)workspace,
                                counters, st);
+  if (dtype == ESGPT_F32 && !force_generic() && esgpt_attn_f32_mfma_supported(hd, Lq, Lk, ld_in, ld_o)) {
+    const int rc = esgpt_attn_bwd_f32_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq,
+                                           dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);
+    if (rc != ESGPT_ERR_UNSUPPORTED) return rc;
+  }
   if (Lk <= kSmallLk && !force_generic()) {
     if (dtype == ESGPT_F32)
       return launch_small<float>(false, q, k, v, ld_in, tq, o, ld_o, nullptr, lse, dout, ld_do, key_mask, query_mask,

@@ -148,10 +148,12 @@ int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
 size_t esgpt_attn_bwd_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd);
 /* The kernel family esgpt_attn_fwd / esgpt_attn_bwd launch for these arguments (labels for measurements): MFMA
  * (attn_fwd_mfma_kernel / attn_bwd_kernel: bf16, hd in {16, 32, 64, 128}, Lk >= 16), SMALL (one wave per (sequence,
- * head), Lk <= 16: the dependency graph) or GENERIC (lane-per-query VALU kernels: f32, other head dims). */
+ * head), Lk <= 16: the dependency graph), MFMA_F32 (f32 operands, exact-f32 MFMA) or GENERIC (lane-per-query VALU
+ * kernels: other head dims, unaligned operands). */
 #define ESGPT_ATTN_PATH_GENERIC 0
 #define ESGPT_ATTN_PATH_MFMA 1
 #define ESGPT_ATTN_PATH_SMALL 2
+#define ESGPT_ATTN_PATH_MFMA_F32 3 /* attn_*_f32_kernel: f32, hd in {16, 32, 64, 128}, Lk > 16, v_mfma_f32_32x32x2_f32 */
 int esgpt_attn_path(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o, int dtype);
 /* Backward exchange tickets: the MFMA backward runs two workgroups per key block (even / odd query tiles) that add
  * their partial dK / dV through the workspace; `counters` (esgpt_attn_bwd_counters(B, H, Lk) int32, zeroed once
