@@ -1108,9 +1108,10 @@ __global__ __launch_bounds__(256) void event_stream_kernel(esgpt_batch bt, Terms
     if (isnan(ll)) set_err(err, ESGPT_FLAG_TTE_NAN);
     if (lane == NT) cvec = obs ? -scale * ll : 0.f;
   }
-  // the workgroup's contributions: rows in order, summed in a fixed order (deterministic). (A last-arriver fold
-  // of reduce_kernel into this launch was measured at C2: the agent-scope release each workgroup then needs
-  // writes back its XCD's L2, full of dirty gradient rows — 56 -> 100 us.)
+  // the workgroup's contributions: rows in order, summed in a fixed order (deterministic). (Folding reduce_kernel
+  // into this launch as a last-arriver sum was measured at C2 and rejected: with __threadfence releases, which
+  // write back the XCD's L2 full of dirty gradient rows, 56 -> 100 us; with the write-through hand-off of common.h,
+  // 53.7 + 4.5 -> 60.8 us, the last workgroup's serial sum of 2048 x 7 write-through contributions.)
   __shared__ float s_part[4][ESGPT_MAX_TERMS + 1];
   if (lane <= NT) s_part[wave][lane] = cvec;
   __syncthreads();
