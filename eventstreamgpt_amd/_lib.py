@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("ESGPT_AMD_LIB", os.path.join(_HERE, "libesgpt_amd.so"
 
 ESGPT_OK, ESGPT_ERR_INVALID_ARG, ESGPT_ERR_LAUNCH, ESGPT_ERR_UNSUPPORTED = 0, 1, 2, 3
 F32, BF16 = 0, 1
-FLAG_BAD_INDEX, FLAG_TTE_NAN, FLAG_TTE_NO_OBS, FLAG_BAD_LABEL = 1, 2, 4, 8
+FLAG_BAD_INDEX, FLAG_TTE_NAN, FLAG_TTE_NO_OBS, FLAG_BAD_LABEL, FLAG_PEER_RANK = 1, 2, 4, 8, 16
 EMB_NORMALIZE, EMB_STATIC, EMB_TIME, EMB_CUMSUM, EMB_TIME_ABS = 1, 2, 4, 8, 16
 BAG_JOINT, BAG_CAT, BAG_NUM = 0, 1, 2
 TERM_SINGLE, TERM_MULTI, TERM_MVREG, TERM_UVREG = 1, 2, 3, 4

@@ -140,6 +140,9 @@ def raise_for_error(code: int, max_index: int, n_total_embeddings: int | None = 
         raise ValueError(f"No observed time-to-event for >= 1 patient in batch{tail}")
     if code & L.FLAG_BAD_LABEL:
         raise IndexError("Target out of bounds in classification / regression labels")
+    if code & L.FLAG_PEER_RANK:
+        raise RuntimeError("eventstreamgpt_amd: a device error on another data-parallel rank in this step (its "
+                           "exception is raised there); this rank skipped the step's update with it")
     raise RuntimeError(f"eventstreamgpt_amd: unknown device error flags {code:#x}")
 
 

@@ -15,7 +15,9 @@
   latest when step k + 2 is submitted (the host never waits for the step it just queued), ``check()`` at once; the
   AdamW and LR-schedule counters of step k and of the discarded later steps are rolled back, and the block
   (sticky word included) is cleared, before the raise;
-* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI). Every ``param.grad`` ends
+* data parallelism: one process per GPU (``torch.distributed`` "nccl" = RCCL over xGMI); a device error on any rank
+  is a collective decision carried by the gradient exchange (GradBuckets): every rank skips the step and raises.
+  Every ``param.grad`` ends
   the step as a view into one flat f32 buffer laid out last-layer-first and cut into buckets; every step issues
   exactly one all-reduce (average) per bucket, in bucket-index order on every rank, whichever path (eager, graph
   capture, graph replay) the rank takes. A bucket is launched as soon as backward has produced its gradients and
@@ -43,6 +45,7 @@ from .data.types import PytorchBatch
 from .kernels import (begin_dropout_step, check_errors, colsum_deferral_active, deferred_colsums,
                       end_dropout_step, err_word, flush_colsums, join_weight_grads, raise_for_error,
                       weight_grad_overlap, weight_grad_overlap_active)
+from ._lib import FLAG_PEER_RANK
 from .transformer.config import OptimizationConfig
 
 
@@ -177,16 +180,25 @@ class GradBuckets:
       "off"     nothing (graph warm-up passes: no collectives).
     ``finish()`` launches the buckets not yet launched (zero-filling gradients that were never produced), in index
     order, waits for every exchange on the current stream, and leaves every ``param.grad`` a view of the buffer
-    (what FusedAdamW reads)."""
+    (what FusedAdamW reads).
 
-    def __init__(self, params: list, world: int, bucket_mb: float = 25.0):
+    Device errors are a collective decision (``err_check``): one f32 slot past the last gradient rides in the last
+    bucket, set by each rank to 1 when its step raised a device error flag; after the exchange it is non-zero on
+    every rank iff some rank failed, and each rank ORs ESGPT_FLAG_PEER_RANK into its error block — so every rank's
+    AdamW skips the step and every rank raises at the same step (the failing rank its own exception, the others
+    RuntimeError), instead of the healthy ranks running on into a collective the failing rank never joins. No
+    extra collective: the flag travels with the gradients."""
+
+    def __init__(self, params: list, world: int, bucket_mb: float = 25.0, err_check: bool = False):
         self.params = params
         self.world = world
         dev = params[0].device
         self.avg = dist.get_backend() == "nccl"  # RCCL has ncclAvg; gloo sums (divided afterwards)
+        self.err_check = err_check and dev.type == "cuda"
         order = list(reversed(range(len(params))))
         total = sum(params[i].numel() for i in order)
-        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.flat = torch.zeros(total + 1, dtype=torch.float32, device=dev)
+        self.slot = self.flat[total:]  # the any-rank-failed flag (last bucket)
         self.views, self.bucket_of, self.buckets = {}, {}, []
         lim = int(bucket_mb * 2**20 / 4)
         off, start, cur = 0, 0, []
@@ -200,6 +212,8 @@ class GradBuckets:
                 cur, start = [], off
         if cur:
             self.buckets.append((cur, start, off))
+        idx, s0, e0 = self.buckets[-1]
+        self.buckets[-1] = (idx, s0, e0 + 1)  # + the error slot
         for b, (idx, _, _) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
@@ -258,6 +272,12 @@ class GradBuckets:
                 torch._foreach_copy_(dst, src)
             for i in idx:
                 self.params[i].grad = self.views[i]
+            if b == len(self.buckets) - 1:  # this rank's verdict on its step: 1 = a device error flag is up
+                if self.err_check:
+                    ew = err_word(dev)[0:1]
+                    self.slot.copy_(torch.bitwise_and(ew, 0xFFFFFFFF).ne(0))
+                else:
+                    self.slot.zero_()
             seg = self.flat[s:e]
             op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
             self._works.append((dist.all_reduce(seg, op=op, async_op=True), seg))
@@ -271,6 +291,9 @@ class GradBuckets:
             w.wait()
             if not self.avg:
                 seg.div_(self.world)
+        if self.err_check:  # some rank failed this step: every rank's AdamW skips it and every rank raises
+            ew = err_word(self.flat.device)[0:1]
+            ew.bitwise_or_(self.slot.gt(0).to(torch.int64) * FLAG_PEER_RANK)
         self.reset()
 
 
@@ -324,7 +347,8 @@ class TrainStep:
         else:
             self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
             self.sched = torch.optim.lr_scheduler.LambdaLR(self.opt, self.lr_lambda)
-        self.grad_buckets = GradBuckets(params, self.world, bucket_mb) if self.distributed else None
+        self.grad_buckets = (GradBuckets(params, self.world, bucket_mb, err_check=check_errors and dev.type == "cuda")
+                             if self.distributed else None)
         # HIP-graph capture for the capturable steps (graph_safe). `_force_graph` is for diagnostics of the other
         # paths (tools/na_graph_*.py).
         self.use_graph = use_graph and (_force_graph or graph_safe(model, compute_dtype))

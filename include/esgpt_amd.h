@@ -42,6 +42,7 @@ extern "C" {
 #define ESGPT_FLAG_TTE_NAN 2      /* "NaNs in TTE_LL"                    (model_output.py:1362-1363)     */
 #define ESGPT_FLAG_TTE_NO_OBS 4   /* "No observed time-to-event ..."     (model_output.py:1366-1367)     */
 #define ESGPT_FLAG_BAD_LABEL 8    /* classification / regression target outside its vocabulary slice      */
+#define ESGPT_FLAG_PEER_RANK 16   /* set by the host DDP exchange: another rank's step raised a flag         */
 
 /* embedding flags */
 #define ESGPT_EMB_NORMALIZE 1     /* do_normalize_by_measurement_index                                     */
