@@ -100,6 +100,8 @@ SIGNATURES = {
     "esgpt_na_split_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "esgpt_na_assemble_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp]),
     "esgpt_na_assemble_bwd": (_int, [_vp, _i64, _i64, _i64, _i64, _vp, _vp, _vp]),
+    "esgpt_na_head_split_fwd": (_int, [_vp, _i64, _i64, _i64, _vp, _vp, _int, _vp]),
+    "esgpt_na_head_split_bwd": (_int, [_vp, _vp, _int, _i64, _i64, _i64, _vp, _vp]),
     "esgpt_attn_bwd_counters": (_i64, [_i64, _i64, _i64]),
     "esgpt_attn_bwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
                               _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _int, _vp, _sz, _vp, _vp]),

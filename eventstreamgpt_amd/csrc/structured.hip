@@ -7,6 +7,7 @@
 //                 xr(r) = r, or with static_kv_first (skip_T = T) the rows of x = [Bs, T, D] after each first one
 //   na_split      per[e] = event_mask[e] ? x[e, G-1] : 0                       (x = [B·L, G, D]: the whole-event element)
 //   na_assemble   seq[e] = [ctx[e-1] (zeros for an event at l = 0), x[e, 0 .. G-2], ctx[e]]   ([B·L, G+1, D])
+//   na_head_split head = x[:, 0 .. G-2], last = x[:, G-1] in the head GEMM's dtype (the NA output layer's operands)
 // and their backwards. Every kernel is an f32 streaming pass (HBM-bound: algorithmic bytes = what it reads + writes
 // once); 16-B accesses, one float4 per thread per iteration, grid-stride. Dropout: the library's counter hash of
 // (seed, r·D + c) (common.h), regenerated in the backward.
@@ -52,7 +53,7 @@ __device__ __forceinline__ int64_t x_row(int64_t r, int64_t skip_T) {
   return skip_T ? (r / (skip_T - 1)) * skip_T + 1 + r % (skip_T - 1) : r;
 }
 
-// h = mask ? x + dropout(y) : 0
+// h = mask ? x + dropout(y) : 0 (x NULL: 0 — a plain dropout, e.g. the NA input layer's)
 template <typename TY>
 __global__ __launch_bounds__(kThreads) void residual_fwd_kernel(const float* __restrict__ x, const TY* __restrict__ y,
                                                                const uint8_t* __restrict__ mask, int64_t mask_div,
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(kThreads) void residual_fwd_kernel(const float* __r
     const int64_t r = i / D4, c = (i - r * D4) * 4;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
     if (mask == nullptr || mask[r / mask_div]) {
-      const float4 xv = ld4(x + x_row(r, skip_T) * D + c);
+      const float4 xv = x ? ld4(x + x_row(r, skip_T) * D + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       float4 yv = ld4y(y + r * D + c);
       if (p > 0.f) {
         float z0, z1, z2, z3;
@@ -182,6 +183,41 @@ __global__ __launch_bounds__(kThreads) void na_assemble_bwd_kernel(const float* 
   }
 }
 
+// NA output-layer operands (model_output.py NA heads: content heads on levels 0..G-2, TTE on level G-1):
+// head[e, 0 .. G-2] = x[e, 0 .. G-2], last[e] = x[e, G-1], cast to the head GEMM's dtype in the same pass
+template <typename TO>
+__global__ __launch_bounds__(kThreads) void na_head_split_fwd_kernel(const float* __restrict__ x, int64_t BL,
+                                                                    int64_t G, int64_t D, TO* __restrict__ head,
+                                                                    TO* __restrict__ last) {
+  const int64_t D4 = D / 4, n4 = BL * G * D4;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
+    const int64_t row = i / D4, c = (i - row * D4) * 4;
+    const int64_t e = row / G, j = row - e * G;
+    const float4 v = ld4(x + row * D + c);
+    if (j + 1 < G) st4y(head + (e * (G - 1) + j) * D + c, v);
+    else st4y(last + e * D + c, v);
+  }
+}
+
+// dx[e, 0 .. G-2] = dhead[e, 0 .. G-2], dx[e, G-1] = dlast[e] (f32; a NULL gradient reads as zeros)
+template <typename TI>
+__global__ __launch_bounds__(kThreads) void na_head_split_bwd_kernel(const TI* __restrict__ dhead,
+                                                                    const TI* __restrict__ dlast, int64_t BL,
+                                                                    int64_t G, int64_t D, float* __restrict__ dx) {
+  const int64_t D4 = D / 4, n4 = BL * G * D4;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kThreads) {
+    const int64_t row = i / D4, c = (i - row * D4) * 4;
+    const int64_t e = row / G, j = row - e * G;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j + 1 < G) {
+      if (dhead) v = ld4y(dhead + (e * (G - 1) + j) * D + c);
+    } else if (dlast) {
+      v = ld4y(dlast + e * D + c);
+    }
+    st4(dx + row * D + c, v);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -189,7 +225,8 @@ extern "C" {
 int esgpt_residual_fwd(const float* x, const void* y, int y_dtype, const uint8_t* row_mask, int64_t mask_div,
                        int64_t skip_T, float dropout_p, const uint64_t* seed, int64_t N, int64_t D, float* h,
                        void* stream) {
-  ESGPT_REQUIRE(x && y && h && N >= 0 && D > 0 && D % 4 == 0 && mask_div >= 1 && (skip_T == 0 || skip_T >= 2));
+  ESGPT_REQUIRE(y && h && N >= 0 && D > 0 && D % 4 == 0 && mask_div >= 1 && (skip_T == 0 || skip_T >= 2));
+  ESGPT_REQUIRE(x || skip_T == 0);
   ESGPT_REQUIRE(y_dtype == ESGPT_F32 || y_dtype == ESGPT_BF16);
   ESGPT_REQUIRE(skip_T == 0 || N % (skip_T - 1) == 0);
   ESGPT_REQUIRE(dropout_p >= 0.f && dropout_p < 1.f && (dropout_p == 0.f || seed));
@@ -266,6 +303,38 @@ int esgpt_na_assemble_bwd(const float* dseq, int64_t B, int64_t L, int64_t G, in
   if (B * L == 0) return ESGPT_OK;
   na_assemble_bwd_kernel<<<grid_for(B * L * G * D / 4), kThreads, 0, as_stream(stream)>>>(dseq, B, L, G, D, dctx,
                                                                                            dx);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_na_head_split_fwd(const float* x, int64_t BL, int64_t G, int64_t D, void* head, void* last, int out_dtype,
+                            void* stream) {
+  ESGPT_REQUIRE(x && head && last && BL >= 0 && G >= 2 && D > 0 && D % 4 == 0);
+  ESGPT_REQUIRE(out_dtype == ESGPT_F32 || out_dtype == ESGPT_BF16);
+  ESGPT_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)head % 8) == 0 && ((uintptr_t)last % 8) == 0);
+  if (BL == 0) return ESGPT_OK;
+  const unsigned g = grid_for(BL * G * D / 4);
+  if (out_dtype == ESGPT_F32)
+    na_head_split_fwd_kernel<float><<<g, kThreads, 0, as_stream(stream)>>>(x, BL, G, D, (float*)head, (float*)last);
+  else
+    na_head_split_fwd_kernel<bf16><<<g, kThreads, 0, as_stream(stream)>>>(x, BL, G, D, (bf16*)head, (bf16*)last);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_na_head_split_bwd(const void* dhead, const void* dlast, int in_dtype, int64_t BL, int64_t G, int64_t D,
+                            float* dx, void* stream) {
+  ESGPT_REQUIRE(dx && BL >= 0 && G >= 2 && D > 0 && D % 4 == 0);
+  ESGPT_REQUIRE(in_dtype == ESGPT_F32 || in_dtype == ESGPT_BF16);
+  ESGPT_REQUIRE(((uintptr_t)dx % 16) == 0 && ((uintptr_t)dhead % 8) == 0 && ((uintptr_t)dlast % 8) == 0);
+  if (BL == 0) return ESGPT_OK;
+  const unsigned g = grid_for(BL * G * D / 4);
+  if (in_dtype == ESGPT_F32)
+    na_head_split_bwd_kernel<float><<<g, kThreads, 0, as_stream(stream)>>>((const float*)dhead, (const float*)dlast,
+                                                                          BL, G, D, dx);
+  else
+    na_head_split_bwd_kernel<bf16><<<g, kThreads, 0, as_stream(stream)>>>((const bf16*)dhead, (const bf16*)dlast, BL,
+                                                                         G, D, dx);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

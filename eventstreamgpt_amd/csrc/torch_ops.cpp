@@ -197,22 +197,27 @@ Tensor embed_bag_bwd(const Tensor& dsrc, BATCH_ARGS, at::IntArrayRef buckets, in
 }
 
 // ---- nested-attention glue + residual (structured.hip) ---------------------------------------------------------
-Tensor residual(const Tensor& x_, const Tensor& y_, const optional<Tensor>& row_mask, int64_t mask_div,
+// x undefined: h = mask ? dropout(y) : 0 (a plain dropout: the NA input layer's embedding_dropout)
+Tensor residual(const optional<Tensor>& x_, const Tensor& y_, const optional<Tensor>& row_mask, int64_t mask_div,
                 int64_t skip_T, double dropout_p, const optional<Tensor>& seed) {
-  const c10::DeviceGuard guard(x_.device());
-  require_hip(x_, "x");
-  Tensor x = x_.contiguous(), y = y_.contiguous();
-  TORCH_CHECK(x.scalar_type() == at::kFloat, "esgpt.residual: x must be f32");
+  const c10::DeviceGuard guard(y_.device());
+  require_hip(y_, "y");
+  const bool has_x = x_.has_value() && x_->defined();
+  Tensor x = has_x ? x_->contiguous() : Tensor(), y = y_.contiguous();
   const int64_t D = y.size(-1), N = y.numel() / D;
-  TORCH_CHECK(x.size(-1) == D && mask_div >= 1 && skip_T >= 0, "esgpt.residual: x / y widths or mask_div / skip_T");
-  TORCH_CHECK(skip_T <= 1 ? x.numel() / D == N : (N % (skip_T - 1) == 0 && x.numel() / D == N / (skip_T - 1) * skip_T),
-              "esgpt.residual: x rows must be N (or N / (T-1) * T with skip_T = T)");
+  TORCH_CHECK(mask_div >= 1 && skip_T >= 0 && (has_x || skip_T == 0), "esgpt.residual: mask_div / skip_T");
+  if (has_x) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat, "esgpt.residual: x must be f32");
+    TORCH_CHECK(x.size(-1) == D, "esgpt.residual: x / y widths");
+    TORCH_CHECK(skip_T <= 1 ? x.numel() / D == N : (N % (skip_T - 1) == 0 && x.numel() / D == N / (skip_T - 1) * skip_T),
+                "esgpt.residual: x rows must be N (or N / (T-1) * T with skip_T = T)");
+  }
   Tensor rm = as_opt(row_mask, at::kBool);
   TORCH_CHECK(!rm.defined() || rm.numel() * mask_div == N, "esgpt.residual: row_mask must hold N / mask_div rows");
-  Tensor h = at::empty({N, D}, x.options());
-  check(esgpt_residual_fwd(ptr<const float>(x), y.data_ptr(), dtype_code(y.scalar_type()),
+  Tensor h = at::empty({N, D}, y.options().dtype(at::kFloat));
+  check(esgpt_residual_fwd(has_x ? ptr<const float>(x) : nullptr, y.data_ptr(), dtype_code(y.scalar_type()),
                            rm.defined() ? ptr<const uint8_t>(rm) : nullptr, mask_div, skip_T, (float)dropout_p,
-                           optr<const uint64_t>(seed), N, D, ptr<float>(h), stream_of(x)),
+                           optr<const uint64_t>(seed), N, D, ptr<float>(h), stream_of(y)),
         "residual");
   return h;
 }
@@ -286,6 +291,38 @@ std::tuple<Tensor, Tensor> na_assemble_bwd(const Tensor& dseq_, int64_t B, int64
   check(esgpt_na_assemble_bwd(ptr<const float>(dseq), B, L, G, D, ptr<float>(dctx), ptr<float>(dx), stream_of(dseq)),
         "na_assemble_bwd");
   return {dctx, dx};
+}
+
+// NA output layer operands: x f32 [B, L, G, D] -> (head [B·L·(G-1), D], last [B·L, D]) in dtype
+std::tuple<Tensor, Tensor> na_head_split(const Tensor& x_, at::ScalarType dtype) {
+  const c10::DeviceGuard guard(x_.device());
+  require_hip(x_, "x");
+  Tensor x = x_.to(at::kFloat).contiguous();
+  TORCH_CHECK(x.dim() == 4 && x.size(2) >= 2, "esgpt.na_head_split: x must be [B, L, G >= 2, D]");
+  const int64_t BL = x.size(0) * x.size(1), G = x.size(2), D = x.size(3);
+  Tensor head = at::empty({BL * (G - 1), D}, x.options().dtype(dtype));
+  Tensor last = at::empty({BL, D}, x.options().dtype(dtype));
+  check(esgpt_na_head_split_fwd(ptr<const float>(x), BL, G, D, head.data_ptr(), last.data_ptr(), dtype_code(dtype),
+                                stream_of(x)),
+        "na_head_split");
+  return {head, last};
+}
+
+Tensor na_head_split_bwd(const optional<Tensor>& dhead_, const optional<Tensor>& dlast_, int64_t B, int64_t L,
+                         int64_t G) {
+  const Tensor& any = (dhead_.has_value() && dhead_->defined()) ? *dhead_ : *dlast_;
+  const c10::DeviceGuard guard(any.device());
+  const at::ScalarType dt = any.scalar_type();
+  Tensor dh = (dhead_.has_value() && dhead_->defined()) ? dhead_->to(dt).contiguous() : Tensor();
+  Tensor dl = (dlast_.has_value() && dlast_->defined()) ? dlast_->to(dt).contiguous() : Tensor();
+  const int64_t D = any.size(-1);
+  TORCH_CHECK(G >= 2 && (!dh.defined() || dh.numel() == B * L * (G - 1) * D) && (!dl.defined() || dl.numel() == B * L * D),
+              "esgpt.na_head_split_bwd: gradient shapes");
+  Tensor dx = at::empty({B, L, G, D}, any.options().dtype(at::kFloat));
+  check(esgpt_na_head_split_bwd(dh.defined() ? dh.data_ptr() : nullptr, dl.defined() ? dl.data_ptr() : nullptr,
+                                dtype_code(dt), B * L, G, D, ptr<float>(dx), stream_of(any)),
+        "na_head_split_bwd");
+  return dx;
 }
 
 // ---- attention (packed qkv [Bs, T, 3D]) ------------------------------------------------------------------------
@@ -852,7 +889,7 @@ TORCH_LIBRARY(esgpt, m) {
         "float dropout_p, Tensor? seed) -> (Tensor, Tensor, Tensor)");
   m.def("attention_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor? key_mask, Tensor? query_mask, int H, "
         "int window, bool static_kv_first, float dropout_p, Tensor? seed, Tensor? keep, Tensor tickets) -> Tensor");
-  m.def("residual(Tensor x, Tensor y, Tensor? row_mask, int mask_div, int skip_T, float dropout_p, Tensor? seed) "
+  m.def("residual(Tensor? x, Tensor y, Tensor? row_mask, int mask_div, int skip_T, float dropout_p, Tensor? seed) "
         "-> Tensor");
   m.def("residual_bwd(Tensor dh, Tensor? row_mask, int mask_div, int skip_T, int x_rows, bool need_dx, "
         "float dropout_p, Tensor? seed, ScalarType y_dtype) -> (Tensor, Tensor)");
@@ -860,6 +897,8 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("na_split_bwd_(Tensor dper, Tensor event_mask, Tensor(a!) dx) -> ()");
   m.def("na_assemble(Tensor ctx, Tensor x) -> Tensor");
   m.def("na_assemble_bwd(Tensor dseq, int B, int L) -> (Tensor, Tensor)");
+  m.def("na_head_split(Tensor x, ScalarType dtype) -> (Tensor, Tensor)");
+  m.def("na_head_split_bwd(Tensor? dhead, Tensor? dlast, int B, int L, int G) -> Tensor");
   m.def("kv_append(Tensor qkv, Tensor(a!) k_cache, Tensor(b!) v_cache, int past) -> ()");
   m.def("attn_decode(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor? key_mask, Tensor? query_mask, int H, "
         "int Lk, int window) -> Tensor");
@@ -909,6 +948,8 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("na_split_bwd_", &na_split_bwd_);
   m.impl("na_assemble", &na_assemble);
   m.impl("na_assemble_bwd", &na_assemble_bwd);
+  m.impl("na_head_split", &na_head_split);
+  m.impl("na_head_split_bwd", &na_head_split_bwd);
   m.impl("attention", &attention);
   m.impl("attention_bwd", &attention_bwd);
   m.impl("kv_append", &kv_append);

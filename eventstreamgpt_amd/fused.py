@@ -42,7 +42,8 @@ def residual_ln(x, y, bias, ln_w, ln_b, row_mask, p: float, eps: float, out_dtyp
 
 def residual(x, y, row_mask, mask_div: int, skip_T: int, p: float):
     """``esgpt::residual``: h = mask(r) ? x[xr(r)] + dropout(y[r]) : 0 (f32), mask(r) = row_mask[r // mask_div];
-    with skip_T = T the rows of x [Bs, T, D] after each first one. Differentiable in x and y."""
+    with skip_T = T the rows of x [Bs, T, D] after each first one; x None: a plain dropout of y. Differentiable in x
+    and y."""
     seed = next_dropout_seed(y.device) if p > 0 else None
     with _timed("residual_fwd"):
         return _ops().residual(x, y, row_mask, int(mask_div), int(skip_T), float(p), seed)

@@ -51,7 +51,8 @@ OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd"
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
        "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank", "residual",
-       "residual_bwd", "na_split", "na_split_bwd_", "na_assemble", "na_assemble_bwd")
+       "residual_bwd", "na_split", "na_split_bwd_", "na_assemble", "na_assemble_bwd", "na_head_split",
+       "na_head_split_bwd")
 
 
 def load():
@@ -148,7 +149,7 @@ def _register():
     @fake(lib + "residual")
     def _(x, y, row_mask, mask_div, skip_T, p, seed):
         D = y.shape[-1]
-        return x.new_empty(y.numel() // D, D, dtype=torch.float32)
+        return y.new_empty(y.numel() // D, D, dtype=torch.float32)
 
     @fake(lib + "residual_bwd")
     def _(dh, row_mask, mask_div, skip_T, x_rows, need_dx, p, seed, y_dtype):
@@ -173,6 +174,16 @@ def _register():
     def _(dseq, B, L):
         G1, D = dseq.shape[-2], dseq.shape[-1]
         return dseq.new_empty(B, L, D, dtype=torch.float32), dseq.new_empty(B, L, G1 - 1, D, dtype=torch.float32)
+
+    @fake(lib + "na_head_split")
+    def _(x, dtype):
+        B, L, G, D = x.shape
+        return x.new_empty(B * L * (G - 1), D, dtype=dtype), x.new_empty(B * L, D, dtype=dtype)
+
+    @fake(lib + "na_head_split_bwd")
+    def _(dhead, dlast, B, L, G):
+        g = dhead if dhead is not None else dlast
+        return g.new_empty(B, L, G, g.shape[-1], dtype=torch.float32)
 
     @fake(lib + "kv_append")
     def _(qkv, k_cache, v_cache, past):
@@ -379,7 +390,8 @@ def _register():
     def _rs_setup(ctx, inputs, output):
         x, y, row_mask, mask_div, skip_T, p, seed = inputs
         ctx.save_for_backward(row_mask, seed)
-        ctx.meta = (mask_div, skip_T, x.numel() // x.shape[-1], p, y.dtype, tuple(x.shape), tuple(y.shape))
+        ctx.meta = (mask_div, skip_T, 0 if x is None else x.numel() // x.shape[-1], p, y.dtype,
+                    None if x is None else tuple(x.shape), tuple(y.shape))
         ctx.set_materialize_grads(False)
 
     def _rs_bwd(ctx, dh):
@@ -387,10 +399,25 @@ def _register():
             return (None,) * 7
         row_mask, seed = ctx.saved_tensors
         mask_div, skip_T, x_rows, p, y_dtype, xs, ys = ctx.meta
-        dx, dy = ops.residual_bwd(dh, row_mask, mask_div, skip_T, x_rows, ctx.needs_input_grad[0], p, seed, y_dtype)
+        need_dx = xs is not None and ctx.needs_input_grad[0]
+        dx, dy = ops.residual_bwd(dh, row_mask, mask_div, skip_T, x_rows, need_dx, p, seed, y_dtype)
         return (None if dx is None else dx.view(xs)), dy.view(ys), None, None, None, None, None
 
     reg(lib + "residual", _rs_bwd, setup_context=_rs_setup)
+
+    # na_head_split: d x from both outputs' gradients in one pass
+    def _hs_setup(ctx, inputs, output):
+        x, dtype = inputs
+        ctx.meta = tuple(x.shape)
+        ctx.set_materialize_grads(False)
+
+    def _hs_bwd(ctx, dhead, dlast):
+        B, L, G, _ = ctx.meta
+        if dhead is None and dlast is None:
+            return None, None
+        return ops.na_head_split_bwd(dhead, dlast, B, L, G), None
+
+    reg(lib + "na_head_split", _hs_bwd, setup_context=_hs_setup)
 
     # residual_ln: d x, d y, d bias, d ln_w, d ln_b (column sums in the same launch)
     def _rl_setup(ctx, inputs, output):

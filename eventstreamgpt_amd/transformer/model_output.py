@@ -693,9 +693,18 @@ def fused_na_losses(layer: GenerativeOutputLayerBase, batch: PytorchBatch, encod
             names.append(nn_)
     mods = layer._content_modules()
     if terms:
+        from ..fused import GEMM_DTYPES, compute_dtype
         from .structured_attention import split_last_level
 
-        head, last = split_last_level(encoded)  # one cat in backward instead of two zero-filled slice gradients
+        dt = compute_dtype()
+        if encoded.is_cuda and dt in GEMM_DTYPES and G >= 2 and D % 8 == 0:
+            # the content levels and the TTE level as the head GEMM's operands, split and cast in one pass (one
+            # pass back in the backward)
+            from ..kernels import _ops
+
+            head, last = _ops().na_head_split(encoded, dt)
+        else:
+            head, last = split_last_level(encoded)  # one cat in backward instead of two zero-filled slice gradients
         fused = head_losses(head.reshape(B * Lq * (G - 1), D), last.reshape(B * Lq, D), batch, terms,
                             layer._tte_spec(0), 0, max(1, G - 1), mods, [layer.TTE_layer.proj])
         if fused is not None:

@@ -493,6 +493,12 @@ class NestedAttentionPointProcessInputLayer(torch.nn.Module):
             # generation: only the graph element preceding the target (transformer.py:926-929; target 0 -> the
             # whole event); the embedding is already masked, so slicing after the mask is the same.
             embed = embed[:, :, dep_graph_el_generation_target - 1].unsqueeze(2)
+        p = self.embedding_dropout.p
+        if self.training and p > 0 and embed.is_cuda and embed.shape[-1] % 4 == 0:
+            # nn.Dropout as the library's counter-hash dropout kernel (esgpt::residual without x; graph-safe seed)
+            from .. import fused
+
+            return fused.residual(None, embed, None, 1, 0, p).view(embed.shape)
         return self.embedding_dropout(embed)
 
 

@@ -323,6 +323,13 @@ int esgpt_na_assemble_fwd(const float* ctx, const float* x, int64_t B, int64_t L
                           void* stream);
 int esgpt_na_assemble_bwd(const float* dseq, int64_t B, int64_t L, int64_t G, int64_t D, float* dctx, float* dx,
                           void* stream);
+/* NA output layer operands (model_output.py NA heads): x f32 [B·L, G, D] -> head [B·L, G-1, D] and last [B·L, D] in
+ * out_dtype (ESGPT_F32 / ESGPT_BF16, the head GEMM's), one pass; backward dx = [dhead | dlast] in f32 (a NULL
+ * gradient reads as zeros). */
+int esgpt_na_head_split_fwd(const float* x, int64_t BL, int64_t G, int64_t D, void* head, void* last, int out_dtype,
+                            void* stream);
+int esgpt_na_head_split_bwd(const void* dhead, const void* dlast, int in_dtype, int64_t BL, int64_t G, int64_t D,
+                            float* dx, void* stream);
 
 /* ---- Projection GEMM -------------------------------------------------------------------------------------
  * C[M, N] = alpha · (A · B) (+ bias[n]) with bf16 operands and f32 accumulation (the q/k/v/out, c_fc/c_proj and head

@@ -389,3 +389,40 @@ def test_bench_configs_capture_without_aten_gemm_or_reduction(name):
     sig = b.shape_signature()
     assert ts.capture_report[sig] == [], ts.capture_report
     assert ts.graphs[sig] is not None
+
+
+@pytest.mark.gpu
+def test_nested_attention_input_dropout_kernel():
+    """The NA input layer's embedding_dropout (nn.Dropout, transformer.py:900-936) runs as the library's
+    counter-hash dropout (esgpt::residual without x): out = embed · keep / (1 - p), keep ≈ 1 - p of the elements, the
+    same keep mask in the backward; identity in eval mode."""
+    from eventstreamgpt_amd.transformer.transformer import NestedAttentionPointProcessInputLayer
+
+    bc = CONFIGS["C4"]
+    p = 0.3
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=p, resid_dropout=0.0)
+    torch.manual_seed(0)
+    layer = NestedAttentionPointProcessInputLayer(cfg).cuda().train()
+    b = bc.batch(0, batch_size=4, device="cuda")
+    out = layer(b)
+    emb = layer.data_embedding_layer.embed(b, time_layer=layer.time_embedding_layer, cumsum=True).detach()
+    assert out.shape == emb.shape
+    live = emb != 0
+    keep = (out != 0) & live
+    frac = keep.sum().item() / live.sum().item()
+    assert abs(frac - (1 - p)) < 0.01, frac
+    torch.testing.assert_close(out.detach()[keep], emb[keep] / (1 - p), rtol=1e-6, atol=0)
+    assert (out.detach()[live & ~keep] == 0).all()
+    # backward: the same keep mask and scale (the op's own gradient w.r.t. its input)
+    from eventstreamgpt_amd import fused
+
+    x = emb.clone().requires_grad_(True)
+    torch.manual_seed(1)
+    y = fused.residual(None, x, None, 1, 0, p).view(x.shape)
+    g = torch.randn_like(y)
+    y.backward(g)
+    kept = (y.detach() != 0) & (x.detach() != 0)
+    torch.testing.assert_close(x.grad[kept], g[kept] / (1 - p), rtol=1e-6, atol=0)
+    assert (x.grad[(x.detach() != 0) & ~kept] == 0).all()
+    layer.eval()
+    torch.testing.assert_close(layer(b), emb, rtol=0, atol=0)
