@@ -659,6 +659,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-opt-graph", action="store_true", help="launch the optimizer step from the host each step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--roofline-only", action="store_true")
@@ -688,7 +689,7 @@ def main():
     opt_cfg = OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=10, max_training_steps=10_000)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     use_graph = not args.no_graph
-    ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph)
+    ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph, capture_optimizer=not args.no_opt_graph)
 
     n_batches = 4
     if args.roofline_only:  # the launches the PMC passes profile (no training steps)

@@ -34,6 +34,12 @@ _int = ctypes.c_int
 _sz = ctypes.c_size_t
 
 
+class EsgptLrSchedule(ctypes.Structure):
+    """esgpt_lr_schedule: kind 0 = constant init_lr, 1 = polynomial decay with warmup (esgpt_adamw_prepare)."""
+    _fields_ = [("kind", ctypes.c_int64), ("warmup", ctypes.c_int64), ("total", ctypes.c_int64),
+                ("power", ctypes.c_double), ("init_lr", ctypes.c_double), ("end_lr", ctypes.c_double)]
+
+
 class EsgptBatch(ctypes.Structure):
     _fields_ = [
         ("dyn_idx", _vp), ("dyn_meas", _vp), ("dyn_vals", _vp), ("dyn_vmask", _vp), ("event_mask", _vp),
@@ -75,6 +81,8 @@ SIGNATURES = {
     "esgpt_version": (ctypes.c_char_p, []),
     "esgpt_adamw_chunk": (_i64, []),
     "esgpt_adamw": (_int, [_vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i64, _vp, _vp, _vp]),
+    "esgpt_adamw_prepare": (_int, [_vp, _vp, _int, _int, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp, _vp]),
+    "esgpt_adamw_dev": (_int, [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_device_arch_ok": (_int, []),
     "esgpt_pack": (_int, [_vp, _i64, _vp]),
     "esgpt_embed_joint_fwd": (_int, [_PB, _PK, _vp, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),

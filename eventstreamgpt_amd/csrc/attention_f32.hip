@@ -210,13 +210,23 @@ __global__ __launch_bounds__(256) void attn_dq_f32_kernel(
   float qf[HD / 2], df[HD / 2];
   row_frag<HD>(qf, q + ((int64_t)b * tq + qi) * ld_in + hh * HD, qin, h);
   row_frag<HD>(df, dout + ((int64_t)b * Lq + qi) * ld_do + hh * HD, qin, h);
+  // δ = rowsum(dO∘O) as the diagonal of O·dOᵀ on the same MFMA sequence as dPᵀ = V·dOᵀ below (same B operand,
+  // same k order): when a query sees one key (P = 1, O = V exactly) dP − δ cancels exactly, as in the reference's
+  // softmax backward, instead of leaving f32 rounding noise in dS
   float dl = 0.f;
   {
     float of[HD / 2];
     row_frag<HD>(of, o + ((int64_t)b * Lq + qi) * ld_o + hh * HD, qin, h);
+    f32x16 od = zero16();
 #pragma unroll
-    for (int t = 0; t < HD / 2; ++t) dl = fmaf(df[t], of[t], dl);
-    dl += __shfl_xor(dl, 32, 64);
+    for (int t = 0; t < HD / 2; ++t) od = mfma2(of[t], df[t], od);
+    // C[q_i][q_r] sits in lane (r, h) register i with acc_row(i, h) = r: h = (r >> 2) & 1, i = (r & 3) + 4 (r >> 3)
+    const int hr = (r >> 2) & 1, ir = (r & 3) + 4 * (r >> 3);
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v = (i == ir) ? od[i] : v;
+    v = (h == hr) ? v : 0.f;
+    dl = v + __shfl_xor(v, 32, 64);
   }
   if (!qvalid) dl = 0.f;
   if (qin && h == 0) delta[(int64_t)bh * Lq + qi] = dl;

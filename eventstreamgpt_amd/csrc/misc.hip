@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __r
                                                     const int64_t* __restrict__ blocks, float lr, float beta1,
                                                     float beta2, float eps, float wd, float step_size_all,
                                                     float bc2_sqrt_all, const float* __restrict__ per_tensor,
-                                                    const int32_t* __restrict__ err) {
+                                                    const int32_t* __restrict__ err, const float* __restrict__ lr_dev) {
   // A data-dependent error raised by this step's forward (bad embedding index, NaN TTE log-likelihood, subject
   // without an observed TTE) leaves the parameters untouched: the reference raises before its optimizer step. The
   // gate also holds while an EARLIER step's flags are pending in the sticky word (err[1], set by the next step's
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __r
   const float bc2_sqrt = per_tensor ? per_tensor[2 * ti + 1] : bc2_sqrt_all;
   const int64_t start = e & ((1ll << 40) - 1);
   const int64_t end = start + kAdamChunk < t.n ? start + kAdamChunk : t.n;
-  const float decay = 1.f - lr * wd;
+  const float decay = 1.f - (lr_dev ? *lr_dev : lr) * wd;
   auto upd = [&](float& p, float g, float& m, float& v) {
     p *= decay;
     m = beta1 * m + (1.f - beta1) * g;
@@ -67,6 +67,39 @@ __global__ __launch_bounds__(256) void adamw_kernel(const esgpt_adam_tensor* __r
     for (int64_t i = start + 4 * n4 + threadIdx.x; i < end; i += blockDim.x) upd(t.p[i], t.g[i], t.m[i], t.v[i]);
   } else {
     for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) upd(t.p[i], t.g[i], t.m[i], t.v[i]);
+  }
+}
+
+// The step's learning rate and per-tensor bias corrections on the device (esgpt_adamw_prepare), so that the
+// optimizer step needs no host arguments and replays inside a HIP graph. One workgroup: counters[t] (the 1-based
+// step of parameter t after this step) for the active tensors, counters[n_params] = the schedule's step; gated by
+// the same error condition as the update, so a failed (or discarded) step advances nothing.
+__global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict__ counters,
+                                                            const int32_t* __restrict__ active, int n_active,
+                                                            int n_params, esgpt_lr_schedule sc, double beta1,
+                                                            double beta2, float* __restrict__ per_tensor,
+                                                            float* __restrict__ lr_out,
+                                                            const int32_t* __restrict__ err) {
+  if (err != nullptr && (err[0] | err[1]) != 0) return;
+  const int64_t s = counters[n_params];  // LambdaLR: the k-th optimizer step uses lambda(k - 1)
+  double f = 1.0;
+  if (sc.kind == 1) {  // transformers.get_polynomial_decay_schedule_with_warmup (train.poly_decay_lambda)
+    if (s < sc.warmup) f = (double)s / (double)(sc.warmup > 1 ? sc.warmup : 1);
+    else if (s > sc.total) f = sc.end_lr / sc.init_lr;
+    else f = ((sc.init_lr - sc.end_lr) * pow(1.0 - (double)(s - sc.warmup) / (double)(sc.total - sc.warmup), sc.power) +
+              sc.end_lr) / sc.init_lr;
+  }
+  const double lr = sc.init_lr * f;
+  for (int t = threadIdx.x; t < n_active; t += blockDim.x) {
+    const int i = active[t];
+    const int64_t c = counters[i] + 1;
+    counters[i] = c;
+    per_tensor[2 * t] = (float)(lr / (1.0 - pow(beta1, (double)c)));
+    per_tensor[2 * t + 1] = (float)sqrt(1.0 - pow(beta2, (double)c));
+  }
+  if (threadIdx.x == 0) {
+    counters[n_params] = s + 1;
+    *lr_out = (float)lr;
   }
 }
 
@@ -181,7 +214,30 @@ int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n
   const double bc1 = 1.0 - pow((double)beta1, s), bc2 = 1.0 - pow((double)beta2, s);
   esgpt::adamw_kernel<<<(unsigned)n_blocks, 256, 0, esgpt::as_stream(stream)>>>(table, blocks, lr, beta1, beta2, eps,
                                                                    weight_decay, (float)(lr / bc1),
-                                                                   (float)sqrt(bc2), per_tensor, err);
+                                                                   (float)sqrt(bc2), per_tensor, err, nullptr);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, int n_params,
+                        const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor, float* lr_out,
+                        const int32_t* err, void* stream) {
+  ESGPT_REQUIRE(counters && sched && per_tensor && lr_out && n_active >= 0 && n_params >= 0);
+  ESGPT_REQUIRE(n_active == 0 || active);
+  ESGPT_REQUIRE(sched->kind == 0 || (sched->kind == 1 && sched->init_lr > sched->end_lr && sched->total > sched->warmup));
+  esgpt::adamw_prepare_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counters, active, n_active, n_params, *sched,
+                                                                       beta1, beta2, per_tensor, lr_out, err);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_adamw_dev(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, const float* lr_dev,
+                    float beta1, float beta2, float eps, float weight_decay, const float* per_tensor,
+                    const int32_t* err, void* stream) {
+  ESGPT_REQUIRE(table && blocks && n_blocks >= 0 && lr_dev && per_tensor);
+  if (n_blocks == 0) return ESGPT_OK;
+  esgpt::adamw_kernel<<<(unsigned)n_blocks, 256, 0, esgpt::as_stream(stream)>>>(table, blocks, 0.f, beta1, beta2, eps,
+                                                                   weight_decay, 0.f, 1.f, per_tensor, err, lr_dev);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -874,6 +874,26 @@ void adamw(const Tensor& table, const Tensor& blocks, double lr, double beta1, d
         "adamw");
 }
 
+// The device-side optimizer step (HIP-graph replayable): prepare (counters, lr, per-tensor table) + update.
+void adamw_dev(const Tensor& table, const Tensor& blocks, const Tensor& counters, const Tensor& active,
+               int64_t n_params, int64_t kind, int64_t warmup, int64_t total, double power, double init_lr,
+               double end_lr, double beta1, double beta2, double eps, double wd, const Tensor& per_tensor,
+               const Tensor& lr_dev, const Tensor& err) {
+  const c10::DeviceGuard guard(table.device());
+  TORCH_CHECK(counters.scalar_type() == at::kLong && counters.numel() == n_params + 1, "adamw_dev: counters");
+  TORCH_CHECK(active.scalar_type() == at::kInt && per_tensor.numel() >= 2 * active.numel(), "adamw_dev: active / per");
+  esgpt_lr_schedule sc{kind, warmup, total, power, init_lr, end_lr};
+  void* st = stream_of(table);
+  check(esgpt_adamw_prepare(ptr<int64_t>(counters), active.numel() ? ptr<const int32_t>(active) : nullptr,
+                            (int)active.numel(), (int)n_params, &sc, beta1, beta2, ptr<float>(per_tensor),
+                            ptr<float>(lr_dev), ptr<const int32_t>(err), st),
+        "adamw_prepare");
+  check(esgpt_adamw_dev(reinterpret_cast<const esgpt_adam_tensor*>(table.data_ptr()), ptr<const int64_t>(blocks),
+                        blocks.numel(), ptr<const float>(lr_dev), (float)beta1, (float)beta2, (float)eps, (float)wd,
+                        ptr<const float>(per_tensor), ptr<const int32_t>(err), st),
+        "adamw_dev");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(esgpt, m) {
@@ -932,6 +952,9 @@ TORCH_LIBRARY(esgpt, m) {
         "int n_levels, Tensor wc, Tensor bc, Tensor? wt, Tensor? bt, Tensor[] cw, Tensor[] cb, Tensor[] tw, "
         "Tensor[] tb, Tensor err, Tensor tickets, Tensor? zb) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("pack(Tensor[] srcs, int[] group_sizes, int[] tails, int[] dtypes) -> Tensor[]");
+  m.def("adamw_dev(Tensor table, Tensor blocks, Tensor(a!) counters, Tensor active, int n_params, int kind, "
+        "int warmup, int total, float power, float init_lr, float end_lr, float beta1, float beta2, float eps, "
+        "float weight_decay, Tensor(b!) per_tensor, Tensor(c!) lr_dev, Tensor err) -> ()");
   m.def("adamw(Tensor table, Tensor blocks, float lr, float beta1, float beta2, float eps, float weight_decay, "
         "int step, Tensor? per_tensor, Tensor err) -> ()");
 }
@@ -973,4 +996,5 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("head_loss", &head_loss);
   m.impl("pack", &pack);
   m.impl("adamw", &adamw);
+  m.impl("adamw_dev", &adamw_dev);
 }

@@ -50,7 +50,7 @@ _state = {"loaded": False}
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
        "attention_bwd", "kv_append", "attn_decode", "output_loss", "residual_ln", "residual_ln_bwd", "bias_act",
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
-       "pack", "adamw", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank", "residual",
+       "pack", "adamw", "adamw_dev", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank", "residual",
        "residual_bwd", "na_split", "na_split_bwd_", "na_assemble", "na_assemble_bwd", "na_head_split",
        "na_head_split_bwd")
 
@@ -301,6 +301,11 @@ def _register():
 
     @fake(lib + "adamw")
     def _(table, blocks, lr, beta1, beta2, eps, wd, step, per_tensor, err):
+        return None
+
+    @fake(lib + "adamw_dev")
+    def _(table, blocks, counters, active, n_params, kind, warmup, total, power, init_lr, end_lr, beta1, beta2, eps,
+          wd, per_tensor, lr_dev, err):
         return None
 
     # ---------------------------------------------------------------- autograd formulas

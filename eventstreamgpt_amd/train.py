@@ -86,26 +86,30 @@ class FusedAdamW:
         self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, betas, eps
         self.exp_avg = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
         self.exp_avg_sq = [torch.zeros_like(p, memory_format=torch.contiguous_format) for p in self.params]
-        self.steps = [0] * len(self.params)
+        self.steps = [0] * len(self.params)  # host mirror of the device counters (state_dict, error rollback)
         self._key = None
-        self._table = self._blocks = None
+        self._plan_cur = None
         self._active = []
-        self._per_dev = None
-        self._per_host = None
+        dev = self.params[0].device
+        # device state of the step: per-parameter step counts + the schedule's step (esgpt_adamw_prepare), the step's lr
+        self._counters = torch.zeros(len(self.params) + 1, dtype=torch.int64, device=dev)
+        self._lr_dev = torch.empty(1, dtype=torch.float32, device=dev)
+        # (kind, warmup, total, power, init_lr, end_lr): kind 0 = constant lr; TrainStep installs its polynomial decay
+        self.schedule = (0, 0, 1, 1.0, float(lr), 0.0)
 
     def zero_grad(self, set_to_none: bool = True):
         for p in self.params:
             p.grad = None
 
-    def _plan(self):
+    def make_plan(self) -> dict:
+        """The launch tables of the parameters that hold a gradient now: tensor table (p / grad / exp_avg /
+        exp_avg_sq pointers), chunk list, active indices (host and device) and the per-tensor bias-correction
+        buffer. A captured optimizer step keeps its own plan alive (its graph reads these buffers)."""
         items = [i for i, p in enumerate(self.params) if p.grad is not None]
         for i in items:
             g = self.params[i].grad
             if not (g.is_contiguous() and g.dtype == torch.float32 and self.params[i].is_contiguous()):
                 raise RuntimeError("FusedAdamW needs contiguous f32 parameters and gradients")
-        key = tuple((i, self.params[i].grad.data_ptr()) for i in items)
-        if key == self._key:
-            return
         chunk = int(self.lib.esgpt_adamw_chunk())
         rows, blocks = [], []
         for t, i in enumerate(items):
@@ -114,33 +118,45 @@ class FusedAdamW:
                          p.numel()])
             blocks += [(t << 40) | s for s in range(0, p.numel(), chunk)]
         dev = self.params[0].device
-        self._table = torch.tensor(rows, dtype=torch.int64).to(dev)
-        self._blocks = torch.tensor(blocks, dtype=torch.int64).to(dev)
-        self._per_dev = torch.empty(2 * max(1, len(items)), dtype=torch.float32, device=dev)
-        self._key = key
-        self._active = items
+        return {"key": tuple((i, self.params[i].grad.data_ptr()) for i in items), "active": items,
+                "table": torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(dev),
+                "blocks": torch.tensor(blocks, dtype=torch.int64).to(dev),
+                "active_dev": torch.tensor(items, dtype=torch.int32).to(dev),
+                "per": torch.empty(2 * max(1, len(items)), dtype=torch.float32, device=dev)}
+
+    def _plan(self):
+        key = tuple((i, p.grad.data_ptr()) for i, p in enumerate(self.params) if p.grad is not None)
+        if self._plan_cur is None or key != self._key:
+            self._plan_cur = self.make_plan()
+            self._key = key
+            self._active = self._plan_cur["active"]
+        return self._plan_cur
+
+    def launch(self, plan: dict, lr: float | None = None):
+        """The device step over ``plan``: esgpt_adamw_prepare (counters, lr, per-tensor bias corrections — torch's
+        one ``step`` per parameter) + the update, both no-ops while the device error block holds a flag. No host
+        arguments change between steps (``lr=None``: the installed schedule), so the launch replays in a graph."""
+        if not plan["active"]:
+            return
+        kind, warm, total, power, init_lr, end_lr = self.schedule
+        if lr is not None:
+            kind, init_lr = 0, float(lr)
+        b1, b2 = self.betas
+        self.ops.adamw_dev(plan["table"], plan["blocks"], self._counters, plan["active_dev"], len(self.params),
+                           int(kind), int(warm), int(total), float(power), float(init_lr), float(end_lr), float(b1),
+                           float(b2), float(self.eps), float(self.weight_decay), plan["per"], self._lr_dev,
+                           err_word(self.params[0].device))
+
+    def note_step(self, active):
+        """Host mirror of the device counters: one step for each active parameter."""
+        for i in active:
+            self.steps[i] += 1
 
     @torch.no_grad()
     def step(self, lr: float | None = None):
-        self._plan()
-        if not self._active:
-            return
-        lr = float(self.lr if lr is None else lr)
-        b1, b2 = self.betas
-        for i in self._active:
-            self.steps[i] += 1
-        steps = [self.steps[i] for i in self._active]
-        per = None
-        if any(s != steps[0] for s in steps):  # torch's per-parameter `step`: own bias corrections per tensor
-            vals = []
-            for s in steps:
-                vals += [lr / (1.0 - b1**s), (1.0 - b2**s) ** 0.5]
-            self._per_host = torch.tensor(vals, dtype=torch.float32).pin_memory()  # kept alive until the next step
-            self._per_dev[: len(vals)].copy_(self._per_host, non_blocking=True)
-            per = self._per_dev
-        dev = self.params[0].device
-        self.ops.adamw(self._table, self._blocks, lr, b1, b2, self.eps, self.weight_decay, steps[0], per,
-                       err_word(dev))
+        plan = self._plan()
+        self.launch(plan, lr)
+        self.note_step(plan["active"])
 
     def state_dict(self):
         return {"state": {i: {"step": self.steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}
@@ -327,7 +343,8 @@ class _GemmSpy(torch.utils._python_dispatch.TorchDispatchMode):
 class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
-                 max_graphs: int = 4, overlap_weight_grads: bool = False, defer_colsums: bool = True, _force_graph: bool = False):
+                 max_graphs: int = 4, overlap_weight_grads: bool = False, defer_colsums: bool = True,
+                 capture_optimizer: bool = False, _force_graph: bool = False):
         self.model = model
         self.cfg = opt_cfg
         self.dtype = compute_dtype
@@ -343,6 +360,9 @@ class TrainStep:
         self.sched_step = 0  # LambdaLR semantics: the first optimizer step uses lambda(0)
         if dev.type == "cuda":
             self.opt = FusedAdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
+            # the schedule runs on the device (esgpt_adamw_prepare), so the optimizer step replays inside the graph
+            self.opt.schedule = (1, warm, total, float(opt_cfg.lr_decay_power), float(opt_cfg.init_lr),
+                                 float(opt_cfg.end_lr))
             self.sched = None
         else:
             self.opt = torch.optim.AdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
@@ -353,6 +373,10 @@ class TrainStep:
         # paths (tools/na_graph_*.py).
         self.use_graph = use_graph and (_force_graph or graph_safe(model, compute_dtype))
         self.max_graphs = max_graphs
+        # the optimizer step as its own graph replayed after the step's segments (no host launch per step). Off by
+        # default: measured on the C2 step, same box, alternating runs, it costs ~10 us (1.7118 / 1.7115 vs 1.6981 /
+        # 1.7045 ms) — the extra graph launch costs more than the two kernel launches it replaces.
+        self.capture_optimizer = capture_optimizer
         self.graphs: dict = {}  # shape signature -> (segments, static batch, static loss, grads) | None (eager)
         self.capture_report: dict = {}  # shape signature -> ATen GEMMs / reductions seen in its warm-up pass
         self.check_errors = check_errors and dev.type == "cuda"
@@ -472,12 +496,32 @@ class TrainStep:
                 segs.append((cur["g"], []))
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
+            # the optimizer step as its own small graph over the captured gradients (its plan's tables are built
+            # here, outside any capture, and kept alive with the entry): no host launch per replayed step
+            opt_graph = plan = None
+            if isinstance(self.opt, FusedAdamW) and self.capture_optimizer:
+                if gb is not None:  # under DDP the step reads the exchanged gradients: the flat buffer's views
+                    saved = [p.grad for p in self.params]
+                    for i, p in enumerate(self.params):
+                        p.grad = gb.views[i]
+                    plan = self.opt.make_plan()
+                    for p, g in zip(self.params, saved):
+                        p.grad = g
+                else:
+                    plan = self.opt.make_plan()
+                opt_graph = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s):
+                    opt_graph.capture_begin(pool=pool)
+                    self.opt.launch(plan)
+                    opt_graph.capture_end()
+                torch.cuda.current_stream().wait_stream(s)
+                torch.cuda.synchronize()
         finally:
             if gb is not None:
                 gb.mode, gb.on_boundary = "launch", None
                 gb.reset()
         grads = [p.grad for p in self.params]
-        self.graphs[sig] = (segs, static, loss, grads)
+        self.graphs[sig] = (segs, static, loss, grads, opt_graph, plan)
 
     def _raise_pending(self, keep: int):
         """Raises the first device error among submitted steps, waiting only for steps older than the newest
@@ -553,11 +597,12 @@ class TrainStep:
                 self._capture(batch)
             entry = self.graphs.get(sig)
         gb = self.grad_buckets
+        opt_graph = plan = None
         if entry is None:
             self.opt.zero_grad(set_to_none=True)
             loss = self._fwd_bwd(batch)
         else:
-            segs, static, sloss, grads = entry
+            segs, static, sloss, grads, opt_graph, plan = entry
             static.copy_(batch, non_blocking=True)
             if self._release is not None:  # the staging buffer is consumed: the next prefetch may refill it
                 self._release.record()
@@ -574,11 +619,17 @@ class TrainStep:
             loss = sloss.mul(1.0)
         if gb is not None:
             gb.finish()
-        if self.sched is None:
-            self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step))
+        if opt_graph is not None:
+            opt_graph.replay()
+            self.opt.note_step(plan["active"])
+            active = list(plan["active"])
+        elif self.sched is None:
+            self.opt.step()  # the installed schedule, on the device
+            active = list(self.opt._active)
         else:
             self.opt.step()
             self.sched.step()
+            active = []
         self.sched_step += 1
         if self._release is not None:  # the staging buffer may be refilled once this step has consumed it
             self._release.record()
@@ -588,7 +639,6 @@ class TrainStep:
             host.copy_(err_word(self.device), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
-            active = list(self.opt._active) if isinstance(self.opt, FusedAdamW) else []
             self._pending.append((ev, host, host_batch, active))
         return loss
 

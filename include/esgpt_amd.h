@@ -451,6 +451,23 @@ int64_t esgpt_adamw_chunk(void);
 int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, float lr, float beta1,
                 float beta2, float eps, float weight_decay, int64_t step, const float* per_tensor,
                 const int32_t* err, void* stream);
+/* The optimizer step with no host arguments (HIP-graph replayable): esgpt_adamw_prepare advances the device step
+ * counters — counters[active[t]] (each parameter's 1-based step) and counters[n_params] (the schedule's step) —
+ * and writes the step's learning rate (*lr_out) and per-tensor table per_tensor[t] = (lr / (1 - beta1^step),
+ * sqrt(1 - beta2^step)) (betas as doubles, like torch's); esgpt_adamw_dev then updates with the device lr and that
+ * table. Both are no-ops while err holds a flag or a sticky word, so a failed or discarded step advances nothing.
+ * Schedule kind 0: constant init_lr; kind 1: transformers' polynomial decay with warmup
+ * (generative_modeling.py:467-485): lr = init_lr · lambda(step), LambdaLR's step counting. */
+typedef struct esgpt_lr_schedule {
+  int64_t kind, warmup, total;
+  double power, init_lr, end_lr;
+} esgpt_lr_schedule;
+int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, int n_params,
+                        const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor, float* lr_out,
+                        const int32_t* err, void* stream);
+int esgpt_adamw_dev(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, const float* lr_dev,
+                    float beta1, float beta2, float eps, float weight_decay, const float* per_tensor,
+                    const int32_t* err, void* stream);
 
 /* ---- Batch producer (host) ----------------------------------------------------------------------------------
  * PytorchDataset.collate (pytorch_dataset.py:527-701) over flat ragged arrays (the DL_reps parquet columns):

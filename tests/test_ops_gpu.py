@@ -181,12 +181,21 @@ def test_adamw_op_equals_c_abi(env):
         p.grad = gr.clone()
     for p, gr in zip(pb, grads):
         p.grad = gr.clone()
-    oa.step()  # torch.ops.esgpt.adamw
-    ob._plan()
-    L.check(lib.esgpt_adamw(ob._table.data_ptr(), ob._blocks.data_ptr(), ob._blocks.numel(), 1e-2, 0.9, 0.999, 1e-8,
-                            0.01, 1, None, None, L.stream()), "adamw")
+    import ctypes
+
+    for _ in range(2):
+        oa.step()  # torch.ops.esgpt.adamw_dev: esgpt_adamw_prepare + esgpt_adamw_dev
+        plan = ob._plan()
+        sc = L.EsgptLrSchedule(0, 0, 1, 1.0, 1e-2, 0.0)
+        L.check(lib.esgpt_adamw_prepare(ob._counters.data_ptr(), plan["active_dev"].data_ptr(), len(plan["active"]),
+                                        len(pb), ctypes.byref(sc), 0.9, 0.999, plan["per"].data_ptr(),
+                                        ob._lr_dev.data_ptr(), None, L.stream()), "adamw_prepare")
+        L.check(lib.esgpt_adamw_dev(plan["table"].data_ptr(), plan["blocks"].data_ptr(), plan["blocks"].numel(),
+                                    ob._lr_dev.data_ptr(), 0.9, 0.999, 1e-8, 0.01, plan["per"].data_ptr(), None,
+                                    L.stream()), "adamw_dev")
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
+    assert torch.equal(oa._counters, ob._counters) and oa._counters.tolist() == [2, 2, 2, 2]  # + the schedule's step
 
 
 def test_pack_equals_cat_cast_and_c_abi(env):

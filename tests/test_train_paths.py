@@ -426,3 +426,58 @@ def test_nested_attention_input_dropout_kernel():
     assert (x.grad[(x.detach() != 0) & ~kept] == 0).all()
     layer.eval()
     torch.testing.assert_close(layer(b), emb, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_device_lr_schedule_matches_host_schedule():
+    """The optimizer step's lr and bias corrections computed on the device (esgpt_adamw_prepare) equal the host
+    restatement of transformers' polynomial decay with warmup (LambdaLR step counting) and torch's per-parameter
+    bias corrections, over warmup, decay and past-the-end steps; a parameter without a gradient keeps its count."""
+    from eventstreamgpt_amd.train import FusedAdamW, poly_decay_lambda
+
+    warm, total, power, init, end = 3, 10, 2.0, 1e-3, 1e-5
+    lam = poly_decay_lambda(warm, total, power, init, end)
+    p = [torch.zeros(8, device="cuda", requires_grad=True), torch.zeros(3, device="cuda", requires_grad=True)]
+    opt = FusedAdamW(p, lr=init)
+    opt.schedule = (1, warm, total, power, init, end)
+    steps = [0, 0]
+    for k in range(14):
+        p[0].grad = torch.ones_like(p[0])
+        p[1].grad = torch.ones_like(p[1]) if k % 3 else None  # skipped on some steps
+        opt.step()
+        for i in range(2):
+            if p[i].grad is not None:
+                steps[i] += 1
+        lr = init * lam(k)
+        assert abs(float(opt._lr_dev) - lr) <= 1.2e-7 * lr + 1e-30, (k, float(opt._lr_dev), lr)  # f32 rounding
+        per = opt._plan()["per"].cpu().tolist()
+        for t, i in enumerate(opt._active):
+            want = [lr / (1.0 - 0.9 ** steps[i]), (1.0 - 0.999 ** steps[i]) ** 0.5]
+            assert abs(per[2 * t] - want[0]) <= 1e-6 * want[0] and abs(per[2 * t + 1] - want[1]) <= 1e-6 * want[1]
+    assert opt._counters.tolist() == steps + [14] and opt.steps == steps
+
+
+@pytest.mark.gpu
+def test_captured_optimizer_step_matches_host_launched():
+    """capture_optimizer=True (the optimizer step replayed as its own graph, lr / bias corrections from the device
+    counters) gives bit-identical parameters and step counts to the host-launched device step."""
+    bc = CONFIGS["C1"]
+    batches = [bc.batch(i, batch_size=8, device="cuda").packed() for i in range(4)]
+    out = {}
+    for cap in (False, True):
+        from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+
+        cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+        torch.manual_seed(0)
+        m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
+        ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=10),
+                       torch.bfloat16, use_graph=True, capture_optimizer=cap)
+        for b in batches:
+            ts.step(b)
+        ts.check()
+        assert all((e[4] is not None) == cap for e in ts.graphs.values() if e is not None)
+        out[cap] = ({k: v.detach().clone() for k, v in m.state_dict().items()}, list(ts.opt.steps),
+                    ts.opt._counters.tolist())
+    for k in out[False][0]:
+        assert torch.equal(out[False][0][k], out[True][0][k]), k
+    assert out[False][1] == out[True][1] and out[False][2] == out[True][2]
