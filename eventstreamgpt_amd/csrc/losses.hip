@@ -80,6 +80,15 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
       atomicOr(tm.kind == ESGPT_TERM_SINGLE ? &s_lut_any[tm.meas_idx] : &s_lut_val[tm.meas_idx], 1u << threadIdx.x);
   }
   __syncthreads();
+  // this thread's event flags (thread = event in the counting pass below), loaded before the entries so their
+  // latency overlaps the entry pass instead of following it
+  const uint8_t* em = bt.event_mask + b * L;
+  bool ev0 = false, evn0 = false;
+  if ((int)threadIdx.x < ne) {
+    const int64_t lg = l0 + threadIdx.x;
+    ev0 = em[lg] != 0;
+    evn0 = lg + 1 < L && em[lg + 1] != 0;
+  }
   const int64_t base = (b * L + l0) * M;
   const int64_t* meas = bt.dyn_meas + base;
   const uint8_t* vmask = bt.dyn_vmask + base;
@@ -115,15 +124,15 @@ __global__ __launch_bounds__(1024) void count_kernel(esgpt_batch bt, Terms terms
   int32_t c[ESGPT_MAX_TERMS + 1];
 #pragma unroll
   for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) c[t] = 0;
-  const uint8_t* em = bt.event_mask + b * L;
   for (int l = threadIdx.x; l < ne; l += blockDim.x) {
     const int64_t lg = l0 + l;
-    const bool ev = em[lg] != 0;
+    const bool first = l == (int)threadIdx.x;
+    const bool ev = first ? ev0 : em[lg] != 0;
     const uint32_t bits = s_bits[l];
 #pragma unroll
     for (int t = 0; t < ESGPT_MAX_TERMS; ++t)
       if (t < T && ev && (terms.t[t].kind == ESGPT_TERM_MULTI || ((bits >> t) & 1u))) ++c[t];
-    if (lg + 1 < L && ev && em[lg + 1]) ++c[ESGPT_MAX_TERMS];
+    if (ev && (first ? evn0 : (lg + 1 < L && em[lg + 1] != 0))) ++c[ESGPT_MAX_TERMS];
   }
 #pragma unroll
   for (int t = 0; t <= ESGPT_MAX_TERMS; ++t) {
