@@ -659,7 +659,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-opt-graph", action="store_true", help="launch the optimizer step from the host each step")
+    ap.add_argument("--opt-graph", action="store_true", help="replay the optimizer step as its own graph "
+                    "(TrainStep capture_optimizer; measured ~10 us slower per C2 step, off by default)")
+    ap.add_argument("--opt-host-args", action="store_true", help="measurement hook: host-computed lr / bias "
+                    "corrections (round 3's optimizer launch) instead of the device schedule")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--roofline-only", action="store_true")
@@ -689,7 +692,9 @@ def main():
     opt_cfg = OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=10, max_training_steps=10_000)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     use_graph = not args.no_graph
-    ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph, capture_optimizer=not args.no_opt_graph)
+    ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph, capture_optimizer=args.opt_graph)
+    if args.opt_host_args:
+        ts.opt.host_args = True
 
     n_batches = 4
     if args.roofline_only:  # the launches the PMC passes profile (no training steps)

@@ -155,8 +155,30 @@ class FusedAdamW:
     @torch.no_grad()
     def step(self, lr: float | None = None):
         plan = self._plan()
-        self.launch(plan, lr)
+        if self.host_args:
+            self._step_host_args(plan, lr)
+        else:
+            self.launch(plan, lr)
         self.note_step(plan["active"])
+
+    host_args = False  # measurement hook (bench.py --opt-host-args): round 3's launch with host lr / bias corrections
+
+    def _step_host_args(self, plan, lr):
+        if not plan["active"]:
+            return
+        lr = float(self.lr if lr is None else lr)
+        b1, b2 = self.betas
+        steps = [self.steps[i] + 1 for i in plan["active"]]
+        per = None
+        if any(s != steps[0] for s in steps):
+            vals = []
+            for s in steps:
+                vals += [lr / (1.0 - b1**s), (1.0 - b2**s) ** 0.5]
+            self._per_host = torch.tensor(vals, dtype=torch.float32).pin_memory()
+            plan["per"][: len(vals)].copy_(self._per_host, non_blocking=True)
+            per = plan["per"]
+        self.ops.adamw(plan["table"], plan["blocks"], lr, b1, b2, self.eps, self.weight_decay, steps[0], per,
+                       err_word(self.params[0].device))
 
     def state_dict(self):
         return {"state": {i: {"step": self.steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}
@@ -624,7 +646,8 @@ class TrainStep:
             self.opt.note_step(plan["active"])
             active = list(plan["active"])
         elif self.sched is None:
-            self.opt.step()  # the installed schedule, on the device
+            # the installed schedule, on the device (or, measurement hook, round 3's host-computed lr)
+            self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None)
             active = list(self.opt._active)
         else:
             self.opt.step()
