@@ -97,71 +97,82 @@ def graph_time_ms(fn, reps: int = 20, iters: int = 5) -> float:
     return e0.elapsed_time(e1) / (reps * iters)
 
 
-def _attention_launchers(B, Lq, D, H, em, p, dev):
+def _attention_launchers(B, Lq, D, H, em, p, dev, dtype=torch.bfloat16):
     """esgpt_attn_fwd_ex / esgpt_attn_bwd_ex launches on preallocated packed-qkv buffers (the step's layout and
-    path: the forward writes the dropout keep bits the backward reads, as the attention operator does)."""
+    path: the forward writes the dropout keep bits the backward reads, as the attention operator does), in the
+    step's compute dtype (bf16, or f32: the reference-precision kernels)."""
     from eventstreamgpt_amd import _lib as L
     from eventstreamgpt_amd.kernels import tickets
 
     lib = L.load()
     hd = D // H
+    code = L.BF16 if dtype == torch.bfloat16 else L.F32
     g = torch.Generator(device=dev).manual_seed(0)
-    bufs = {"qkv": (0.5 * torch.randn(B, Lq, 3 * D, device=dev, generator=g)).bfloat16(),
-            "o": torch.empty(B, Lq, D, device=dev, dtype=torch.bfloat16),
+    bufs = {"qkv": (0.5 * torch.randn(B, Lq, 3 * D, device=dev, generator=g)).to(dtype),
+            "o": torch.empty(B, Lq, D, device=dev, dtype=dtype),
             "lse": torch.empty(B, H, Lq, device=dev),
-            "do": torch.randn(B, Lq, D, device=dev, generator=g).bfloat16(),
+            "do": torch.randn(B, Lq, D, device=dev, generator=g).to(dtype),
             "seed": torch.tensor([12345], dtype=torch.int64, device=dev),
             "em": em.to(torch.bool).contiguous()}
     bufs["dqkv"] = torch.empty_like(bufs["qkv"])
     nbytes = lib.esgpt_attn_bwd_workspace(B, H, Lq, Lq, hd)
     bufs["ws"] = torch.empty(max(1, nbytes), dtype=torch.uint8, device=dev)
-    nkeep = lib.esgpt_attn_keep_words(B, H, Lq, Lq, hd, Lq, 3 * D, D, L.BF16, p)
+    nkeep = lib.esgpt_attn_keep_words(B, H, Lq, Lq, hd, Lq, 3 * D, D, code, p)
     bufs["keep"] = torch.empty(max(1, nkeep), dtype=torch.int32, device=dev)
     kp = bufs["keep"].data_ptr() if nkeep else None
-    base, dbase, m, es = bufs["qkv"].data_ptr(), bufs["dqkv"].data_ptr(), bufs["em"].data_ptr(), 2
+    es = bufs["qkv"].element_size()
+    base, dbase, m = bufs["qkv"].data_ptr(), bufs["dqkv"].data_ptr(), bufs["em"].data_ptr()
     cnt = tickets(torch.device(dev))
 
     def fwd():
         L.check(lib.esgpt_attn_fwd_ex(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
                                       bufs["lse"].data_ptr(), m, m, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(),
-                                      L.BF16, kp, L.stream()), "attn_fwd")
+                                      code, kp, L.stream()), "attn_fwd")
 
     def bwd():
         L.check(lib.esgpt_attn_bwd_ex(base, base + D * es, base + 2 * D * es, 3 * D, Lq, bufs["o"].data_ptr(), D,
                                       bufs["do"].data_ptr(), D, bufs["lse"].data_ptr(), m, m, dbase, dbase + D * es,
                                       dbase + 2 * D * es, 3 * D, B, H, Lq, Lq, hd, 0, p, bufs["seed"].data_ptr(), kp,
-                                      L.BF16, bufs["ws"].data_ptr(), nbytes, cnt.data_ptr(), L.stream()), "attn_bwd")
+                                      code, bufs["ws"].data_ptr(), nbytes, cnt.data_ptr(), L.stream()), "attn_bwd")
 
     fwd()
     return fwd, bwd, bufs, cnt
 
 
-def _gemm_launchers(T, D, F, dev):
-    """c_fc on the step's shapes: forward with the bias + GELU epilogue, and its grouped backward."""
+def _gemm_launchers(T, D, F, dev, dtype=torch.bfloat16):
+    """c_fc on the step's shapes: forward with the bias + GELU epilogue, and its grouped backward (bf16 MFMA, or the
+    exact-f32 MFMA kernels of the reference-precision step)."""
     from eventstreamgpt_amd import _lib as L
     from eventstreamgpt_amd.kernels import tickets
 
     lib = L.load()
+    f32 = dtype == torch.float32
     g = torch.Generator(device=dev).manual_seed(1)
-    bufs = {"x": torch.randn(T, D, device=dev, generator=g).bfloat16(),
-            "w": (0.05 * torch.randn(F, D, device=dev, generator=g)).bfloat16(),
-            "b": torch.zeros(F, device=dev), "pre": torch.empty(T, F, device=dev, dtype=torch.bfloat16),
-            "y": torch.empty(T, F, device=dev, dtype=torch.bfloat16),
-            "dy": torch.randn(T, F, device=dev, generator=g).bfloat16(),
-            "dx": torch.empty(T, D, device=dev, dtype=torch.bfloat16),
+    bufs = {"x": torch.randn(T, D, device=dev, generator=g).to(dtype),
+            "w": (0.05 * torch.randn(F, D, device=dev, generator=g)).to(dtype),
+            "b": torch.zeros(F, device=dev), "pre": torch.empty(T, F, device=dev, dtype=dtype),
+            "y": torch.empty(T, F, device=dev, dtype=dtype),
+            "dy": torch.randn(T, F, device=dev, generator=g).to(dtype),
+            "dx": torch.empty(T, D, device=dev, dtype=dtype),
             "dw": torch.empty(F, D, device=dev), "db": torch.empty(F, device=dev)}
-    nb = lib.esgpt_linear_bwd_workspace(T, D, F, 1)
+    nb = (lib.esgpt_linear_bwd_f32_workspace if f32 else lib.esgpt_linear_bwd_workspace)(T, D, F, 1)
     bufs["ws"] = torch.empty(max(1, nb), dtype=torch.uint8, device=dev)
     cnt = tickets(torch.device(dev))
     P = {k: v.data_ptr() for k, v in bufs.items()}
 
     def fwd():
-        L.check(lib.esgpt_linear_fwd(P["x"], D, P["w"], T, D, F, P["b"], 0, P["pre"], P["y"], F, L.stream()),
+        L.check((lib.esgpt_linear_fwd_f32 if f32 else lib.esgpt_linear_fwd)(P["x"], D, P["w"], T, D, F, P["b"], 0,
+                                                                            P["pre"], P["y"], F, L.stream()),
                 "linear_fwd")
 
     def bwd():
-        L.check(lib.esgpt_linear_bwd(P["dy"], F, P["x"], D, P["w"], T, D, F, None, -1, None, 0, P["dx"], D, P["dw"],
-                                     P["db"], P["ws"], nb, cnt.data_ptr(), L.stream()), "linear_bwd")
+        if f32:
+            L.check(lib.esgpt_linear_bwd_f32(P["dy"], F, P["x"], D, P["w"], T, D, F, None, -1, None, 0, P["dx"], D,
+                                             P["dw"], P["db"], P["ws"], nb, cnt.data_ptr(), None, 0, L.stream()),
+                    "linear_bwd_f32")
+        else:
+            L.check(lib.esgpt_linear_bwd(P["dy"], F, P["x"], D, P["w"], T, D, F, None, -1, None, 0, P["dx"], D,
+                                         P["dw"], P["db"], P["ws"], nb, cnt.data_ptr(), L.stream()), "linear_bwd")
 
     return fwd, bwd, bufs
 
@@ -218,7 +229,7 @@ def _embed_bwd_launcher(model, batch):
     return bwd, keep
 
 
-def _loss_launcher(model, batch):
+def _loss_launcher(model, batch, dtype=torch.bfloat16):
     """esgpt_output_loss on the step's head layout (bf16 logits [B·L, C], every C2 loss term + TTE): count, event
     and reduce kernels. Algorithmic bytes: logits read + d(logits) written (C·2 each per row) + the batch's entries
     (idx 8 + meas 8 + value 4 + mask 1 per slot) + event mask / time delta + the position-0 bias-gradient rows."""
@@ -241,8 +252,9 @@ def _loss_launcher(model, batch):
     C += (-C) % 8
     dev = batch.device
     g = torch.Generator(device=dev).manual_seed(4)
-    zc = torch.randn(B * Lq, C, device=dev, generator=g).bfloat16()
-    bias = torch.zeros(C, device=dev).bfloat16()
+    zc = torch.randn(B * Lq, C, device=dev, generator=g).to(dtype)
+    bias = torch.zeros(C, device=dev).to(dtype)
+    code, es = (L.BF16, 2) if dtype == torch.bfloat16 else (L.F32, 4)
     dzc = torch.empty_like(zc)
     dbias = torch.empty(B, C, device=dev)
     losses = torch.empty(len(terms) + 2, device=dev)
@@ -252,12 +264,12 @@ def _loss_launcher(model, batch):
     err = err_word(dev)
 
     def fwd():
-        L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), C, 1, 1, bias.data_ptr(), zc.data_ptr(), C, L.BF16, arr,
+        L.check(lib.esgpt_output_loss(bv.ref, zc.data_ptr(), C, 1, 1, bias.data_ptr(), zc.data_ptr(), C, code, arr,
                                       len(terms), ctypes.byref(tte), dzc.data_ptr(), dzc.data_ptr(),
                                       dbias.data_ptr(), losses.data_ptr(), ws.data_ptr(), nb, err.data_ptr(),
                                       L.stream()), "output_loss")
 
-    nbytes = B * Lq * C * 2 * 2 + B * Lq * M * 21 + B * Lq * 5 + B * C * 4
+    nbytes = B * Lq * C * es * 2 + B * Lq * M * 21 + B * Lq * 5 + B * C * 4
     return fwd, float(nbytes), {"zc": zc, "dzc": dzc, "ws": ws, "arr": arr, "tte": tte}
 
 
@@ -273,6 +285,7 @@ def gemm_bwd_in_step(model, opt_cfg, batch, dtype) -> dict:
     from eventstreamgpt_amd.train import TrainStep
 
     ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=False, check_errors=False)
+    f32 = dtype == torch.float32
     fused.SHAPES["linear_bwd"].clear()
     fused.SHAPES["enabled"] = True
     try:
@@ -290,21 +303,28 @@ def gemm_bwd_in_step(model, opt_cfg, batch, dtype) -> dict:
     rows = []
     for (T, din, dout, need_dx, act, need_db), n in sorted(shapes.items()):
         g = torch.Generator(device=dev).manual_seed(T + din + dout)
-        dy = torch.randn(T, dout, device=dev, generator=g).bfloat16()
-        x = torch.randn(T, din, device=dev, generator=g).bfloat16()
-        w = torch.randn(dout, din, device=dev, generator=g).bfloat16()
-        pre = torch.randn(T, din, device=dev, generator=g).bfloat16() if act >= 0 else None
-        dx = torch.empty(T, din, device=dev, dtype=torch.bfloat16) if need_dx else None
+        dy = torch.randn(T, dout, device=dev, generator=g).to(dtype)
+        x = torch.randn(T, din, device=dev, generator=g).to(dtype)
+        w = torch.randn(dout, din, device=dev, generator=g).to(dtype)
+        pre = torch.randn(T, din, device=dev, generator=g).to(dtype) if act >= 0 else None
+        dx = torch.empty(T, din, device=dev, dtype=dtype) if need_dx else None
         dw = torch.empty(dout, din, device=dev)
         db = torch.empty(dout, device=dev) if need_db else None
-        nb = lib.esgpt_linear_bwd_workspace(T, din, dout, int(need_dx))
+        nb = (lib.esgpt_linear_bwd_f32_workspace if f32 else lib.esgpt_linear_bwd_workspace)(T, din, dout, int(need_dx))
         ws = torch.empty(max(1, nb), dtype=torch.uint8, device=dev)
 
         def fn(dy=dy, x=x, w=w, pre=pre, dx=dx, dw=dw, db=db, ws=ws, nb=nb, T=T, din=din, dout=dout, act=act):
-            L.check(lib.esgpt_linear_bwd(dy.data_ptr(), dout, x.data_ptr(), din, w.data_ptr(), T, din, dout, None, act,
-                                         L.ptr(pre), din if pre is not None else 0, L.ptr(dx),
-                                         din if dx is not None else 0, dw.data_ptr(), L.ptr(db), ws.data_ptr(), nb,
-                                         cnt.data_ptr(), L.stream()), "linear_bwd")
+            if f32:  # the reference-precision step's kernel (exact-f32 MFMA)
+                L.check(lib.esgpt_linear_bwd_f32(dy.data_ptr(), dout, x.data_ptr(), din, w.data_ptr(), T, din, dout,
+                                                 None, act, L.ptr(pre), din if pre is not None else 0, L.ptr(dx),
+                                                 din if dx is not None else 0, dw.data_ptr(), L.ptr(db),
+                                                 ws.data_ptr(), nb, cnt.data_ptr(), None, 0, L.stream()),
+                        "linear_bwd_f32")
+            else:
+                L.check(lib.esgpt_linear_bwd(dy.data_ptr(), dout, x.data_ptr(), din, w.data_ptr(), T, din, dout, None,
+                                             act, L.ptr(pre), din if pre is not None else 0, L.ptr(dx),
+                                             din if dx is not None else 0, dw.data_ptr(), L.ptr(db), ws.data_ptr(), nb,
+                                             cnt.data_ptr(), L.stream()), "linear_bwd")
 
         ms = graph_time_ms(fn)
         flops = 2.0 * T * din * dout * (2 if need_dx else 1)
@@ -316,14 +336,18 @@ def gemm_bwd_in_step(model, opt_cfg, batch, dtype) -> dict:
             "ms_per_step": tot_ms, "shapes": rows}
 
 
-def _attn_symbol(lib, fwd: bool, hd: int, Lq: int, Lk: int, ld_in: int, ld_o: int, drop: bool) -> str:
+def _attn_symbol(lib, fwd: bool, hd: int, Lq: int, Lk: int, ld_in: int, ld_o: int, drop: bool,
+                 dtype=torch.bfloat16) -> str:
     """The kernel esgpt_attn_fwd / _bwd actually launches for these arguments (the library's own dispatch rule)."""
     from eventstreamgpt_amd import _lib as L
 
-    path = lib.esgpt_attn_path(hd, Lq, Lk, Lq, ld_in, ld_o, L.BF16)
+    path = lib.esgpt_attn_path(hd, Lq, Lk, Lq, ld_in, ld_o, L.BF16 if dtype == torch.bfloat16 else L.F32)
     d = "true" if drop else "false"
     if path == 1:
         return f"attn_fwd_mfma_kernel<{hd}, {d}>" if fwd else f"attn_bwd_kernel<{hd}, {d}>"
+    if path == 3:
+        return (f"attn_fwd_f32_kernel<{hd}, {d}>" if fwd
+                else f"attn_dq_f32_kernel<{hd}, {d}> + attn_dkv_f32_kernel<{hd}, {d}>")
     if path == 2:
         return "attn_fwd_small<bf16>" if fwd else "attn_bwd_small<bf16>"
     return "attn_fwd_generic<bf16>" if fwd else "attn_bwd_dq_generic<bf16> + attn_bwd_dkv_generic<bf16>"
@@ -455,7 +479,7 @@ def _c5_embed_bf16_microbench(dev, V_big: int = 1 << 22):
     return fwd, nbytes, nnz, (table, out, batch, div)
 
 
-def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str) -> list:
+def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype=torch.bfloat16) -> list:
     """The kernels measured for this configuration, at its own shapes: (name, symbol, bound, algorithmic work per
     launch, launcher, extras). Each launcher issues exactly one launch set of the kernel."""
     from eventstreamgpt_amd import _lib as L
@@ -473,16 +497,20 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str) -> li
 
     drop = p_attn > 0
     layer = f"{cfg_name} layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"
-    fa, ba, ka, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev)
-    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop), "mfma", 4.0 * H * hd * T_pairs, fa,
+    f32 = dtype == torch.float32
+    fa, ba, ka, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev, dtype)
+    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop, dtype), "mfma", 4.0 * H * hd * T_pairs, fa,
         {"shape": layer + " (global)"}, ka)
-    add("attn_bwd", _attn_symbol(lib, False, hd, Lq, Lq, 3 * D, D, drop), "mfma", 8.0 * H * hd * T_pairs, ba,
+    add("attn_bwd", _attn_symbol(lib, False, hd, Lq, Lq, 3 * D, D, drop, dtype), "mfma", 8.0 * H * hd * T_pairs, ba,
         {"shape": layer + " (global)"}, None)
-    gf, gb, kg = _gemm_launchers(B * Lq, D, F, dev)
-    add("gemm_fc_fwd", "gemm_kernel<true, true, 3, 1, 1>", "mfma", 2.0 * B * Lq * D * F, gf,
-        {"shape": f"{cfg_name} c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"}, kg)
-    add("gemm_fc_bwd", "gemm_bwd_pair_kernel", "mfma", 4.0 * B * Lq * D * F, gb,
-        {"shape": f"{cfg_name} c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"}, None)
+    gf, gb, kg = _gemm_launchers(B * Lq, D, F, dev, dtype)
+    add("gemm_fc_fwd", "gemm_kernel<true, true, ..., F32>" if f32 else "gemm_kernel<true, true, 3, 1, 1>", "mfma",
+        2.0 * B * Lq * D * F, gf,
+        {"shape": f"{cfg_name} c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"
+                  + (", f32 operands (v_mfma_f32_32x32x2_f32)" if f32 else "")}, kg)
+    add("gemm_fc_bwd", "gemm_bwd_pair_kernel" + ("<..., F32>" if f32 else ""), "mfma", 4.0 * B * Lq * D * F, gb,
+        {"shape": f"{cfg_name} c_fc backward: dX [{B * Lq}, {D}] + dW [{F}, {D}] f32 + db, one launch"
+                  + (", f32 operands" if f32 else "")}, None)
     emb = model.encoder.input_layer.data_embedding_layer
     ci = cfg.structured_event_processing_mode == "conditionally_independent"
     if hasattr(emb, "embed_layer"):
@@ -504,9 +532,10 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str) -> li
         add("embed_split_bwd", "esgpt_embed_bag_bwd x2 (categorical + numerical selectors)", "hbm", sbb, sb,
             {"shape": f"{cfg_name}: SPLIT, G={emb.n_levels}"}, None)
     if ci:
-        lf, lbytes, kl = _loss_launcher(model, batch)
-        add("output_loss", "count_kernel + event_stream_kernel<bf16> + reduce_kernel (esgpt_output_loss)", "hbm",
-            lbytes, lf, {"shape": f"{cfg_name}: bf16 logits [{B * Lq}, {kl['zc'].shape[1]}]"}, kl)
+        lf, lbytes, kl = _loss_launcher(model, batch, dtype)
+        ln = "f32" if f32 else "bf16"
+        add("output_loss", f"count_kernel + event_stream_kernel<{ln}> + reduce_kernel (esgpt_output_loss)", "hbm",
+            lbytes, lf, {"shape": f"{cfg_name}: {ln} logits [{B * Lq}, {kl['zc'].shape[1]}]"}, kl)
     else:
         nf, nbytes, kn = _na_loss_launcher(model, batch)
         add("na_output_loss", "count_kernel + event_stream_kernel<bf16> + reduce_kernel (esgpt_output_loss, levels)",
@@ -520,11 +549,11 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str) -> li
     # long-sequence attention: MFMA efficiency once the grid fills the chip
     Bl, Ll, Hl = 4, 4096, 8
     fl, bl, kll, _ = _attention_launchers(Bl, Ll, Hl * hd, Hl, torch.ones(Bl, Ll, dtype=torch.bool, device=dev), 0.0,
-                                          dev)
+                                          dev, dtype)
     long_pairs = Bl * Ll * (Ll + 1) / 2
-    add("attn_fwd_long", _attn_symbol(lib, True, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False), "mfma",
+    add("attn_fwd_long", _attn_symbol(lib, True, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False, dtype), "mfma",
         4.0 * Hl * hd * long_pairs, fl, {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"}, kll)
-    add("attn_bwd_long", _attn_symbol(lib, False, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False), "mfma",
+    add("attn_bwd_long", _attn_symbol(lib, False, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False, dtype), "mfma",
         8.0 * Hl * hd * long_pairs, bl, {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"}, None)
     for Bd in (B, 8 * B):
         fd, dbytes, kd = _decode_launcher(Bd, H, hd, Lq, dev)
@@ -563,10 +592,11 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_c
     configuration's shapes; ``traffic`` = HBM bytes per launch set from this configuration's own PMC passes
     (profiles/pmc_traffic_<config>.json), null when that file has no entry for the kernel."""
     traffic = {}
-    if os.path.exists(pmc_file(cfg_name)):
-        with open(pmc_file(cfg_name)) as f:
+    pmc = pmc_file(cfg_name + ("" if dtype == torch.bfloat16 else "_f32"))  # counters of the same kernels only
+    if os.path.exists(pmc):
+        with open(pmc) as f:
             traffic = json.load(f).get("bytes_per_launch", {})
-    ents, keep = roofline_entries(model, cfg, batch, dev, p_attn, cfg_name)
+    ents, keep = roofline_entries(model, cfg, batch, dev, p_attn, cfg_name, dtype)
     out = []
     for e in ents:
         ms = graph_time_ms(e["fn"])
@@ -701,8 +731,9 @@ def main():
         if args.pmc_pass:
             pmc_pass(model, cfg, bc.batch(0, device=dev), dev, 0.1, args.config, args.pmc_pass)
             return
-        roofline, aux = roofline_report(model, cfg, bc.batch(0, device=dev), dev, 0.1, PEAK_BF16_TFLOPS,
-                                        cfg_name=args.config)
+        roofline, aux = roofline_report(model, cfg, bc.batch(0, device=dev), dev, 0.1,
+                                        PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS,
+                                        dtype=dtype, cfg_name=args.config)
         print(json.dumps({"roofline": roofline, "roofline_aux": aux}))
         return
     # Pre-collated batches in pinned host memory, packed like the native collate's output (one buffer per batch):

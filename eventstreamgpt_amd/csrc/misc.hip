@@ -86,6 +86,8 @@ __global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict_
   if (sc.kind == 1) {  // transformers.get_polynomial_decay_schedule_with_warmup (train.poly_decay_lambda)
     if (s < sc.warmup) f = (double)s / (double)(sc.warmup > 1 ? sc.warmup : 1);
     else if (s > sc.total) f = sc.end_lr / sc.init_lr;
+    else if (sc.total == sc.warmup) f = sc.end_lr / sc.init_lr;  // s == total == warmup: the reference's lambda
+                                                                   // divides 0 / 0 there (the host raises first)
     else f = ((sc.init_lr - sc.end_lr) * pow(1.0 - (double)(s - sc.warmup) / (double)(sc.total - sc.warmup), sc.power) +
               sc.end_lr) / sc.init_lr;
   }
@@ -97,6 +99,7 @@ __global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict_
     per_tensor[2 * t] = (float)(lr / (1.0 - pow(beta1, (double)c)));
     per_tensor[2 * t + 1] = (float)sqrt(1.0 - pow(beta2, (double)c));
   }
+  __syncthreads();  // every wave has read counters[n_params] before it advances
   if (threadIdx.x == 0) {
     counters[n_params] = s + 1;
     *lr_out = (float)lr;
@@ -224,7 +227,7 @@ int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, 
                         const int32_t* err, void* stream) {
   ESGPT_REQUIRE(counters && sched && per_tensor && lr_out && n_active >= 0 && n_params >= 0);
   ESGPT_REQUIRE(n_active == 0 || active);
-  ESGPT_REQUIRE(sched->kind == 0 || (sched->kind == 1 && sched->init_lr > sched->end_lr && sched->total > sched->warmup));
+  ESGPT_REQUIRE(sched->kind == 0 || (sched->kind == 1 && sched->init_lr > sched->end_lr && sched->total >= sched->warmup));
   esgpt::adamw_prepare_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counters, active, n_active, n_params, *sched,
                                                                        beta1, beta2, per_tensor, lr_out, err);
   ESGPT_LAUNCH_CHECK();

@@ -181,7 +181,11 @@ class FusedAdamW:
                        err_word(self.params[0].device))
 
     def state_dict(self):
-        return {"state": {i: {"step": self.steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}
+        # the step counts AdamW actually used: the device counters (a step discarded on the device — an error flag
+        # up with TrainStep(check_errors=False) — advanced the host mirror but not them); the host-argument
+        # measurement path keeps no device counters
+        steps = self.steps if self.host_args else [int(c) for c in self._counters[:-1].tolist()]
+        return {"state": {i: {"step": steps[i], "exp_avg": self.exp_avg[i], "exp_avg_sq": self.exp_avg_sq[i]}
                           for i in range(len(self.params))},
                 "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
                                   "weight_decay": self.weight_decay}]}
@@ -257,6 +261,9 @@ class GradBuckets:
                 self.bucket_of[i] = b
         self.mode = "launch"
         self.on_boundary = None
+        # gradient accumulation (TrainStep, OptimizationConfig.gradient_accumulation): the buffer already holds the
+        # window's earlier batches — a release ADDS the batch's gradients instead of copying them
+        self.add = False
         self.reset()
         self._hooks = [params[i].register_post_accumulate_grad_hook(self._make_hook(i)) for i in range(len(params))]
 
@@ -302,18 +309,25 @@ class GradBuckets:
             for i in idx:
                 p, v = self.params[i], self.views[i]
                 if p.grad is None:
-                    v.zero_()
+                    if not self.add:
+                        v.zero_()
                 elif p.grad.data_ptr() != v.data_ptr():
                     src.append(p.grad)
                     dst.append(v)
             if src:
-                torch._foreach_copy_(dst, src)
+                if self.add:
+                    torch._foreach_add_(dst, src)
+                else:
+                    torch._foreach_copy_(dst, src)
             for i in idx:
                 self.params[i].grad = self.views[i]
             if b == len(self.buckets) - 1:  # this rank's verdict on its step: 1 = a device error flag is up
                 if self.err_check:
+                    # the flag word or the sticky word: an earlier batch of an accumulation window that failed
+                    # holds only the sticky word by now (symmetric across ranks otherwise: a failed exchange
+                    # raised the peer flag on every rank)
                     ew = err_word(dev)[0:1]
-                    self.slot.copy_(torch.bitwise_and(ew, 0xFFFFFFFF).ne(0))
+                    self.slot.copy_(ew.ne(0))
                 else:
                     self.slot.zero_()
             seg = self.flat[s:e]
@@ -398,7 +412,14 @@ class TrainStep:
         # the optimizer step as its own graph replayed after the step's segments (no host launch per step). Off by
         # default: measured on the C2 step, same box, alternating runs, it costs ~10 us (1.7118 / 1.7115 vs 1.6981 /
         # 1.7045 ms) — the extra graph launch costs more than the two kernel launches it replaces.
-        self.capture_optimizer = capture_optimizer
+        # gradient accumulation (generative_modeling.py:661-664: Lightning's accumulate_grad_batches): each batch's
+        # backward is seeded with 1 / k (Lightning normalises the closure loss), the gradients of k batches are
+        # summed, and the optimizer / LR schedule step (and, under DDP, the exchange) happen on every k-th batch
+        self.accum = max(1, int(opt_cfg.gradient_accumulation or 1))
+        self._micro = 0  # batches already accumulated in the current window
+        self._acc = None  # (flat f32 buffer, per-parameter views) without DDP; GradBuckets' buffer under DDP
+        self._touched: set = set()  # parameters that received a gradient in the current window
+        self.capture_optimizer = capture_optimizer and self.accum == 1
         self.graphs: dict = {}  # shape signature -> (segments, static batch, static loss, grads) | None (eager)
         self.capture_report: dict = {}  # shape signature -> ATen GEMMs / reductions seen in its warm-up pass
         self.check_errors = check_errors and dev.type == "cuda"
@@ -425,8 +446,44 @@ class TrainStep:
         reads it in place)."""
         one = getattr(self, "_one", None)
         if one is None or one.shape != loss.shape or one.dtype != loss.dtype or one.device != loss.device:
-            one = self._one = torch.ones_like(loss)
+            one = self._one = torch.full_like(loss, 1.0 / self.accum)
         return one
+
+    # ---- gradient accumulation -------------------------------------------------------------------------------
+    def _acc_views(self):
+        if self.grad_buckets is not None:
+            return self.grad_buckets.views
+        if self._acc is None:
+            flat = torch.zeros(sum(p.numel() for p in self.params), dtype=torch.float32, device=self.device)
+            views, off = {}, 0
+            for i, p in enumerate(self.params):
+                views[i] = flat[off: off + p.numel()].view_as(p)
+                off += p.numel()
+            self._acc = (flat, views)
+        return self._acc[1]
+
+    @torch.no_grad()
+    def _accumulate(self):
+        """Adds this batch's gradients into the window's buffer (one multi-tensor add; torch's accumulate order)."""
+        views = self._acc_views()
+        src, dst = [], []
+        for i, p in enumerate(self.params):
+            if p.grad is not None:
+                src.append(p.grad)
+                dst.append(views[i])
+                self._touched.add(i)
+        if src:
+            torch._foreach_add_(dst, src)
+
+    @torch.no_grad()
+    def _reset_accumulation(self):
+        self._micro = 0
+        self._touched.clear()
+        if self.accum > 1:
+            if self.grad_buckets is not None:
+                self.grad_buckets.flat.zero_()
+            elif self._acc is not None:
+                self._acc[0].zero_()
 
     @staticmethod
     def _make_accumulate_guard(p):
@@ -548,22 +605,27 @@ class TrainStep:
     def _raise_pending(self, keep: int):
         """Raises the first device error among submitted steps, waiting only for steps older than the newest
         ``keep`` (``keep = 0``: all of them)."""
-        while len(self._pending) > keep or (self._pending and self._pending[0][0].query()):
-            ev, host, batch, active = self._pending.popleft()
+        # Under DDP a step's error is raised exactly at the submission of step k + 2 (or at check()), never earlier
+        # because its event happens to have completed: every rank then raises at the same step, whatever its
+        # timing, and no rank runs step k + 1's collectives alone.
+        while len(self._pending) > keep or (not self.distributed and self._pending and self._pending[0][0].query()):
+            ev, host, batch, active, stepped = self._pending.popleft()
             ev.synchronize()
             code, mx = int(host[0]), int(host[1])
             if code & 0xFFFFFFFF:
                 # the failing step's AdamW was a no-op on the device, and so is every step queued behind it (the
                 # sticky word): take back their step counts and LR steps. The block is cleared after them in
                 # stream order.
-                discarded = [active] + [e[3] for e in self._pending]
+                discarded = [(active, stepped)] + [(e[3], e[4]) for e in self._pending]
                 self._pending.clear()
                 err_word(self.device).zero_()
-                for act in discarded:
+                for act, st in discarded:
                     if isinstance(self.opt, FusedAdamW):
                         for i in act:
                             self.opt.steps[i] -= 1
-                    self.sched_step -= 1
+                    if st:
+                        self.sched_step -= 1
+                self._reset_accumulation()  # the window's partial sums belong to the discarded batches
                 raise_for_error(code, mx, self._vocab, batch)
 
     def prefetch(self, batch: PytorchBatch) -> None:
@@ -619,10 +681,21 @@ class TrainStep:
                 self._capture(batch)
             entry = self.graphs.get(sig)
         gb = self.grad_buckets
+        accumulating = self.accum > 1
+        last = self._micro + 1 >= self.accum  # this batch closes the accumulation window: exchange + step
+        exchange = gb is not None and last
+        if gb is not None:
+            gb.add = accumulating
         opt_graph = plan = None
         if entry is None:
             self.opt.zero_grad(set_to_none=True)
-            loss = self._fwd_bwd(batch)
+            if gb is not None and not exchange:
+                gb.mode = "off"  # Lightning's no_sync on the window's earlier batches
+            try:
+                loss = self._fwd_bwd(batch)
+            finally:
+                if gb is not None:
+                    gb.mode = "launch"
         else:
             segs, static, sloss, grads, opt_graph, plan = entry
             static.copy_(batch, non_blocking=True)
@@ -633,14 +706,31 @@ class TrainStep:
                 p.grad = gr
             for g, released in segs:
                 g.replay()
-                if gb is not None:  # exchanged while the next segment replays
+                if exchange:  # exchanged while the next segment replays
                     for b in released:
                         gb._launch(b)
             # the next replay overwrites the static loss: hand back a copy, made by an elementwise kernel (x * 1 is
             # exact) rather than clone()'s D2D blit, which costs ~5 us of device time for 4 bytes
             loss = sloss.mul(1.0)
+        if accumulating and not exchange:
+            self._accumulate()  # into the window's buffer (GradBuckets' under DDP)
+        if not last:
+            self._micro += 1
+            if self._release is not None:
+                self._release.record()
+                self._release = None
+            if self.check_errors:
+                self._record_pending(host_batch, [], False)
+            return loss
+        self._micro = 0
         if gb is not None:
             gb.finish()
+        elif accumulating:  # the window's sums are the gradients AdamW reads
+            views = self._acc_views()
+            for i, p in enumerate(self.params):
+                p.grad = views[i] if i in self._touched else None
+        if self.sched is None and self.sched_step == self.lr_lambda_warm_total():
+            self.lr_lambda(self.sched_step)  # warmup == total: the reference's lambda raises ZeroDivisionError here
         if opt_graph is not None:
             opt_graph.replay()
             self.opt.note_step(plan["active"])
@@ -654,16 +744,28 @@ class TrainStep:
             self.sched.step()
             active = []
         self.sched_step += 1
+        if accumulating:
+            self._reset_accumulation()  # stream-ordered after the optimizer's reads
         if self._release is not None:  # the staging buffer may be refilled once this step has consumed it
             self._release.record()
             self._release = None
         if self.check_errors:
-            host = torch.empty(2, dtype=torch.int64, pin_memory=True)
-            host.copy_(err_word(self.device), non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            self._pending.append((ev, host, host_batch, active))
+            self._record_pending(host_batch, active, True)
         return loss
+
+    def _record_pending(self, host_batch, active, stepped: bool):
+        host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        host.copy_(err_word(self.device), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._pending.append((ev, host, host_batch, active, stepped))
+
+    def lr_lambda_warm_total(self) -> int:
+        """The schedule step at which warmup == max_training_steps makes the reference's lambda divide 0 / 0
+        (-1: never)."""
+        total = self.cfg.max_training_steps or 1_000_000
+        warm = self.cfg.lr_num_warmup_steps or 0
+        return total if total == warm else -1
 
     def check(self):
         """Waits for every submitted step and raises the first device error (the reference's exception)."""

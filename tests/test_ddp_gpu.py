@@ -284,3 +284,45 @@ def test_rccl_exchange_single_rank_matches_no_ddp():
     # equal to f32 rounding: the segmented capture flushes the deferred LayerNorm column sums at each segment
     # boundary, a different launch grouping of the same sums (measured: 7.5e-9 after three steps)
     assert diff < 1e-6, diff
+
+
+def _worker_peer_error_no_check(rank, world, port, q):
+    """As _worker_peer_error, but without check() between steps: the error of step k must be raised on BOTH ranks at
+    the submission of step k + 2, never earlier on one rank because its event happened to be complete (then the
+    other rank would run step k + 1's collectives alone)."""
+    import datetime
+    import traceback
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+        from eventstreamgpt_amd.train import TrainStep
+
+        bc, m, opt = _setup()
+        ts = TrainStep(m, opt, torch.bfloat16, use_graph=True, bucket_mb=0.05)
+        batches = [bc.batch(10 * rank + s, batch_size=8) for s in range(6)]
+        if rank == 1:
+            batches[1].dynamic_indices[2, 3, 0] = m.config.vocab_size + 5
+        batches = [b.to("cuda:0").packed() for b in batches]
+        raised_at = []
+        for i, b in enumerate(batches):
+            torch.cuda.synchronize()  # every earlier step's event is complete when step i is submitted
+            try:
+                ts.step(b)
+            except (AssertionError, RuntimeError) as e:
+                raised_at.append((i, type(e).__name__))
+        ts.check()
+        q.put(("done", rank, (raised_at, {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()})))
+        dist.destroy_process_group()
+    except BaseException:
+        q.put(("error", rank, traceback.format_exc()))
+        raise
+
+
+def test_device_error_raised_at_the_same_step_on_every_rank_without_check():
+    res = _run_ranks(_worker_peer_error_no_check)
+    assert res[1][0] == [(3, "AssertionError")], res[1][0]
+    assert res[0][0] == [(3, "RuntimeError")], res[0][0]
+    for k in res[0][1]:  # in lockstep afterwards
+        assert (torch.from_numpy(res[0][1][k]).float() - torch.from_numpy(res[1][1][k]).float()).abs().max() == 0, k

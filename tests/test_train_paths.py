@@ -481,3 +481,123 @@ def test_captured_optimizer_step_matches_host_launched():
     for k in out[False][0]:
         assert torch.equal(out[False][0][k], out[True][0][k]), k
     assert out[False][1] == out[True][1] and out[False][2] == out[True][2]
+
+
+def test_gradient_accumulation_single_process_cpu():
+    """OptimizationConfig.gradient_accumulation = 3 (Lightning's accumulate_grad_batches, generative_modeling.py:661-664)
+    without DDP: the optimizer and the LR schedule step once per 3 batches on the sum of the 3 batches' gradients of
+    loss / 3; a parameter that receives no gradient in a window is skipped."""
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(6, 5)
+            self.b = torch.nn.Linear(5, 3)
+            self.unused = torch.nn.Linear(2, 2)
+
+        def forward(self, x):
+            class Out:
+                pass
+
+            o = Out()
+            o.loss = self.b(torch.tanh(self.a(x))).pow(2).mean()
+            return o
+
+    from eventstreamgpt_amd.train import poly_decay_lambda
+
+    def data(i):
+        return torch.randn(4 + i, 6, generator=torch.Generator().manual_seed(77 + i))
+
+    k, windows = 3, 2
+    cfg = OptimizationConfig(init_lr=0.05, lr_num_warmup_steps=1, max_training_steps=8, gradient_accumulation=k)
+    torch.manual_seed(0)
+    m = Toy()
+    ts = TrainStep(m, cfg, compute_dtype=torch.float32)
+    losses = []
+    for i in range(k * windows):
+        losses.append(float(ts.step(data(i))))
+        assert ts.sched_step == (i + 1) // k
+    torch.manual_seed(0)
+    ref = Toy()
+    opt = torch.optim.AdamW(ref.parameters(), lr=cfg.init_lr, weight_decay=cfg.weight_decay)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, poly_decay_lambda(1, 8, 1.0, cfg.init_lr, cfg.end_lr))
+    for w in range(windows):
+        opt.zero_grad(set_to_none=True)
+        for i in range(w * k, (w + 1) * k):
+            loss = ref(data(i)).loss
+            assert float(loss) == pytest.approx(losses[i], rel=1e-6)
+            (loss / k).backward()
+        opt.step()
+        sched.step()
+    for (name, a), b in zip(m.state_dict().items(), ref.state_dict().values()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=name)
+    assert m.unused.weight.grad is None  # never touched: AdamW skipped it, as torch does
+
+
+def test_warmup_not_below_total_schedule():
+    """lr_num_warmup_steps >= max_training_steps: the reference schedule never reaches its decay branch when warmup
+    exceeds total, and divides 0 / 0 at step == warmup == total (transformers raises ZeroDivisionError there)."""
+    from transformers import get_polynomial_decay_schedule_with_warmup
+
+    from eventstreamgpt_amd.train import poly_decay_lambda
+
+    f = poly_decay_lambda(6, 4, 1.0, 1e-3, 1e-6)
+    opt = torch.optim.AdamW([torch.nn.Parameter(torch.zeros(1))], lr=1e-3)
+    sched = get_polynomial_decay_schedule_with_warmup(opt, num_warmup_steps=6, num_training_steps=4, lr_end=1e-6)
+    for step in range(10):
+        assert 1e-3 * f(step) == pytest.approx(opt.param_groups[0]["lr"], rel=1e-12), step
+        opt.step()
+        sched.step()
+    g = poly_decay_lambda(3, 3, 1.0, 1e-3, 1e-6)
+    with pytest.raises(ZeroDivisionError):
+        g(3)
+
+
+@pytest.mark.gpu
+def test_gradient_accumulation_graph_matches_eager_and_reference():
+    """gradient_accumulation = 2 on the GPU: the HIP-graph step (gradients summed into the window buffer after each
+    replay) equals the eager step, and both equal a hand-written loop (backward of loss / 2 per batch, summed
+    gradients, FusedAdamW at the schedule's lr once per window)."""
+    from eventstreamgpt_amd.train import FusedAdamW
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C1"]
+    cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+    opt_cfg = OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=1, max_training_steps=50, gradient_accumulation=2)
+    batches = [bc.batch(s, batch_size=8, device="cuda:0").packed() for s in range(4)]
+
+    def run(graph):
+        torch.manual_seed(0)
+        m = CIPPTForGenerativeSequenceModeling(cfg).to("cuda:0").train()
+        ts = TrainStep(m, opt_cfg, torch.bfloat16, use_graph=graph)
+        for b in batches:
+            ts.step(b)
+        ts.check()
+        assert ts.sched_step == 2 and {s for s in ts.opt.steps if s} == {2}
+        return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+    got_graph, got_eager = run(True), run(False)
+    torch.manual_seed(0)
+    m = CIPPTForGenerativeSequenceModeling(cfg).to("cuda:0").train()
+    params = [p for p in m.parameters() if p.requires_grad]
+    opt = FusedAdamW(params, lr=opt_cfg.init_lr, weight_decay=opt_cfg.weight_decay)
+    from eventstreamgpt_amd.train import poly_decay_lambda
+
+    lam = poly_decay_lambda(1, 50, 1.0, opt_cfg.init_lr, opt_cfg.end_lr)
+    for w in range(2):
+        acc = [torch.zeros_like(p) for p in params]
+        for b in batches[2 * w: 2 * w + 2]:
+            for p in params:
+                p.grad = None
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = m(b).loss
+            (loss / 2).backward()
+            for a, p in zip(acc, params):
+                if p.grad is not None:
+                    a += p.grad
+        for a, p in zip(acc, params):
+            p.grad = a
+        opt.step(opt_cfg.init_lr * lam(w))
+    want = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    for k in want:
+        assert (got_graph[k].float() - got_eager[k].float()).abs().max().item() < 1e-6, k
+        assert (got_graph[k].float() - want[k].float()).abs().max().item() < 1e-5, k
