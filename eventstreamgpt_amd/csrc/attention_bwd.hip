@@ -23,14 +23,18 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "attn_common.h"
 
 using namespace esgpt;
+using namespace esgpt::attnb;
+
+int esgpt_attn_bwd_mfma_split(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                              int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask,
+                              const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
+                              int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
+                              const uint32_t* keep, int keys_per_wg, hipStream_t st);
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 #ifdef ESGPT_STAMPS
 __device__ uint64_t g_stamps[64];
@@ -46,77 +50,6 @@ constexpr int KB = 256;      // keys per workgroup
 constexpr int NW = 8;        // waves
 constexpr int THREADS = 64 * NW;
 
-__device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ bf16x8 zero8() {
-  bf16x8 z;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) z[i] = (__bf16)0.f;
-  return z;
-}
-
-__device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)p);
-}
-
-__device__ __forceinline__ bf16x8 join(bf16x4 lo, bf16x4 hi) {
-  bf16x8 f;
-  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
-  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
-  return f;
-}
-
-// Accumulator registers 8s..8s+7 -> bf16 operand fragment (permuted k order).
-__device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
-  bf16x8 f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = (__bf16)x[8 * s + j];
-  return f;
-}
-
-__device__ __forceinline__ int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
-
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  const __bf16 a = (__bf16)lo, b = (__bf16)hi;
-  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-}
-
-// Stores the 32 accumulator-row values of one lane's column (x[i] = row acc_row(i, h)) as bf16 into
-// dst[0 .. 31] with 16-B stores: register groups g and g+1 are joined across the half-waves with
-// v_permlane32_swap (lanes 0-31 end up with rows 8g..8g+7, lanes 32-63 with rows 8g+8..8g+15). N = 16: rows 0..15.
-template <int N = 32>
-__device__ __forceinline__ void store_col32(__bf16* dst, const f32x16& x, int h) {
-#pragma unroll
-  for (int g = 0; g < N / 8; g += 2) {
-    uint32_t a0 = pack2(x[4 * g], x[4 * g + 1]), a1 = pack2(x[4 * g + 2], x[4 * g + 3]);
-    uint32_t b0 = pack2(x[4 * g + 4], x[4 * g + 5]), b1 = pack2(x[4 * g + 6], x[4 * g + 7]);
-    const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-    const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-    *reinterpret_cast<uint4*>(dst + 8 * g + 8 * h) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-  }
-}
-
-// LDS images with W bf16 columns per row, unpadded, 16-B chunks XOR-swizzled per row so that BOTH access kinds
-// are bank-conflict free: 16-B row reads (ds_read_b128: lane r reads row r, one chunk; 16-lane groups
-// {0-3,12-15,20-27} / {4-11,16-19,28-31}) and transposed reads (ds_read_b64_tr_b16: a 32-lane half reads 4
-// consecutive rows x 32 columns), plus 8-B stores of 16 consecutive rows at one column.
-//   W = 32  (64-B rows):  chunk ^ ((row >> 2) & 3)
-//   W = 64  (128-B rows): chunk ^ g(row >> 1),  g(m) = ((m & 1) << 2) | ((m >> 1) & 3)
-//   W = 128 (256-B rows): chunk ^ (((row & 3) << 2) | ((row >> 2) & 3))
-// off(row, col) is an element offset; col % 4 == 0 (8-B accesses stay inside one chunk).
-template <int W>
-struct Img {
-  __device__ __forceinline__ static int off(int row, int col) {
-    int sw;
-    if (W == 32) sw = (row >> 2) & 3;
-    else if (W == 64) sw = (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
-    else sw = ((row & 3) << 2) | ((row >> 2) & 3);
-    return row * W + (((col >> 3) ^ sw) << 3) + (col & 7);
-  }
-};
-
 template <int HD>
 struct Cfg {
   static constexpr int HDP = HD < 32 ? 32 : HD;   // image / accumulator width (hd = 16: zero-padded to 32)
@@ -126,8 +59,6 @@ struct Cfg {
   static constexpr int LDS_BYTES = 2 * (KB * HDP + 2 * QT * HDP + KB * QT) + 4 * QT * NKW + 8 * QT;
 };
 
-// Dropout in the backward: none, regenerated from the counter hash, or the forward's keep bits.
-enum : int { DROP_NONE = 0, DROP_HASH = 1, DROP_BITS = 2 };
 
 // Query tile j (counted from the first tile that can see the key block) of split s out of S: S = 1 takes every
 // tile; S = 2 deals the tiles zig-zag (s = 0: 0, 3, 4, 7, 8, …; s = 1: 1, 2, 5, 6, …), so that under a causal mask
@@ -149,7 +80,7 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
     __bf16* __restrict__ dq, __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d,
     float* __restrict__ dq32, int H, int Lq, int Lk, int window, float drop_p, const uint64_t* __restrict__ seed,
     const uint32_t* __restrict__ keep, int nw, int nsplit, int32_t* __restrict__ xcnt, float* __restrict__ xbuf,
-    int64_t dq_slab) {
+    int64_t dq_slab, int order) {
   using C = Cfg<HD>;
   constexpr int QT = C::QT, HDP = C::HDP, NKW = C::NKW;
   constexpr bool DROP = DM != DROP_NONE, bits = DM == DROP_BITS;
@@ -167,13 +98,22 @@ __global__ __launch_bounds__(THREADS) void attn_bwd_kernel(
 
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;  // transposed-read lane roles
   const int nxb = ((Lk + KB - 1) / KB) * nsplit;       // workgroups per (batch, head)
-  const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the key-block halves of one (batch, head) share an XCD
-  const int bh = lin / nxb, b = bh / H, hh = bh % H;
+  // order 0: XCD-contiguous runs per (batch, head); order 1: the (batch, head)s of one XCD kept together and their
+  // key blocks dealt longest causal chain (first block) first, the two halves of a split block adjacent
+  int bh, item;
+  if (order == 1) {
+    deal(blockIdx.x, gridDim.x, (int)(gridDim.x / nxb), item, bh);
+  } else {
+    const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the key-block halves of one (batch, head) share an XCD
+    bh = lin / nxb;
+    item = lin % nxb;
+  }
+  const int b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const bool idx32 = (uint64_t)(gridDim.x / nxb) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;  // B·H = grid / nxb
   const int off = Lk - Lq;
-  const int kblk = (lin % nxb) / nsplit;
-  const int split = (lin % nxb) % nsplit, S = nsplit;  // this workgroup's share of the query tiles
+  const int kblk = item / nsplit;
+  const int split = item % nsplit, S = nsplit;  // this workgroup's share of the query tiles
   const int kb0 = kblk * KB;
   const int kw0 = kb0 + 32 * wave;  // this wave's first key
   const int key = kw0 + r;
@@ -558,11 +498,31 @@ int set_lds_attr() {
              : 1;
 }
 
+// The split backward (attention_bwd2.hip: dK / dV kernel + dQ kernel, no partial sums) for more than one key block
+// of the fused kernel, where that kernel's per-key-block f32 dQ partials dominate its traffic. ESGPT_ATTN_BWD_SPLIT2
+// tuning hook (read once): 0 = never, 1 = always, 64 / 128 = always with that many keys per dK / dV workgroup.
+int split2_keys(int64_t Lk, int64_t hd) {
+  static const int forced = [] {
+    const char* e = tuning_env("ESGPT_ATTN_BWD_SPLIT2");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced == 0) return 0;
+  if (forced == 64 || forced == 128) return forced;
+  if (forced == 1) return 128;
+  // measured (tools/attn_split_ab.py, profiles/r05_attn_split_ab.log): faster past one key block at hd = 16 and 128
+  // (L = 520 local-40: 20.0 -> 15.6 us; L = 600: 161.6 -> 118.9 us), slower at hd = 32 / 64 (L = 4096 hd = 64:
+  // 488 -> 520 us; C5 L = 1024: 105.8 -> 106.8 us, 124.8 -> 133.7 us with dropout)
+  return (Lk > KB && (hd == 16 || hd == 128)) ? 128 : 0;
+}
+
 template <int HD>
 int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o, int64_t ld_o,
            const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask, void* dq,
            void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t window,
            float drop_p, const uint64_t* seed, const uint32_t* keep, float* dq32, int32_t* counters, hipStream_t st) {
+  if (const int kpw = split2_keys(Lk, HD))
+    return esgpt_attn_bwd_mfma_split(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H,
+                                     Lq, Lk, HD, window, drop_p, seed, keep, kpw, st);
   constexpr int lds = Cfg<HD>::LDS_BYTES;
   static bool attr = false;
   if (!attr) {
@@ -593,6 +553,10 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   const bool want_split = forced_split ? forced_split == 2 : (nkb * B * H < n_cu || chain > 1024);
   const int nsplit = (counters && Lq > Cfg<HD>::QT && want_split) ? 2 : 1;
   const int64_t slab = B * H * Lq * HD;  // one f32 dQ partial per key block (nkb > 1)
+  static const int order = [] {  // workgroup order: ESGPT_ATTN_ORDER tuning hook, read once
+    const char* e = tuning_env("ESGPT_ATTN_ORDER");
+    return e ? atoi(e) : 1;  // longest chain first: profiles/r05_attn_order_ab.log
+  }();
   float* xbuf = dq32 + (nkb > 1 ? (size_t)(nkb * slab) : 0);
   const dim3 grid((unsigned)(nkb * nsplit * B * H));  // 1-D: XCD-aware order in the kernel
   const int nw = (int)cdiv(Lk, 32);
@@ -600,7 +564,7 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   attn_bwd_kernel<HD, DM_><<<grid, THREADS, lds, st>>>(                                                           \
       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (const __bf16*)o, ld_o, (const __bf16*)dout, \
       ld_do, lse, kmask, qmask, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, ld_d, acc, (int)H, (int)Lq, (int)Lk,         \
-      (int)window, drop_p, seed, keep, nw, nsplit, counters, xbuf, slab)
+      (int)window, drop_p, seed, keep, nw, nsplit, counters, xbuf, slab, order)
   if (!(drop_p > 0.f)) ESGPT_ATTN_BWD_LAUNCH(DROP_NONE);
   else if (keep) ESGPT_ATTN_BWD_LAUNCH(DROP_BITS);
   else ESGPT_ATTN_BWD_LAUNCH(DROP_HASH);
@@ -623,6 +587,7 @@ extern "C" int esgpt_debug_stamps(uint64_t* out) {
 
 // f32 dQ partials, one per key block (more than one key block) + the dK / dV exchange slabs of the query-split pairs.
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
+  if (split2_keys(Lk, hd)) return 0;  // the split backward needs none
   const size_t dq = Lk > KB ? sizeof(float) * (size_t)(cdiv(Lk, KB) * B * H * Lq * hd) : 0;
   const int64_t hdp = hd < 32 ? 32 : hd;  // exchange slabs hold the padded accumulator tiles
   return dq + sizeof(float) * (size_t)(B * H * cdiv(Lk, KB)) * 2 * KB * hdp;

@@ -15,6 +15,7 @@
 // query half splitting its key tiles by parity; K/V tiles of 64 rows are staged in LDS in pairs. Causal /
 // local-window / fully-padded key tiles are skipped.
 // Roofline: MFMA-bound at large L (algorithmic FLOPs: fwd 4*H*hd*T, bwd 8*H*hd*T, T = allowed (q,k) pairs).
+#include "attn_common.h"
 #include "common.h"
 
 using namespace esgpt;
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
                                                                const uint8_t* __restrict__ qmask, int H, int Lq,
                                                                int Lk, int window, float drop_p,
                                                                const uint64_t* __restrict__ seed,
-                                                               uint32_t* __restrict__ keep, int nw) {
+                                                               uint32_t* __restrict__ keep, int nw, int order) {
   constexpr int HDP = HD < 32 ? 32 : HD;           // output (P·V) width: hd = 16 runs one 32-wide tile
   constexpr int NP = HD + 8, VLD = VImg<HD>::LD;
   constexpr int CH = HD / 8;                        // 16-B chunks per row
@@ -144,12 +145,23 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int qh = wave & 1, kp = wave >> 1;
   const int nqb = (Lq + ROWS - 1) / ROWS;
-  const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the query blocks of one (batch, head) share an XCD
-  const int bh = lin / nqb, b = bh / H, hh = bh % H;
+  // order 0: XCD-contiguous runs, query blocks ascending per (batch, head); order 1: the (batch, head)s of one XCD
+  // kept together and their query blocks dealt longest causal chain (last block) first
+  int bh, qbi;
+  if (order == 1) {
+    int rank;
+    esgpt::attnb::deal(blockIdx.x, gridDim.x, (int)(gridDim.x / nqb), rank, bh);
+    qbi = nqb - 1 - rank;
+  } else {
+    const int lin = xcd_linear(blockIdx.x, gridDim.x);  // the query blocks of one (batch, head) share an XCD
+    bh = lin / nqb;
+    qbi = lin % nqb;
+  }
+  const int b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
   const bool idx32 = (uint64_t)(gridDim.x / nqb) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;  // B·H = grid / nqb
   const int off = Lk - Lq;
-  const int qb = (lin % nqb) * ROWS;
+  const int qb = qbi * ROWS;
   const int qi = qb + qh * 32 + r;
   const bool qin = qi < Lq;
   const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
@@ -393,6 +405,16 @@ bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, i
   return (ld_in % 8 == 0) && (ld_o % 8 == 0) && (tq >= Lq);
 }
 
+// Workgroup order (ESGPT_ATTN_ORDER tuning hook, read once; see attn_fwd_mfma_kernel)
+static int attn_order() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = tuning_env("ESGPT_ATTN_ORDER");
+    v = e ? atoi(e) : 1;  // measured (tools/attn_order_ab.sh, profiles/r05_attn_order_ab.log): order 1 wins everywhere
+  }
+  return v;
+}
+
 template <int HD>
 static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, const void* v, int64_t ld_in,
                        int64_t tq, void* o, int64_t ld_o, float* lse, const uint8_t* kmask, const uint8_t* qmask,
@@ -403,11 +425,13 @@ static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, 
     attn_fwd_mfma_kernel<HD, true><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k,
                                                                     (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o,
                                                                     lse, kmask, qmask, (int)H, (int)Lq, (int)Lk,
-                                                                    (int)window, drop_p, seed, keep, nw);
+                                                                    (int)window, drop_p, seed, keep, nw,
+                                                                    attn_order());
   else
   attn_fwd_mfma_kernel<HD, false><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                                                            ld_in, tq, (__bf16*)o, ld_o, lse, kmask, qmask, (int)H,
-                                                           (int)Lq, (int)Lk, (int)window, drop_p, seed, nullptr, nw);
+                                                           (int)Lq, (int)Lk, (int)window, drop_p, seed, nullptr, nw,
+                                                           attn_order());
 }
 
 int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, void* o, int64_t ld_o,
