@@ -464,10 +464,16 @@ def _c5_embed_bf16_microbench(dev, V_big: int = 1 << 22):
     lib = L.load()
     bv = batch_view(batch)
     err = err_word(dev)
-    flags = L.EMB_STATIC | L.EMB_TIME
+    # as the input-layer operator runs it: the event times once per subject (esgpt_event_times), then the bag kernel
+    # reading them as absolute times (both launches timed)
+    times = torch.empty(batch.event_mask.shape, device=dev)
+    tv = batch_view(batch)
+    tv.struct.time_abs = times.data_ptr()
+    flags = L.EMB_STATIC | L.EMB_TIME | L.EMB_TIME_ABS
 
     def fwd():
-        L.check(lib.esgpt_embed_joint_fwd_ex(bv.ref, None, table.data_ptr(), L.BF16, V_big, D, div.data_ptr(),
+        L.check(lib.esgpt_event_times(tv.ref, times.data_ptr(), L.stream()), "event_times")
+        L.check(lib.esgpt_embed_joint_fwd_ex(tv.ref, None, table.data_ptr(), L.BF16, V_big, D, div.data_ptr(),
                                              div.data_ptr(), flags, 0.5, 0.5, out.data_ptr(), err.data_ptr(),
                                              L.stream()), "embed_bf16")
 
@@ -476,7 +482,7 @@ def _c5_embed_bf16_microbench(dev, V_big: int = 1 << 22):
     nnz = float((em.unsqueeze(-1) & (batch.dynamic_indices > 0)).sum())
     S = batch.static_indices.shape[1]
     nbytes = nnz * D * 2 + B * Lq * M * 21 + B * Lq * D * 4 + float(em.sum()) * S * D * 2 + B * Lq * 5
-    return fwd, nbytes, nnz, (table, out, batch, div)
+    return fwd, nbytes, nnz, (table, out, batch, div, times)
 
 
 def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype=torch.bfloat16) -> list:
@@ -543,7 +549,7 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype
                                          f"TTE rows [{kn['zt'].shape[0]}, {kn['zt'].shape[1]}]"}, kn)
     if cfg_name in ("C2", "C5"):
         cf, cbytes, nnz5, kc = _c5_embed_bf16_microbench(dev)
-        add("embed_c5_bf16_microbench", "embed_joint_fwd_kernel<4, 1, bf16>", "hbm", cbytes, cf,
+        add("embed_c5_bf16_microbench", "event_times_kernel + embed_joint_fwd_kernel<4, 1, bf16>", "hbm", cbytes, cf,
             {"shape": f"C5 batch shape B=128, L=1024, M=32, nnz={int(nnz5)}, indices uniform over a bf16 table "
                       "V=2^22 x 256 (2 GiB, 8x the Infinity Cache); per-occurrence bytes"}, kc)
     # long-sequence attention: MFMA efficiency once the grid fills the chip

@@ -87,6 +87,7 @@ SIGNATURES = {
     "esgpt_pack": (_int, [_vp, _i64, _vp]),
     "esgpt_embed_joint_fwd": (_int, [_PB, _PK, _vp, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_attn_path": (_int, [_i64, _i64, _i64, _i64, _i64, _i64, _int]),
+    "esgpt_event_times": (_int, [_PB, _vp, _vp]),
     "esgpt_embed_joint_fwd_ex": (_int, [_PB, _PK, _vp, _int, _i64, _i64, _vp, _vp, _int, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_embed_split_bags_fwd": (_int, [_PB, _PK, _vp, _i64, _vp, _i64, _i64, _int, _f32, _f32, _f32, _vp, _vp,
                                           _vp]),

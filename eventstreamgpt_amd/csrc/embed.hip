@@ -151,6 +151,31 @@ __device__ __forceinline__ float time_enc(float t, int64_t d, const float* sin_d
   return (d & 1) ? cosf(t * cos_div[d >> 1]) : sinf(t * sin_div[d >> 1]);
 }
 
+// The encodings of dims d0 .. d0+VEC-1 (d0 even): the sine and cosine of one frequency share one sincosf (one
+// argument reduction, the same results as sinf / cosf) when the two divisor tables agree there (they are one tensor
+// in the reference, TemporalPositionEncoding); the libm argument reductions of t·w at large event times were 40 us
+// of the 2 GiB-table microbench (C5 shape).
+template <int VEC>
+__device__ __forceinline__ void time_enc_vec(float t, int64_t d0, int64_t D, const float* sin_div, const float* cos_div,
+                                             float (&te)[VEC]) {
+  if ((VEC & 1) == 0 && (d0 & 1) == 0 && d0 + VEC <= D) {
+#pragma unroll
+    for (int v = 0; v < VEC; v += 2) {
+      const int64_t k = (d0 + v) >> 1;
+      const float ws = sin_div[k], wc = cos_div[k];
+      if (ws == wc) {
+        sincosf(t * ws, &te[v], &te[v + 1]);
+      } else {
+        te[v] = sinf(t * ws);
+        te[v + 1] = cosf(t * wc);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) te[v] = d0 + v < D ? time_enc(t, d0 + v, sin_div, cos_div) : 0.f;
+}
+
 Buckets make_buckets(const esgpt_buckets* b) {
   Buckets k{};
   if (b == nullptr) {
@@ -323,6 +348,8 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
     double run[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) run[v] = 0.0;
+    float te[VEC];
+    if (flags & ESGPT_EMB_TIME) time_enc_vec<VEC>(t, d0, D, sin_div, cos_div, te);
 #pragma unroll
     for (int g = 0; g < GMAX; ++g) {
       if (g >= G) break;
@@ -331,7 +358,7 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
       for (int v = 0; v < VEC; ++v) {
         float x = acc[g][v];
         if (use_static) x = dw * x + sw * st[v];
-        if ((flags & ESGPT_EMB_TIME) && g == 0 && d0 + v < D) x = x + time_enc(t, d0 + v, sin_div, cos_div);
+        if ((flags & ESGPT_EMB_TIME) && g == 0 && d0 + v < D) x = x + te[v];
         if (flags & ESGPT_EMB_CUMSUM) {
           run[v] += (double)x;
           x = (float)run[v];
@@ -348,6 +375,38 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
           if (d0 + v < D) dst[v] = o[v];
       }
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Event times (esgpt_event_times): t[b][l] = Σ_{j<l} mask[b][j] · Δt[b][j], the reference's time_from_deltas
+// (transformer.py:305-313), once per subject instead of once per event inside the input-layer kernels (an O(L)
+// prefix per event: 22 % of the C5 microbench at L = 1024). One workgroup per subject: each thread sums a contiguous
+// run of events in double, the run totals are scanned in double through LDS, and each event's exclusive prefix is
+// rounded to f32 (f32 deltas summed in double, as the event_time prefix: the same values).
+// ------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void event_times_kernel(esgpt_batch bt, float* __restrict__ times) {
+  __shared__ double s_tot[256];
+  const int64_t b = blockIdx.x, L = bt.L;
+  const int tid = threadIdx.x;
+  const int64_t per = (L + 255) / 256, j0 = tid * per, j1 = min(L, j0 + per);
+  const uint8_t* em = bt.event_mask + b * L;
+  const float* td = bt.time_delta + b * L;
+  double run = 0.0;
+  for (int64_t j = j0; j < j1; ++j) run += (double)(em[j] ? td[j] : 0.0f);
+  s_tot[tid] = run;
+  __syncthreads();
+  // inclusive scan of the 256 run totals (Hillis-Steele, double)
+  for (int o = 1; o < 256; o <<= 1) {
+    const double v = tid >= o ? s_tot[tid - o] : 0.0;
+    __syncthreads();
+    s_tot[tid] += v;
+    __syncthreads();
+  }
+  double acc = tid > 0 ? s_tot[tid - 1] : 0.0;
+  for (int64_t j = j0; j < j1; ++j) {
+    times[b * L + j] = (float)acc;
+    acc += (double)(em[j] ? td[j] : 0.0f);
   }
 }
 
@@ -1215,6 +1274,14 @@ int esgpt_embed_joint_fwd(const esgpt_batch* batch, const esgpt_buckets* buckets
                           float dynamic_w, float* out, int32_t* err, void* stream) {
   return esgpt_embed_joint_fwd_ex(batch, buckets, table, ESGPT_F32, V, D, sin_div, cos_div, flags, static_w, dynamic_w,
                                   out, err, stream);
+}
+
+int esgpt_event_times(const esgpt_batch* batch, float* times, void* stream) {
+  ESGPT_REQUIRE(batch && times && batch->event_mask && batch->time_delta && batch->B >= 0 && batch->L >= 0);
+  if (batch->B * batch->L == 0) return ESGPT_OK;
+  event_times_kernel<<<(unsigned)batch->B, 256, 0, as_stream(stream)>>>(*batch, times);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
 }
 
 int esgpt_embed_joint_fwd_ex(const esgpt_batch* batch, const esgpt_buckets* buckets, const void* table,

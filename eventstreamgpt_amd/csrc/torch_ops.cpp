@@ -120,6 +120,18 @@ bool make_buckets(at::IntArrayRef v, esgpt_buckets& k) {
   "Tensor dyn_vmask, Tensor? st_idx, Tensor? st_meas"
 
 // ---- input layer ---------------------------------------------------------------------------------------------
+// The temporal encoding's event times (the exclusive masked cumsum of time_delta) computed once per subject by
+// esgpt_event_times and handed to the kernel as absolute times (flags gains ESGPT_EMB_TIME_ABS); the kernels would
+// otherwise sum each event's prefix themselves. No-op when the batch carries absolute times or no encoding is asked.
+Tensor event_times_for(Batch& bt, int64_t& flags, const Tensor& like) {
+  if (!(flags & ESGPT_EMB_TIME) || (flags & ESGPT_EMB_TIME_ABS)) return Tensor();
+  Tensor t = at::empty({bt.b.B, bt.b.L}, like.options().dtype(at::kFloat));
+  check(esgpt_event_times(&bt.b, ptr<float>(t), stream_of(like)), "event_times");
+  bt.b.time_abs = ptr<const float>(t);
+  flags |= ESGPT_EMB_TIME_ABS;
+  return t;
+}
+
 Tensor embed_joint(const Tensor& table, BATCH_ARGS, at::IntArrayRef buckets, const optional<Tensor>& sin_div,
                    const optional<Tensor>& cos_div, int64_t flags, double static_w, double dynamic_w, int64_t G,
                    const Tensor& err) {
@@ -130,6 +142,7 @@ Tensor embed_joint(const Tensor& table, BATCH_ARGS, at::IntArrayRef buckets, con
   Tensor tab = as(table, at::kFloat);
   const int64_t V = tab.size(0), D = tab.size(1);
   Tensor out = at::empty({bt.b.B, bt.b.L, G, D}, tab.options());
+  Tensor times = event_times_for(bt, flags, tab);
   check(esgpt_embed_joint_fwd(&bt.b, has_bk ? &bk : nullptr, ptr<const float>(tab), V, D, optr<const float>(sin_div),
                               optr<const float>(cos_div), (int)flags, (float)static_w, (float)dynamic_w,
                               ptr<float>(out), ptr<int32_t>(err), stream_of(tab)),
@@ -161,6 +174,7 @@ Tensor embed_epilogue(const Tensor& y, BATCH_ARGS, int64_t G, int64_t flags, con
   Tensor yc = as(y, at::kFloat);
   const int64_t D = yc.size(-1);
   Tensor out = at::empty({bt.b.B, bt.b.L, G, D}, yc.options());
+  Tensor times = event_times_for(bt, flags, yc);
   check(esgpt_embed_epilogue_fwd(&bt.b, G, D, ptr<const float>(yc), optr<const float>(sin_div),
                                  optr<const float>(cos_div), (int)flags, ptr<float>(out), stream_of(yc)),
         "embed_epilogue");

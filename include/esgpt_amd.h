@@ -93,6 +93,12 @@ int esgpt_embed_joint_fwd_ex(const esgpt_batch* batch, const esgpt_buckets* buck
                              int table_dtype, int64_t V, int64_t D, const float* sin_div, const float* cos_div,
                              int flags, float static_w, float dynamic_w, float* out, int32_t* err, void* stream);
 
+/* Event times t[b][l] = sum_{j<l} event_mask[b][j] * time_delta[b][j] (f32 deltas summed in double; the reference's
+ * time_from_deltas, transformer.py:305-313 / TemporalPositionEncoding's input), f32 [B, L]: computed once per subject
+ * and handed to the input-layer kernels as batch->time_abs with ESGPT_EMB_TIME_ABS (replaces their per-event
+ * O(L) prefix). */
+int esgpt_event_times(const esgpt_batch* batch, float* times, void* stream);
+
 /* SPLIT_CATEGORICAL_NUMERICAL mode, the gather part of _split_embed (:390-450) for every (event, bucket):
  * x[e,g] = [cat_scale * bag_cat + static_scale * static_bag_cat , num_scale * bag_num]  (f32, [B*L*G, Dc+Dn]).
  * The caller applies one GEMM with [cat_proj | num_proj] and then esgpt_embed_epilogue_fwd. */
