@@ -194,20 +194,26 @@ Tensor embed_epilogue_bwd(const Tensor& dout, BATCH_ARGS, int64_t G, int64_t fla
 
 // dsrc: rows of leading dimension ld (elements), D columns used (may be a column slice of a wider matrix)
 Tensor embed_bag_bwd(const Tensor& dsrc, BATCH_ARGS, at::IntArrayRef buckets, int64_t selector, int64_t flags,
-                     double dyn_scale, double static_scale, int64_t ld, int64_t D, int64_t V, int64_t G) {
+                     double dyn_scale, double static_scale, int64_t ld, int64_t D, int64_t V, int64_t G,
+                     const optional<Tensor>& out) {
   const c10::DeviceGuard guard(dsrc.device());
   TORCH_CHECK(dsrc.scalar_type() == at::kFloat && dsrc.stride(-1) == 1, "embed_bag_bwd: f32 rows expected");
   Batch bt = make_batch(BATCH_PASS);
   esgpt_buckets bk;
   const bool has_bk = make_buckets(buckets, bk);
-  Tensor dtable = at::empty({V, D}, dsrc.options());
+  // out given (TrainStep's zero-copy exchange buffer region): the table gradient is written there, fully
+  const bool has_out = out.has_value() && out->defined();
+  if (has_out)
+    TORCH_CHECK(out->scalar_type() == at::kFloat && out->is_contiguous() && out->numel() == V * D &&
+                    out->device() == dsrc.device(), "embed_bag_bwd: out must be contiguous f32 [V * D]");
+  Tensor dtable = has_out ? out->view({V, D}) : at::empty({V, D}, dsrc.options());
   const size_t nb = esgpt_embed_bag_bwd_workspace(&bt.b, G, V, D);
   Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, dsrc.options().dtype(at::kByte));
   check(esgpt_embed_bag_bwd(&bt.b, has_bk ? &bk : nullptr, (int)selector, (int)flags, (float)dyn_scale,
                             (float)static_scale, ptr<const float>(dsrc), ld, D, V, ptr<float>(dtable), ws.data_ptr(),
                             nb, stream_of(dsrc)),
         "embed_bag_bwd");
-  return dtable;
+  return has_out ? at::empty({0}, dsrc.options()) : dtable;  // never an alias of `out`
 }
 
 // ---- nested-attention glue + residual (structured.hip) ---------------------------------------------------------
@@ -714,7 +720,8 @@ void used_on(const Tensor& t, const c10::hip::HIPStream& s) {
 std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x, const Tensor& w,
                                               const optional<Tensor>& alpha, int64_t act, const optional<Tensor>& pre,
                                               bool need_dx, bool need_db, const Tensor& tickets,
-                                              const optional<Tensor>& db_extra_, const optional<Tensor>& dw_tickets) {
+                                              const optional<Tensor>& db_extra_, const optional<Tensor>& dw_tickets,
+                                              const optional<Tensor>& dw_out, const optional<Tensor>& db_out) {
   const c10::DeviceGuard guard(x.device());
   // dw_tickets given: split form — dX on the current stream, dW / db on the device's weight-gradient stream (with
   // their own ticket array, workspace and outputs allocated in that stream's order); weight_grad_join before use
@@ -742,12 +749,24 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
   // fork first: under HIP-graph capture the side stream must have joined the capture before it allocates, so that
   // its blocks come from the graph's private pool (and no allocation reaches the driver mid-capture)
   if (split) check(esgpt_stream_wait(reinterpret_cast<void*>(side.stream()), s_cur), "linear_bwd fork");
+  // dw_out / db_out given: the gradients go there (a DDP exchange buffer region, TrainStep's zero-copy exchange)
+  // and the returned dw / db are empty
+  const bool has_dwo = dw_out.has_value() && dw_out->defined();
+  const bool has_dbo = need_db && db_out.has_value() && db_out->defined();
+  if (has_dwo)
+    TORCH_CHECK(dw_out->scalar_type() == at::kFloat && dw_out->is_contiguous() && dw_out->numel() == dout * din &&
+                    dw_out->device() == x.device(), "linear_bwd: dw_out must be contiguous f32 [out * in]");
+  if (has_dbo)
+    TORCH_CHECK(db_out->scalar_type() == at::kFloat && db_out->is_contiguous() && db_out->numel() == dout &&
+                    db_out->device() == x.device(), "linear_bwd: db_out must be contiguous f32 [out]");
   {
     const c10::hip::HIPStreamGuard sg(side);  // the dW product's allocations in its stream's order
-    dw = at::empty({dout, din}, f32);
-    db = need_db ? at::empty({dout}, f32) : at::empty({0}, f32);
+    dw = has_dwo ? at::empty({0}, f32) : at::empty({dout, din}, f32);
+    db = (need_db && !has_dbo) ? at::empty({dout}, f32) : at::empty({0}, f32);
     ws = nb ? at::empty({(int64_t)nb}, x.options().dtype(at::kByte)) : Tensor();
   }
+  float* dwp = has_dwo ? ptr<float>(*dw_out) : ptr<float>(dw);
+  float* dbp = need_db ? (has_dbo ? ptr<float>(*db_out) : ptr<float>(db)) : nullptr;
   const void* dxp = need_dx ? dx.data_ptr() : nullptr;
   if (f32op) {
     TORCH_CHECK(w.scalar_type() == at::kFloat && (!has_pre || pre->scalar_type() == at::kFloat),
@@ -755,16 +774,15 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
     check(esgpt_linear_bwd_f32(ptr<const float>(dy), dy.stride(0), ptr<const float>(x), x.stride(0),
                                ptr<const float>(w), T, din, dout, optr<const float>(alpha), (int)act,
                                has_pre ? ptr<const float>(*pre) : nullptr, has_pre ? pre->stride(0) : 0,
-                               reinterpret_cast<float*>(const_cast<void*>(dxp)), need_dx ? din : 0, ptr<float>(dw),
-                               need_db ? ptr<float>(db) : nullptr, ws.defined() ? ws.data_ptr() : nullptr, nb,
+                               reinterpret_cast<float*>(const_cast<void*>(dxp)), need_dx ? din : 0, dwp, dbp,
+                               ws.defined() ? ws.data_ptr() : nullptr, nb,
                                ptr<int32_t>(tickets), db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
                                db_extra.defined() ? db_extra.size(0) : 0, s_cur),
           "linear_bwd_f32");
   } else if (split) {
     check(esgpt_linear_bwd_split(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
                                  optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
-                                 has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0,
-                                 ptr<float>(dw), need_db ? ptr<float>(db) : nullptr,
+                                 has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0, dwp, dbp,
                                  ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tk),
                                  db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
                                  db_extra.defined() ? db_extra.size(0) : 0, s_cur,
@@ -780,8 +798,7 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
   } else {
     check(esgpt_linear_bwd_ex(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), w.data_ptr(), T, din, dout,
                               optr<const float>(alpha), (int)act, has_pre ? pre->data_ptr() : nullptr,
-                              has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0,
-                              ptr<float>(dw), need_db ? ptr<float>(db) : nullptr,
+                              has_pre ? pre->stride(0) : 0, const_cast<void*>(dxp), need_dx ? din : 0, dwp, dbp,
                               ws.defined() ? ws.data_ptr() : nullptr, nb, ptr<int32_t>(tickets),
                               db_extra.defined() ? ptr<const float>(db_extra) : nullptr,
                               db_extra.defined() ? db_extra.size(0) : 0, s_cur),
@@ -918,7 +935,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("embed_epilogue(Tensor y, " BATCH_SCHEMA ", int G, int flags, Tensor? sin_div, Tensor? cos_div) -> Tensor");
   m.def("embed_epilogue_bwd(Tensor dout, " BATCH_SCHEMA ", int G, int flags) -> Tensor");
   m.def("embed_bag_bwd(Tensor dsrc, " BATCH_SCHEMA ", int[] buckets, int selector, int flags, float dyn_scale, "
-        "float static_scale, int ld, int D, int V, int G) -> Tensor");
+        "float static_scale, int ld, int D, int V, int G, Tensor(a!)? out=None) -> Tensor");
   m.def("attention(Tensor qkv, Tensor? key_mask, Tensor? query_mask, int H, int window, bool static_kv_first, "
         "float dropout_p, Tensor? seed) -> (Tensor, Tensor, Tensor)");
   m.def("attention_bwd(Tensor qkv, Tensor o, Tensor dout, Tensor lse, Tensor? key_mask, Tensor? query_mask, int H, "
@@ -952,7 +969,8 @@ TORCH_LIBRARY(esgpt, m) {
         "Tensor? bias, Tensor? alpha, bool accumulate, Tensor tickets) -> ()");
   m.def("linear_act(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
-        "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None, Tensor(a!)? dw_out=None, "
+        "Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)");
   m.def("weight_grad_join(Tensor like) -> ()");
   m.def("seed_bank(Tensor(a!) counter, Tensor(b!) bank, Tensor(c!)? err=None) -> ()");
   m.def("residual_ln_bwd_partials(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, "

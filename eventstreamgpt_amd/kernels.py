@@ -269,6 +269,57 @@ class deferred_colsums:
         return False
 
 
+_DEST: dict[int, tuple] = {}  # device index -> (recorder, destination | None) of the running training pass
+
+
+class grad_destinations:
+    """Context of one training pass (forward + backward) under DDP: the backward formulas write weight / bias
+    gradients straight into the exchange buffer instead of fresh tensors (AccumulateGrad then takes the buffer's
+    view as ``param.grad`` without a copy). ``recorder`` (a GradBuckets) learns, from the forward, which parameters
+    one kernel output covers (``note_grad_group``: the q|k|v rows of one projection, a LayerNorm's (w, b) column
+    sums, the padded head weights), so that its next layout keeps them adjacent; ``dest`` (the same object, or None
+    when this pass must not write into the buffer — gradient accumulation, no-sync passes) hands out those regions
+    (``grad_region``), each parameter at most once per pass."""
+
+    def __init__(self, device: torch.device, recorder, dest):
+        self.device = device
+        self.enabled = recorder is not None and device.type == "cuda"
+        self.recorder, self.dest = recorder, dest
+
+    def __enter__(self):
+        if self.enabled:
+            if self.dest is not None:
+                self.dest.begin_pass()
+            _DEST[_dev_idx(self.device)] = (self.recorder, self.dest)
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            _DEST.pop(_dev_idx(self.device), None)
+        return False
+
+
+def note_grad_group(tensors, pad: int = 0) -> None:
+    """Forward side: ``tensors`` (leaf parameters, in the order of one kernel output's rows) followed by ``pad``
+    scratch elements are produced by one gradient kernel."""
+    if _DEST and tensors and tensors[0] is not None and tensors[0].is_cuda:
+        ent = _DEST.get(_dev_idx(tensors[0].device))
+        if ent is not None:
+            ent[0].note_group(tensors, pad)
+
+
+def grad_region(tensors, pad: int = 0):
+    """Backward side: the exchange buffer's f32 region holding ``tensors``' gradients back to back (+ ``pad``
+    elements), claimed for this pass — or None (no destination active, a layout without this group, or a parameter
+    already claimed: a second contribution is accumulated by autograd as usual)."""
+    if not _DEST or not tensors or tensors[0] is None or not tensors[0].is_cuda:
+        return None
+    ent = _DEST.get(_dev_idx(tensors[0].device))
+    if ent is None or ent[1] is None:
+        return None
+    return ent[1].region(tensors, pad)
+
+
 def join_weight_grads(device: torch.device) -> None:
     """The current stream waits for every weight-gradient launch queued so far on ``device``."""
     _ops().weight_grad_join(tickets(device, 1))

@@ -83,10 +83,12 @@ def _leaves(*ts) -> bool:
     return all(t is None or t.is_leaf for t in ts)
 
 
-def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None, split_ok=False):
+def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None, split_ok=False, dw_out=None,
+                db_out=None):
     """``esgpt::linear_bwd`` from a registered backward (records the launch shape for bench.py when asked). With
     ``split_ok`` (the weight / bias gradients go straight to leaf parameters) and inside ``weight_grad_overlap``,
-    the weight gradient runs on the weight-gradient stream."""
+    the weight gradient runs on the weight-gradient stream. ``dw_out`` / ``db_out`` (exchange-buffer regions,
+    ``_dest``): the gradients are written there and returned as views of them."""
     from . import fused
 
     if fused.SHAPES["enabled"]:
@@ -95,8 +97,31 @@ def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None, spli
     from .kernels import tickets, weight_grad_overlap_active
 
     dw_tickets = tickets(x.device, 1) if (split_ok and weight_grad_overlap_active(x.device)) else None
-    return torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device), db_extra,
-                                      dw_tickets)
+    dx, dw, db = torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device),
+                                            db_extra, dw_tickets, dw_out, db_out if need_db else None)
+    if dw_out is not None:
+        dw = dw_out.view(dy.shape[1], x.shape[1])
+    if need_db and db_out is not None:
+        db = db_out
+    return dx, dw, db
+
+
+def _dest(ok: bool, tensors, pad: int = 0, shape=None):
+    """The exchange-buffer region for the gradients of the leaf parameters ``tensors`` (kernels.grad_region; None
+    when ``ok`` is False, e.g. a non-leaf recipient, or no destination is active), viewed as ``shape``."""
+    if not ok:
+        return None
+    from .kernels import grad_region
+
+    r = grad_region(tensors, pad)
+    return r if (r is None or shape is None) else r.view(shape)
+
+
+def _note(ok: bool, tensors, pad: int = 0):
+    if ok:
+        from .kernels import note_grad_group
+
+        note_grad_group(tensors, pad)
 
 
 def _batch_d(args, start):
@@ -128,8 +153,9 @@ def _register():
         return dout.new_empty(di.shape[0] * di.shape[1] * G, dout.shape[-1], dtype=torch.float32)
 
     @fake(lib + "embed_bag_bwd")
-    def _(dsrc, em, td, tm, di, dm, dv, dvm, si, sm, buckets, selector, flags, dyn_scale, static_scale, ld, D, V, G):
-        return dsrc.new_empty(V, D, dtype=torch.float32)
+    def _(dsrc, em, td, tm, di, dm, dv, dvm, si, sm, buckets, selector, flags, dyn_scale, static_scale, ld, D, V, G,
+          out=None):
+        return dsrc.new_empty(0 if out is not None else V, D, dtype=torch.float32)
 
     @fake(lib + "attention")
     def _(qkv, key_mask, query_mask, H, window, skf, p, seed):
@@ -275,11 +301,12 @@ def _register():
         return None
 
     @fake(lib + "linear_bwd")
-    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None, dw_tickets=None):
+    def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None, dw_tickets=None, dw_out=None,
+          db_out=None):
         f32 = torch.float32
         return (x.new_empty(dy.shape[0], x.shape[1], dtype=dy.dtype) if need_dx else x.new_empty(0, dtype=dy.dtype),
-                x.new_empty(dy.shape[1], x.shape[1], dtype=f32),
-                x.new_empty(dy.shape[1], dtype=f32) if need_db else x.new_empty(0, dtype=f32))
+                x.new_empty(0, dtype=f32) if dw_out is not None else x.new_empty(dy.shape[1], x.shape[1], dtype=f32),
+                x.new_empty(dy.shape[1], dtype=f32) if (need_db and db_out is None) else x.new_empty(0, dtype=f32))
 
     @fake(lib + "pack")
     def _(srcs, group_sizes, tails, dtypes):
@@ -318,6 +345,7 @@ def _register():
         buckets, sin_div, cos_div, flags, static_w, dynamic_w, G, err = inputs[10:]
         ctx.save_for_backward(*batch)
         ctx.meta = (tuple(buckets), flags, static_w, dynamic_w, G, table.shape[0], table.shape[1])
+        ctx.table = table if table.is_leaf else None
 
     def _ej_bwd(ctx, dout):
         batch = ctx.saved_tensors
@@ -329,9 +357,10 @@ def _register():
             dsrc = dout.view(-1, D)
         S = 0 if batch[7] is None else batch[7].shape[1]
         static = bool(flags & L.EMB_STATIC) and S > 0
+        out = _dest(ctx.table is not None, [ctx.table])
         dtable = ops.embed_bag_bwd(dsrc, *batch, list(buckets), L.BAG_JOINT, flags,
-                                   dynamic_w if static else 1.0, static_w, D, D, V, G)
-        return (dtable,) + (None,) * 17
+                                   dynamic_w if static else 1.0, static_w, D, D, V, G, out)
+        return (dtable if out is None else out.view(V, D),) + (None,) * 17
 
     reg(lib + "embed_joint", _ej_bwd, setup_context=_ej_setup)
 
@@ -343,6 +372,7 @@ def _register():
         ctx.save_for_backward(*batch)
         ctx.meta = (tuple(buckets), flags, cat_scale, num_scale, static_scale, G, ct.shape[0], ct.shape[1],
                     nt.shape[1])
+        ctx.tables = (ct, nt) if _leaves(ct, nt) else None
 
     def _es_bwd(ctx, dx):
         batch = ctx.saved_tensors
@@ -350,11 +380,14 @@ def _register():
         dx = dx.contiguous().float()
         if static_scale == 0.0:
             flags &= ~L.EMB_STATIC
+        ok = ctx.tables is not None
+        oc = _dest(ok, ctx.tables[:1] if ok else None)
+        on = _dest(ok, ctx.tables[1:] if ok else None)
         dcat = ops.embed_bag_bwd(dx, *batch, list(buckets), L.BAG_CAT, flags, cat_scale, static_scale, Dc + Dn, Dc,
-                                 V, G)
+                                 V, G, oc)
         dnum = ops.embed_bag_bwd(dx[:, Dc:], *batch, list(buckets), L.BAG_NUM, flags, num_scale, 0.0, Dc + Dn, Dn,
-                                 V, G)
-        return (dcat, dnum) + (None,) * 16
+                                 V, G, on)
+        return (dcat if oc is None else oc.view(V, Dc), dnum if on is None else on.view(V, Dn)) + (None,) * 16
 
     reg(lib + "embed_split_bags", _es_bwd, setup_context=_es_setup)
 
@@ -435,6 +468,9 @@ def _register():
         ctx.meta = (x is not None, y is not None, bias is not None, y.dtype if y is not None else torch.float32,
                     out_dtype, p, skip_T, len(inputs))
         ctx.defer_ok = bias is None and _leaves(ln_w, ln_b)
+        # the deferred column sums [d ln_w | d ln_b | unused bias row] as one exchange-buffer region
+        ctx.lnp = (ln_w, ln_b) if ctx.defer_ok else None
+        _note(ctx.defer_ok, (ln_w, ln_b), ln_w.numel())
 
     def _rl_bwd(ctx, dh, dout, _dm, _dr):
         from .kernels import colsum_deferral_active, defer_colsum
@@ -447,7 +483,9 @@ def _register():
             # partials now, the column sums in the pass's one esgpt::colsum_flush launch
             dx, dy, part = ops.residual_ln_bwd_partials(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x,
                                                         has_y, y_dtype, out_dtype, skip_T)
-            sums = torch.empty(3, h.shape[1], dtype=torch.float32, device=h.device)
+            sums = _dest(True, ctx.lnp, h.shape[1], (3, h.shape[1]))
+            if sums is None:
+                sums = torch.empty(3, h.shape[1], dtype=torch.float32, device=h.device)
             defer_colsum(h.device, part, sums.view(-1))
         else:
             dx, dy, sums = ops.residual_ln_bwd(dh, dout, h, mean, rstd, ln_w, row_mask, p, seed, has_x, has_y,
@@ -477,11 +515,17 @@ def _register():
         ctx.rows = [m.shape[0] for m in masters]
         ctx.has_bias = bias is not None
         ctx.split_ok = _leaves(bias, *masters)
+        ctx.gp = (list(masters), bias) if ctx.split_ok and masters else None
+        _note(ctx.gp is not None and len(masters) > 1, masters)
 
     def _li_bwd(ctx, dy):
         x, w = ctx.saved_tensors
         need_db = ctx.has_bias and ctx.needs_input_grad[2]
-        dx, dw, db = _linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db, split_ok=ctx.split_ok)
+        ok = ctx.gp is not None
+        dw_out = _dest(ok, ctx.gp[0] if ok else None)
+        db_out = _dest(ok and need_db, [ctx.gp[1]] if ok else None)
+        dx, dw, db = _linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db, split_ok=ctx.split_ok,
+                                 dw_out=dw_out, db_out=db_out)
         return (dx if ctx.needs_input_grad[0] else None, None, db if need_db else None,
                 list(torch.split(dw, ctx.rows, 0)), None)
 
@@ -498,15 +542,20 @@ def _register():
         ctx.act = act
         ctx.has_bpj = b_pj is not None
         ctx.split_ok = _leaves(b_fc, b_pj, p_fc, p_pj)
+        ctx.gp = (p_fc, p_pj, b_fc, b_pj) if ctx.split_ok else None
 
     def _ml_bwd(ctx, dy, _dpre, _dg):
         if dy is None:
             return (None,) * 9
         x, w_fc, w_pj, pre, g = ctx.saved_tensors
         need_dbpj = ctx.has_bpj and ctx.needs_input_grad[4]
-        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj, split_ok=ctx.split_ok)
+        ok = ctx.gp is not None
+        gp = ctx.gp if ok else (None,) * 4
+        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj, split_ok=ctx.split_ok,
+                                       dw_out=_dest(ok, [gp[1]]), db_out=_dest(ok and need_dbpj, [gp[3]]))
         need_dx = ctx.needs_input_grad[0]
-        dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True, split_ok=ctx.split_ok)
+        dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True, split_ok=ctx.split_ok,
+                                       dw_out=_dest(ok, [gp[0]]), db_out=_dest(ok, [gp[2]]))
         return (dx if need_dx else None, None, None, db_fc, db_pj if need_dbpj else None, None, dw_fc, dw_pj, None)
 
     reg(lib + "mlp", _ml_bwd, setup_context=_ml_setup)
@@ -542,6 +591,17 @@ def _register():
         ctx.rows = ([w.shape[0] for w in cw], [w.shape[0] for w in tw])
         ctx.n = (len(cw), len(tw))
         ctx.split_ok = _leaves(*cw, *cb, *tw, *tb)
+        # the padded head GEMM's dW / db rows [params | pad] as exchange-buffer regions
+        D = xc.shape[1]
+        pc = wc.shape[0] - sum(ctx.rows[0])
+        pt = (wt.shape[0] - sum(ctx.rows[1])) if tw else 0
+        ctx.gp = (list(cw), list(cb), list(tw), list(tb), pc, pt, D) if ctx.split_ok else None
+        if ctx.gp is not None:
+            _note(True, cw, pc * D)
+            _note(True, cb, pc)
+            if tw:
+                _note(True, tw, pt * D)
+                _note(True, tb, pt)
 
     def _hl_bwd(ctx, g, *_):
         if g is None:
@@ -551,14 +611,19 @@ def _register():
         rows_c, rows_t = ctx.rows
         alpha = g[-1:]  # a 1-element view (g may be a stride-0 expansion of the total's gradient)
         # the loss kernel's per-subject position-0 bias rows are summed into db inside the same launch
+        gp = ctx.gp
+        ok = gp is not None
         dxc, dwc, dbc = _linear_bwd(dzc, xc, wc, alpha, -1, None, True, True, dbias if dbias.numel() else None,
-                                    split_ok=ctx.split_ok)
+                                    split_ok=ctx.split_ok, dw_out=_dest(ok, gp and gp[0], gp and gp[4] * gp[6]),
+                                    db_out=_dest(ok, gp and gp[1], gp and gp[4]))
         nc = sum(rows_c)
         gw_c = list(torch.split(dwc[:nc], rows_c, 0))
         gb_c = list(torch.split(dbc[:nc], rows_c, 0))
         dxt, gw_t, gb_t = None, [], []
         if n_tw:
-            dxt, dwt, dbt = _linear_bwd(dzt, xt, wt, alpha, -1, None, True, True, split_ok=ctx.split_ok)
+            dxt, dwt, dbt = _linear_bwd(dzt, xt, wt, alpha, -1, None, True, True, split_ok=ctx.split_ok,
+                                        dw_out=_dest(ok, gp and gp[2], gp and gp[5] * gp[6]),
+                                        db_out=_dest(ok, gp and gp[3], gp and gp[5]))
             nt = sum(rows_t)
             gw_t = list(torch.split(dwt[:nt], rows_t, 0))
             gb_t = list(torch.split(dbt[:nt], rows_t, 0))

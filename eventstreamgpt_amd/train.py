@@ -43,8 +43,8 @@ import torch.distributed as dist
 
 from .data.types import PytorchBatch
 from .kernels import (begin_dropout_step, check_errors, colsum_deferral_active, deferred_colsums,
-                      end_dropout_step, err_word, flush_colsums, join_weight_grads, raise_for_error,
-                      weight_grad_overlap, weight_grad_overlap_active)
+                      end_dropout_step, err_word, flush_colsums, grad_destinations, join_weight_grads,
+                      raise_for_error, weight_grad_overlap, weight_grad_overlap_active)
 from ._lib import FLAG_PEER_RANK
 from .transformer.config import OptimizationConfig
 
@@ -229,7 +229,16 @@ class GradBuckets:
     every rank iff some rank failed, and each rank ORs ESGPT_FLAG_PEER_RANK into its error block — so every rank's
     AdamW skips the step and every rank raises at the same step (the failing rank its own exception, the others
     RuntimeError), instead of the healthy ranks running on into a collective the failing rank never joins. No
-    extra collective: the flag travels with the gradients."""
+    extra collective: the flag travels with the gradients.
+
+    Zero-copy exchange (``zero_copy``; TrainStep turns it on without gradient accumulation): the backward formulas
+    write their dW / db / table / column-sum outputs straight into the buffer (kernels.grad_destinations), so a
+    release only re-points ``p.grad`` and launches the all-reduce — no copy kernel, eager or under HIP-graph
+    capture. One kernel output may cover several parameters (q|k|v, a LayerNorm's (w, b) sums + the unused bias
+    row, the padded head): the forward records those groups (``note_group``) and ``relayout()`` — run by TrainStep
+    before anything has been captured, at the same point on every rank — keeps each group adjacent, in its kernel's
+    row order and followed by its scratch pad, at the position of its first member in the reversed order. Any
+    gradient the kernels did not write into the buffer is still copied in at release."""
 
     def __init__(self, params: list, world: int, bucket_mb: float = 25.0, err_check: bool = False):
         self.params = params
@@ -237,19 +246,50 @@ class GradBuckets:
         dev = params[0].device
         self.avg = dist.get_backend() == "nccl"  # RCCL has ncclAvg; gloo sums (divided afterwards)
         self.err_check = err_check and dev.type == "cuda"
-        order = list(reversed(range(len(params))))
-        total = sum(params[i].numel() for i in order)
-        self.flat = torch.zeros(total + 1, dtype=torch.float32, device=dev)
+        self.lim = int(bucket_mb * 2**20 / 4)
+        self.index = {id(p): i for i, p in enumerate(params)}
+        self.groups: dict = {}  # tuple of parameter indices -> pad elements (recorded by the forward)
+        self.laid_out: dict = {}  # the groups the current layout honours
+        self.zero_copy = False
+        self._claimed: set = set()
+        self._layout()
+        self.mode = "launch"
+        self.on_boundary = None
+        # gradient accumulation (TrainStep, OptimizationConfig.gradient_accumulation): the buffer already holds the
+        # window's earlier batches — a release ADDS the batch's gradients instead of copying them
+        self.add = False
+        self.reset()
+        self._hooks = [params[i].register_post_accumulate_grad_hook(self._make_hook(i)) for i in range(len(params))]
+
+    def _layout(self):
+        """Flat buffer, per-parameter views and buckets for the groups in ``self.laid_out``."""
+        params = self.params
+        member = {}
+        for g, pad in self.laid_out.items():
+            for i in g:
+                member[i] = (g, pad)
+        seq, placed = [], set()
+        for i in reversed(range(len(params))):
+            if i in placed:
+                continue
+            g, pad = member.get(i, ((i,), 0))
+            seq.append((g, pad))
+            placed.update(g)
+        total = sum(sum(params[i].numel() for i in g) + pad for g, pad in seq)
+        self.flat = torch.zeros(total + 1, dtype=torch.float32, device=params[0].device)
         self.slot = self.flat[total:]  # the any-rank-failed flag (last bucket)
-        self.views, self.bucket_of, self.buckets = {}, {}, []
-        lim = int(bucket_mb * 2**20 / 4)
+        self.views, self.offset, self.pad_after, self.bucket_of, self.buckets = {}, {}, {}, {}, []
         off, start, cur = 0, 0, []
-        for i in order:
-            n = params[i].numel()
-            self.views[i] = self.flat[off: off + n].view_as(params[i])
-            cur.append(i)
-            off += n
-            if off - start >= lim:
+        for g, pad in seq:
+            for i in g:
+                n = params[i].numel()
+                self.views[i] = self.flat[off: off + n].view_as(params[i])
+                self.offset[i] = off
+                cur.append(i)
+                off += n
+            self.pad_after[g[-1]] = pad
+            off += pad
+            if off - start >= self.lim:
                 self.buckets.append((cur, start, off))
                 cur, start = [], off
         if cur:
@@ -259,13 +299,42 @@ class GradBuckets:
         for b, (idx, _, _) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
-        self.mode = "launch"
-        self.on_boundary = None
-        # gradient accumulation (TrainStep, OptimizationConfig.gradient_accumulation): the buffer already holds the
-        # window's earlier batches — a release ADDS the batch's gradients instead of copying them
-        self.add = False
+
+    # ---- zero-copy destinations (kernels.grad_destinations) ----------------------------------------------------
+    def note_group(self, tensors, pad: int):
+        idx = tuple(self.index.get(id(t), -1) for t in tensors)
+        if -1 in idx or (len(idx) == 1 and pad == 0) or idx in self.groups:
+            return
+        if any(i in g for g in self.groups for i in idx):  # overlapping groups: the first one recorded wins
+            return
+        self.groups[idx] = int(pad)
+
+    def layout_stale(self) -> bool:
+        return self.zero_copy and self.groups != self.laid_out
+
+    def relayout(self):
+        """Re-cuts the buffer for the recorded groups. Only while no captured graph writes into the buffer and no
+        exchange is in flight; ``param.grad`` views of the old buffer stay valid until replaced."""
+        self.laid_out = dict(self.groups)
+        self._layout()
         self.reset()
-        self._hooks = [params[i].register_post_accumulate_grad_hook(self._make_hook(i)) for i in range(len(params))]
+
+    def begin_pass(self):
+        self._claimed.clear()
+
+    def region(self, tensors, pad: int):
+        idx = [self.index.get(id(t), -1) for t in tensors]
+        if -1 in idx or any(i in self._claimed for i in idx):
+            return None
+        if self.pad_after.get(idx[-1], 0) != pad and not (pad == 0 and len(idx) == 1):
+            return None
+        off = self.offset[idx[0]]
+        for a, b in zip(idx, idx[1:]):  # adjacent in the kernel's row order
+            if self.offset[b] != self.offset[a] + self.params[a].numel():
+                return None
+        self._claimed.update(idx)
+        n = sum(self.params[i].numel() for i in idx) + pad
+        return self.flat[off: off + n]
 
     def _make_hook(self, i: int):
         def hook(p):
@@ -380,7 +449,7 @@ class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
                  max_graphs: int = 4, overlap_weight_grads: bool = False, defer_colsums: bool = True,
-                 capture_optimizer: bool = False, _force_graph: bool = False):
+                 capture_optimizer: bool = False, zero_copy_grads: bool = True, _force_graph: bool = False):
         self.model = model
         self.cfg = opt_cfg
         self.dtype = compute_dtype
@@ -416,6 +485,8 @@ class TrainStep:
         # backward is seeded with 1 / k (Lightning normalises the closure loss), the gradients of k batches are
         # summed, and the optimizer / LR schedule step (and, under DDP, the exchange) happen on every k-th batch
         self.accum = max(1, int(opt_cfg.gradient_accumulation or 1))
+        if self.grad_buckets is not None:  # gradients written into the exchange buffer by the backward kernels
+            self.grad_buckets.zero_copy = zero_copy_grads and self.accum == 1 and dev.type == "cuda"
         self._micro = 0  # batches already accumulated in the current window
         self._acc = None  # (flat f32 buffer, per-parameter views) without DDP; GradBuckets' buffer under DDP
         self._touched: set = set()  # parameters that received a gradient in the current window
@@ -485,6 +556,16 @@ class TrainStep:
             elif self._acc is not None:
                 self._acc[0].zero_()
 
+    def _maybe_relayout(self):
+        """Zero-copy exchange: adopt the parameter groups the last forward recorded — only before any graph has been
+        captured (a captured backward writes into the buffer it was captured with) and between windows. Every rank
+        reaches this at the same step with the same groups (same model, same code path)."""
+        gb = self.grad_buckets
+        if (gb is not None and gb.layout_stale() and self._micro == 0
+                and not any(e is not None for e in self.graphs.values())):
+            torch.cuda.synchronize(self.device)  # the old buffer's last readers (AdamW, all-reduce) are done
+            gb.relayout()
+
     @staticmethod
     def _make_accumulate_guard(p):
         def hook(grad):
@@ -502,12 +583,18 @@ class TrainStep:
         dev = self.device
         if dev.type == "cuda":
             begin_dropout_step(dev, reset_errors=True)  # this step's error flags start clear
-        # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive capture).
-        with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32, cache_enabled=autocast_cache):
-            out = self.model(batch)
-        with deferred_colsums(dev, enabled=self.defer_colsums), \
-                weight_grad_overlap(dev, enabled=self.overlap_weight_grads):
-            out.loss.backward(self._ones(out.loss))
+        gb = self.grad_buckets
+        rec = gb if (gb is not None and gb.zero_copy) else None
+        # the backward writes gradients into the exchange buffer only on a pass whose release copies (not adds) them
+        dest = rec if (rec is not None and rec.mode != "off" and not rec.add) else None
+        with grad_destinations(dev, rec, dest):
+            # The autocast weight-cast cache must be off under HIP-graph capture (cached casts would outlive it).
+            with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32,
+                                cache_enabled=autocast_cache):
+                out = self.model(batch)
+            with deferred_colsums(dev, enabled=self.defer_colsums), \
+                    weight_grad_overlap(dev, enabled=self.overlap_weight_grads):
+                out.loss.backward(self._ones(out.loss))
         if dev.type == "cuda":
             end_dropout_step(dev)
         return out.loss.detach()
@@ -542,6 +629,7 @@ class TrainStep:
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
             check_errors(self.device, self._vocab)  # a warm-up error is this batch's error: raise it now
+            self._maybe_relayout()  # the warm-up recorded the gradient kernels' parameter groups
             self.opt.zero_grad(set_to_none=True)
             self.capture_report[sig] = sorted(spy.hits)
             if spy.hits:  # a PyTorch-ROCm BLAS fallback or ATen reduction in the step: not captured
@@ -689,6 +777,7 @@ class TrainStep:
         opt_graph = plan = None
         if entry is None:
             self.opt.zero_grad(set_to_none=True)
+            self._maybe_relayout()
             if gb is not None and not exchange:
                 gb.mode = "off"  # Lightning's no_sync on the window's earlier batches
             try:

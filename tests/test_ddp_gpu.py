@@ -47,6 +47,20 @@ def _batches(bc, rank):
             for s, n in zip(range(STEPS), LENGTHS[rank])]
 
 
+class _CopySpy(torch.utils._python_dispatch.TorchDispatchMode):
+    """Records the gradient copies / adds of the exchange's release (GradBuckets._launch)."""
+
+    def __init__(self):
+        super().__init__()
+        self.hits = []
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        name = func.__name__.split(".")[0]
+        if name in ("_foreach_copy_", "_foreach_add_"):
+            self.hits.append(name)
+        return func(*args, **(kwargs or {}))
+
+
 def _worker(rank, world, port, q):
     import datetime
     import traceback
@@ -68,18 +82,25 @@ def _worker(rank, world, port, q):
             orig(b)
 
         ts.grad_buckets._launch = spy
+        assert ts.grad_buckets.zero_copy
+        copies = _CopySpy()
         losses = []
         for i, b in enumerate(_batches(bc, rank)):
             order.clear()
-            losses.append(float(ts.step(b)))
+            with copies:  # capture (warm-up + segmented capture), replay and the eager step past max_graphs
+                losses.append(float(ts.step(b)))
             nb = len(ts.grad_buckets.buckets)
             assert order == list(range(nb)), (i, order)  # one exchange per bucket, in index order, every step
             q.put(("progress", rank, f"step {i} loss {losses[-1]:.6f}"))
         ts.check()
         segs = [len(e[0]) for e in ts.graphs.values() if e is not None]
         assert len(ts.graphs) == (1 if rank == 0 else 2) and all(n > 1 for n in segs), segs
-        base = ts.grad_buckets.flat.data_ptr()
-        in_flat = all(base <= p.grad.data_ptr() < base + 4 * ts.grad_buckets.flat.numel() for p in ts.params)
+        gb = ts.grad_buckets
+        # zero-copy exchange: every gradient was written by its backward kernel into its own view of the buffer
+        # (the q|k|v, LayerNorm and head groups laid out adjacently by the warm-up's relayout); no copy kernel ran
+        in_flat = all(p.grad.data_ptr() == gb.views[i].data_ptr() for i, p in enumerate(ts.params))
+        assert copies.hits == [], copies.hits
+        assert len(gb.laid_out) > 0, "no parameter groups recorded"
         q.put(("done", rank, (losses, in_flat, {k: v.detach().cpu().numpy().copy() for k, v in m.state_dict().items()})))
         dist.destroy_process_group()
     except BaseException:
@@ -147,7 +168,7 @@ def test_two_ranks_on_one_gpu_match_averaged_gradients():
         opt.step(opt_cfg.init_lr * lam(s))
     want = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     for r in range(world):
-        assert res[r][1], "param.grad must be views into the flat exchange buffer"
+        assert res[r][1], "param.grad must be the exchange buffer's own views"
         for k, v in want.items():
             got = torch.from_numpy(res[r][2][k])
             assert (got.float() - v.float()).abs().max().item() < 1e-4, (r, k)
@@ -258,6 +279,7 @@ def _worker_rccl_single(rank, world, port, q):
             ts = TrainStep(m, opt, torch.bfloat16, use_graph=True, bucket_mb=0.05)
             if ddp:
                 ts.grad_buckets = GradBuckets(ts.params, 1, 0.05, err_check=True)
+                ts.grad_buckets.zero_copy = True  # the backward kernels write into the RCCL exchange buffer
                 assert ts.grad_buckets.avg and len(ts.grad_buckets.buckets) > 1
             for s in range(STEPS):
                 ts.step(bc.batch(s, batch_size=8, device="cuda:0").packed())
