@@ -93,6 +93,11 @@ SIGNATURES = {
                                           _vp]),
     "esgpt_embed_epilogue_fwd": (_int, [_PB, _i64, _i64, _vp, _vp, _vp, _int, _vp, _vp]),
     "esgpt_embed_epilogue_bwd": (_int, [_PB, _i64, _i64, _vp, _int, _vp, _vp]),
+    "esgpt_embed_epilogue_bwd_ex": (_int, [_PB, _i64, _i64, _vp, _int, _vp, _int, _vp]),
+    "esgpt_split_proj_prep": (_int, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _f32, _f32, _vp, _vp,
+                                     _int, _vp]),
+    "esgpt_split_proj_post": (_int, [_vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _f32, _f32, _vp, _vp, _vp, _vp,
+                                     _int, _vp]),
     "esgpt_embed_bag_bwd_workspace": (_sz, [_PB, _i64, _i64, _i64]),
     "esgpt_embed_bag_bwd": (_int, [_PB, _PK, _int, _int, _f32, _f32, _vp, _i64, _i64, _i64, _vp, _vp, _sz, _vp]),
     "esgpt_attn_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
@@ -102,6 +107,9 @@ SIGNATURES = {
                                  _i64, _f32, _vp, _int, _vp, _vp]),
     "esgpt_attn_bwd_ex": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _vp, _int, _vp, _sz, _vp, _vp]),
+    "esgpt_attn_bwd_lead": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _vp, _int, _vp, _sz, _vp, _i64,
+                                   _vp]),
     "esgpt_attn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
     "esgpt_residual_fwd": (_int, [_vp, _vp, _int, _vp, _i64, _i64, _f32, _vp, _i64, _i64, _vp, _vp]),
     "esgpt_residual_bwd": (_int, [_vp, _vp, _i64, _i64, _f32, _vp, _i64, _i64, _vp, _vp, _int, _vp]),

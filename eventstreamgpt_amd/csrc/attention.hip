@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small(
     const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, T* __restrict__ dk,
     T* __restrict__ dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window,
-    float drop_p, const uint64_t* __restrict__ seed) {
+    float drop_p, const uint64_t* __restrict__ seed, int64_t dq_lead) {
   const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bh >= B * H) return;  // wave-uniform
   const int lane = lane_id();
@@ -367,6 +367,13 @@ __global__ __launch_bounds__(256) void attn_bwd_small(
 #pragma unroll
     for (int u = 0; u < DPL; ++u)
       if (lane + 64 * u < hd) dqp[lane + 64 * u] = from_f32<T>(dqa[u]);
+  }
+  // the rows before the first query (static_kv_first: token 0) have no query: their dq is zero
+  for (int64_t r = 1; r <= dq_lead; ++r) {
+    T* dqp = dq + (b * tq - r) * ld_d + h * hd;
+#pragma unroll
+    for (int u = 0; u < DPL; ++u)
+      if (lane + 64 * u < hd) dqp[lane + 64 * u] = from_f32<T>(0.f);
   }
 #pragma unroll
   for (int j = 0; j < LKM; ++j) {
@@ -537,7 +544,7 @@ __global__ __launch_bounds__(256) void attn_bwd_small4(
     const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, T* __restrict__ dk,
     T* __restrict__ dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window,
-    float drop_p, const uint64_t* __restrict__ seed) {
+    float drop_p, const uint64_t* __restrict__ seed, int64_t dq_lead) {
   const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (bh >= B * H) return;  // wave-uniform
   const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
@@ -599,6 +606,13 @@ __global__ __launch_bounds__(256) void attn_bwd_small4(
     }
     if (qin) store_vec<T, VE>(dq + (b * tq + ii) * ld_d + h * hd + c, dqa);
   }
+  // the rows before the first query (static_kv_first: token 0) have no query: their dq is zero
+  if (g < dq_lead) {
+    float z[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) z[e] = 0.f;
+    store_vec<T, VE>(dq + (b * tq - 1 - g) * ld_d + h * hd + c, z);
+  }
   // dK / dV: the four query groups' partials summed (every group ends with the sums); group g stores the rows
   // j = g, g + 4
 #pragma unroll
@@ -633,7 +647,7 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
                  int64_t ld_o, float* lse_w, const float* lse_r, const void* dout, int64_t ld_do,
                  const uint8_t* kmask, const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B,
                  int64_t H, int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
-                 hipStream_t st) {
+                 int64_t dq_lead, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(B * H, 4)), block(256);
   if (small4_ok<T>(Lk, hd, {q, k, v, o, dout, dq, dk, dv}, {ld_in, ld_o, ld_do, ld_d})) {
 // key registers sized to the sequence (LKM = 4, 6 or 8 keys): the C4 dependency graph (5 keys) holds 3/4 of the
@@ -647,7 +661,7 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
     else                                                                                                             \
       attn_bwd_small4<T, VE, LKM, I32><<<grid, block, 0, st>>>(                                                      \
           (const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o, ld_o, (const T*)dout, ld_do, lse_r, kmask,  \
-          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed);                         \
+          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed, dq_lead);                \
   } while (0)
   // 32-bit dropout element indices whenever the launch's indices fit (the same keep bits); the 64-bit form only for
   // launches past 2^32 elements
@@ -675,7 +689,7 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
     else                                                                                                            \
       attn_bwd_small<T, DPL, LKM><<<grid, block, 0, st>>>(                                                          \
           (const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o, ld_o, (const T*)dout, ld_do, lse_r, kmask, \
-          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed);                        \
+          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed, dq_lead);               \
   } while (0)
   if (hd <= 64) {
     if (Lk <= 8) SMALL(1, 8);
@@ -730,6 +744,16 @@ int launch_bwd_generic(const void* q, const void* k, const void* v, int64_t ld_i
   else BWD(128);
 #undef BWD
   return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
+}
+
+// dq rows [-lead, 0) of every sequence <- 0 (the paths whose kernels do not write them: MFMA, generic)
+template <typename T>
+__global__ __launch_bounds__(256) void dq_lead_zero_kernel(T* __restrict__ dq, int64_t ld_d, int64_t tq, int64_t B,
+                                                           int64_t lead, int64_t D) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, n = B * lead * D;
+  if (i >= n) return;
+  const int64_t b = i / (lead * D), r = (i / D) % lead, d = i % D;
+  dq[(b * tq - 1 - r) * ld_d + d] = from_f32<T>(0.f);
 }
 
 }  // namespace
@@ -815,9 +839,9 @@ int esgpt_attn_fwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
   if (Lk <= kSmallLk && !force_generic()) {
     if (dtype == ESGPT_F32)
       return launch_small<float>(true, q, k, v, ld_in, tq, o, ld_o, lse, nullptr, nullptr, 0, key_mask, query_mask,
-                                 nullptr, nullptr, nullptr, 0, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+                                 nullptr, nullptr, nullptr, 0, B, H, Lq, Lk, hd, window, dropout_p, seed, 0, st);
     return launch_small<bf16>(true, q, k, v, ld_in, tq, o, ld_o, lse, nullptr, nullptr, 0, key_mask, query_mask,
-                              nullptr, nullptr, nullptr, 0, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+                              nullptr, nullptr, nullptr, 0, B, H, Lq, Lk, hd, window, dropout_p, seed, 0, st);
   }
   if (dtype == ESGPT_F32)
     return launch_fwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, lse, key_mask, query_mask, B, H, Lq, Lk, hd, window,
@@ -860,7 +884,19 @@ int esgpt_attn_bwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
                       int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
                       const uint32_t* keep, int dtype, void* workspace, size_t workspace_bytes, int32_t* counters,
                       void* stream) {
+  return esgpt_attn_bwd_lead(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
+                             ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, keep, dtype, workspace,
+                             workspace_bytes, counters, 0, stream);
+}
+
+int esgpt_attn_bwd_lead(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                        int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                        const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
+                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
+                        const uint32_t* keep, int dtype, void* workspace, size_t workspace_bytes, int32_t* counters,
+                        int64_t dq_lead, void* stream) {
   ESGPT_REQUIRE(q && k && v && o && dout && lse && dq && dk && dv && hd > 0 && hd <= 128 && Lq <= Lk);
+  ESGPT_REQUIRE(dq_lead >= 0 && dq_lead <= 4 && Lq + dq_lead <= tq);
   if (esgpt_attn_keep_words(B, H, Lq, Lk, hd, tq, ld_in, ld_o, dtype, dropout_p) == 0) keep = nullptr;
   ESGPT_REQUIRE(keep == nullptr || ((uintptr_t)keep % 4) == 0);
   ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
@@ -869,21 +905,32 @@ int esgpt_attn_bwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
   if (B * H * Lk == 0) return ESGPT_OK;
   hipStream_t st = as_stream(stream);
   float* delta = (float*)workspace;
-  if (dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o))
+  const bool small = Lk <= kSmallLk && !force_generic();
+  const bool mfma = dtype == ESGPT_BF16 && !force_generic() && esgpt_attn_mfma_supported(hd, Lq, Lk, tq, ld_in, ld_o);
+  const bool mfma32 = dtype == ESGPT_F32 && !force_generic() && esgpt_attn_f32_mfma_supported(hd, Lq, Lk, ld_in, ld_o);
+  if (dq_lead > 0 && (mfma || mfma32 || !small)) {  // the small kernels write these rows themselves
+    const int64_t n = B * dq_lead * H * hd;
+    if (dtype == ESGPT_F32)
+      dq_lead_zero_kernel<float><<<(unsigned)cdiv(n, 256), 256, 0, st>>>((float*)dq, ld_dqkv, tq, B, dq_lead, H * hd);
+    else
+      dq_lead_zero_kernel<bf16><<<(unsigned)cdiv(n, 256), 256, 0, st>>>((bf16*)dq, ld_dqkv, tq, B, dq_lead, H * hd);
+    dq_lead = 0;
+  }
+  if (mfma)
     return esgpt_attn_bwd_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,
                                ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, keep, (float*)workspace,
                                counters, st);
-  if (dtype == ESGPT_F32 && !force_generic() && esgpt_attn_f32_mfma_supported(hd, Lq, Lk, ld_in, ld_o)) {
+  if (mfma32) {
     const int rc = esgpt_attn_bwd_f32_mfma(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq,
                                            dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, delta, st);
     if (rc != ESGPT_ERR_UNSUPPORTED) return rc;
   }
-  if (Lk <= kSmallLk && !force_generic()) {
+  if (small) {
     if (dtype == ESGPT_F32)
       return launch_small<float>(false, q, k, v, ld_in, tq, o, ld_o, nullptr, lse, dout, ld_do, key_mask, query_mask,
-                                 dq, dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+                                 dq, dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, dq_lead, st);
     return launch_small<bf16>(false, q, k, v, ld_in, tq, o, ld_o, nullptr, lse, dout, ld_do, key_mask, query_mask,
-                              dq, dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, st);
+                              dq, dk, dv, ld_dqkv, B, H, Lq, Lk, hd, window, dropout_p, seed, dq_lead, st);
   }
   if (dtype == ESGPT_F32)
     return launch_bwd_generic<float>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, key_mask, query_mask, dq, dk, dv,

@@ -520,9 +520,11 @@ __global__ __launch_bounds__(256) void embed_epilogue_fwd_kernel(esgpt_batch bt,
   }
 }
 
+// dy in OT: f32, or bf16 when it feeds the SPLIT projection's bf16 backward GEMM directly (no separate cast pass)
+template <typename OT>
 __global__ __launch_bounds__(256) void embed_epilogue_bwd_kernel(esgpt_batch bt, int64_t G, int64_t D,
                                                                  const float* __restrict__ dout, int flags,
-                                                                 float* __restrict__ dy) {
+                                                                 OT* __restrict__ dy) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t n = bt.B * bt.L * D;
   if (i >= n) return;
@@ -532,10 +534,78 @@ __global__ __launch_bounds__(256) void embed_epilogue_bwd_kernel(esgpt_batch bt,
     float run = 0.f;  // reverse cumsum in f32 (autograd of cumsum = flip-cumsum-flip in f32)
     for (int64_t g = G - 1; g >= 0; --g) {
       run += dout[(e * G + g) * D + d];
-      dy[(e * G + g) * D + d] = valid ? run : 0.f;
+      dy[(e * G + g) * D + d] = from_f32<OT>(valid ? run : 0.f);
     }
   } else {
-    for (int64_t g = 0; g < G; ++g) dy[(e * G + g) * D + d] = valid ? dout[(e * G + g) * D + d] : 0.f;
+    for (int64_t g = 0; g < G; ++g) dy[(e * G + g) * D + d] = from_f32<OT>(valid ? dout[(e * G + g) * D + d] : 0.f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// SPLIT projection operands (data_embedding_layer.py:390-450: cat_proj(cat bags) + num_proj(num bags) as ONE GEMM
+// over the concatenated bag columns). prep: W = [cat_w | num_w] in the GEMM dtype (column concatenation),
+// bias = a_c·cat_b + a_n·num_b (f32, no fused multiply-add: PyTorch's scalar-times-tensor then add), and the bag
+// matrix in the GEMM dtype (bf16; the f32 form reads the bags as they are). post: the grouped backward's dW columns
+// back to the two weights, d bias = a·db for each, and dx to f32 for the bag backward.
+// ------------------------------------------------------------------------------------------------------------
+template <typename LT>
+__global__ __launch_bounds__(256) void split_proj_prep_kernel(const float* __restrict__ x, int64_t nx4,
+                                                              LT* __restrict__ x_lp, const float* __restrict__ wc,
+                                                              const float* __restrict__ wn, int64_t D, int64_t Dc,
+                                                              int64_t Dn, const float* __restrict__ bc,
+                                                              const float* __restrict__ bn, float a_c, float a_n,
+                                                              LT* __restrict__ w_lp, float* __restrict__ bias,
+                                                              int64_t nw_blocks) {
+  const int64_t Dx = Dc + Dn;
+  if ((int64_t)blockIdx.x < nw_blocks) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < D * Dx) {
+      const int64_t r = i / Dx, c = i % Dx;
+      w_lp[i] = from_f32<LT>(c < Dc ? wc[r * Dc + c] : wn[r * Dn + (c - Dc)]);
+    } else if (i < D * Dx + D) {
+      const int64_t r = i - D * Dx;
+      bias[r] = __fadd_rn(__fmul_rn(a_c, bc[r]), __fmul_rn(a_n, bn[r]));
+    }
+    return;
+  }
+  const int64_t j = ((int64_t)blockIdx.x - nw_blocks) * 256 + threadIdx.x;  // 4 bag values per thread
+  if (j >= nx4) return;
+  const float4 v = reinterpret_cast<const float4*>(x)[j];
+  if constexpr (sizeof(LT) == 2) {
+    uint2 o;
+    o.x = (uint32_t)f32_to_bf16_bits(v.x) | ((uint32_t)f32_to_bf16_bits(v.y) << 16);
+    o.y = (uint32_t)f32_to_bf16_bits(v.z) | ((uint32_t)f32_to_bf16_bits(v.w) << 16);
+    reinterpret_cast<uint2*>(x_lp)[j] = o;
+  }
+}
+
+template <typename LT>
+__global__ __launch_bounds__(256) void split_proj_post_kernel(const LT* __restrict__ dx_lp, int64_t ndx4,
+                                                              float* __restrict__ dx, const float* __restrict__ dw,
+                                                              const float* __restrict__ db, int64_t D, int64_t Dc,
+                                                              int64_t Dn, float a_c, float a_n, float* __restrict__ dwc,
+                                                              float* __restrict__ dwn, float* __restrict__ dbc,
+                                                              float* __restrict__ dbn, int64_t nw_blocks) {
+  const int64_t Dx = Dc + Dn;
+  if ((int64_t)blockIdx.x < nw_blocks) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < D * Dx) {
+      const int64_t r = i / Dx, c = i % Dx;
+      if (c < Dc) dwc[r * Dc + c] = dw[i];
+      else dwn[r * Dn + (c - Dc)] = dw[i];
+    } else if (i < D * Dx + D) {
+      const int64_t r = i - D * Dx;
+      if (dbc) dbc[r] = __fmul_rn(db[r], a_c);
+      if (dbn) dbn[r] = __fmul_rn(db[r], a_n);
+    }
+    return;
+  }
+  const int64_t j = ((int64_t)blockIdx.x - nw_blocks) * 256 + threadIdx.x;
+  if (j >= ndx4) return;
+  if constexpr (sizeof(LT) == 2) {
+    const uint2 t = reinterpret_cast<const uint2*>(dx_lp)[j];
+    reinterpret_cast<float4*>(dx)[j] = make_float4(__uint_as_float(t.x << 16), __uint_as_float(t.x & 0xffff0000u),
+                                                   __uint_as_float(t.y << 16), __uint_as_float(t.y & 0xffff0000u));
   }
 }
 
@@ -1359,11 +1429,61 @@ int esgpt_embed_epilogue_fwd(const esgpt_batch* batch, int64_t G, int64_t D, con
 
 int esgpt_embed_epilogue_bwd(const esgpt_batch* batch, int64_t G, int64_t D, const float* dout, int flags, float* dy,
                              void* stream) {
-  ESGPT_REQUIRE(batch && dout && dy && G >= 1 && D > 0);
+  return esgpt_embed_epilogue_bwd_ex(batch, G, D, dout, flags, dy, ESGPT_F32, stream);
+}
+
+int esgpt_embed_epilogue_bwd_ex(const esgpt_batch* batch, int64_t G, int64_t D, const float* dout, int flags, void* dy,
+                                int dy_dtype, void* stream) {
+  ESGPT_REQUIRE(batch && dout && dy && G >= 1 && D > 0 && (dy_dtype == ESGPT_F32 || dy_dtype == ESGPT_BF16));
   const int64_t n = batch->B * batch->L * D;
   if (n == 0) return ESGPT_OK;
-  embed_epilogue_bwd_kernel<<<dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream)>>>(*batch, G, D, dout,
-                                                                                               flags, dy);
+  const dim3 grid((unsigned)cdiv(n, 256)), block(256);
+  if (dy_dtype == ESGPT_BF16)
+    embed_epilogue_bwd_kernel<bf16><<<grid, block, 0, as_stream(stream)>>>(*batch, G, D, dout, flags, (bf16*)dy);
+  else
+    embed_epilogue_bwd_kernel<float><<<grid, block, 0, as_stream(stream)>>>(*batch, G, D, dout, flags, (float*)dy);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_split_proj_prep(const float* x, int64_t N, void* x_lp, const float* cat_w, const float* num_w, int64_t D,
+                          int64_t Dc, int64_t Dn, const float* cat_b, const float* num_b, float a_c, float a_n,
+                          void* w_lp, float* bias, int dtype, void* stream) {
+  ESGPT_REQUIRE(cat_w && num_w && cat_b && num_b && w_lp && bias && D > 0 && Dc > 0 && Dn > 0 && N >= 0);
+  ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  const int64_t Dx = Dc + Dn;
+  const bool conv = dtype == ESGPT_BF16;
+  ESGPT_REQUIRE(!conv || (x && x_lp && Dx % 4 == 0 && ((uintptr_t)x % 16) == 0 && ((uintptr_t)x_lp % 8) == 0));
+  const int64_t nw = cdiv(D * Dx + D, 256), nx4 = conv ? N * Dx / 4 : 0;
+  const dim3 grid((unsigned)(nw + cdiv(nx4, 256))), block(256);
+  hipStream_t st = as_stream(stream);
+  if (conv)
+    split_proj_prep_kernel<bf16><<<grid, block, 0, st>>>(x, nx4, (bf16*)x_lp, cat_w, num_w, D, Dc, Dn, cat_b, num_b,
+                                                         a_c, a_n, (bf16*)w_lp, bias, nw);
+  else
+    split_proj_prep_kernel<float><<<grid, block, 0, st>>>(x, 0, nullptr, cat_w, num_w, D, Dc, Dn, cat_b, num_b, a_c,
+                                                          a_n, (float*)w_lp, bias, nw);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_split_proj_post(const void* dx_lp, int64_t N, float* dx, const float* dw, const float* db, int64_t D,
+                          int64_t Dc, int64_t Dn, float a_c, float a_n, float* cat_dw, float* num_dw, float* cat_db,
+                          float* num_db, int dtype, void* stream) {
+  ESGPT_REQUIRE(dw && db && cat_dw && num_dw && D > 0 && Dc > 0 && Dn > 0 && N >= 0);
+  ESGPT_REQUIRE(dtype == ESGPT_F32 || dtype == ESGPT_BF16);
+  const int64_t Dx = Dc + Dn;
+  const bool conv = dtype == ESGPT_BF16 && dx_lp;
+  ESGPT_REQUIRE(!conv || (dx && Dx % 4 == 0 && ((uintptr_t)dx % 16) == 0 && ((uintptr_t)dx_lp % 8) == 0));
+  const int64_t nw = cdiv(D * Dx + D, 256), ndx4 = conv ? N * Dx / 4 : 0;
+  const dim3 grid((unsigned)(nw + cdiv(ndx4, 256))), block(256);
+  hipStream_t st = as_stream(stream);
+  if (conv)
+    split_proj_post_kernel<bf16><<<grid, block, 0, st>>>((const bf16*)dx_lp, ndx4, dx, dw, db, D, Dc, Dn, a_c, a_n,
+                                                         cat_dw, num_dw, cat_db, num_db, nw);
+  else
+    split_proj_post_kernel<float><<<grid, block, 0, st>>>(nullptr, 0, nullptr, dw, db, D, Dc, Dn, a_c, a_n, cat_dw,
+                                                          num_dw, cat_db, num_db, nw);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -181,15 +181,70 @@ Tensor embed_epilogue(const Tensor& y, BATCH_ARGS, int64_t G, int64_t flags, con
   return out;
 }
 
-Tensor embed_epilogue_bwd(const Tensor& dout, BATCH_ARGS, int64_t G, int64_t flags) {
+Tensor embed_epilogue_bwd(const Tensor& dout, BATCH_ARGS, int64_t G, int64_t flags,
+                          optional<at::ScalarType> dtype) {
   const c10::DeviceGuard guard(dout.device());
   Batch bt = make_batch(BATCH_PASS);
   Tensor d = as(dout, at::kFloat);
   const int64_t D = d.size(-1);
-  Tensor dy = at::empty({bt.b.B * bt.b.L * G, D}, d.options());
-  check(esgpt_embed_epilogue_bwd(&bt.b, G, D, ptr<const float>(d), (int)flags, ptr<float>(dy), stream_of(d)),
+  const at::ScalarType dt = dtype.value_or(at::kFloat);
+  TORCH_CHECK(dt == at::kFloat || dt == at::kBFloat16, "embed_epilogue_bwd: f32 or bf16 output");
+  Tensor dy = at::empty({bt.b.B * bt.b.L * G, D}, d.options().dtype(dt));
+  check(esgpt_embed_epilogue_bwd_ex(&bt.b, G, D, ptr<const float>(d), (int)flags, dy.data_ptr(), dtype_code(dt),
+                                    stream_of(d)),
         "embed_epilogue_bwd");
   return dy;
+}
+
+// SPLIT projection operands: (x_lp | empty for f32, w_lp [D, Dc+Dn], bias f32 [D])
+std::tuple<Tensor, Tensor, Tensor> split_proj_prep(const Tensor& x, const Tensor& cat_w, const Tensor& num_w,
+                                                   const Tensor& cat_b, const Tensor& num_b, double a_c, double a_n,
+                                                   at::ScalarType dtype) {
+  const c10::DeviceGuard guard(x.device());
+  TORCH_CHECK(dtype == at::kFloat || dtype == at::kBFloat16, "split_proj_prep: f32 or bf16");
+  Tensor xf = as(x, at::kFloat), wc = as(cat_w, at::kFloat), wn = as(num_w, at::kFloat);
+  Tensor bc = as(cat_b, at::kFloat), bn = as(num_b, at::kFloat);
+  const int64_t D = wc.size(0), Dc = wc.size(1), Dn = wn.size(1), Dx = Dc + Dn;
+  TORCH_CHECK(wn.size(0) == D && bc.numel() == D && bn.numel() == D && xf.size(-1) == Dx,
+              "split_proj_prep: shapes");
+  const int64_t N = xf.numel() / Dx;
+  const bool conv = dtype == at::kBFloat16;
+  Tensor x_lp = conv ? at::empty({N, Dx}, xf.options().dtype(dtype)) : at::empty({0}, xf.options());
+  Tensor w_lp = at::empty({D, Dx}, xf.options().dtype(dtype));
+  Tensor bias = at::empty({D}, xf.options());
+  check(esgpt_split_proj_prep(ptr<const float>(xf), N, conv ? x_lp.data_ptr() : nullptr, ptr<const float>(wc),
+                              ptr<const float>(wn), D, Dc, Dn, ptr<const float>(bc), ptr<const float>(bn), (float)a_c,
+                              (float)a_n, w_lp.data_ptr(), ptr<float>(bias), dtype_code(dtype), stream_of(xf)),
+        "split_proj_prep");
+  return {x_lp, w_lp, bias};
+}
+
+// SPLIT projection gradients: the four parameter gradients written into the given tensors; returns dx f32 (empty
+// without dx_lp)
+Tensor split_proj_post(const optional<Tensor>& dx_lp_, const Tensor& dw, const Tensor& db, int64_t Dc, double a_c,
+                       double a_n, const Tensor& cat_dw, const Tensor& num_dw, const Tensor& cat_db,
+                       const Tensor& num_db) {
+  const c10::DeviceGuard guard(dw.device());
+  const int64_t D = dw.size(0), Dx = dw.size(1), Dn = Dx - Dc;
+  TORCH_CHECK(dw.scalar_type() == at::kFloat && db.scalar_type() == at::kFloat && dw.is_contiguous() &&
+                  db.is_contiguous() && db.numel() == D && Dc > 0 && Dn > 0,
+              "split_proj_post: dw f32 [D, Dc+Dn], db f32 [D]");
+  for (const Tensor* t : {&cat_dw, &num_dw, &cat_db, &num_db})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->device() == dw.device(),
+                "split_proj_post: contiguous f32 outputs");
+  TORCH_CHECK(cat_dw.numel() == D * Dc && num_dw.numel() == D * Dn && cat_db.numel() == D && num_db.numel() == D,
+              "split_proj_post: output sizes");
+  const bool has_dx = dx_lp_.has_value() && dx_lp_->defined();
+  Tensor dx_lp = has_dx ? dx_lp_->contiguous() : Tensor();
+  TORCH_CHECK(!has_dx || (dx_lp.scalar_type() == at::kBFloat16 && dx_lp.size(-1) == Dx), "split_proj_post: dx_lp");
+  const int64_t N = has_dx ? dx_lp.numel() / Dx : 0;
+  Tensor dx = has_dx ? at::empty({N, Dx}, dw.options()) : at::empty({0}, dw.options());
+  check(esgpt_split_proj_post(has_dx ? dx_lp.data_ptr() : nullptr, N, has_dx ? ptr<float>(dx) : nullptr,
+                              ptr<const float>(dw), ptr<const float>(db), D, Dc, Dn, (float)a_c, (float)a_n,
+                              ptr<float>(cat_dw), ptr<float>(num_dw), ptr<float>(cat_db), ptr<float>(num_db),
+                              has_dx ? ESGPT_BF16 : ESGPT_F32, stream_of(dw)),
+        "split_proj_post");
+  return dx;
 }
 
 // dsrc: rows of leading dimension ld (elements), D columns used (may be a column slice of a wider matrix)
@@ -382,9 +437,8 @@ Tensor attention_bwd(const Tensor& qkv_, const Tensor& o, const Tensor& dout_, c
   const int64_t Bs = qkv.size(0), T = qkv.size(1), D3 = qkv.size(2), D = D3 / 3, hd = D / H;
   const int64_t skf = static_kv_first ? 1 : 0, Lk = T, Lq = T - skf;
   const int64_t es = qkv.element_size();
-  // static_kv_first: the kernels write every row of dk / dv and the dq rows after token 0; token 0's dq is zero
+  // static_kv_first: the kernels write every row of dk / dv and the dq rows after token 0, and zero token 0's dq
   Tensor dqkv = at::empty_like(qkv);
-  if (skf) dqkv.select(1, 0).narrow(-1, 0, D).zero_();
   const size_t nb = esgpt_attn_bwd_workspace(Bs, H, Lq, Lk, hd);
   Tensor ws = at::empty({(int64_t)std::max<size_t>(nb, 1)}, qkv.options().dtype(at::kByte));
   int32_t* counters = esgpt_attn_bwd_counters(Bs, H, Lk) <= tickets.numel() ? ptr<int32_t>(tickets) : nullptr;
@@ -399,12 +453,12 @@ Tensor attention_bwd(const Tensor& qkv_, const Tensor& o, const Tensor& dout_, c
                 "esgpt.attention_bwd: keep must be the int32 tensor attention returned");
     kp = reinterpret_cast<const uint32_t*>(keep->data_ptr());
   }
-  check(esgpt_attn_bwd_ex(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
+  check(esgpt_attn_bwd_lead(base + skf * D3 * es, base + D * es, base + 2 * D * es, D3, T, o.data_ptr(), D,
                           dout.data_ptr(), D, ptr<const float>(lse), km.defined() ? ptr<const uint8_t>(km) : nullptr,
                           qm.defined() ? ptr<const uint8_t>(qm) : nullptr, dbase + skf * D3 * es, dbase + D * es,
                           dbase + 2 * D * es, D3, Bs, H, Lq, Lk, hd, window, (float)dropout_p,
                           optr<const uint64_t>(seed), kp, dtype_code(qkv.scalar_type()), ws.data_ptr(), nb, counters,
-                          stream_of(qkv)),
+                          skf, stream_of(qkv)),
         "attention_bwd");
   return dqkv;
 }
@@ -933,7 +987,11 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("embed_split_bags(Tensor cat_table, Tensor num_table, " BATCH_SCHEMA ", int[] buckets, int flags, "
         "float cat_scale, float num_scale, float static_scale, int G, Tensor err) -> Tensor");
   m.def("embed_epilogue(Tensor y, " BATCH_SCHEMA ", int G, int flags, Tensor? sin_div, Tensor? cos_div) -> Tensor");
-  m.def("embed_epilogue_bwd(Tensor dout, " BATCH_SCHEMA ", int G, int flags) -> Tensor");
+  m.def("embed_epilogue_bwd(Tensor dout, " BATCH_SCHEMA ", int G, int flags, ScalarType? dtype=None) -> Tensor");
+  m.def("split_proj_prep(Tensor x, Tensor cat_w, Tensor num_w, Tensor cat_b, Tensor num_b, float a_c, float a_n, "
+        "ScalarType dtype) -> (Tensor, Tensor, Tensor)");
+  m.def("split_proj_post(Tensor? dx_lp, Tensor dw, Tensor db, int Dc, float a_c, float a_n, Tensor(a!) cat_dw, "
+        "Tensor(b!) num_dw, Tensor(c!) cat_db, Tensor(d!) num_db) -> Tensor");
   m.def("embed_bag_bwd(Tensor dsrc, " BATCH_SCHEMA ", int[] buckets, int selector, int flags, float dyn_scale, "
         "float static_scale, int ld, int D, int V, int G, Tensor(a!)? out=None) -> Tensor");
   m.def("attention(Tensor qkv, Tensor? key_mask, Tensor? query_mask, int H, int window, bool static_kv_first, "
@@ -996,6 +1054,8 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("embed_split_bags", &embed_split_bags);
   m.impl("embed_epilogue", &embed_epilogue);
   m.impl("embed_epilogue_bwd", &embed_epilogue_bwd);
+  m.impl("split_proj_prep", &split_proj_prep);
+  m.impl("split_proj_post", &split_proj_post);
   m.impl("embed_bag_bwd", &embed_bag_bwd);
   m.impl("residual", &residual);
   m.impl("residual_bwd", &residual_bwd);

@@ -178,12 +178,20 @@ class DataEmbeddingLayer(torch.nn.Module):
         spec = EmbedSpec(flags, self.static_weight, self.dynamic_weight, self._buckets, G)
         x = split_bags(self.categorical_embed_layer.weight, self.numerical_embed_layer.weight, batch, spec,
                        cat_scale, num_scale, static_scale)
-        w = torch.cat([self.cat_proj.weight, self.num_proj.weight], dim=1)
-        bias = (cat_scale + static_scale) * self.cat_proj.bias + num_scale * self.num_proj.bias
         from ..fused import GEMM_DTYPES, compute_dtype, gemm_supported, linear_op
+        from ..kernels import split_projection
 
         x2 = x.reshape(-1, x.shape[-1])
         dt = compute_dtype()
+        D = self.cat_proj.weight.shape[0]
+        if (x2.is_cuda and dt in GEMM_DTYPES and gemm_supported(x2.shape[0], x2.shape[1], D)
+                and self.cat_proj.bias is not None and self.num_proj.bias is not None):
+            # projection + epilogue in one autograd node: no weight cat, bias arithmetic or dtype casts as
+            # framework kernels (kernels._SplitProjection)
+            return split_projection(x2, self.cat_proj, self.num_proj, cat_scale + static_scale, num_scale, batch, G,
+                                    post, sin_div, cos_div, dt)
+        w = torch.cat([self.cat_proj.weight, self.num_proj.weight], dim=1)
+        bias = (cat_scale + static_scale) * self.cat_proj.bias + num_scale * self.num_proj.bias
         if x2.is_cuda and dt in GEMM_DTYPES and gemm_supported(x2.shape[0], w.shape[1], w.shape[0]):
             # the HIP GEMM, bf16 or exact f32 (bias in the epilogue; dW, db in one grouped backward launch)
             with torch.autocast("cuda", enabled=False):

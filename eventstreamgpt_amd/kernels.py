@@ -419,6 +419,59 @@ def embed_epilogue(y, batch: PytorchBatch, G: int, flags: int, sin_div, cos_div)
     return _ops().embed_epilogue(y, *batch_args(batch), G, flags, sin_div, cos_div)
 
 
+class _SplitProjection(torch.autograd.Function):
+    """SPLIT input projection + epilogue (data_embedding_layer.py:390-450 cat_proj / num_proj, then the temporal
+    encoding / level cumsum / event mask): ``esgpt::split_proj_prep`` (the two weights column-concatenated in the
+    GEMM dtype, the combined bias, the bags in the GEMM dtype — one launch), one GEMM with f32 output and the bias in
+    its epilogue, ``esgpt::embed_epilogue``. Backward: the epilogue backward writes dy in the GEMM dtype, one grouped
+    ``linear_bwd`` (dx, dW, db), ``esgpt::split_proj_post`` (dW column blocks and scaled bias gradients to the four
+    parameters — straight into DDP exchange-buffer regions when active — and dx to f32). No framework kernels."""
+
+    @staticmethod
+    def forward(ctx, x, cat_w, num_w, cat_b, num_b, a_c, a_n, dt, batch, G, flags, sin_div, cos_div):
+        ops = _ops()
+        N, Dx = x.shape
+        D, Dc = cat_w.shape
+        x_lp, w_lp, bias = ops.split_proj_prep(x, cat_w, num_w, cat_b, num_b, float(a_c), float(a_n), dt)
+        a = x_lp if dt == torch.bfloat16 else x
+        y = torch.empty(N, D, dtype=torch.float32, device=x.device)
+        ops.gemm_(y, L.GEMM_K_CONTIG, a, Dx, L.GEMM_K_CONTIG, w_lp, Dx, N, D, Dx, bias, None, False,
+                  tickets(x.device))
+        out = ops.embed_epilogue(y, *batch_args(batch), G, flags, sin_div, cos_div)
+        ctx.save_for_backward(a, w_lp)
+        ctx.batch, ctx.meta = batch, (G, flags, dt, Dc, float(a_c), float(a_n))
+        ctx.params = (cat_w, num_w, cat_b, num_b)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .ops import _dest, _leaves, _linear_bwd
+
+        a, w_lp = ctx.saved_tensors
+        G, flags, dt, Dc, a_c, a_n = ctx.meta
+        ops = _ops()
+        dy = ops.embed_epilogue_bwd(dout.contiguous().float(), *batch_args(ctx.batch), G, flags, dt)
+        need_dx = ctx.needs_input_grad[0]
+        dx_lp, dw, db = _linear_bwd(dy, a, w_lp, None, -1, None, need_dx, True)
+        ok = _leaves(*ctx.params)
+        outs = []
+        for p in ctx.params:
+            r = _dest(ok, [p], 0, p.shape)
+            outs.append(r if r is not None else torch.empty(p.shape, dtype=torch.float32, device=p.device))
+        dx = ops.split_proj_post(dx_lp if (need_dx and dt == torch.bfloat16) else None, dw, db, Dc, a_c, a_n, *outs)
+        if dt != torch.bfloat16:
+            dx = dx_lp
+        return (dx if need_dx else None, *outs) + (None,) * 8
+
+
+def split_projection(x, cat_proj, num_proj, a_c: float, a_n: float, batch: PytorchBatch, G: int, flags: int,
+                     sin_div, cos_div, dt):
+    """SPLIT projection of the bag matrix x [B*L*G, Dc+Dn] (f32) + epilogue → f32 [B, L, G, D] (_SplitProjection);
+    the GEMM runs in ``dt`` (bf16, or f32 in the reference-precision mode)."""
+    return _SplitProjection.apply(x, cat_proj.weight, num_proj.weight, cat_proj.bias, num_proj.bias, a_c, a_n, dt,
+                                  batch, G, flags, sin_div, cos_div)
+
+
 def bag_bwd(batch: PytorchBatch, groups: list, selector: int, flags: int, dyn_scale: float, static_scale: float,
             dsrc, ld: int, D: int, V: int, G: int):
     """``esgpt::embed_bag_bwd``: the table gradient of the bag sums (dsrc rows of leading dimension ``ld``)."""

@@ -12,7 +12,8 @@ Differentiable operators and the reference code they replace:
 ``embed_joint``       DataEmbeddingLayer JOINT (+ static SUM_ALL, temporal encoding, NA level cumsum, mask):
                       data_embedding_layer.py:351-388, 609-708; transformer.py:594-672, 903-936
 ``embed_split_bags``  the two EmbeddingBag gathers of ``_split_embed`` (data_embedding_layer.py:390-450)
-``embed_epilogue``    temporal encoding / level cumsum / mask after the SPLIT projection
+``embed_epilogue``    temporal encoding / level cumsum / mask after the SPLIT projection (the bf16 / f32 SPLIT
+                      path runs ``split_proj_prep`` + GEMM + ``embed_epilogue`` in kernels._SplitProjection)
 ``attention``         InnerSelfAttention._attn (transformer.py:171-217) on a packed q|k|v buffer
 ``residual_ln``       residual + resid dropout + event mask + LayerNorm (transformer.py:350-461, 810-831)
 ``bias_act``          c_fc bias + activation (transformer.py:378-391)
@@ -52,7 +53,7 @@ OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd"
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
        "pack", "adamw", "adamw_dev", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank", "residual",
        "residual_bwd", "na_split", "na_split_bwd_", "na_assemble", "na_assemble_bwd", "na_head_split",
-       "na_head_split_bwd")
+       "na_head_split_bwd", "split_proj_prep", "split_proj_post")
 
 
 def load():
@@ -149,8 +150,19 @@ def _register():
         return y.new_empty(di.shape[0], di.shape[1], G, y.shape[-1], dtype=torch.float32)
 
     @fake(lib + "embed_epilogue_bwd")
-    def _(dout, em, td, tm, di, dm, dv, dvm, si, sm, G, flags):
-        return dout.new_empty(di.shape[0] * di.shape[1] * G, dout.shape[-1], dtype=torch.float32)
+    def _(dout, em, td, tm, di, dm, dv, dvm, si, sm, G, flags, dtype=None):
+        return dout.new_empty(di.shape[0] * di.shape[1] * G, dout.shape[-1], dtype=dtype or torch.float32)
+
+    @fake(lib + "split_proj_prep")
+    def _(x, cat_w, num_w, cat_b, num_b, a_c, a_n, dtype):
+        D, Dx = cat_w.shape[0], cat_w.shape[1] + num_w.shape[1]
+        n = x.numel() // Dx if dtype == torch.bfloat16 else 0
+        return (x.new_empty(n, Dx, dtype=dtype) if n else x.new_empty(0, dtype=torch.float32),
+                x.new_empty(D, Dx, dtype=dtype), x.new_empty(D, dtype=torch.float32))
+
+    @fake(lib + "split_proj_post")
+    def _(dx_lp, dw, db, Dc, a_c, a_n, cat_dw, num_dw, cat_db, num_db):
+        return dw.new_empty(0) if dx_lp is None else dw.new_empty(dx_lp.numel() // dw.shape[1], dw.shape[1])
 
     @fake(lib + "embed_bag_bwd")
     def _(dsrc, em, td, tm, di, dm, dv, dvm, si, sm, buckets, selector, flags, dyn_scale, static_scale, ld, D, V, G,

@@ -418,6 +418,14 @@ class GradBuckets:
         self.reset()
 
 
+def _copy_scalar(t: torch.Tensor) -> torch.Tensor:
+    """A device copy of a small f32 tensor (one esgpt::pack launch)."""
+    from . import _lib as L
+    from .kernels import _ops
+
+    return _ops().pack([t.reshape(-1)], [1], [0], [L.F32])[0].view(t.shape)
+
+
 class _GemmSpy(torch.utils._python_dispatch.TorchDispatchMode):
     """Records the ATen ops of a step that must not be captured into a HIP graph (forward or backward: the mode
     follows autograd into its worker threads):
@@ -798,9 +806,9 @@ class TrainStep:
                 if exchange:  # exchanged while the next segment replays
                     for b in released:
                         gb._launch(b)
-            # the next replay overwrites the static loss: hand back a copy, made by an elementwise kernel (x * 1 is
-            # exact) rather than clone()'s D2D blit, which costs ~5 us of device time for 4 bytes
-            loss = sloss.mul(1.0)
+            # the next replay overwrites the static loss: hand back a copy, made by the library's pack kernel rather
+            # than clone()'s D2D blit (~5 us of device time for 4 bytes) or a framework elementwise kernel
+            loss = _copy_scalar(sloss)
         if accumulating and not exchange:
             self._accumulate()  # into the window's buffer (GradBuckets' under DDP)
         if not last:

@@ -113,6 +113,23 @@ int esgpt_embed_epilogue_fwd(const esgpt_batch* batch, int64_t G, int64_t D, con
 /* dy[e,g] = mask_e * sum_{g'>=g} dout[e,g'] (CUMSUM) or mask_e * dout[e,g]. */
 int esgpt_embed_epilogue_bwd(const esgpt_batch* batch, int64_t G, int64_t D, const float* dout, int flags,
                              float* dy, void* stream);
+/* The same with dy in dy_dtype (ESGPT_F32 or ESGPT_BF16: the SPLIT projection's bf16 backward GEMM operand). */
+int esgpt_embed_epilogue_bwd_ex(const esgpt_batch* batch, int64_t G, int64_t D, const float* dout, int flags, void* dy,
+                                int dy_dtype, void* stream);
+/* SPLIT projection (data_embedding_layer.py:390-450, cat_proj(cat bags) + num_proj(num bags)) as one GEMM over the
+ * concatenated bag columns x [N, Dc+Dn] (esgpt_embed_split_bags_fwd's output):
+ *   esgpt_split_proj_prep: w_lp [D, Dc+Dn] = [cat_w | num_w] in `dtype` (ESGPT_BF16 / ESGPT_F32), bias [D] =
+ *     a_c·cat_b + a_n·num_b (f32, unfused multiply then add), and for ESGPT_BF16 x_lp = bf16(x) (x f32, 16-B
+ *     aligned, (Dc+Dn) % 4 == 0); the f32 form leaves x as the GEMM operand (x / x_lp unused). One launch.
+ *   esgpt_split_proj_post: from the grouped backward's dw [D, Dc+Dn] and db [D]: cat_dw [D, Dc], num_dw [D, Dn]
+ *     (the column blocks), cat_db = a_c·db and num_db = a_n·db (either may be NULL), and for ESGPT_BF16 with dx_lp
+ *     given dx = f32(dx_lp) [N, Dc+Dn] (the bag backward's operand). One launch. */
+int esgpt_split_proj_prep(const float* x, int64_t N, void* x_lp, const float* cat_w, const float* num_w, int64_t D,
+                          int64_t Dc, int64_t Dn, const float* cat_b, const float* num_b, float a_c, float a_n,
+                          void* w_lp, float* bias, int dtype, void* stream);
+int esgpt_split_proj_post(const void* dx_lp, int64_t N, float* dx, const float* dw, const float* db, int64_t D,
+                          int64_t Dc, int64_t Dn, float a_c, float a_n, float* cat_dw, float* num_dw, float* cat_db,
+                          float* num_db, int dtype, void* stream);
 
 /* Table gradient of the bag sums (EmbeddingBag backward, atomic-free CSR form):
  * dtable[v,:] = sum over entries (e,g,m) with index v of w(e,g,m) * dsrc[e*G+g, :]
@@ -129,7 +146,7 @@ int esgpt_embed_bag_bwd(const esgpt_batch* batch, const esgpt_buckets* buckets, 
  * Element (b,t,h,d) of k/v lives at base + (b*Lk + t)*ld_in + h*hd + d, of q (and dq) at base + (b*tq + t)*ld_in
  * + h*hd + d, of o/dout at base + (b*Lq + t)*ld_o + h*hd + d (q/k/v may alias one packed [.,3D] buffer).
  * Query i sits at key position i + (Lk - Lq): static_kv_first (transformer.py:256-259) drops query 0, i.e. pass
- * q = packed + ld_in, tq = Lk, Lq = Lk - 1 (the caller zero-fills the dq rows of token 0).
+ * q = packed + ld_in, tq = Lk, Lq = Lk - 1 (esgpt_attn_bwd_lead with dq_lead = 1 also writes token 0's zero dq).
  * Rows whose query is padded (query_mask == 0) are written as zeros (the reference zeroes them downstream,
  * transformer.py:818-823). lse: f32 [B,H,Lq] (natural-log softmax normaliser, for the backward).
  * Attention-probability dropout (transformer.py:208): dropout_p in [0,1); keep(b,h,i,j) is a counter hash of
@@ -179,6 +196,15 @@ int esgpt_attn_bwd_ex(const void* q, const void* k, const void* v, int64_t ld_in
                       int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
                       const uint32_t* keep, int dtype, void* workspace, size_t workspace_bytes, int32_t* counters,
                       void* stream);
+/* The same, also zero-filling the dq rows t in [-dq_lead, 0) of every sequence (0 <= dq_lead <= 4, Lq + dq_lead <=
+ * tq): static_kv_first's token 0, which is no query (transformer.py:256-259), in the same launch on the small
+ * (dependency-graph) path, one small extra kernel on the others. Replaces a strided framework fill. */
+int esgpt_attn_bwd_lead(const void* q, const void* k, const void* v, int64_t ld_in, int64_t tq, const void* o,
+                        int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const uint8_t* key_mask,
+                        const uint8_t* query_mask, void* dq, void* dk, void* dv, int64_t ld_dqkv, int64_t B, int64_t H,
+                        int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float dropout_p, const uint64_t* seed,
+                        const uint32_t* keep, int dtype, void* workspace, size_t workspace_bytes, int32_t* counters,
+                        int64_t dq_lead, void* stream);
 
 /* ---- Generation: KV-cache decode -------------------------------------------------------------------------
  * InnerSelfAttention.forward with layer_past / use_cache (transformer.py:261-268 + _attn :171-217), driven by
