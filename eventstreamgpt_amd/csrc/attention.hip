@@ -469,7 +469,93 @@ __device__ __forceinline__ float small_keep(const DropoutSpec& dr, int64_t bh, i
   return dropout_mult(dr, elem_index(bh, Lq, Lk, qi, kj));
 }
 
-template <typename T, int VE, int LKM, bool I32>
+// Operands of one (sequence, head) item kept as raw packed words (bf16 pairs: half the registers of f32 copies),
+// widened at each use: the wave's register footprint sets how many waves — and row loads — a CU keeps in flight,
+// which is what bounds these kernels (a few hundred bytes of rows per wave, ~30 % of HBM at 4-5 waves per SIMD).
+// The forward takes NI items per wave with every item's loads issued before the first computes.
+template <typename T, int VE>
+struct Raw {
+  static constexpr int W = (VE * (int)sizeof(T) + 3) / 4;
+  uint32_t w[W];
+};
+
+template <typename T, int VE>
+__device__ __forceinline__ void raw_load(const T* p, Raw<T, VE>& r) {
+  if constexpr (sizeof(T) == 4) {
+    if constexpr (VE == 4) {
+      const uint4 t = *reinterpret_cast<const uint4*>(p);
+      r.w[0] = t.x, r.w[1] = t.y, r.w[2] = t.z, r.w[3] = t.w;
+    } else if constexpr (VE == 2) {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      r.w[0] = t.x, r.w[1] = t.y;
+    } else {
+      r.w[0] = *reinterpret_cast<const uint32_t*>(p);
+    }
+  } else {
+    if constexpr (VE == 4) {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      r.w[0] = t.x, r.w[1] = t.y;
+    } else if constexpr (VE == 2) {
+      r.w[0] = *reinterpret_cast<const uint32_t*>(p);
+    } else {
+      r.w[0] = (uint32_t)(*reinterpret_cast<const uint16_t*>(p)) << 16;
+    }
+  }
+}
+
+template <typename T, int VE>
+__device__ __forceinline__ float raw_at(const Raw<T, VE>& r, int e) {
+  if constexpr (sizeof(T) == 4) return __uint_as_float(r.w[e]);
+  else if constexpr (VE == 1) return __uint_as_float(r.w[0]);
+  else return (e & 1) ? __uint_as_float(r.w[e >> 1] & 0xffff0000u) : __uint_as_float(r.w[e >> 1] << 16);
+}
+
+template <typename T, int VE, int LKM>
+struct S4Item {
+  Raw<T, VE> k[LKM], v[LKM];
+  Raw<T, VE> q, dout, o;  // the item's first query block (query i = g); bwd: + dO, O rows
+  float ls;
+  uint32_t km;  // bit j: key j not padded
+  bool qm;      // query g not padded
+};
+
+template <typename T, int VE, int LKM, bool BWD>
+__device__ __forceinline__ void s4_load(const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v,
+                                        int64_t ld_in, int64_t tq, const T* __restrict__ o, int64_t ld_o,
+                                        const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
+                                        const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
+                                        int64_t bh, int64_t H, int64_t Lq, int64_t Lk, int hd, int g, int c,
+                                        S4Item<T, VE, LKM>& r) {
+  const int64_t h = bh % H, b = bh / H;
+  r.km = 0;
+#pragma unroll
+  for (int j = 0; j < LKM; ++j) {
+    if (j >= Lk) break;  // wave-uniform: only the sequence's keys are loaded
+    if (!kmask || kmask[b * Lk + j] != 0) r.km |= 1u << j;
+    raw_load<T, VE>(k + (b * Lk + j) * ld_in + h * hd + c, r.k[j]);
+    raw_load<T, VE>(v + (b * Lk + j) * ld_in + h * hd + c, r.v[j]);
+  }
+  r.qm = false;
+  if (Lq > 0) {
+    const int64_t ii = min<int64_t>(g, Lq - 1);
+    r.qm = !qmask || qmask[b * Lq + ii] != 0;
+    raw_load<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, r.q);
+    if constexpr (BWD) {
+      raw_load<T, VE>(dout + (b * Lq + ii) * ld_do + h * hd + c, r.dout);
+      raw_load<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, r.o);
+      r.ls = lse[bh * Lq + ii];
+    }
+  }
+}
+
+// item t of the wave: the NI items of a workgroup's wave w are bh = (blockIdx·NI + t)·4 + w (consecutive heads of
+// one sequence per t: every row the workgroup reads is read whole)
+template <int NI>
+__device__ __forceinline__ int64_t s4_item(int t) {
+  return ((int64_t)blockIdx.x * NI + t) * 4 + (threadIdx.x >> 6);
+}
+
+template <typename T, int VE, int LKM, bool I32, int NI, bool ONE>
 __global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, const T* __restrict__ k,
                                                        const T* __restrict__ v, int64_t ld_in, int64_t tq,
                                                        T* __restrict__ o, int64_t ld_o, float* __restrict__ lse,
@@ -477,157 +563,197 @@ __global__ __launch_bounds__(256) void attn_fwd_small4(const T* __restrict__ q, 
                                                        const uint8_t* __restrict__ qmask, int64_t B, int64_t H,
                                                        int64_t Lq, int64_t Lk, int hd, int64_t window, float drop_p,
                                                        const uint64_t* __restrict__ seed) {
-  const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (bh >= B * H) return;  // wave-uniform
+  const int64_t W = B * H;
+  if (s4_item<NI>(0) >= W) return;  // wave-uniform
   const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
-  const int64_t h = bh % H, b = bh / H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
-  float kr[LKM][VE], vr[LKM][VE];
-  bool kv[LKM];
+  S4Item<T, VE, LKM> it[NI];
 #pragma unroll
-  for (int j = 0; j < LKM; ++j) {
-    kv[j] = j < Lk && (!kmask || kmask[b * Lk + j] != 0);
-    if (j >= Lk) break;  // wave-uniform: only the sequence's keys are loaded and walked
-    load_vec<T, VE>(k + (b * Lk + j) * ld_in + h * hd + c, kr[j]);
-    load_vec<T, VE>(v + (b * Lk + j) * ld_in + h * hd + c, vr[j]);
-  }
-  for (int64_t i0 = 0; i0 < Lq; i0 += 4) {
-    const int64_t i = i0 + g;
-    const bool qin = i < Lq;
-    const int64_t ii = qin ? i : Lq - 1;
-    const int64_t pos = ii + (Lk - Lq);
-    const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
-    const bool qvalid = qin && (qmask ? (qmask[b * Lq + ii] != 0) : true);
-    float qr[VE];
-    load_vec<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, qr);
-    float s[LKM];
-    float m = -INFINITY;
+  for (int t = 0; t < NI; ++t)
+    if (s4_item<NI>(t) < W)
+      s4_load<T, VE, LKM, false>(q, k, v, ld_in, tq, nullptr, 0, nullptr, 0, nullptr, kmask, qmask, s4_item<NI>(t), H,
+                                 Lq, Lk, hd, g, c, it[t]);
 #pragma unroll
-    for (int j = 0; j < LKM; ++j) {
-      s[j] = -INFINITY;
-      if (j >= Lk) break;
-      float t = 0.f;
+  for (int t = 0; t < NI; ++t) {
+    const int64_t bh = s4_item<NI>(t);
+    if (bh >= W) break;  // wave-uniform
+    const S4Item<T, VE, LKM>& cur = it[t];
+    const int64_t h = bh % H, b = bh / H;
+    // ONE (Lq <= 4): a single query block, no loop — the packed operands are widened where they are used instead
+    // of being hoisted out of a loop as f32 copies
+    for (int64_t i0 = 0; i0 < (ONE ? 1 : Lq); i0 += 4) {
+      const int64_t i = i0 + g;
+      const bool qin = i < Lq;
+      const int64_t ii = qin ? i : Lq - 1;
+      const int64_t pos = ii + (Lk - Lq);
+      const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+      float qr[VE];
+      bool qvalid;
+      if (i0 == 0) {
 #pragma unroll
-      for (int e = 0; e < VE; ++e) t = fmaf(qr[e], kr[j][e], t);
-      t = row_sum16(t);  // every lane of the wave takes part (DPP)
-      const bool ok = qvalid && kv[j] && j >= jlo && j <= pos;
-      s[j] = ok ? t : -INFINITY;
-      m = fmaxf(m, s[j]);
-    }
-    float l = 0.f, acc[VE];
+        for (int e = 0; e < VE; ++e) qr[e] = raw_at<T, VE>(cur.q, e);
+        qvalid = qin && cur.qm;
+      } else {
+        qvalid = qin && (qmask ? (qmask[b * Lq + ii] != 0) : true);
+        load_vec<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, qr);
+      }
+      float s[LKM];
+      float m = -INFINITY;
 #pragma unroll
-    for (int e = 0; e < VE; ++e) acc[e] = 0.f;
+      for (int j = 0; j < LKM; ++j) {
+        s[j] = -INFINITY;
+        if (j >= Lk) break;
+        float tt = 0.f;
 #pragma unroll
-    for (int j = 0; j < LKM; ++j) {
-      if (j >= Lk) break;
-      if (s[j] == -INFINITY) continue;
-      const float p = expf(s[j] - m);
-      l += p;  // normaliser over undropped probabilities
-      const float pd = dr.p > 0.f ? p * small_keep<I32>(dr, bh, Lq, Lk, ii, j) : p;
+        for (int e = 0; e < VE; ++e) tt = fmaf(qr[e], raw_at<T, VE>(cur.k[j], e), tt);
+        tt = row_sum16(tt);  // every lane of the wave takes part (DPP)
+        const bool ok = qvalid && ((cur.km >> j) & 1u) && j >= jlo && j <= pos;
+        s[j] = ok ? tt : -INFINITY;
+        m = fmaxf(m, s[j]);
+      }
+      float l = 0.f, acc[VE];
 #pragma unroll
-      for (int e = 0; e < VE; ++e) acc[e] = fmaf(pd, vr[j][e], acc[e]);
-    }
-    const bool ok = qvalid && l > 0.f;
-    const float inv = ok ? 1.f / l : 0.f;
+      for (int e = 0; e < VE; ++e) acc[e] = 0.f;
 #pragma unroll
-    for (int e = 0; e < VE; ++e) acc[e] *= inv;
-    if (qin) {
-      store_vec<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, acc);
-      if ((lane & 15) == 0) lse[bh * Lq + ii] = ok ? m + logf(l) : 0.f;
+      for (int j = 0; j < LKM; ++j) {
+        if (j >= Lk) break;
+        if (s[j] == -INFINITY) continue;
+        const float p = expf(s[j] - m);
+        l += p;  // normaliser over undropped probabilities
+        const float pd = dr.p > 0.f ? p * small_keep<I32>(dr, bh, Lq, Lk, ii, j) : p;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) acc[e] = fmaf(pd, raw_at<T, VE>(cur.v[j], e), acc[e]);
+      }
+      const bool ok = qvalid && l > 0.f;
+      const float inv = ok ? 1.f / l : 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) acc[e] *= inv;
+      if (qin) {
+        store_vec<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, acc);
+        if ((lane & 15) == 0) lse[bh * Lq + ii] = ok ? m + logf(l) : 0.f;
+      }
     }
   }
 }
 
-template <typename T, int VE, int LKM, bool I32>
+template <typename T, int VE, int LKM, bool I32, int NI, bool ONE>
 __global__ __launch_bounds__(256) void attn_bwd_small4(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, int64_t ld_in, int64_t tq,
     const T* __restrict__ o, int64_t ld_o, const T* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask, T* __restrict__ dq, T* __restrict__ dk,
     T* __restrict__ dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int hd, int64_t window,
     float drop_p, const uint64_t* __restrict__ seed, int64_t dq_lead) {
-  const int64_t bh = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (bh >= B * H) return;  // wave-uniform
+  const int64_t W = B * H;
+  if (s4_item<NI>(0) >= W) return;  // wave-uniform
   const int lane = lane_id(), g = lane >> 4, c = (lane & 15) * VE;
-  const int64_t h = bh % H, b = bh / H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
-  float kr[LKM][VE], vr[LKM][VE], dka[LKM][VE], dva[LKM][VE];
-  bool kv[LKM];
+  S4Item<T, VE, LKM> it[NI];
 #pragma unroll
-  for (int j = 0; j < LKM; ++j) {
-    kv[j] = j < Lk && (!kmask || kmask[b * Lk + j] != 0);
+  for (int t = 0; t < NI; ++t)
+    if (s4_item<NI>(t) < W)
+      s4_load<T, VE, LKM, true>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, s4_item<NI>(t), H, Lq, Lk,
+                                hd, g, c, it[t]);
 #pragma unroll
-    for (int e = 0; e < VE; ++e) dka[j][e] = dva[j][e] = 0.f;
-    if (j >= Lk) break;  // wave-uniform
-    load_vec<T, VE>(k + (b * Lk + j) * ld_in + h * hd + c, kr[j]);
-    load_vec<T, VE>(v + (b * Lk + j) * ld_in + h * hd + c, vr[j]);
-  }
-  for (int64_t i0 = 0; i0 < Lq; i0 += 4) {
-    const int64_t i = i0 + g;
-    const bool qin = i < Lq;
-    const int64_t ii = qin ? i : Lq - 1;
-    const int64_t pos = ii + (Lk - Lq);
-    const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
-    const bool qvalid = qin && (qmask ? (qmask[b * Lq + ii] != 0) : true);
-    float qr[VE], dor[VE], orr[VE], dqa[VE];
-    load_vec<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, qr);
-    load_vec<T, VE>(dout + (b * Lq + ii) * ld_do + h * hd + c, dor);
-    load_vec<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, orr);
-    const float ls = lse[bh * Lq + ii];
-    float dl = 0.f;
+  for (int t = 0; t < NI; ++t) {
+    const int64_t bh = s4_item<NI>(t);
+    if (bh >= W) break;  // wave-uniform
+    const S4Item<T, VE, LKM>& cur = it[t];
+    const int64_t h = bh % H, b = bh / H;
+    float dka[LKM][VE], dva[LKM][VE];
 #pragma unroll
-    for (int e = 0; e < VE; ++e) {
-      dl = fmaf(dor[e], orr[e], dl);
-      dqa[e] = 0.f;
+    for (int j = 0; j < LKM; ++j)
+#pragma unroll
+      for (int e = 0; e < VE; ++e) dka[j][e] = dva[j][e] = 0.f;
+    // ONE (Lq <= 4): a single query block, no loop — the packed operands are widened where they are used instead
+    // of being hoisted out of a loop as f32 copies
+    for (int64_t i0 = 0; i0 < (ONE ? 1 : Lq); i0 += 4) {
+      const int64_t i = i0 + g;
+      const bool qin = i < Lq;
+      const int64_t ii = qin ? i : Lq - 1;
+      const int64_t pos = ii + (Lk - Lq);
+      const int64_t jlo = (window > 0) ? max((int64_t)0, pos - window + 1) : 0;
+      float qr[VE], dor[VE], orr[VE], dqa[VE], ls;
+      bool qvalid;
+      if (i0 == 0) {
+#pragma unroll
+        for (int e = 0; e < VE; ++e)
+          qr[e] = raw_at<T, VE>(cur.q, e), dor[e] = raw_at<T, VE>(cur.dout, e), orr[e] = raw_at<T, VE>(cur.o, e);
+        ls = cur.ls;
+        qvalid = qin && cur.qm;
+      } else {
+        qvalid = qin && (qmask ? (qmask[b * Lq + ii] != 0) : true);
+        load_vec<T, VE>(q + (b * tq + ii) * ld_in + h * hd + c, qr);
+        load_vec<T, VE>(dout + (b * Lq + ii) * ld_do + h * hd + c, dor);
+        load_vec<T, VE>(o + (b * Lq + ii) * ld_o + h * hd + c, orr);
+        ls = lse[bh * Lq + ii];
+      }
+      float dl = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        dl = fmaf(dor[e], orr[e], dl);
+        dqa[e] = 0.f;
+      }
+      dl = row_sum16(dl);  // delta = rowsum(dO o O)
+      if (!qvalid) dl = 0.f;
+#pragma unroll
+      for (int j = 0; j < LKM; ++j) {
+        if (j >= Lk) break;  // wave-uniform
+        float sv = 0.f, dpv = 0.f;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) {
+          sv = fmaf(qr[e], raw_at<T, VE>(cur.k[j], e), sv);
+          dpv = fmaf(dor[e], raw_at<T, VE>(cur.v[j], e), dpv);
+        }
+        sv = row_sum16(sv);
+        dpv = row_sum16(dpv);
+        if (!(qvalid && ((cur.km >> j) & 1u) && j >= jlo && j <= pos)) continue;  // row-uniform
+        const float keep = dr.p > 0.f ? small_keep<I32>(dr, bh, Lq, Lk, ii, j) : 1.f;
+        const float p = expf(sv - ls);
+        const float ds = p * (dpv * keep - dl);
+        const float pd = p * keep;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) {
+          dqa[e] = fmaf(ds, raw_at<T, VE>(cur.k[j], e), dqa[e]);
+          dka[j][e] = fmaf(ds, qr[e], dka[j][e]);
+          dva[j][e] = fmaf(pd, dor[e], dva[j][e]);
+        }
+      }
+      if (qin) store_vec<T, VE>(dq + (b * tq + ii) * ld_d + h * hd + c, dqa);
     }
-    dl = row_sum16(dl);  // delta = rowsum(dO o O)
-    if (!qvalid) dl = 0.f;
+    // the rows before the first query (static_kv_first: token 0) have no query: their dq is zero
+    if (g < dq_lead) {
+      float z[VE];
+#pragma unroll
+      for (int e = 0; e < VE; ++e) z[e] = 0.f;
+      store_vec<T, VE>(dq + (b * tq - 1 - g) * ld_d + h * hd + c, z);
+    }
+    // dK / dV: the four query groups' partials summed (every group ends with the sums); group g stores the rows
+    // j = g, g + 4
 #pragma unroll
     for (int j = 0; j < LKM; ++j) {
       if (j >= Lk) break;  // wave-uniform
-      float sv = 0.f, dpv = 0.f;
 #pragma unroll
       for (int e = 0; e < VE; ++e) {
-        sv = fmaf(qr[e], kr[j][e], sv);
-        dpv = fmaf(dor[e], vr[j][e], dpv);
+        dka[j][e] = cross_rows(dka[j][e]);
+        dva[j][e] = cross_rows(dva[j][e]);
       }
-      sv = row_sum16(sv);
-      dpv = row_sum16(dpv);
-      if (!(qvalid && kv[j] && j >= jlo && j <= pos)) continue;  // row-uniform
-      const float keep = dr.p > 0.f ? small_keep<I32>(dr, bh, Lq, Lk, ii, j) : 1.f;
-      const float p = expf(sv - ls);
-      const float ds = p * (dpv * keep - dl);
-      const float pd = p * keep;
-#pragma unroll
-      for (int e = 0; e < VE; ++e) {
-        dqa[e] = fmaf(ds, kr[j][e], dqa[e]);
-        dka[j][e] = fmaf(ds, qr[e], dka[j][e]);
-        dva[j][e] = fmaf(pd, dor[e], dva[j][e]);
+      if ((j & 3) == g) {
+        store_vec<T, VE>(dk + (b * Lk + j) * ld_d + h * hd + c, dka[j]);
+        store_vec<T, VE>(dv + (b * Lk + j) * ld_d + h * hd + c, dva[j]);
       }
     }
-    if (qin) store_vec<T, VE>(dq + (b * tq + ii) * ld_d + h * hd + c, dqa);
   }
-  // the rows before the first query (static_kv_first: token 0) have no query: their dq is zero
-  if (g < dq_lead) {
-    float z[VE];
-#pragma unroll
-    for (int e = 0; e < VE; ++e) z[e] = 0.f;
-    store_vec<T, VE>(dq + (b * tq - 1 - g) * ld_d + h * hd + c, z);
+}
+
+// Items per wave of the small4 forward / backward (ESGPT_SMALL4_NI = "fwd,bwd" overrides: 1 or 2 each)
+static void small4_ni(int& f, int& b) {
+  static int nf = -1, nb = -1;
+  if (nf < 0) {
+    nf = 1, nb = 1;
+    const char* e = tuning_env("ESGPT_SMALL4_NI");
+    if (e && e[0] && e[1] == ',' && e[2]) nf = e[0] == '1' ? 1 : 2, nb = e[2] == '1' ? 1 : 2;
   }
-  // dK / dV: the four query groups' partials summed (every group ends with the sums); group g stores the rows
-  // j = g, g + 4
-#pragma unroll
-  for (int j = 0; j < LKM; ++j) {
-    if (j >= Lk) break;  // wave-uniform
-#pragma unroll
-    for (int e = 0; e < VE; ++e) {
-      dka[j][e] = cross_rows(dka[j][e]);
-      dva[j][e] = cross_rows(dva[j][e]);
-    }
-    if (j < Lk && (j & 3) == g) {
-      store_vec<T, VE>(dk + (b * Lk + j) * ld_d + h * hd + c, dka[j]);
-      store_vec<T, VE>(dv + (b * Lk + j) * ld_d + h * hd + c, dva[j]);
-    }
-  }
+  f = nf, b = nb;
 }
 
 // The four-query form applies (aligned VE-element rows).
@@ -650,18 +776,47 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
                  int64_t dq_lead, hipStream_t st) {
   const dim3 grid((unsigned)cdiv(B * H, 4)), block(256);
   if (small4_ok<T>(Lk, hd, {q, k, v, o, dout, dq, dk, dv}, {ld_in, ld_o, ld_do, ld_d})) {
+    int nif, nib;
+    small4_ni(nif, nib);
+    const int ni = fwd ? nif : nib;  // items per wave
+    const bool one = Lq <= 4;        // one query block per item
+    const dim3 grid4((unsigned)cdiv(B * H, 4 * ni));
+#define SMALL4_FWD_NI(VE, LKM, I32, NI, ONE)                                                                       \
+  attn_fwd_small4<T, VE, LKM, I32, NI, ONE><<<grid4, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in,   \
+                                                                     tq, (T*)o, ld_o, lse_w, kmask, qmask, B, H, Lq, \
+                                                                     Lk, (int)hd, window, drop_p, seed)
+#define SMALL4_BWD_NI(VE, LKM, I32, NI, ONE)                                                                       \
+  attn_bwd_small4<T, VE, LKM, I32, NI, ONE><<<grid4, block, 0, st>>>(                                                \
+      (const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o, ld_o, (const T*)dout, ld_do, lse_r, kmask,      \
+      qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed, dq_lead)
+#define SMALL4_FWD(VE, LKM, I32)                                        \
+  do {                                                                  \
+    if (ni == 2) {                                                      \
+      if (one) SMALL4_FWD_NI(VE, LKM, I32, 2, true);                    \
+      else SMALL4_FWD_NI(VE, LKM, I32, 2, false);                       \
+    } else {                                                            \
+      if (one) SMALL4_FWD_NI(VE, LKM, I32, 1, true);                    \
+      else SMALL4_FWD_NI(VE, LKM, I32, 1, false);                       \
+    }                                                                   \
+  } while (0)
+#define SMALL4_BWD(VE, LKM, I32)                                        \
+  do {                                                                  \
+    if (ni == 2) {                                                      \
+      if (one) SMALL4_BWD_NI(VE, LKM, I32, 2, true);                    \
+      else SMALL4_BWD_NI(VE, LKM, I32, 2, false);                       \
+    } else {                                                            \
+      if (one) SMALL4_BWD_NI(VE, LKM, I32, 1, true);                    \
+      else SMALL4_BWD_NI(VE, LKM, I32, 1, false);                       \
+    }                                                                   \
+  } while (0)
 // key registers sized to the sequence (LKM = 4, 6 or 8 keys): the C4 dependency graph (5 keys) holds 3/4 of the
 // 8-key form's K / V / dK / dV registers
 #define SMALL4_L(VE, LKM, I32)                                                                                       \
   do {                                                                                                               \
     if (fwd)                                                                                                         \
-      attn_fwd_small4<T, VE, LKM, I32><<<grid, block, 0, st>>>((const T*)q, (const T*)k, (const T*)v, ld_in, tq,     \
-                                                               (T*)o, ld_o, lse_w, kmask, qmask, B, H, Lq, Lk,      \
-                                                               (int)hd, window, drop_p, seed);                      \
+      SMALL4_FWD(VE, LKM, I32);                                                                                      \
     else                                                                                                             \
-      attn_bwd_small4<T, VE, LKM, I32><<<grid, block, 0, st>>>(                                                      \
-          (const T*)q, (const T*)k, (const T*)v, ld_in, tq, (const T*)o, ld_o, (const T*)dout, ld_do, lse_r, kmask,  \
-          qmask, (T*)dq, (T*)dk, (T*)dv, ld_d, B, H, Lq, Lk, (int)hd, window, drop_p, seed, dq_lead);                \
+      SMALL4_BWD(VE, LKM, I32);                                                                                      \
   } while (0)
   // 32-bit dropout element indices whenever the launch's indices fit (the same keep bits); the 64-bit form only for
   // launches past 2^32 elements
@@ -678,6 +833,10 @@ int launch_small(bool fwd, const void* q, const void* k, const void* v, int64_t 
     else SMALL4(4);
 #undef SMALL4
 #undef SMALL4_L
+#undef SMALL4_FWD
+#undef SMALL4_BWD
+#undef SMALL4_FWD_NI
+#undef SMALL4_BWD_NI
     return hipGetLastError() == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
   }
 #define SMALL(DPL, LKM)                                                                                             \

@@ -87,6 +87,8 @@ def main():
                 break
             rec = {"path": pname, "terms": name, "us": round(us, 2)}
             if name == "all":
+                rec["losses"] = [round(x, 6) for x in losses[: len(sub) + 2].tolist()]
+                rec["dz_sum"] = round(float(dzc.float().sum()), 6)
                 rec["algorithmic_MB"] = round(algo / 1e6, 2)
                 rec["TB_s"] = round(algo / us / 1e6, 3)
             print(json.dumps(rec))
