@@ -110,6 +110,8 @@ SIGNATURES = {
     "esgpt_attn_bwd_lead": (_int, [_vp, _vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _i64, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _vp, _vp, _int, _vp, _sz, _vp, _i64,
                                    _vp]),
+    "esgpt_row_tiles": (_int, [_vp, _i64, _i64, _vp, _vp]),
+    "esgpt_gemm_row_tiles": (_int, [_vp]),
     "esgpt_attn_bwd_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
     "esgpt_residual_fwd": (_int, [_vp, _vp, _int, _vp, _i64, _i64, _f32, _vp, _i64, _i64, _vp, _vp]),
     "esgpt_residual_bwd": (_int, [_vp, _vp, _i64, _i64, _f32, _vp, _i64, _i64, _vp, _vp, _int, _vp]),

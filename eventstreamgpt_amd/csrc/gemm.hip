@@ -68,7 +68,8 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
   const int M = p.M, N = p.N;
   const int m0 = by * BM, n0 = bx * BN;
   const int kb = bz * p.kchunk, ke = min(p.K, kb + p.kchunk);
-  const int nk = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+  // rows of padded events only (row-tile mask): no k loop — the epilogue stores act(0·alpha + bias), or zeros
+  const int nk = (ke > kb && !rows_skipped(p, m0, BM)) ? (ke - kb + BK - 1) / BK : 0;
   const __bf16* __restrict__ A = p.A;
   const __bf16* __restrict__ B = p.B;
   const bool want_rs = kRowSum && p.rowsum != nullptr && bx == 0 && wn == 0;  // wave-uniform
@@ -224,7 +225,7 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
     float* sm = reinterpret_cast<float*>(smem);
     const float* Af = reinterpret_cast<const float*>(A);
     const float* Bf = reinterpret_cast<const float*>(B);
-    const int nkf = ke > kb ? (ke - kb + BKF - 1) / BKF : 0;
+    const int nkf = (ke > kb && !rows_skipped(p, m0, BM)) ? (ke - kb + BKF - 1) / BKF : 0;
     float4 ra[FA::kChunks], rb[FB::kChunks];
     if (nkf > 0) {
       FA::load(ra, Af, p.lda, m0, M, kb, ke);
@@ -794,6 +795,10 @@ Plan plan(int64_t M, int64_t N, int64_t K, int64_t target, TileCfg c) {
   return p;
 }
 
+// Row-tile mask of the next launches on this host thread (esgpt_gemm_row_tiles): applied to products whose M is
+// token rows — the forward projections and the dX half of the grouped backward.
+static thread_local const uint8_t* g_row_tiles = nullptr;
+
 Prob make_prob(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K, void* C,
                int64_t ldc, int out_f32, int accumulate, const float* bias, const float* alpha, int64_t target,
                TileCfg c) {
@@ -968,6 +973,7 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
   if (has_dx) {
     p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, f32 ? 1 : 0, 0, nullptr, alpha, 0,
                    f32 ? TileCfg{1, 1} : dx_tile(T, in, out));
+    p0.row_tiles = g_row_tiles;  // dX rows are token rows (dW's M is the output feature: never masked)
     if (act >= 0) {
       p0.epi = EPI_ACT_GRAD;
       p0.act = act;
@@ -1030,6 +1036,16 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
 
 extern "C" {
 
+int esgpt_gemm_row_tiles(const uint8_t* tiles) {
+  static int use = -1;  // tools build: ESGPT_ROW_TILES_IGNORE=1 drops the mask (A/B of the in-kernel check)
+  if (use < 0) {
+    const char* e = tuning_env("ESGPT_ROW_TILES_IGNORE");
+    use = (e && e[0] == '1') ? 0 : 1;
+  }
+  g_row_tiles = use ? tiles : nullptr;
+  return ESGPT_OK;
+}
+
 size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K) {
   return slab_bytes(plan(M, N, K, kTarget, TileCfg{1, 1}).splits, M, N, TileCfg{1, 1});
 }
@@ -1052,6 +1068,7 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   const bool fwd_form = akc && bkc && !f32 && !accumulate && alpha == nullptr;
   const TileCfg tc = fwd_form ? fwd_tile(M, N, K, false) : TileCfg{1, 1};
   Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget, tc);
+  p.row_tiles = g_row_tiles;
   if (fwd_form && p.splits == 1) {
     if (const char* e = tuning_env("ESGPT_GEMM_DBG")) p.dbg = atoi(e);
     hipStream_t st = as_stream(stream);
@@ -1066,6 +1083,7 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   }
   if (tc.fm != 1 || tc.fn != 1) p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, 0, accumulate, bias, alpha, kTarget,
                                                 TileCfg{1, 1});
+  p.row_tiles = g_row_tiles;
   if (p.splits > 1) {
     p.ext_reduce = f32 && p.splits > in_launch_splits();
     ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N, tc) && (p.ext_reduce || counters));
@@ -1093,6 +1111,7 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
   if (T == 0 || out == 0) return ESGPT_OK;
   const TileCfg tc = fwd_tile(T, out, in, act >= 0);
   Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 0, 0, bias, nullptr, 0, tc);  // never split
+  p.row_tiles = g_row_tiles;
   if (act >= 0) {
     p.epi = EPI_BIAS_ACT;
     p.act = act;
@@ -1153,6 +1172,7 @@ int esgpt_linear_fwd_f32(const float* x, int64_t ldx, const float* w, int64_t T,
   ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
   if (T == 0 || out == 0) return ESGPT_OK;
   Prob p = make_prob(x, ldx, w, in, T, out, in, y, ldy, 1, 0, bias, nullptr, 0, TileCfg{1, 1});  // never split
+  p.row_tiles = g_row_tiles;
   if (act >= 0) {
     p.epi = EPI_BIAS_ACT;
     p.act = act;
@@ -1174,6 +1194,7 @@ int esgpt_gemm_f32(int a_layout, const float* A, int64_t lda, int b_layout, cons
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   if (M == 0 || N == 0) return ESGPT_OK;
   Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, 1, accumulate, bias, alpha, kTarget, TileCfg{1, 1});
+  p.row_tiles = g_row_tiles;
   if (p.splits > 1) {
     p.ext_reduce = p.splits > in_launch_splits();
     ESGPT_REQUIRE(workspace && workspace_bytes >= slab_bytes(p.splits, M, N, TileCfg{1, 1}) &&

@@ -353,7 +353,18 @@ struct Prob {
   int rps;   // xmap 2: dX row blocks per dW split chunk
   int dbg;   // tools build only (ESGPT_GEMM_DBG): bit 0 = skip the bf16 output stores, bit 1 = skip the MFMA k-steps,
              // bit 2 / 3 = grouped backward without its dW / dX workgroups
+  const uint8_t* row_tiles;  // optional, one byte per 64 rows of M (esgpt_gemm_row_tiles): 0 = every row of the block
+                             // is a padded event's — a tile covering only such blocks skips its k loop
 };
+
+// True when the tile's rows [m0, m0 + BM) all lie in 64-row blocks the row-tile mask marks padded.
+__device__ __forceinline__ bool rows_skipped(const Prob& p, int m0, int BM) {
+  if (p.row_tiles == nullptr) return false;
+  const int b0 = m0 >> 6, b1 = min(m0 + BM, p.M) - 1;
+  for (int b = b0; b <= (b1 >> 6); ++b)
+    if (p.row_tiles[b]) return false;
+  return true;
+}
 
 // Split-major order of a projection backward (xmap): workgroup id -> XCD x = id % 8 (the dispatcher's round robin),
 // slot = id / 8. XCD x takes the dW splits s ≡ x (mod 8) — every tile of each — and the dX row blocks of the same

@@ -220,6 +220,18 @@ __global__ __launch_bounds__(kThreads) void na_head_split_bwd_kernel(const TI* _
 
 }  // namespace
 
+// Row-tile mask of a token matrix whose event e owns rows [e·rpe, (e+1)·rpe): byte t = 1 iff some event overlapping
+// rows [64t, 64t + 64) is not padded (esgpt_gemm_row_tiles).
+__global__ __launch_bounds__(256) void row_tiles_kernel(const uint8_t* __restrict__ em, int64_t n_events, int64_t rpe,
+                                                        uint8_t* __restrict__ tiles, int64_t nt) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= nt) return;
+  const int64_t e0 = (64 * t) / rpe, e1 = min(n_events - 1, (64 * t + 63) / rpe);
+  uint8_t any = 0;
+  for (int64_t e = e0; e <= e1; ++e) any |= em[e] != 0;
+  tiles[t] = any;
+}
+
 extern "C" {
 
 int esgpt_residual_fwd(const float* x, const void* y, int y_dtype, const uint8_t* row_mask, int64_t mask_div,
@@ -335,6 +347,17 @@ int esgpt_na_head_split_bwd(const void* dhead, const void* dlast, int in_dtype, 
   else
     na_head_split_bwd_kernel<bf16><<<g, kThreads, 0, as_stream(stream)>>>((const bf16*)dhead, (const bf16*)dlast, BL,
                                                                          G, D, dx);
+  ESGPT_LAUNCH_CHECK();
+  return ESGPT_OK;
+}
+
+int esgpt_row_tiles(const uint8_t* event_mask, int64_t n_events, int64_t rows_per_event, uint8_t* tiles,
+                    void* stream) {
+  ESGPT_REQUIRE(event_mask && tiles && n_events >= 0 && rows_per_event >= 1);
+  const int64_t nt = cdiv(n_events * rows_per_event, 64);
+  if (nt == 0) return ESGPT_OK;
+  row_tiles_kernel<<<dim3((unsigned)cdiv(nt, 256)), dim3(256), 0, as_stream(stream)>>>(event_mask, n_events,
+                                                                                        rows_per_event, tiles, nt);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -735,6 +735,28 @@ std::tuple<Tensor, Tensor> linear_act(const Tensor& x, const Tensor& w, const op
   return {pre, y};
 }
 
+// Row-tile mask (esgpt_gemm_row_tiles) of the GEMM launches issued while it lives; cleared on exit.
+struct RowTilesScope {
+  explicit RowTilesScope(const optional<Tensor>& t, int64_t rows) {
+    const bool on = t.has_value() && t->defined();
+    if (on)
+      TORCH_CHECK(t->scalar_type() == at::kByte && t->is_contiguous() && t->numel() >= (rows + 63) / 64,
+                  "row_tiles: uint8 [ceil(rows / 64)] expected");
+    esgpt_gemm_row_tiles(on ? ptr<const uint8_t>(*t) : nullptr);
+  }
+  ~RowTilesScope() { esgpt_gemm_row_tiles(nullptr); }
+};
+
+// tiles[t] = 1 iff some event overlapping rows [64t, 64t + 64) is not padded (event e owns rows_per_event rows)
+Tensor row_tiles(const Tensor& event_mask, int64_t rows_per_event) {
+  const c10::DeviceGuard guard(event_mask.device());
+  Tensor em = as(event_mask, at::kBool);
+  const int64_t n = em.numel();
+  Tensor t = at::empty({(n * rows_per_event + 63) / 64}, em.options().dtype(at::kByte));
+  check(esgpt_row_tiles(ptr<const uint8_t>(em), n, rows_per_event, ptr<uint8_t>(t), stream_of(em)), "row_tiles");
+  return t;
+}
+
 // (dx bf16 [T, in] | empty, dw f32 [out, in], db f32 [out] | empty) of y = x·wᵀ (one grouped launch)
 // The weight-gradient stream of a device: one pool stream per device for the life of the process (every split
 // backward's dW launch is ordered on it, so they may share one split-K workspace pool and ticket array).
@@ -775,8 +797,10 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
                                               const optional<Tensor>& alpha, int64_t act, const optional<Tensor>& pre,
                                               bool need_dx, bool need_db, const Tensor& tickets,
                                               const optional<Tensor>& db_extra_, const optional<Tensor>& dw_tickets,
-                                              const optional<Tensor>& dw_out, const optional<Tensor>& db_out) {
+                                              const optional<Tensor>& dw_out, const optional<Tensor>& db_out,
+                                              const optional<Tensor>& row_tiles_) {
   const c10::DeviceGuard guard(x.device());
+  const RowTilesScope rts(row_tiles_, dy_.size(0));  // the dX rows (token rows)
   // dw_tickets given: split form — dX on the current stream, dW / db on the device's weight-gradient stream (with
   // their own ticket array, workspace and outputs allocated in that stream's order); weight_grad_join before use
   const bool f32op = x.scalar_type() == at::kFloat;
@@ -864,8 +888,9 @@ std::tuple<Tensor, Tensor, Tensor> linear_bwd(const Tensor& dy_, const Tensor& x
 // y = x·wᵀ (+ bias) with the bf16 weight shadow w; `masters` are the f32 parameters (row blocks of w) that receive
 // the weight gradient in the registered backward — unused here (ProjFn of the drop-in modules).
 Tensor linear(const Tensor& x_, const Tensor& w, const optional<Tensor>& bias, at::TensorList masters,
-              const Tensor& tickets) {
+              const Tensor& tickets, const optional<Tensor>& row_tiles_) {
   const c10::DeviceGuard guard(x_.device());
+  const RowTilesScope rts(row_tiles_, x_.size(0));
   Tensor x = x_.contiguous();
   const int64_t T = x.size(0), din = x.size(1), dout = w.size(0);
   Tensor y = at::empty({T, dout}, x.options());
@@ -878,8 +903,10 @@ Tensor linear(const Tensor& x_, const Tensor& w, const optional<Tensor>& bias, a
 // Returns (y, pre, g); pre and g are kept for the backward.
 std::tuple<Tensor, Tensor, Tensor> mlp(const Tensor& x_, const Tensor& w_fc, const Tensor& w_pj, const Tensor& b_fc,
                                        const optional<Tensor>& b_pj, int64_t act, const Tensor& p_fc,
-                                       const Tensor& p_pj, const Tensor& tickets) {
+                                       const Tensor& p_pj, const Tensor& tickets,
+                                       const optional<Tensor>& row_tiles_) {
   const c10::DeviceGuard guard(x_.device());
+  const RowTilesScope rts(row_tiles_, x_.size(0));
   Tensor x = x_.contiguous();
   auto pg = linear_act(x, w_fc, b_fc, act);
   Tensor g = std::get<1>(pg);
@@ -901,9 +928,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> head_loss(const Tensor& xc, const opt
                                                      at::TensorList tw, at::TensorList tb, const Tensor& err,
                                                      const Tensor& tickets, const optional<Tensor>& zb_in) {
   const c10::DeviceGuard guard(xc.device());
-  Tensor zc = linear(xc, wc, bc, {}, tickets);
+  Tensor zc = linear(xc, wc, bc, {}, tickets, c10::nullopt);
   optional<Tensor> zt;
-  if (wt.has_value() && wt->defined()) zt = linear(*xt, *wt, bt, {}, tickets);
+  if (wt.has_value() && wt->defined()) zt = linear(*xt, *wt, bt, {}, tickets, c10::nullopt);
   optional<Tensor> zb;  // the head bias in the logits' dtype: position 0 reads Linear(zeros) = bias
   if (shift) zb = (zb_in.has_value() && zb_in->defined()) ? *zb_in : bc.to(zc.scalar_type());
   return output_loss(zc, zt, zb, BATCH_PASS, n_levels, shift, terms, tte_i, tte_f, err, ESGPT_LOSS_PATH_AUTO);
@@ -1028,16 +1055,18 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("linear_act(Tensor x, Tensor w, Tensor? bias, int act) -> (Tensor, Tensor)");
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor w, Tensor? alpha, int act, Tensor? pre, bool need_dx, bool need_db, "
         "Tensor tickets, Tensor? db_extra=None, Tensor? dw_tickets=None, Tensor(a!)? dw_out=None, "
-        "Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)");
+        "Tensor(b!)? db_out=None, Tensor? row_tiles=None) -> (Tensor, Tensor, Tensor)");
   m.def("weight_grad_join(Tensor like) -> ()");
   m.def("seed_bank(Tensor(a!) counter, Tensor(b!) bank, Tensor(c!)? err=None) -> ()");
   m.def("residual_ln_bwd_partials(Tensor? dh, Tensor dout, Tensor h, Tensor mean, Tensor rstd, Tensor ln_w, "
         "Tensor? row_mask, float p, Tensor? seed, bool need_dx, bool need_dy, ScalarType y_dtype, "
         "ScalarType out_dtype, int skip_T=0) -> (Tensor, Tensor, Tensor)");
   m.def("colsum_flush(Tensor[] parts, Tensor(a!)[] sums) -> ()");
-  m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets) -> Tensor");
+  m.def("linear(Tensor x, Tensor w, Tensor? bias, Tensor[] masters, Tensor tickets, Tensor? row_tiles=None) "
+        "-> Tensor");
+  m.def("row_tiles(Tensor event_mask, int rows_per_event) -> Tensor");
   m.def("mlp(Tensor x, Tensor w_fc, Tensor w_pj, Tensor b_fc, Tensor? b_pj, int act, Tensor p_fc, Tensor p_pj, "
-        "Tensor tickets) -> (Tensor, Tensor, Tensor)");
+        "Tensor tickets, Tensor? row_tiles=None) -> (Tensor, Tensor, Tensor)");
   m.def("head_loss(Tensor xc, Tensor? xt, " BATCH_SCHEMA ", int[] terms, int[] tte_i, float[] tte_f, int shift, "
         "int n_levels, Tensor wc, Tensor bc, Tensor? wt, Tensor? bt, Tensor[] cw, Tensor[] cb, Tensor[] tw, "
         "Tensor[] tb, Tensor err, Tensor tickets, Tensor? zb) -> (Tensor, Tensor, Tensor, Tensor)");
@@ -1084,6 +1113,7 @@ TORCH_LIBRARY_IMPL(esgpt, CUDA, m) {
   m.impl("residual_ln_bwd_partials", &residual_ln_bwd_partials);
   m.impl("colsum_flush", &colsum_flush);
   m.impl("linear", &linear);
+  m.impl("row_tiles", &row_tiles);
   m.impl("mlp", &mlp);
   m.impl("head_loss", &head_loss);
   m.impl("pack", &pack);

@@ -74,6 +74,10 @@ def compute_dtype() -> torch.dtype:
 
 
 ENABLED = True  # tests flip this to exercise the module-by-module path
+# padded-event row blocks skipped by the dependency-graph projections (esgpt_gemm_row_tiles; exact, tested). Off:
+# measured no gain on the C4 step — the mask launches cost ~20-30 us and the skipped ~8 % of the row blocks do not
+# shorten the latency-bound launches (profiles/r05_row_tiles_ab.log; bench.py --row-tiles turns it on)
+ROW_TILES = False
 
 
 def fused_supported(encoder) -> bool:
@@ -105,12 +109,13 @@ def gemm_supported(n_tokens: int, d_in: int, d_out: int) -> bool:
 GEMM_DTYPES = (torch.bfloat16, torch.float32)  # bf16 MFMA, or exact-f32 MFMA (the reference's precision)
 
 
-def linear_op(x, w_lp, bias, masters):
+def linear_op(x, w_lp, bias, masters, row_tiles=None):
     """``esgpt::linear``: y = x · w_lpᵀ (+ bias) with the bf16 weight shadow ``w_lp``; the backward (one grouped
     launch: dx, f32 dW, db) hands the weight gradient to ``masters`` (the f32 parameters whose row-concatenation
-    ``w_lp`` shadows) without a bf16 round trip."""
+    ``w_lp`` shadows) without a bf16 round trip. ``row_tiles``: the padded-event row-block mask of x's rows
+    (``esgpt::row_tiles``): fully padded 64-row blocks skip the forward and dX products."""
     with _timed("gemm"):
-        return _ops().linear(x, w_lp, bias, list(masters), tickets(x.device))
+        return _ops().linear(x, w_lp, bias, list(masters), tickets(x.device), row_tiles)
 
 
 def linear_fwd(x, w, bias=None):
@@ -169,17 +174,17 @@ class ProjFn:
         return linear_op(x, w_lp, bias, params)
 
 
-def proj(x, w_lp, bias, params):
+def proj(x, w_lp, bias, params, row_tiles=None):
     """Projection through the HIP GEMM (bf16 shadow, or the f32 weights themselves in the reference-precision mode)
     when the shapes allow it, else ``F.linear`` on the (differentiable) compute-dtype weights."""
     if w_lp is not None and w_lp.dtype in GEMM_DTYPES and gemm_supported(x.shape[0], x.shape[1], w_lp.shape[0]):
-        return linear_op(x.to(w_lp.dtype).contiguous(), w_lp, bias, params)
+        return linear_op(x.to(w_lp.dtype).contiguous(), w_lp, bias, params, row_tiles)
     w = params[0] if len(params) == 1 else torch.cat(list(params), 0)
     dt = x.dtype
     return F.linear(x, w.to(dt), None if bias is None else bias.to(dt))
 
 
-def mlp_op(x, w_fc, w_pj, b_fc, act: int, p_fc, p_pj, b_pj=None):
+def mlp_op(x, w_fc, w_pj, b_fc, act: int, p_fc, p_pj, b_pj=None, row_tiles=None):
     """``esgpt::mlp``: InnerMLP (transformer.py:378-391): y = act(x · W_fcᵀ + b_fc) · W_projᵀ (+ b_proj) in two
     GEMM launches (c_fc's bias + activation in its epilogue, the bf16 pre-activation kept; c_proj's bias in its
     epilogue) and two grouped backward launches (c_proj: d(pre) = (dy · W_proj) · act'(pre) in the dX epilogue, +
@@ -187,7 +192,7 @@ def mlp_op(x, w_fc, w_pj, b_fc, act: int, p_fc, p_pj, b_pj=None):
     dropout belongs to the following residual_ln. ``w_fc`` / ``w_pj`` are the bf16 shadows; the f32 parameters
     ``p_fc`` / ``p_pj`` receive the gradients."""
     with _timed("gemm"):
-        y, _pre, _g = _ops().mlp(x, w_fc, w_pj, b_fc, b_pj, int(act), p_fc, p_pj, tickets(x.device))
+        y, _pre, _g = _ops().mlp(x, w_fc, w_pj, b_fc, b_pj, int(act), p_fc, p_pj, tickets(x.device), row_tiles)
     return y
 
 
@@ -197,13 +202,13 @@ class MLPFn:
     apply = staticmethod(mlp_op)
 
 
-def mlp(x, w_fc, w_pj, fc, pj, act: int, with_bias: bool = False):
+def mlp(x, w_fc, w_pj, fc, pj, act: int, with_bias: bool = False, row_tiles=None):
     """InnerMLP (c_proj's bias included only with ``with_bias``): ``mlp_op`` when the bf16 GEMM shapes allow it,
     else proj + bias_act + proj."""
     if (w_fc is not None and w_fc.dtype in GEMM_DTYPES
             and gemm_supported(x.shape[0], x.shape[1], w_fc.shape[0])):
         return mlp_op(x.to(w_fc.dtype).contiguous(), w_fc, w_pj, fc.bias, act, fc.weight, pj.weight,
-                      pj.bias if with_bias else None)
+                      pj.bias if with_bias else None, row_tiles)
     f = proj(x, w_fc, None, (fc.weight,))
     g = bias_act(f, fc.bias, act)
     return proj(g, w_pj, pj.bias if with_bias else None, (pj.weight,))
@@ -380,17 +385,28 @@ def inner_block_fused(blk, hidden: torch.Tensor, key_padding_mask, static_kv_fir
     kpm = None if key_padding_mask is None else key_padding_mask.contiguous()
     qpm = None if (kpm is None or static_kv_first) else kpm
     window = att.window_size if att.attention_type == "local" else 0
+    Tq = T - skf
+    # Rows of masked-out events (the padded events of the dependency graph, which the reference compacts away,
+    # structured_attention.py:162-165): their outputs are zeroed and their gradients are zero, so the projections
+    # skip the 64-row blocks holding nothing else (forward and dX products; esgpt_gemm_row_tiles). Row-wise valid
+    # results are bitwise unchanged.
+    tiles_in = tiles_out = None
+    if (ROW_TILES and out_row_mask is not None and hidden.is_cuda and out_mask_div == Tq
+            and out_row_mask.numel() * Tq == Bs * Tq):
+        em = out_row_mask.reshape(-1)
+        tiles_in, tiles_out = _ops().row_tiles(em, T), _ops().row_tiles(em, Tq)
     with torch.autocast("cuda", enabled=False):
         # h0 (= x2) feeds the block's residual: its gradient comes back into this LayerNorm's backward as dh_in
         # (one kernel), not as a second gradient of x2 that autograd would add
         h0, ln = residual_ln(None, x2, None, ln1.weight, ln1.bias, None, 0.0, eps, dt)
-        qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight)).view(Bs, T, 3 * D)
+        qkv = proj(ln, wqkv, None, (att.q_proj.weight, att.k_proj.weight, att.v_proj.weight),
+                   tiles_in).view(Bs, T, 3 * D)
         o = attention(qkv, kpm, qpm, att.num_heads, window, static_kv_first, p_att)
-        Tq = T - skf
-        y = proj(o.reshape(Bs * Tq, D), wo, att.out_proj.bias, (att.out_proj.weight,))
+        y = proj(o.reshape(Bs * Tq, D), wo, att.out_proj.bias, (att.out_proj.weight,), tiles_out)
         # the residual rows: every row of h0, or (static_kv_first) all but each sequence's first, mapped in-kernel
         h1, ln2 = residual_ln(h0, y, None, blk.layer_norm.weight, blk.layer_norm.bias, None, p_res, eps, dt,
                               skip_T=T if skf else 0)
-        y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name], with_bias=True)
+        y2 = mlp(ln2, wfc, wpj, blk.mlp.c_fc, blk.mlp.c_proj, _ACTS[blk.mlp.act_name], with_bias=True,
+                 row_tiles=tiles_out)
         out = residual(h1, y2, out_row_mask, out_mask_div, 0, p_res)
     return out.view(Bs, Tq, D)

@@ -53,7 +53,7 @@ OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd"
        "bias_act_bwd", "column_sum", "gemm", "gemm_", "linear_act", "linear_bwd", "linear", "mlp", "head_loss",
        "pack", "adamw", "adamw_dev", "weight_grad_join", "residual_ln_bwd_partials", "colsum_flush", "seed_bank", "residual",
        "residual_bwd", "na_split", "na_split_bwd_", "na_assemble", "na_assemble_bwd", "na_head_split",
-       "na_head_split_bwd", "split_proj_prep", "split_proj_post")
+       "na_head_split_bwd", "split_proj_prep", "split_proj_post", "row_tiles")
 
 
 def load():
@@ -85,7 +85,7 @@ def _leaves(*ts) -> bool:
 
 
 def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None, split_ok=False, dw_out=None,
-                db_out=None):
+                db_out=None, row_tiles=None):
     """``esgpt::linear_bwd`` from a registered backward (records the launch shape for bench.py when asked). With
     ``split_ok`` (the weight / bias gradients go straight to leaf parameters) and inside ``weight_grad_overlap``,
     the weight gradient runs on the weight-gradient stream. ``dw_out`` / ``db_out`` (exchange-buffer regions,
@@ -99,7 +99,7 @@ def _linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, db_extra=None, spli
 
     dw_tickets = tickets(x.device, 1) if (split_ok and weight_grad_overlap_active(x.device)) else None
     dx, dw, db = torch.ops.esgpt.linear_bwd(dy, x, w, alpha, act, pre, need_dx, need_db, _tickets(x.device),
-                                            db_extra, dw_tickets, dw_out, db_out if need_db else None)
+                                            db_extra, dw_tickets, dw_out, db_out if need_db else None, row_tiles)
     if dw_out is not None:
         dw = dw_out.view(dy.shape[1], x.shape[1])
     if need_db and db_out is not None:
@@ -123,6 +123,13 @@ def _note(ok: bool, tensors, pad: int = 0):
         from .kernels import note_grad_group
 
         note_grad_group(tensors, pad)
+
+
+def _tail(ctx, n: int) -> tuple:
+    """Nones for the trailing optional arguments the caller passed explicitly: the backward returns one entry per
+    argument of the call as dispatched (trailing arguments left at their defaults are not part of it), which is
+    what ``ctx.needs_input_grad`` lists."""
+    return (None,) * (len(ctx.needs_input_grad) - n)
 
 
 def _batch_d(args, start):
@@ -314,7 +321,7 @@ def _register():
 
     @fake(lib + "linear_bwd")
     def _(dy, x, w, alpha, act, pre, need_dx, need_db, tickets, db_extra=None, dw_tickets=None, dw_out=None,
-          db_out=None):
+          db_out=None, row_tiles=None):
         f32 = torch.float32
         return (x.new_empty(dy.shape[0], x.shape[1], dtype=dy.dtype) if need_dx else x.new_empty(0, dtype=dy.dtype),
                 x.new_empty(0, dtype=f32) if dw_out is not None else x.new_empty(dy.shape[1], x.shape[1], dtype=f32),
@@ -330,11 +337,15 @@ def _register():
         return outs
 
     @fake(lib + "linear")
-    def _(x, w, bias, masters, tickets):
+    def _(x, w, bias, masters, tickets, row_tiles=None):
         return x.new_empty(x.shape[0], w.shape[0])
 
+    @fake(lib + "row_tiles")
+    def _(event_mask, rows_per_event):
+        return event_mask.new_empty((event_mask.numel() * rows_per_event + 63) // 64, dtype=torch.uint8)
+
     @fake(lib + "mlp")
-    def _(x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets):
+    def _(x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets, row_tiles=None):
         T = x.shape[0]
         return x.new_empty(T, w_pj.shape[0]), x.new_empty(T, w_fc.shape[0]), x.new_empty(T, w_fc.shape[0])
 
@@ -522,7 +533,8 @@ def _register():
 
     # linear: d x, d bias, and the f32 weight gradient split over the master parameters (one grouped launch)
     def _li_setup(ctx, inputs, output):
-        x, w, bias, masters, tickets = inputs
+        x, w, bias, masters, tickets, *rest = inputs
+        ctx.row_tiles = rest[0] if rest else None  # padded-event row blocks: the dX product skips them too
         ctx.save_for_backward(x, w)
         ctx.rows = [m.shape[0] for m in masters]
         ctx.has_bias = bias is not None
@@ -537,16 +549,17 @@ def _register():
         dw_out = _dest(ok, ctx.gp[0] if ok else None)
         db_out = _dest(ok and need_db, [ctx.gp[1]] if ok else None)
         dx, dw, db = _linear_bwd(dy, x, w, None, -1, None, ctx.needs_input_grad[0], need_db, split_ok=ctx.split_ok,
-                                 dw_out=dw_out, db_out=db_out)
+                                 dw_out=dw_out, db_out=db_out, row_tiles=ctx.row_tiles)
         return (dx if ctx.needs_input_grad[0] else None, None, db if need_db else None,
-                list(torch.split(dw, ctx.rows, 0)), None)
+                list(torch.split(dw, ctx.rows, 0)), None) + _tail(ctx, 5)
 
     reg(lib + "linear", _li_bwd, setup_context=_li_setup)
 
     # mlp: d x, d b_fc, d b_proj, d W_fc, d W_proj (activation gradient in c_proj's dX epilogue, the bias gradients
     # as row sums inside the dW products)
     def _ml_setup(ctx, inputs, output):
-        x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets = inputs
+        x, w_fc, w_pj, b_fc, b_pj, act, p_fc, p_pj, tickets, *rest = inputs
+        ctx.row_tiles = rest[0] if rest else None
         y, pre, g = output
         ctx.mark_non_differentiable(pre, g)
         ctx.set_materialize_grads(False)
@@ -558,17 +571,19 @@ def _register():
 
     def _ml_bwd(ctx, dy, _dpre, _dg):
         if dy is None:
-            return (None,) * 9
+            return (None,) * 9 + _tail(ctx, 9)
         x, w_fc, w_pj, pre, g = ctx.saved_tensors
         need_dbpj = ctx.has_bpj and ctx.needs_input_grad[4]
         ok = ctx.gp is not None
         gp = ctx.gp if ok else (None,) * 4
         dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj, split_ok=ctx.split_ok,
-                                       dw_out=_dest(ok, [gp[1]]), db_out=_dest(ok and need_dbpj, [gp[3]]))
+                                       dw_out=_dest(ok, [gp[1]]), db_out=_dest(ok and need_dbpj, [gp[3]]),
+                                       row_tiles=ctx.row_tiles)
         need_dx = ctx.needs_input_grad[0]
         dx, dw_fc, db_fc = _linear_bwd(dz, x, w_fc, None, -1, None, need_dx, True, split_ok=ctx.split_ok,
-                                       dw_out=_dest(ok, [gp[0]]), db_out=_dest(ok, [gp[2]]))
-        return (dx if need_dx else None, None, None, db_fc, db_pj if need_dbpj else None, None, dw_fc, dw_pj, None)
+                                       dw_out=_dest(ok, [gp[0]]), db_out=_dest(ok, [gp[2]]), row_tiles=ctx.row_tiles)
+        return (dx if need_dx else None, None, None, db_fc, db_pj if need_dbpj else None, None, dw_fc, dw_pj,
+                None) + _tail(ctx, 9)
 
     reg(lib + "mlp", _ml_bwd, setup_context=_ml_setup)
 

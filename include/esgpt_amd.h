@@ -377,6 +377,17 @@ int esgpt_na_head_split_bwd(const void* dhead, const void* dlast, int in_dtype, 
  * none needed) and one int32 ticket per output tile in `counters` (esgpt_gemm_counters(M, N) entries, zeroed once
  * by the caller; every launch leaves them zeroed; launches sharing a counter array must be stream-ordered). The
  * last workgroup of each tile sums the slabs in a fixed order inside the same launch: results are deterministic. */
+/* Row-tile mask for the token-row GEMMs of the NA dependency-graph module, whose token matrix holds every padded
+ * event's G+1 rows (the reference compacts padded events away first, structured_attention.py:162-165,186-193):
+ *   esgpt_row_tiles: tiles[t] = 1 iff some event overlapping rows [64t, 64t+64) of a matrix with rows_per_event rows
+ *     per event is not padded (event_mask [n_events]); ceil(n_events·rows_per_event / 64) bytes.
+ *   esgpt_gemm_row_tiles: the mask (or NULL) of the next esgpt_linear_fwd / _f32 launches and of the dX half of
+ *     esgpt_linear_bwd_* issued from this host thread. A tile whose rows all fall in 0-blocks skips its k loop: its
+ *     output rows hold act(bias) (forward) or zeros (dX); every other row is bitwise unchanged. Valid when those
+ *     rows' values reach no unmasked output and their incoming gradients are zero (the padded events': masked at
+ *     the module output). The dW half is never masked (padded rows contribute exact zeros). */
+int esgpt_row_tiles(const uint8_t* event_mask, int64_t n_events, int64_t rows_per_event, uint8_t* tiles, void* stream);
+int esgpt_gemm_row_tiles(const uint8_t* tiles);
 #define ESGPT_GEMM_K_CONTIG 0
 #define ESGPT_GEMM_MN_CONTIG 1
 size_t esgpt_gemm_workspace(int64_t M, int64_t N, int64_t K);
