@@ -93,9 +93,19 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * kWaves + wave) * R;
   if (row0 >= N) return;
-  // loads of every row first (rows past N clamped, results dropped)
-  V4 xv[R][KC], yv[R][KC];
+  // loads of every row first (rows past N clamped, results dropped), with the LayerNorm weight / bias chunks (read
+  // before the row reductions, not after them: one memory round trip per row instead of two)
+  V4 xv[R][KC], yv[R][KC], wv[KC], bv[KC], yb[KC];
   bool keep[R];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int64_t c = 4 * lane + 256 * k;
+    wv[k] = bv[k] = yb[k] = zero4();
+    if (c < D) {
+      wv[k] = load4(w + c), bv[k] = load4(b + c);
+      if (bias) yb[k] = load4(bias + c);
+    }
+  }
 #pragma unroll
   for (int rr = 0; rr < R; ++rr) {
     const int64_t row = min(row0 + rr, N - 1), xrow = skip_row(row, skip_T);
@@ -130,7 +140,7 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
           }
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            float u = yv[rr][k].v[j] + (bias ? bias[c + j] : 0.f);
+            float u = yv[rr][k].v[j] + yb[k].v[j];  // (+0 without a bias: exact)
             if (dr.p > 0.f) u *= z[j];
             v[k].v[j] += u;
           }
@@ -158,10 +168,9 @@ __global__ __launch_bounds__(256) void residual_ln_fwd_kernel(const float* __res
       const int64_t c = 4 * lane + 256 * k;
       if (c < D) {
         if (h) store4(h + row * D + c, v[k]);
-        const V4 wv = load4(w + c), bv = load4(b + c);
         V4 o;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o.v[j] = (v[k].v[j] - mean) * rstd * wv.v[j] + bv.v[j];
+        for (int j = 0; j < 4; ++j) o.v[j] = (v[k].v[j] - mean) * rstd * wv[k].v[j] + bv[k].v[j];
         store4(out + row * D + c, o);
       }
     }
