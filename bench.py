@@ -695,6 +695,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--loss-pack", action="store_true", help="measurement hook: the replayed step's loss copy "
+                    "made by its own pack launch instead of riding in the optimizer's prepare launch")
     ap.add_argument("--row-tiles", action="store_true", help="measurement hook: the dependency-graph projections "
                     "skip the padded events' row blocks (esgpt_gemm_row_tiles; off by default, measured no gain)")
     ap.add_argument("--opt-graph", action="store_true", help="replay the optimizer step as its own graph "
@@ -730,6 +732,10 @@ def main():
     opt_cfg = OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=10, max_training_steps=10_000)
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     use_graph = not args.no_graph
+    if args.loss_pack:
+        from eventstreamgpt_amd import train as _train
+
+        _train.LOSS_IN_OPT = False
     if args.row_tiles:
         from eventstreamgpt_amd import fused
 

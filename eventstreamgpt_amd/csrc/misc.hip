@@ -79,7 +79,12 @@ __global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict_
                                                             int n_params, esgpt_lr_schedule sc, double beta1,
                                                             double beta2, float* __restrict__ per_tensor,
                                                             float* __restrict__ lr_out,
-                                                            const int32_t* __restrict__ err) {
+                                                            const int32_t* __restrict__ err,
+                                                            const float* __restrict__ copy_src,
+                                                            float* __restrict__ copy_dst, int n_copy) {
+  // a small hand-off copy riding in this launch (the replayed step's loss, which the next replay overwrites): done
+  // whatever the error state, so the caller always gets its value
+  for (int i = threadIdx.x; i < n_copy; i += blockDim.x) copy_dst[i] = copy_src[i];
   if (err != nullptr && (err[0] | err[1]) != 0) return;
   const int64_t s = counters[n_params];  // LambdaLR: the k-th optimizer step uses lambda(k - 1)
   double f = 1.0;
@@ -225,11 +230,21 @@ int esgpt_adamw(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n
 int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, int n_params,
                         const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor, float* lr_out,
                         const int32_t* err, void* stream) {
+  return esgpt_adamw_prepare_ex(counters, active, n_active, n_params, sched, beta1, beta2, per_tensor, lr_out, err,
+                                nullptr, nullptr, 0, stream);
+}
+
+int esgpt_adamw_prepare_ex(int64_t* counters, const int32_t* active, int n_active, int n_params,
+                           const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
+                           float* lr_out, const int32_t* err, const float* copy_src, float* copy_dst,
+                           int64_t n_copy, void* stream) {
   ESGPT_REQUIRE(counters && sched && per_tensor && lr_out && n_active >= 0 && n_params >= 0);
   ESGPT_REQUIRE(n_active == 0 || active);
+  ESGPT_REQUIRE(n_copy >= 0 && n_copy <= 1024 && (n_copy == 0 || (copy_src && copy_dst)));
   ESGPT_REQUIRE(sched->kind == 0 || (sched->kind == 1 && sched->init_lr > sched->end_lr && sched->total >= sched->warmup));
   esgpt::adamw_prepare_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counters, active, n_active, n_params, *sched,
-                                                                       beta1, beta2, per_tensor, lr_out, err);
+                                                                       beta1, beta2, per_tensor, lr_out, err,
+                                                                       copy_src, copy_dst, (int)n_copy);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -132,12 +132,14 @@ class FusedAdamW:
             self._active = self._plan_cur["active"]
         return self._plan_cur
 
-    def launch(self, plan: dict, lr: float | None = None):
+    def launch(self, plan: dict, lr: float | None = None, copy=None) -> bool:
         """The device step over ``plan``: esgpt_adamw_prepare (counters, lr, per-tensor bias corrections — torch's
         one ``step`` per parameter) + the update, both no-ops while the device error block holds a flag. No host
-        arguments change between steps (``lr=None``: the installed schedule), so the launch replays in a graph."""
+        arguments change between steps (``lr=None``: the installed schedule), so the launch replays in a graph.
+        ``copy`` = (src, dst): a small f32 copy done by the prepare launch (the replayed step's loss hand-off).
+        Returns whether the launch (and so the copy) happened."""
         if not plan["active"]:
-            return
+            return False
         kind, warm, total, power, init_lr, end_lr = self.schedule
         if lr is not None:
             kind, init_lr = 0, float(lr)
@@ -145,7 +147,8 @@ class FusedAdamW:
         self.ops.adamw_dev(plan["table"], plan["blocks"], self._counters, plan["active_dev"], len(self.params),
                            int(kind), int(warm), int(total), float(power), float(init_lr), float(end_lr), float(b1),
                            float(b2), float(self.eps), float(self.weight_decay), plan["per"], self._lr_dev,
-                           err_word(self.params[0].device))
+                           err_word(self.params[0].device), *(copy if copy is not None else (None, None)))
+        return True
 
     def note_step(self, active):
         """Host mirror of the device counters: one step for each active parameter."""
@@ -153,13 +156,16 @@ class FusedAdamW:
             self.steps[i] += 1
 
     @torch.no_grad()
-    def step(self, lr: float | None = None):
+    def step(self, lr: float | None = None, copy=None) -> bool:
+        """One optimizer step; returns whether ``copy`` (see ``launch``) was done by it."""
         plan = self._plan()
+        done = False
         if self.host_args:
             self._step_host_args(plan, lr)
         else:
-            self.launch(plan, lr)
+            done = self.launch(plan, lr, copy)
         self.note_step(plan["active"])
+        return done
 
     host_args = False  # measurement hook (bench.py --opt-host-args): round 3's launch with host lr / bias corrections
 
@@ -416,6 +422,10 @@ class GradBuckets:
             ew = err_word(self.flat.device)[0:1]
             ew.bitwise_or_(self.slot.gt(0).to(torch.int64) * FLAG_PEER_RANK)
         self.reset()
+
+
+# the replayed step's loss copy rides in the optimizer's prepare launch (False, measurement hook: the pack kernel)
+LOSS_IN_OPT = True
 
 
 def _copy_scalar(t: torch.Tensor) -> torch.Tensor:
@@ -806,9 +816,13 @@ class TrainStep:
                 if exchange:  # exchanged while the next segment replays
                     for b in released:
                         gb._launch(b)
-            # the next replay overwrites the static loss: hand back a copy, made by the library's pack kernel rather
-            # than clone()'s D2D blit (~5 us of device time for 4 bytes) or a framework elementwise kernel
-            loss = _copy_scalar(sloss)
+            # the next replay overwrites the static loss: hand back a copy — made by the optimizer's prepare launch
+            # when this step runs one (no launch of its own, no host-launch gap), else by the library's pack kernel
+            # (not clone()'s D2D blit: ~5 us of device time for 4 bytes)
+            loss = None
+        if loss is None and not (LOSS_IN_OPT and last and opt_graph is None and self.sched is None
+                                 and not self.opt.host_args):
+            loss = _copy_scalar(sloss)  # no device optimizer launch to carry the copy
         if accumulating and not exchange:
             self._accumulate()  # into the window's buffer (GradBuckets' under DDP)
         if not last:
@@ -834,7 +848,13 @@ class TrainStep:
             active = list(plan["active"])
         elif self.sched is None:
             # the installed schedule, on the device (or, measurement hook, round 3's host-computed lr)
-            self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None)
+            pending = loss is None
+            if pending:
+                loss = torch.empty_like(sloss)
+            done = self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None,
+                                 copy=(sloss.reshape(-1), loss.reshape(-1)) if pending else None)
+            if pending and not done:  # no active parameter: no launch carried the copy
+                loss.copy_(sloss)
             active = list(self.opt._active)
         else:
             self.opt.step()

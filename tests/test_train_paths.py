@@ -192,6 +192,38 @@ def test_nested_attention_graph_replay_matches_eager_with_allocations_between_re
         assert (sg[k] - se[k]).abs().max().item() < 1e-4, k
 
 
+@pytest.mark.gpu
+def test_replayed_losses_held_across_steps():
+    """The replayed step hands back a copy of its static loss made inside the optimizer's prepare launch
+    (train.LOSS_IN_OPT): losses held unread across later replays keep their own step's value, equal bitwise to the
+    pack-kernel copy's and to what each step returned when read at once."""
+    from eventstreamgpt_amd import train as train_mod
+    from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
+
+    bc = CONFIGS["C2"]
+    batches = [bc.batch(i, batch_size=8, device="cuda").packed() for i in range(6)]
+
+    def run(in_opt, read_now):
+        cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
+        torch.manual_seed(0)
+        m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
+        ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=100),
+                       torch.bfloat16, use_graph=True)
+        saved = train_mod.LOSS_IN_OPT
+        train_mod.LOSS_IN_OPT = in_opt
+        try:
+            held = [ts.step(b) for b in batches] if not read_now else [float(ts.step(b)) for b in batches]
+        finally:
+            train_mod.LOSS_IN_OPT = saved
+        ts.check()
+        assert ts.use_graph
+        return [float(x) for x in held]
+
+    a = run(True, False)
+    assert a == run(False, False) == run(True, True)
+    assert len(set(a)) == len(a), a  # every step's own value, not the last replay's
+
+
 def _na_graph_vs_eager(batches, fused_enabled=True):
     from eventstreamgpt_amd import fused
     from eventstreamgpt_amd.transformer.nested_attention_model import NAPPTForGenerativeSequenceModeling
