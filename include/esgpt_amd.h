@@ -508,13 +508,16 @@ typedef struct esgpt_lr_schedule {
 int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, int n_params,
                         const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor, float* lr_out,
                         const int32_t* err, void* stream);
-/* The same, also copying n_copy (<= 1024) floats copy_src -> copy_dst in that launch, whatever the error state: a
- * replayed step's small outputs (its loss, which the next replay overwrites) handed to the caller without a launch of
- * their own. */
+/* The same, also writing the step's hand-off entry, whatever the error state: with ring (16-B aligned, ring_len
+ * entries of round_up(n_copy, 4) + 4 floats) entry ring_ctr % ring_len (entry 0 without a counter) receives n_copy
+ * (<= 1024) floats of copy_src (a replayed step's loss, which the next replay overwrites) followed, at float offset
+ * round_up(n_copy, 4), by the error block's four 32-bit words; *ring_ctr then advances by one. The caller reads its
+ * step's loss and error words from the ring without a copy launch of their own (the error words by a D2H copy off
+ * the compute stream). */
 int esgpt_adamw_prepare_ex(int64_t* counters, const int32_t* active, int n_active, int n_params,
                            const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
-                           float* lr_out, const int32_t* err, const float* copy_src, float* copy_dst,
-                           int64_t n_copy, void* stream);
+                           float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy, float* ring,
+                           int64_t* ring_ctr, int64_t ring_len, void* stream);
 int esgpt_adamw_dev(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, const float* lr_dev,
                     float beta1, float beta2, float eps, float weight_decay, const float* per_tensor,
                     const int32_t* err, void* stream);

@@ -194,34 +194,43 @@ def test_nested_attention_graph_replay_matches_eager_with_allocations_between_re
 
 @pytest.mark.gpu
 def test_replayed_losses_held_across_steps():
-    """The replayed step hands back a copy of its static loss made inside the optimizer's prepare launch
-    (train.LOSS_IN_OPT): losses held unread across later replays keep their own step's value, equal bitwise to the
-    pack-kernel copy's and to what each step returned when read at once."""
+    """The replayed step hands back its loss through the optimizer launch's hand-off ring (with the optimizer
+    launched after the replay, and captured at the end of the step's graph, TrainStep.fuse_optimizer): losses held
+    unread across later replays — more of them than the ring has entries — keep their own step's value, equal bitwise
+    to the pack-launch copy's and to what each step returned when read at once; the parameters after the steps are
+    bitwise equal too."""
     from eventstreamgpt_amd import train as train_mod
     from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
 
     bc = CONFIGS["C2"]
     batches = [bc.batch(i, batch_size=8, device="cuda").packed() for i in range(6)]
 
-    def run(in_opt, read_now):
+    def run(fuse, read_now, ring_len=4):
         cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
         torch.manual_seed(0)
         m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
         ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=100),
-                       torch.bfloat16, use_graph=True)
+                       torch.bfloat16, use_graph=True, fuse_optimizer=fuse is True)
+        ts.ring_len = ring_len
         saved = train_mod.LOSS_IN_OPT
-        train_mod.LOSS_IN_OPT = in_opt
+        train_mod.LOSS_IN_OPT = bool(fuse)  # "ring": host-launched optimizer, loss through its ring entry
         try:
             held = [ts.step(b) for b in batches] if not read_now else [float(ts.step(b)) for b in batches]
         finally:
             train_mod.LOSS_IN_OPT = saved
         ts.check()
         assert ts.use_graph
-        return [float(x) for x in held]
+        assert all(e[4] == ("fused" if fuse is True else None) for e in ts.graphs.values() if e is not None)
+        return [float(x) for x in held], [p.detach().clone() for p in m.parameters()]
 
-    a = run(True, False)
-    assert a == run(False, False) == run(True, True)
-    assert len(set(a)) == len(a), a  # every step's own value, not the last replay's
+    a, pa = run(True, False)
+    b, pb = run(False, False)
+    c, _ = run(True, True, ring_len=64)
+    d, pd = run("ring", False)
+    assert a == b == c == d
+    assert all(torch.equal(x, y) for x, y in zip(pa, pd))
+    assert len(set(a)) == len(a), a  # every step's own value, not a later replay's
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
 
 
 def _na_graph_vs_eager(batches, fused_enabled=True):
@@ -491,28 +500,32 @@ def test_device_lr_schedule_matches_host_schedule():
 
 @pytest.mark.gpu
 def test_captured_optimizer_step_matches_host_launched():
-    """capture_optimizer=True (the optimizer step replayed as its own graph, lr / bias corrections from the device
-    counters) gives bit-identical parameters and step counts to the host-launched device step."""
+    """The optimizer step captured at the end of the step's graph (the default, fuse_optimizer) and replayed as its
+    own graph (capture_optimizer=True) — lr / bias corrections from the device counters in both — give bit-identical
+    parameters and step counts to the host-launched device step."""
     bc = CONFIGS["C1"]
     batches = [bc.batch(i, batch_size=8, device="cuda").packed() for i in range(4)]
     out = {}
-    for cap in (False, True):
+    for mode in ("host", "own-graph", "fused"):
         from eventstreamgpt_amd.transformer.conditionally_independent_model import CIPPTForGenerativeSequenceModeling
 
         cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
         torch.manual_seed(0)
         m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
         ts = TrainStep(m, OptimizationConfig(init_lr=1e-3, lr_num_warmup_steps=2, max_training_steps=10),
-                       torch.bfloat16, use_graph=True, capture_optimizer=cap)
+                       torch.bfloat16, use_graph=True, capture_optimizer=mode == "own-graph",
+                       fuse_optimizer=mode == "fused")
         for b in batches:
             ts.step(b)
         ts.check()
-        assert all((e[4] is not None) == cap for e in ts.graphs.values() if e is not None)
-        out[cap] = ({k: v.detach().clone() for k, v in m.state_dict().items()}, list(ts.opt.steps),
-                    ts.opt._counters.tolist())
-    for k in out[False][0]:
-        assert torch.equal(out[False][0][k], out[True][0][k]), k
-    assert out[False][1] == out[True][1] and out[False][2] == out[True][2]
+        kinds = {type(e[4]).__name__ if not isinstance(e[4], str) else e[4] for e in ts.graphs.values() if e is not None}
+        assert kinds == {"host": {"NoneType"}, "own-graph": {"CUDAGraph"}, "fused": {"fused"}}[mode], kinds
+        out[mode] = ({k: v.detach().clone() for k, v in m.state_dict().items()}, list(ts.opt.steps),
+                     ts.opt._counters.tolist())
+    for mode in ("own-graph", "fused"):
+        for k in out["host"][0]:
+            assert torch.equal(out["host"][0][k], out[mode][0][k]), (mode, k)
+        assert out["host"][1] == out[mode][1] and out["host"][2] == out[mode][2]
 
 
 def test_gradient_accumulation_single_process_cpu():
