@@ -748,14 +748,19 @@ constexpr int kDwTiles[] = {11, 22};
 // Forward tiles: 128x64 for the plain-store products with K <= 256 and at least 512 output columns (tools/fwd_sweep.sh,
 // C2 shapes: qkv 11.2 -> 10.2 us, head 20.3 -> 19.2 us), 64x64 otherwise (out_proj and c_fc with its activation
 // epilogue are 5-13 % slower at 128x64, c_proj at K = 1024 equal).
+// Wide products (K and N >= 512, e.g. C3's d = 512 / 2048 layers) on 128x128 tiles: four times the MFMAs per
+// operand tile load where the 64x64 tile's per-tile overhead dominates (C3 step, tools/tile_sweep_cfg.sh C3: every
+// forward on 128x128 12.69 -> 12.50 ms, every dX 12.69 -> 11.76 ms; at d = 256 (C2, C4) 64x64 stays best).
 TileCfg fwd_tile(int64_t M, int64_t N, int64_t K, bool act) {
   static const TileCfg forced = env_tile("ESGPT_GEMM_TILE_FWD", TileCfg{0, 0}, kFwdTiles, 4);
   if (forced.fm) return forced;
-  return (!act && K <= 256 && N >= 512 && M >= 128) ? TileCfg{2, 1} : TileCfg{1, 1};
+  if (!act && K <= 256 && N >= 512 && M >= 128) return TileCfg{2, 1};
+  return (K >= 512 && N >= 512 && M >= 4096) ? TileCfg{2, 2} : TileCfg{1, 1};
 }
-TileCfg dx_tile(int64_t /*T*/, int64_t /*in*/, int64_t /*out*/) {
-  static const TileCfg t = env_tile("ESGPT_GEMM_TILE_DX", TileCfg{1, 1}, kDxTiles, 3);
-  return t;
+TileCfg dx_tile(int64_t T, int64_t in, int64_t out) {
+  static const TileCfg forced = env_tile("ESGPT_GEMM_TILE_DX", TileCfg{0, 0}, kDxTiles, 3);
+  if (forced.fm) return forced;
+  return (in >= 512 && out >= 512 && T >= 4096) ? TileCfg{2, 2} : TileCfg{1, 1};
 }
 // dW [out, in] over K = T tokens: 128x128 tiles once the 64x64 plan (at its minimum split count, one split per
 // kMaxChunk of tokens) would put more than three workgroups per CU on the chip — their f32 slab traffic then costs
