@@ -533,11 +533,13 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
   const int nkb = (int)cdiv(Lk, KB);
   float* acc = nkb > 1 ? dq32 : nullptr;
   // Two workgroups per key block (the zig-zag query-tile split, partial dKᵀ / dVᵀ exchanged through write-through
-  // slabs: 2 x 128 KB per pair at hd = 64) only where the parallelism pays for that exchange: fewer key-block
-  // workgroups than CUs, or a causal chain of more than 16 query tiles for the first key block. Measured
+  // slabs: 2 x 128 KB per pair at hd = 64) only where the parallelism pays for that exchange: no more key-block
+  // workgroups than CUs, or a causal chain of at least 16 query tiles for the first key block. Measured
   // (tools/attn_bench.py, dropout 0.1): C2 (128 key blocks) 29.5 vs 30.2 us split / not; C3 L=512 H=8 global
-  // (512 blocks) 161 vs 130 us, local-32 121 vs 81 us; C5 L=1024 (256 blocks) 134 vs 123 us; L=4096 B=4 H=8
-  // (512 blocks, 64-tile chains) 574 vs 819 us. (ESGPT_ATTN_BWD_NSPLIT=1 / 2: forced — tuning hook, read once.)
+  // (512 blocks) 161 vs 130 us, local-32 121 vs 81 us; L=4096 B=4 H=8 (512 blocks, 64-tile chains) 574 vs 819 us.
+  // C5 (L = 1024, 256 blocks: one per CU) measured 134 vs 123 us in isolation before the longest-chain-first order;
+  // with it, the C5 step is 3.4 % faster split (4.065 -> 3.926 ms, profiles/r05b_c5_sweep.log), hence "no more
+  // than". (ESGPT_ATTN_BWD_NSPLIT=1 / 2: forced — tuning hook, read once.)
   static const int forced_split = [] {
     const char* e = tuning_env("ESGPT_ATTN_BWD_NSPLIT");
     return e ? atoi(e) : 0;
@@ -550,7 +552,7 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
     return n;
   }();
   const int64_t chain = window > 0 ? std::min<int64_t>(Lq, KB + window) : Lq;  // queries seen by one key block
-  const bool want_split = forced_split ? forced_split == 2 : (nkb * B * H < n_cu || chain > 1024);
+  const bool want_split = forced_split ? forced_split == 2 : (nkb * B * H <= n_cu || chain >= 1024);
   const int nsplit = (counters && Lq > Cfg<HD>::QT && want_split) ? 2 : 1;
   const int64_t slab = B * H * Lq * HD;  // one f32 dQ partial per key block (nkb > 1)
   static const int order = [] {  // workgroup order: ESGPT_ATTN_ORDER tuning hook, read once
