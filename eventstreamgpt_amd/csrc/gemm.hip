@@ -583,14 +583,17 @@ int fwd_buffers() {
 
 // LDS-DMA staging buffers of the whole-tile k loops (0 = register staging; ESGPT_GEMM_FWD_GLDS /
 // ESGPT_GEMM_BWD_GLDS tuning hooks, read once). Measured at the C2 shapes (tools/glds_check.sh,
-// tools/glds_bwd_sweep.sh, profiles/r04_glds_*.log): the forward projections gain 3-12 % from two LDS-DMA buffers
-// (qkv 10.3 -> 9.1-9.4 us, head 20.0 -> 17.7-19.0 us; three buffers lose); the grouped backward loses 4-6 % with
-// either depth (627 -> 659 / 671 us per step's set) and at every dX / dW tile size, so it keeps register staging.
+// tools/glds_bwd_sweep.sh, profiles/r04_glds_*.log): in isolation the forward projections gain 3-12 % from two
+// LDS-DMA buffers (qkv 10.3 -> 9.1-9.4 us, head 20.0 -> 17.7-19.0 us; three buffers lose), but inside the training
+// step register staging is faster on every bench config (tools/env_sweep.sh, ESGPT_GEMM_FWD_GLDS=0: C2 1.695 ->
+// 1.651 ms, C3 11.52 -> 11.38, C4 6.65 -> 6.59, C5 3.95 -> 3.89; profiles/r05b_fwd_glds_sweep.log), so the forward
+// keeps register staging by default too; the grouped backward loses 4-6 % with either depth (627 -> 659 / 671 us
+// per step's set) and at every dX / dW tile size.
 int fwd_glds() {
   static int v = -1;
   if (v < 0) {
     const char* e = tuning_env("ESGPT_GEMM_FWD_GLDS");
-    v = e ? std::min(3, std::max(0, atoi(e))) : 2;
+    v = e ? std::min(3, std::max(0, atoi(e))) : 0;
     if (v == 1) v = 2;
   }
   return v;
