@@ -763,7 +763,8 @@ TileCfg fwd_tile(int64_t M, int64_t N, int64_t K, bool act) {
 TileCfg dx_tile(int64_t T, int64_t in, int64_t out) {
   static const TileCfg forced = env_tile("ESGPT_GEMM_TILE_DX", TileCfg{0, 0}, kDxTiles, 3);
   if (forced.fm) return forced;
-  return (in >= 512 && out >= 512 && T >= 4096) ? TileCfg{2, 2} : TileCfg{1, 1};
+  if (in >= 512 && out >= 512 && T >= 4096) return TileCfg{2, 2};
+  return T >= 16384 ? TileCfg{2, 1} : TileCfg{1, 1};  // long token runs (C4's dependency graph, C5): 128x64
 }
 // dW [out, in] over K = T tokens: 128x128 tiles once the 64x64 plan (at its minimum split count, one split per
 // kMaxChunk of tokens) would put more than three workgroups per CU on the chip — their f32 slab traffic then costs
