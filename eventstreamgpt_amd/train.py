@@ -882,21 +882,26 @@ class TrainStep:
         else:
             segs, static, sloss, grads, opt_graph, plan = entry
             fused_slot = None
-            if opt_graph == "fused":  # the optimizer step ends the step's graph
-                if self.sched_step == self.lr_lambda_warm_total():
-                    self.lr_lambda(self.sched_step)  # warmup == total: the reference's lambda raises here
-                fused_slot = self._claim()
+            if opt_graph == "fused" and self.sched_step == self.lr_lambda_warm_total():
+                self.lr_lambda(self.sched_step)  # warmup == total: the reference's lambda raises here
             static.copy_(batch, non_blocking=True)
             if self._release is not None:  # the staging buffer is consumed: the next prefetch may refill it
                 self._release.record()
                 self._release = None
             for p, gr in zip(self.params, grads):  # the graph writes its gradients into its own pool
                 p.grad = gr
-            for g, released in segs:
-                g.replay()
-                if exchange:  # exchanged while the next segment replays
-                    for b in released:
-                        gb._launch(b)
+            if opt_graph == "fused":  # the optimizer step (and its ring entry) ends the step's graph
+                fused_slot = self._claim()
+            try:
+                for g, released in segs:
+                    g.replay()
+                    if exchange:  # exchanged while the next segment replays
+                        for b in released:
+                            gb._launch(b)
+            except BaseException:
+                if fused_slot is not None:
+                    self._unclaim()
+                raise
             # the next replay overwrites the static loss: hand back a copy — written by the optimizer's prepare launch
             # into the hand-off ring when this step runs one (no launch of its own, no host-launch gap), else by the
             # library's pack kernel (not clone()'s D2D blit: ~5 us of device time for 4 bytes)
@@ -937,8 +942,13 @@ class TrainStep:
             # launch writes the step's hand-off entry (the replayed step's loss, the error block)
             pending = loss is None
             slot = None if self.opt.host_args else self._claim()
-            done = self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None,
-                                 hand=self._hand(sloss if pending else loss) if slot is not None else None)
+            try:
+                done = self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None,
+                                     hand=self._hand(sloss if pending else loss) if slot is not None else None)
+            except BaseException:  # no launch: the device ring counter did not advance
+                if slot is not None:
+                    self._unclaim()
+                raise
             if slot is not None and not done:  # no active parameter: no launch wrote the entry
                 self._unclaim()
                 slot = None
