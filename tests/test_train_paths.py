@@ -528,6 +528,30 @@ def test_captured_optimizer_step_matches_host_launched():
         assert out["host"][1] == out[mode][1] and out["host"][2] == out[mode][2]
 
 
+def test_hand_off_ring_claims_cpu():
+    """The optimizer hand-off ring's host side (TrainStep._claim / _unclaim / _ring_loss): a loss the caller still
+    holds when its ring entry comes round again is moved to its own storage first (its value kept), a loss already
+    dropped costs nothing, and a claim with no launch behind it is taken back."""
+    m = torch.nn.Linear(3, 2)
+    ts = TrainStep(m, OptimizationConfig(init_lr=1e-3), compute_dtype=torch.float32)
+    ts.ring_len = 2
+    like = torch.zeros(())
+    s0 = ts._claim()
+    ts._ring[s0, 0] = 1.0
+    held = ts._ring_loss(s0, like)
+    s1 = ts._claim()
+    ts._ring[s1, 0] = 2.0
+    dropped = ts._ring_loss(s1, like)
+    del dropped
+    assert (s0, s1) == (0, 1)
+    s2 = ts._claim()  # entry 0 again: `held` moves to its own storage before the entry is rewritten
+    ts._ring[s2, 0] = 3.0
+    assert s2 == 0 and float(held) == 1.0 and held.data_ptr() != ts._ring[0].data_ptr()
+    s3 = ts._claim()  # entry 1: its loss was dropped, nothing to move
+    ts._unclaim()  # (no launch followed)
+    assert s3 == 1 and ts._claim() == 1
+
+
 def test_gradient_accumulation_single_process_cpu():
     """OptimizationConfig.gradient_accumulation = 3 (Lightning's accumulate_grad_batches, generative_modeling.py:661-664)
     without DDP: the optimizer and the LR schedule step once per 3 batches on the sum of the 3 batches' gradients of
