@@ -512,7 +512,9 @@ int split2_keys(int64_t Lk, int64_t hd) {
   // measured (tools/attn_split_ab.py, profiles/r05_attn_split_ab.log): faster past one key block at hd = 16 and 128
   // (L = 520 local-40: 20.0 -> 15.6 us; L = 600: 161.6 -> 118.9 us), slower at hd = 32 / 64 (L = 4096 hd = 64:
   // 488 -> 520 us; C5 L = 1024: 105.8 -> 106.8 us, 124.8 -> 133.7 us with dropout)
-  return (Lk > KB && (hd == 16 || hd == 128)) ? 128 : 0;
+  // hd = 128: always (the fused kernel's 512-thread workgroups cap it at 256 registers, where its hd-128 instances
+  // spilled 464-572 B per lane to scratch; the split kernels run one wave per SIMD at hd 128 and do not spill)
+  return ((Lk > KB && hd == 16) || hd == 128) ? 128 : 0;
 }
 
 template <int HD>
@@ -611,6 +613,12 @@ int esgpt_attn_bwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
   if (hd == 64)
     return launch<64>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
                       window, drop_p, seed, keep, dq32, counters, st);
+#ifdef ESGPT_TUNING_HOOKS
   return launch<128>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,
                      window, drop_p, seed, keep, dq32, counters, st);
+#else
+  // hd = 128 always takes the split backward (split2_keys); the fused hd-128 kernel is built in the tools build only
+  return esgpt_attn_bwd_mfma_split(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H,
+                                   Lq, Lk, 128, window, drop_p, seed, keep, 128, st);
+#endif
 }

@@ -46,7 +46,7 @@ struct DkvCfg {
 };
 
 template <int HD, int DM, int NWK>
-__global__ __launch_bounds__(64 * NWK, 2) void attn_bwd_dkv_kernel(
+__global__ __launch_bounds__(64 * NWK, HD == 128 ? 1 : 2) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
@@ -480,6 +480,7 @@ int esgpt_attn_bwd_mfma_split(const void* q, const void* k, const void* v, int64
                               const uint8_t* qmask, void* dq, void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H,
                               int64_t Lq, int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed,
                               const uint32_t* keep, int keys_per_wg, hipStream_t st) {
+#ifdef ESGPT_TUNING_HOOKS
 #define ESGPT_BWD2_HD(HD_)                                                                                           \
   return keys_per_wg == 64                                                                                           \
              ? launch2<HD_, 2>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, \
@@ -490,5 +491,16 @@ int esgpt_attn_bwd_mfma_split(const void* q, const void* k, const void* v, int64
   if (hd == 32) ESGPT_BWD2_HD(32);
   if (hd == 64) ESGPT_BWD2_HD(64);
   ESGPT_BWD2_HD(128);
+#else
+  // the product takes the split form only at hd = 16 / 128 with 128 keys per dK / dV workgroup (split2_keys); the
+  // hd = 32 / 64 and 64-key forms (measured slower, and the hd-64 ones spill) exist in the tools build only
+  (void)keys_per_wg;
+#define ESGPT_BWD2_HD(HD_)                                                                                           \
+  return launch2<HD_, 4>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,  \
+                         window, drop_p, seed, keep, st)
+  if (hd == 16) ESGPT_BWD2_HD(16);
+  if (hd == 128) ESGPT_BWD2_HD(128);
+  return ESGPT_ERR_UNSUPPORTED;
+#endif
 #undef ESGPT_BWD2_HD
 }

@@ -119,7 +119,9 @@ __device__ __forceinline__ bf16x4 tr_read(const __bf16* p) {
 // ds_read_b64_tr_b16 (no transposing LDS writes). The next pair of K/V tiles is prefetched into registers while the
 // current pair is consumed. Key validity is a 64-bit ballot per tile; tiles that are fully valid and fully inside the
 // causal / local band skip the per-element masks. Softmax in the exp2 domain (v_exp_f32).
-template <int HD, bool DROP>
+// IDX64: some element counter of the launch exceeds 32 bits (the dropout hash then runs on 64-bit counters); a
+// template parameter, so each instance carries one hash path (with both, the hd-64 dropout instance spilled).
+template <int HD, bool DROP, bool IDX64 = false>
 __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kernel(const __bf16* __restrict__ q,
                                                                const __bf16* __restrict__ k,
                                                                const __bf16* __restrict__ v, int64_t ld_in, int64_t tq,
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   }
   const int b = bh / H, hh = bh % H;
   const DropoutSpec dr = make_dropout(drop_p, seed);
-  const bool idx32 = (uint64_t)(gridDim.x / nqb) * (uint64_t)Lq * (uint64_t)Lk <= 0xffffffffull;  // B·H = grid / nqb
+  constexpr bool idx32 = !IDX64;
   const int off = Lk - Lq;
   const int qb = qbi * ROWS;
   const int qi = qb + qh * 32 + r;
@@ -275,7 +277,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
     if (DROP) {
       uint32_t kw[2] = {0u, 0u};  // keep bits of this lane's keys, at their key position within the 32-key group
       // registers (i, i+1), i even, hold consecutive keys: one hash per pair when the pair is aligned
-      if (idx32) {  // every element index of the launch fits 32 bits (wave-uniform)
+      if constexpr (idx32) {  // every element index of the launch fits 32 bits
         const uint32_t rowbase = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk;
         const bool aligned = (rowbase & 1) == 0;
 #pragma unroll
@@ -383,17 +385,25 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
         oacc[dt][i] = oacc[dt][i] * a0 + cO[((qh * (HDP / 32) + dt) * 16 + i) * 64 + lane] * a1;
   }
 
-  const bool ok = qvalid && l > 0.f;
+  // the query's row, mask and validity recomputed here rather than kept live across the key loop (an opaque copy of
+  // the thread id the compiler cannot fold into the pre-loop values: at 2 waves per SIMD the hd-64 dropout instance
+  // otherwise spilled two of them to scratch)
+  int tid2;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid2) : "v"(tid));
+  const int qi_e = qb + qh * 32 + (tid2 & 31);
+  const bool qin_e = qi_e < Lq;
+  const bool qvalid_e = qin_e && (qmask == nullptr || qmask[(int64_t)b * Lq + qi_e] != 0);
+  const bool ok = qvalid_e && l > 0.f;
   const float inv = ok ? 1.f / l : 0.f;
-  if (qin) {
-    __bf16* orow = o + ((int64_t)b * Lq + qi) * ld_o + hh * HD;
+  if (qin_e) {
+    __bf16* orow = o + ((int64_t)b * Lq + qi_e) * ld_o + hh * HD;
 #pragma unroll
     for (int dt = 0; dt < HDP / 32; ++dt) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) oacc[dt][i] *= inv;
-      store_col32<HD < 32 ? HD : 32>(orow + 32 * dt, oacc[dt], h);
+      store_col32<HD < 32 ? HD : 32>(orow + 32 * dt, oacc[dt], (tid2 >> 5) & 1);
     }
-    if (h == 0) lse[(int64_t)bh * Lq + qi] = ok ? m * kLn2 + logf(l) : 0.f;
+    if ((tid2 & 32) == 0) lse[(int64_t)bh * Lq + qi_e] = ok ? m * kLn2 + logf(l) : 0.f;
   }
 }
 
@@ -421,7 +431,15 @@ static void launch_fwd(dim3 grid, hipStream_t st, const void* q, const void* k, 
                        int64_t H, int64_t Lq, int64_t Lk, int64_t window, float drop_p, const uint64_t* seed,
                        uint32_t* keep) {
   const int nw = (int)cdiv(Lk, 32);
-  if (drop_p > 0.f)
+  // B·H·Lq·Lk element counters: 32-bit hash path when they all fit (B·H = grid / query blocks)
+  const bool idx64 = (uint64_t)(grid.x / cdiv(Lq, ROWS)) * (uint64_t)Lq * (uint64_t)Lk > 0xffffffffull;
+  if (drop_p > 0.f && idx64)
+    attn_fwd_mfma_kernel<HD, true, true><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k,
+                                                                          (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o,
+                                                                          lse, kmask, qmask, (int)H, (int)Lq, (int)Lk,
+                                                                          (int)window, drop_p, seed, keep, nw,
+                                                                          attn_order());
+  else if (drop_p > 0.f)
     attn_fwd_mfma_kernel<HD, true><<<grid, dim3(THREADS), 0, st>>>((const __bf16*)q, (const __bf16*)k,
                                                                     (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o,
                                                                     lse, kmask, qmask, (int)H, (int)Lq, (int)Lk,

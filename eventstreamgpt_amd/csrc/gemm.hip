@@ -884,7 +884,9 @@ int64_t dw_target(bool has_dx, int64_t T, int64_t in, int64_t out, bool f32 = fa
 
 template <int FM, int FN>
 void launch_fwd(const Prob& p, hipStream_t st) {
-  if (esgpt::gk::launch_stream(p, true, st)) return;
+#ifdef ESGPT_TUNING_HOOKS
+  if (esgpt::gk::launch_stream(p, true, st)) return;  // tools/lab/gemm_stream.hip (tools build only)
+#endif
   const dim3 grid((unsigned)n_wg(p));
   static const int persist = [] {
     const char* e = tuning_env("ESGPT_GEMM_PERSIST");

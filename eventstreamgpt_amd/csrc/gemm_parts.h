@@ -1,5 +1,5 @@
 // Device-side pieces shared by the projection GEMM kernels (gemm.hip: tile GEMM, grouped backward, slab reduce;
-// gemm_stream.hip: the streamed-tile persistent GEMM): bf16 / f32 operand tiles, LDS-DMA tiles, the problem
+// tools/lab/gemm_stream.hip: the streamed-tile persistent GEMM, tools build): bf16 / f32 operand tiles, LDS-DMA tiles, the problem
 // descriptor and small helpers. Included by those two translation units only.
 #pragma once
 #include <algorithm>
@@ -394,7 +394,7 @@ __device__ __forceinline__ float rowsum_extra(const Prob& p, int m) {
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
-// gemm_stream.hip: launches the streamed-tile kernel for p when enabled and applicable (false: caller launches)
+// tools/lab/gemm_stream.hip (tools build only): launches the streamed-tile kernel for p when enabled and applicable (false: caller launches)
 bool launch_stream(const Prob& p, bool bkc, hipStream_t st);
 
 }  // namespace gk

@@ -812,8 +812,9 @@ __device__ __forceinline__ uint4 pack_chunk(const float (&o)[16 / sizeof(T)]) {
 }
 
 template <typename T>
-// six waves per SIMD (80 VGPRs; measured 53.7 -> 53.0 us at C2; eight spill to scratch)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void event_stream_kernel(esgpt_batch bt, Terms terms, StreamPlan plan,
+// f32 logits: six waves per SIMD (80 VGPRs; measured 53.7 -> 53.0 us at C2; eight spill to scratch). bf16 logits:
+// five (at six the bf16 instance spills 48 B/lane to scratch — 25 MB of scratch stores per C2 step)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 6 : 5))) void event_stream_kernel(esgpt_batch bt, Terms terms, StreamPlan plan,
                                                            esgpt_tte_spec tte, const T* __restrict__ zc, int64_t ldc,
                                                            int64_t n_levels, int shift, const T* __restrict__ zc_bias,
                                                            const T* __restrict__ zt, int64_t ldt, T* __restrict__ dzc,

@@ -30,7 +30,11 @@ int bwd_rows() {
   if (r == 0) {
     const char* e = tuning_env("ESGPT_LN_BWD_ROWS");
     const int v = e ? atoi(e) : kBwdRowsPerWave;
+#ifdef ESGPT_TUNING_HOOKS
     r = (v == 2 || v == 4 || v == 8) ? v : kBwdRowsPerWave;
+#else
+    r = (v == 2 || v == 4) ? v : kBwdRowsPerWave;
+#endif
   }
   return r;
 }
@@ -506,12 +510,20 @@ void launch_ln_bwd(const float* dh_in, const void* dout, const float* h, const f
 #define LN_BWD(KC, RR)                                                                                             \
   residual_ln_bwd_kernel<TY, TO, KC, RR><<<grid, 256, 0, st>>>(dh_in, (const TO*)dout, h, mean, rstd, w, rmask, p, \
                                                                seed, N, D, dx, (TY*)dy, part, skip_T)
+#ifdef ESGPT_TUNING_HOOKS
 #define LN_BWD_R(KC)              \
   do {                            \
     if (R == 2) LN_BWD(KC, 2);    \
     else if (R == 8) LN_BWD(KC, 8); \
     else LN_BWD(KC, 4);           \
   } while (0)
+#else  // 8 rows per wave (measured slower; spills at D > 768) in the tools build only
+#define LN_BWD_R(KC)              \
+  do {                            \
+    if (R == 2) LN_BWD(KC, 2);    \
+    else LN_BWD(KC, 4);           \
+  } while (0)
+#endif
   switch (cdiv(D, 256)) {
     case 1: LN_BWD_R(1); break;
     case 2: LN_BWD_R(2); break;

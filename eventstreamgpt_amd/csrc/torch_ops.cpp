@@ -991,14 +991,20 @@ void adamw_dev(const Tensor& table, const Tensor& blocks, const Tensor& counters
                int64_t n_params, int64_t kind, int64_t warmup, int64_t total, double power, double init_lr,
                double end_lr, double beta1, double beta2, double eps, double wd, const Tensor& per_tensor,
                const Tensor& lr_dev, const Tensor& err, const optional<Tensor>& copy_src,
-               const optional<Tensor>& ring, const optional<Tensor>& ring_ctr) {
+               const optional<Tensor>& ring, const optional<Tensor>& ring_ctr, const optional<Tensor>& ring_tab) {
   const c10::DeviceGuard guard(table.device());
   TORCH_CHECK(counters.scalar_type() == at::kLong && counters.numel() == n_params + 1, "adamw_dev: counters");
+  const bool tb = ring_tab.has_value() && ring_tab->defined();
   const bool rg = ring.has_value() && ring->defined();
   const bool cp = copy_src.has_value() && copy_src->defined();
   const bool rc = ring_ctr.has_value() && ring_ctr->defined();
   const int64_t n_copy = cp ? copy_src->numel() : 0;
-  TORCH_CHECK(!cp || rg, "adamw_dev: copy_src needs a ring");
+  TORCH_CHECK(!cp || rg || tb, "adamw_dev: copy_src needs a ring");
+  TORCH_CHECK(!(rg && tb), "adamw_dev: ring and ring_tab are exclusive");
+  if (tb)
+    TORCH_CHECK(ring_tab->scalar_type() == at::kLong && ring_tab->dim() == 1 && ring_tab->is_contiguous() &&
+                    ring_tab->numel() >= 1 && (!rc || (ring_ctr->scalar_type() == at::kLong && ring_ctr->numel() == 1)),
+                "adamw_dev: ring_tab: contiguous int64 [entries] of entry addresses, ring_ctr int64 [1]");
   if (cp)
     TORCH_CHECK(copy_src->scalar_type() == at::kFloat && copy_src->is_contiguous() && n_copy <= 1024,
                 "adamw_dev: copy_src: contiguous f32, at most 1024 elements");
@@ -1010,12 +1016,22 @@ void adamw_dev(const Tensor& table, const Tensor& blocks, const Tensor& counters
   TORCH_CHECK(active.scalar_type() == at::kInt && per_tensor.numel() >= 2 * active.numel(), "adamw_dev: active / per");
   esgpt_lr_schedule sc{kind, warmup, total, power, init_lr, end_lr};
   void* st = stream_of(table);
-  check(esgpt_adamw_prepare_ex(ptr<int64_t>(counters), active.numel() ? ptr<const int32_t>(active) : nullptr,
-                               (int)active.numel(), (int)n_params, &sc, beta1, beta2, ptr<float>(per_tensor),
-                               ptr<float>(lr_dev), ptr<const int32_t>(err), cp ? ptr<const float>(*copy_src) : nullptr,
-                               n_copy, rg ? ptr<float>(*ring) : nullptr, rc ? ptr<int64_t>(*ring_ctr) : nullptr,
-                               rg ? ring->size(0) : 1, st),
-        "adamw_prepare");
+  if (tb)
+    check(esgpt_adamw_prepare_tab(ptr<int64_t>(counters), active.numel() ? ptr<const int32_t>(active) : nullptr,
+                                  (int)active.numel(), (int)n_params, &sc, beta1, beta2, ptr<float>(per_tensor),
+                                  ptr<float>(lr_dev), ptr<const int32_t>(err),
+                                  cp ? ptr<const float>(*copy_src) : nullptr, n_copy,
+                                  reinterpret_cast<float* const*>(ring_tab->data_ptr()),
+                                  rc ? ptr<int64_t>(*ring_ctr) : nullptr, ring_tab->numel(), st),
+          "adamw_prepare_tab");
+  else
+    check(esgpt_adamw_prepare_ex(ptr<int64_t>(counters), active.numel() ? ptr<const int32_t>(active) : nullptr,
+                                 (int)active.numel(), (int)n_params, &sc, beta1, beta2, ptr<float>(per_tensor),
+                                 ptr<float>(lr_dev), ptr<const int32_t>(err),
+                                 cp ? ptr<const float>(*copy_src) : nullptr, n_copy,
+                                 rg ? ptr<float>(*ring) : nullptr, rc ? ptr<int64_t>(*ring_ctr) : nullptr,
+                                 rg ? ring->size(0) : 1, st),
+          "adamw_prepare");
   check(esgpt_adamw_dev(reinterpret_cast<const esgpt_adam_tensor*>(table.data_ptr()), ptr<const int64_t>(blocks),
                         blocks.numel(), ptr<const float>(lr_dev), (float)beta1, (float)beta2, (float)eps, (float)wd,
                         ptr<const float>(per_tensor), ptr<const int32_t>(err), st),
@@ -1090,7 +1106,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("adamw_dev(Tensor table, Tensor blocks, Tensor(a!) counters, Tensor active, int n_params, int kind, "
         "int warmup, int total, float power, float init_lr, float end_lr, float beta1, float beta2, float eps, "
         "float weight_decay, Tensor(b!) per_tensor, Tensor(c!) lr_dev, Tensor err, Tensor? copy_src=None, "
-        "Tensor(d!)? ring=None, Tensor(e!)? ring_ctr=None) -> ()");
+        "Tensor(d!)? ring=None, Tensor(e!)? ring_ctr=None, Tensor? ring_tab=None) -> ()");
   m.def("adamw(Tensor table, Tensor blocks, float lr, float beta1, float beta2, float eps, float weight_decay, "
         "int step, Tensor? per_tensor, Tensor err) -> ()");
 }

@@ -148,8 +148,8 @@ class FusedAdamW:
         """The device step over ``plan``: esgpt_adamw_prepare (counters, lr, per-tensor bias corrections — torch's
         one ``step`` per parameter) + the update, both no-ops while the device error block holds a flag. No host
         arguments change between steps (``lr=None``: the installed schedule), so the launch replays in a graph.
-        ``hand`` = (src, ring, ring_ctr): the step's hand-off entry written by the prepare launch (src — the step's
-        loss — and the error block into ring entry ring_ctr % len(ring); TrainStep._claim). Returns whether the
+        ``hand`` = (src, ring, ring_ctr, ring_tab): the step's hand-off entry written by the prepare launch (src — the
+        step's loss — and the error block into ring entry ring_ctr % len(ring_tab); TrainStep._claim). Returns whether the
         launch (and so the hand-off) happened."""
         if not plan["active"]:
             return False
@@ -160,7 +160,7 @@ class FusedAdamW:
         self.ops.adamw_dev(plan["table"], plan["blocks"], self._counters, plan["active_dev"], len(self.params),
                            int(kind), int(warm), int(total), float(power), float(init_lr), float(end_lr), float(b1),
                            float(b2), float(self.eps), float(self.weight_decay), plan["per"], self._lr_dev,
-                           err_word(self.params[0].device), *(hand if hand is not None else (None, None, None)))
+                           err_word(self.params[0].device), *(hand if hand is not None else (None, None, None, None)))
         return True
 
     def note_step(self, active):
@@ -277,6 +277,7 @@ class GradBuckets:
         # gradient accumulation (TrainStep, OptimizationConfig.gradient_accumulation): the buffer already holds the
         # window's earlier batches — a release ADDS the batch's gradients instead of copying them
         self.add = False
+        self.loss_src = None  # the current step's loss (TrainStep sets it before backward / the replay)
         self.reset()
         self._hooks = [params[i].register_post_accumulate_grad_hook(self._make_hook(i)) for i in range(len(params))]
 
@@ -295,8 +296,11 @@ class GradBuckets:
             seq.append((g, pad))
             placed.update(g)
         total = sum(sum(params[i].numel() for i in g) + pad for g, pad in seq)
-        self.flat = torch.zeros(total + 1, dtype=torch.float32, device=params[0].device)
-        self.slot = self.flat[total:]  # the any-rank-failed flag (last bucket)
+        self.flat = torch.zeros(total + 2, dtype=torch.float32, device=params[0].device)
+        self.slot = self.flat[total:total + 1]  # the any-rank-failed flag (last bucket)
+        # the step's loss (last bucket): after the exchange, the mean of the ranks' losses — the reference's
+        # self.log("train_loss", ..., sync_dist=True) (generative_modeling.py:317-318) at no extra collective
+        self.loss_slot = self.flat[total + 1:total + 2]
         self.views, self.offset, self.pad_after, self.bucket_of, self.buckets = {}, {}, {}, {}, []
         off, start, cur = 0, 0, []
         for g, pad in seq:
@@ -314,7 +318,7 @@ class GradBuckets:
         if cur:
             self.buckets.append((cur, start, off))
         idx, s0, e0 = self.buckets[-1]
-        self.buckets[-1] = (idx, s0, e0 + 1)  # + the error slot
+        self.buckets[-1] = (idx, s0, e0 + 2)  # + the error and loss slots
         for b, (idx, _, _) in enumerate(self.buckets):
             for i in idx:
                 self.bucket_of[i] = b
@@ -418,6 +422,10 @@ class GradBuckets:
                     self.slot.copy_(ew.ne(0))
                 else:
                     self.slot.zero_()
+                if self.loss_src is not None:
+                    self.loss_slot.copy_(self.loss_src.detach().reshape(1))
+                else:
+                    self.loss_slot.zero_()
             seg = self.flat[s:e]
             op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
             self._works.append((dist.all_reduce(seg, op=op, async_op=True), seg))
@@ -439,6 +447,11 @@ class GradBuckets:
 
 # the replayed step's loss copy rides in the optimizer's prepare launch (False, measurement hook: the pack kernel)
 LOSS_IN_OPT = True
+
+
+def _storage_users(t: torch.Tensor) -> int:
+    """Use count of t's storage (every tensor viewing it holds one reference)."""
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata)
 
 
 def _copy_scalar(t: torch.Tensor) -> torch.Tensor:
@@ -544,18 +557,22 @@ class TrainStep:
             for p in params:
                 p.register_hook(self._make_accumulate_guard(p))
         self._pending: deque = deque()  # (event, pinned error block copy, batch) of submitted steps
-        # the optimizer launch's hand-off ring (esgpt_adamw_prepare_ex): entry k = [loss, pad x3, error block x4
-        # words] of the k-th launch; the returned loss of a replayed step is a view of its entry (re-pointed to a copy
-        # before the entry is reused while the caller still holds it), the error words go to the host for check()
+        # the optimizer launch's hand-off ring (esgpt_adamw_prepare_tab): entry k = [loss, pad x3, error block x4
+        # words] of the k-th launch; the returned loss of a replayed step is a view of its entry (the entry is given a
+        # fresh allocation before reuse while anything still shares it), the error words go to the host for check()
         self.ring_len = 64
-        self._ring = None
+        self._ring_tab = None
+        self._slots: list = []
         self._ring_n = 0  # host mirror of the device ring counter
-        self._ring_refs: list = []
         self._vocab = getattr(getattr(model, "config", None), "vocab_size", None)
         self._copy_stream = None
         self._staging: dict = {}
         self._prefetched = None
         self._release = None
+        # the step's loss as the reference logs it (train_loss, sync_dist=True): under DDP the mean over ranks,
+        # carried in the exchange's last bucket (a view of the exchange buffer, valid until the next step);
+        # otherwise the step's own loss
+        self.logged_loss = None
 
     def _ones(self, loss: torch.Tensor) -> torch.Tensor:
         """d(loss)/d(loss) = 1 as a persistent tensor (no fill launch in the step; under HIP-graph capture the graph
@@ -566,23 +583,28 @@ class TrainStep:
         return one
 
     # ---- optimizer hand-off ring -------------------------------------------------------------------------------
+    # Entry k is its own 8-float allocation ([loss, pad x3, error block x4 words]) reached through a device table of
+    # entry addresses (esgpt_adamw_prepare_tab). A returned loss is a view of its entry; when the entry comes round
+    # again while ANY tensor still shares its storage (the returned object, a detach(), a view, an index — counted by
+    # the storage's use count, not by object identity), the entry gets a fresh allocation and its table slot is
+    # re-pointed (one stream-ordered fill) — the caller's tensors keep their value and nothing is copied.
     def _ring_state(self):
-        if self._ring is None:
-            self._ring = torch.zeros(self.ring_len, 8, dtype=torch.float32, device=self.device)
+        if self._ring_tab is None:
+            self._slots = [torch.zeros(8, dtype=torch.float32, device=self.device) for _ in range(self.ring_len)]
+            self._ring_tab = torch.tensor([t.data_ptr() for t in self._slots], dtype=torch.int64, device=self.device)
             self._ring_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
-            self._ring_refs = [None] * self.ring_len
-        return self._ring, self._ring_ctr
+            self._slot_users = _storage_users(self._slots[0])  # the ring's own reference alone
+        return None, self._ring_ctr, self._ring_tab
 
     def _claim(self) -> int:
-        """The ring entry the next optimizer launch writes (its device counter advances with every launch); a loss
-        the caller still holds from that entry's previous use is moved to its own storage first."""
-        ring, _ = self._ring_state()
-        slot = self._ring_n % len(ring)
-        ref = self._ring_refs[slot]
-        held = ref() if ref is not None else None
-        if held is not None:
-            held.set_(held.clone())
-        self._ring_refs[slot] = None
+        """The ring entry the next optimizer launch writes (its device counter advances with every launch); an entry
+        whose storage is still shared by a tensor the caller holds is given a fresh allocation first."""
+        self._ring_state()
+        slot = self._ring_n % self.ring_len
+        if _storage_users(self._slots[slot]) > self._slot_users:
+            new = torch.zeros_like(self._slots[slot])
+            self._slots[slot] = new
+            self._ring_tab[slot].fill_(new.data_ptr())  # stream-ordered before the launch that writes the entry
         self._ring_n += 1
         return slot
 
@@ -590,13 +612,11 @@ class TrainStep:
         self._ring_n -= 1  # no launch happened: the device counter did not advance
 
     def _ring_loss(self, slot: int, like: torch.Tensor) -> torch.Tensor:
-        loss = self._ring[slot, : like.numel()].view(like.shape)
-        self._ring_refs[slot] = weakref.ref(loss)
-        return loss
+        loss = self._slots[slot][: like.numel()].view(like.shape)
+        return loss if like.dtype == torch.float32 else loss.to(like.dtype)
 
     def _hand(self, src: torch.Tensor):
-        ring, ctr = self._ring_state()
-        return (src.detach().reshape(-1).float(), ring, ctr)
+        return (src.detach().reshape(-1).float(),) + self._ring_state()
 
     # ---- gradient accumulation -------------------------------------------------------------------------------
     def _acc_views(self):
@@ -626,13 +646,50 @@ class TrainStep:
 
     @torch.no_grad()
     def _reset_accumulation(self):
+        """Ends the window. The buffer is zeroed lazily, at the start of the next window (_zero_window), so the
+        gradients the optimizer just read (``param.grad`` views of it) stay readable until the next ``step``."""
         self._micro = 0
         self._touched.clear()
-        if self.accum > 1:
+        self._acc_dirty = self.accum > 1
+
+    @torch.no_grad()
+    def _zero_window(self):
+        if getattr(self, "_acc_dirty", False):
             if self.grad_buckets is not None:
                 self.grad_buckets.flat.zero_()
             elif self._acc is not None:
                 self._acc[0].zero_()
+            self._acc_dirty = False
+
+    @torch.no_grad()
+    def flush(self):
+        """Applies a partial accumulation window (Lightning steps the optimizer on an epoch's last, incomplete
+        window of ``accumulate_grad_batches``): the exchange (under DDP every rank must call it at the same point), the
+        optimizer and the LR schedule step on the window's sums. As in Lightning, each batch's loss was scaled by
+        1 / gradient_accumulation whatever the window's length. Returns whether a step was taken."""
+        if self.accum == 1 or self._micro == 0:
+            return False
+        gb = self.grad_buckets
+        views = self._acc_views()
+        for i, p in enumerate(self.params):  # the sums are already in the buffer: a release must not add them again
+            p.grad = views[i] if i in self._touched else None
+        if gb is not None:
+            gb.add, gb.loss_src = True, None
+            gb.finish()
+        if self.sched is None:
+            if self.sched_step == self.lr_lambda_warm_total():
+                self.lr_lambda(self.sched_step)
+            self.opt.step(self.cfg.init_lr * self.lr_lambda(self.sched_step) if self.opt.host_args else None)
+            active = list(self.opt._active)
+        else:
+            self.opt.step()
+            self.sched.step()
+            active = []
+        self.sched_step += 1
+        self._reset_accumulation()
+        if self.check_errors:
+            self._record_pending(None, active, True)
+        return True
 
     def _maybe_relayout(self):
         """Zero-copy exchange: adopt the parameter groups the last forward recorded — only before any graph has been
@@ -670,6 +727,8 @@ class TrainStep:
             with torch.autocast("cuda", dtype=self.dtype, enabled=self.dtype != torch.float32,
                                 cache_enabled=autocast_cache):
                 out = self.model(batch)
+            if gb is not None:
+                gb.loss_src = out.loss
             with deferred_colsums(dev, enabled=self.defer_colsums), \
                     weight_grad_overlap(dev, enabled=self.overlap_weight_grads):
                 out.loss.backward(self._ones(out.loss))
@@ -865,6 +924,8 @@ class TrainStep:
         gb = self.grad_buckets
         accumulating = self.accum > 1
         last = self._micro + 1 >= self.accum  # this batch closes the accumulation window: exchange + step
+        if accumulating and self._micro == 0:
+            self._zero_window()  # the previous window's sums, left readable until now
         exchange = gb is not None and last
         if gb is not None:
             gb.add = accumulating
@@ -890,6 +951,8 @@ class TrainStep:
                 self._release = None
             for p, gr in zip(self.params, grads):  # the graph writes its gradients into its own pool
                 p.grad = gr
+            if gb is not None:
+                gb.loss_src = sloss
             if opt_graph == "fused":  # the optimizer step (and its ring entry) ends the step's graph
                 fused_slot = self._claim()
             try:
@@ -911,6 +974,7 @@ class TrainStep:
             loss = _copy_scalar(sloss)  # no device optimizer launch to carry the copy
         if accumulating and not exchange:
             self._accumulate()  # into the window's buffer (GradBuckets' under DDP)
+        self.logged_loss = loss if gb is None else None
         if not last:
             self._micro += 1
             if self._release is not None:
@@ -922,6 +986,7 @@ class TrainStep:
         self._micro = 0
         if gb is not None:
             gb.finish()
+            self.logged_loss = gb.loss_slot.view(())
         elif accumulating:  # the window's sums are the gradients AdamW reads
             views = self._acc_views()
             for i, p in enumerate(self.params):
@@ -974,7 +1039,7 @@ class TrainStep:
         # (Copied on the compute stream: on a side stream — waiting on an event recorded after the step — the C2
         # step measured ~50 us slower, tools/host_bound.py.)
         host = torch.empty(2, dtype=torch.int64, pin_memory=True)
-        host.copy_(err_word(self.device) if slot is None else self._ring[slot, 4:8].view(torch.int64),
+        host.copy_(err_word(self.device) if slot is None else self._slots[slot][4:8].view(torch.int64),
                    non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
@@ -995,7 +1060,10 @@ class TrainStep:
 
 
 def init_distributed():
-    """Initialises the process group from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*)."""
+    """Initialises the process group from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK / MASTER_*): RCCL ("nccl")
+    with one GPU per rank, gloo without a GPU. Test override (the multi-rank bench rehearsed on a one-GPU box):
+    ESGPT_DIST_BACKEND=gloo with ESGPT_DIST_ONE_DEVICE=1 puts every rank on device 0 (RCCL refuses two ranks on one
+    device)."""
     import os
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -1003,11 +1071,11 @@ def init_distributed():
         return 0, 1, 0
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    if os.environ.get("ESGPT_DIST_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("ESGPT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
-        backend = "nccl"
-    else:
-        backend = "gloo"
     dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
 

@@ -518,6 +518,13 @@ int esgpt_adamw_prepare_ex(int64_t* counters, const int32_t* active, int n_activ
                            const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
                            float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy, float* ring,
                            int64_t* ring_ctr, int64_t ring_len, void* stream);
+/* The same with the hand-off entries as separate allocations: ring_tab is a device array of ring_len pointers (8-B
+ * aligned), entry k = ring_tab[k] (16-B aligned, round_up(n_copy, 4) + 4 floats), read at launch time — the caller
+ * may re-point an entry between launches (TrainStep does so when it still holds a loss returned from that entry). */
+int esgpt_adamw_prepare_tab(int64_t* counters, const int32_t* active, int n_active, int n_params,
+                            const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
+                            float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy,
+                            float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, void* stream);
 int esgpt_adamw_dev(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, const float* lr_dev,
                     float beta1, float beta2, float eps, float weight_decay, const float* per_tensor,
                     const int32_t* err, void* stream);

@@ -62,7 +62,13 @@ def _worker(rank, world, port, q):
         orig(b)
 
     gb._launch = spy
-    ts.step(_data(rank))
+    loss = ts.step(_data(rank))
+    # the logged loss (generative_modeling.py:317-318, sync_dist=True): the mean of the ranks' losses, carried in
+    # the exchange's last bucket (no collective of its own)
+    both = [torch.zeros(()) for _ in range(world)]
+    dist.all_gather(both, loss.detach().reshape(()).clone())
+    assert torch.allclose(ts.logged_loss, sum(both) / world, rtol=1e-6), (ts.logged_loss, both)
+    assert not torch.equal(both[0], both[1])
     assert launched_in_backward and all(in_bwd for _, in_bwd in launched_in_backward)
     assert [b for b, _ in launched_in_backward] == list(range(len(gb.buckets)))  # index order, once each
     # every gradient is a view into the one flat exchange buffer

@@ -348,3 +348,28 @@ def test_device_error_raised_at_the_same_step_on_every_rank_without_check():
     assert res[0][0] == [(3, "RuntimeError")], res[0][0]
     for k in res[0][1]:  # in lockstep afterwards
         assert (torch.from_numpy(res[0][1][k]).float() - torch.from_numpy(res[1][1][k]).float()).abs().max() == 0, k
+
+
+def test_bench_two_ranks_end_to_end():
+    """bench.py --gpus 2 as the driver's scaling run launches it (its own torch.distributed.run child, the ranks'
+    barriers, the MAX / SUM reductions of the timed region, rank 0's one JSON line), rehearsed on the one-GPU box:
+    both ranks on device 0 over gloo (init_distributed's ESGPT_DIST_BACKEND / ESGPT_DIST_ONE_DEVICE test override)."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ESGPT_DIST_BACKEND="gloo", ESGPT_DIST_ONE_DEVICE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-roofline", "--no-cpu-baseline", "--no-hbm-line"], cwd=repo, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 alone prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 2 * 32 and d["scaling"] == "weak"
+    # value = the events of BOTH ranks over the max-over-ranks wall time of the 3 timed steps
+    per_rank_events = d["config"]["events_per_step_per_gpu"]
+    assert d["value"] > 0 and abs(d["value"] * d["ms_per_step"] * 1e-3 - 2 * per_rank_events) < 0.25 * 2 * per_rank_events

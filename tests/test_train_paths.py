@@ -205,7 +205,7 @@ def test_replayed_losses_held_across_steps():
     bc = CONFIGS["C2"]
     batches = [bc.batch(i, batch_size=8, device="cuda").packed() for i in range(6)]
 
-    def run(fuse, read_now, ring_len=4):
+    def run(fuse, read_now, ring_len=4, alias=None):
         cfg = bc.model_config(attention_dropout=0.0, input_dropout=0.0, resid_dropout=0.0)
         torch.manual_seed(0)
         m = CIPPTForGenerativeSequenceModeling(cfg).cuda().train()
@@ -215,15 +215,21 @@ def test_replayed_losses_held_across_steps():
         saved = train_mod.LOSS_IN_OPT
         train_mod.LOSS_IN_OPT = bool(fuse)  # "ring": host-launched optimizer, loss through its ring entry
         try:
-            held = [ts.step(b) for b in batches] if not read_now else [float(ts.step(b)) for b in batches]
+            if alias is not None:  # aliases of the returned loss (not the object itself) held across the ring
+                held = [alias(ts.step(b)) for b in batches]
+            else:
+                held = [ts.step(b) for b in batches] if not read_now else [float(ts.step(b)) for b in batches]
         finally:
             train_mod.LOSS_IN_OPT = saved
         ts.check()
         assert ts.use_graph
         assert all(e[4] == ("fused" if fuse is True else None) for e in ts.graphs.values() if e is not None)
-        return [float(x) for x in held], [p.detach().clone() for p in m.parameters()]
+        return [float(x.reshape(())) for x in held], [p.detach().clone() for p in m.parameters()]
 
     a, pa = run(True, False)
+    for fuse in (True, "ring"):
+        for alias in (lambda x: x.detach(), lambda x: x.view(1), lambda x: x[None]):
+            assert run(fuse, False, alias=alias)[0] == a
     b, pb = run(False, False)
     c, _ = run(True, True, ring_len=64)
     d, pd = run("ring", False)
@@ -529,27 +535,34 @@ def test_captured_optimizer_step_matches_host_launched():
 
 
 def test_hand_off_ring_claims_cpu():
-    """The optimizer hand-off ring's host side (TrainStep._claim / _unclaim / _ring_loss): a loss the caller still
-    holds when its ring entry comes round again is moved to its own storage first (its value kept), a loss already
-    dropped costs nothing, and a claim with no launch behind it is taken back."""
+    """The optimizer hand-off ring's host side (TrainStep._claim / _unclaim / _ring_loss): an entry whose storage the
+    caller still shares when it comes round again — through the returned object or any alias of it (detach, view,
+    index) — gets a fresh allocation and its table slot is re-pointed, so the held values never change; an entry
+    nobody holds is reused as is; a claim with no launch behind it is taken back."""
     m = torch.nn.Linear(3, 2)
     ts = TrainStep(m, OptimizationConfig(init_lr=1e-3), compute_dtype=torch.float32)
-    ts.ring_len = 2
+    ts.ring_len = 3
     like = torch.zeros(())
-    s0 = ts._claim()
-    ts._ring[s0, 0] = 1.0
-    held = ts._ring_loss(s0, like)
-    s1 = ts._claim()
-    ts._ring[s1, 0] = 2.0
-    dropped = ts._ring_loss(s1, like)
-    del dropped
-    assert (s0, s1) == (0, 1)
-    s2 = ts._claim()  # entry 0 again: `held` moves to its own storage before the entry is rewritten
-    ts._ring[s2, 0] = 3.0
-    assert s2 == 0 and float(held) == 1.0 and held.data_ptr() != ts._ring[0].data_ptr()
-    s3 = ts._claim()  # entry 1: its loss was dropped, nothing to move
+    _, _, tab = ts._ring_state()
+    kept = []
+    for alias in (lambda x: x, lambda x: x.detach(), lambda x: x.view(1)[None]):
+        s = ts._claim()
+        ts._slots[s][0] = 10.0 + s  # what the launch would write
+        kept.append(alias(ts._ring_loss(s, like)))
+    assert [ts._slots[i].data_ptr() for i in range(3)] == tab.tolist()
+    for i in range(3):  # every entry comes round again while an alias of its loss is held: fresh allocations
+        s = ts._claim()
+        assert s == i and ts._slots[s].data_ptr() == int(tab[s]) and ts._slots[s].data_ptr() != kept[i].data_ptr()
+        ts._slots[s][0] = -1.0
+    assert [float(k.reshape(())) for k in kept] == [10.0, 11.0, 12.0]
+    kept.clear()  # nothing held any more: the entries are reused in place
+    before = tab.tolist()
+    for i in range(3):
+        ts._ring_loss(ts._claim(), like)
+    assert tab.tolist() == before
+    s = ts._claim()
     ts._unclaim()  # (no launch followed)
-    assert s3 == 1 and ts._claim() == 1
+    assert ts._claim() == s
 
 
 def test_gradient_accumulation_single_process_cpu():
@@ -600,6 +613,57 @@ def test_gradient_accumulation_single_process_cpu():
     for (name, a), b in zip(m.state_dict().items(), ref.state_dict().values()):
         torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=name)
     assert m.unused.weight.grad is None  # never touched: AdamW skipped it, as torch does
+
+
+def test_gradient_accumulation_partial_window_flush_cpu():
+    """After the window's optimizer step the gradients it read stay readable (the buffer is zeroed at the start of
+    the next window, not right after the step), and ``flush()`` applies an incomplete last window as Lightning does
+    (each batch's loss scaled by 1 / k whatever the window's length)."""
+    from eventstreamgpt_amd.train import poly_decay_lambda
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(6, 5)
+
+        def forward(self, x):
+            class Out:
+                pass
+
+            o = Out()
+            o.loss = torch.tanh(self.a(x)).pow(2).mean()
+            return o
+
+    def data(i):
+        return torch.randn(3 + i, 6, generator=torch.Generator().manual_seed(5 + i))
+
+    k = 3
+    cfg = OptimizationConfig(init_lr=0.05, lr_num_warmup_steps=1, max_training_steps=8, gradient_accumulation=k)
+    torch.manual_seed(0)
+    m = Toy()
+    ts = TrainStep(m, cfg, compute_dtype=torch.float32)
+    for i in range(k):
+        ts.step(data(i))
+    g_after = m.a.weight.grad.clone()
+    assert g_after.abs().sum() > 0  # still the window's sums after the step that consumed them
+    assert not ts.flush()  # nothing pending
+    for i in range(k, k + 2):  # an incomplete window of 2
+        ts.step(data(i))
+    assert ts.sched_step == 1 and ts.flush() and ts.sched_step == 2
+    torch.manual_seed(0)
+    ref = Toy()
+    opt = torch.optim.AdamW(ref.parameters(), lr=cfg.init_lr, weight_decay=cfg.weight_decay)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, poly_decay_lambda(1, 8, 1.0, cfg.init_lr, cfg.end_lr))
+    for win in (range(0, k), range(k, k + 2)):
+        opt.zero_grad(set_to_none=True)
+        for i in win:
+            (ref(data(i)).loss / k).backward()
+        if win.start == 0:
+            torch.testing.assert_close(ref.a.weight.grad, g_after, rtol=1e-6, atol=1e-7)
+        opt.step()
+        sched.step()
+    for (name, a), b in zip(m.state_dict().items(), ref.state_dict().values()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=name)
 
 
 def test_warmup_not_below_total_schedule():

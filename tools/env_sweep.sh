@@ -5,7 +5,7 @@
 for spec in "$@"; do
   envs=()
   if [ "$spec" != "-" ]; then IFS=';' read -ra envs <<< "$spec"; fi
-  out=$(env "${envs[@]}" timeout -k 10 120 python bench.py --config ${CONFIG:-C2} --steps ${STEPS:-100} --warmup 10 --no-roofline --no-cpu-baseline --no-pcie-line 2>/dev/null | grep '^{')
+  out=$(env "${envs[@]}" timeout -k 10 120 python bench.py --config ${CONFIG:-C2} --steps ${STEPS:-100} --warmup 10 --no-roofline --no-cpu-baseline --no-hbm-line 2>/dev/null | grep '^{')
   rc=$?
   if [ $rc -ne 0 ]; then echo "$spec: failed rc=$rc"; exit $rc; fi
   echo "$spec: $(echo "$out" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["ms_per_step_median"])')"

@@ -1,5 +1,6 @@
-// Streamed-tile persistent GEMM for the projections (bf16): see the kernel comment below. Launched by gemm.hip
-// (esgpt::gk::launch_stream) for the forward projections and the input-gradient products.
+// Streamed-tile persistent GEMM for the projections (bf16): see the kernel comment below. Measured and rejected
+// (round 5, profiles/r05_gemm_stream_ab.log); built into the tools build only (csrc/Makefile TUNING=1), launched by
+// gemm.hip (esgpt::gk::launch_stream) for the forward projections and the input-gradient products.
 #include "gemm_parts.h"
 
 namespace esgpt {

@@ -23,7 +23,7 @@ rm -rf gpurun_out/pmcF_$C gpurun_out/pmcW_$C &&
 timeout -k 10 300 python bench.py --config $C --steps $STEPS --warmup 5 > gpurun_out/bench_$C.log 2>&1 &&
 grep '^{' gpurun_out/bench_$C.log > gpurun_out/bench_$C.json &&
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/step_$C -o run -- \
-    python bench.py --config $C --steps $STEPS --warmup 3 --no-cpu-baseline --no-roofline --no-pcie-line > gpurun_out/step_$C.log 2>&1
+    python bench.py --config $C --steps $STEPS --warmup 3 --no-cpu-baseline --no-roofline --no-hbm-line > gpurun_out/step_$C.log 2>&1
 rc=$?
 echo "measure_config $C rc=$rc"
 exit $rc

@@ -3,7 +3,7 @@ set -o pipefail
 cfg=${1:-C4}
 run() {  # label, env
   env $2 timeout -k 10 200 bash tools/with_tuning.sh python bench.py --config $cfg --steps 10 --warmup 3 \
-    --no-cpu-baseline --no-roofline --no-pcie-line 2>/dev/null | tail -1 | \
+    --no-cpu-baseline --no-roofline --no-hbm-line 2>/dev/null | tail -1 | \
     python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$1', d['ms_per_step'], d['ms_per_step_median'])"
 }
 run default "ESGPT_X=0" || exit 1
