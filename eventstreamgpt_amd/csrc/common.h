@@ -149,6 +149,31 @@ __device__ __forceinline__ float act_grad(float z, int act) {
   return z > 0.f ? 1.f : 0.f;
 }
 
+// act(z) and act'(z) together (one normal-density / tanh evaluation for both): the c_fc epilogue under
+// ESGPT_ACT_DERIV, which stores the derivative for the backward in place of the pre-activation.
+__device__ __forceinline__ void act_fwd_grad(float z, int act, float& y, float& g) {
+  if (act == 0) {
+    float cdf, pdf;
+    normal_cdf_pdf(z, cdf, pdf);
+    y = z * cdf;
+    g = cdf + z * pdf;
+    return;
+  }
+  if (act == 1) {
+    const float k = 0.79788456080286535588f;
+    const float t = fast_tanh(k * (z + 0.044715f * z * z * z));
+    y = 0.5f * z * (1.f + t);
+    g = 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k * (1.f + 3.f * 0.044715f * z * z);
+    return;
+  }
+  y = z > 0.f ? z : 0.f;
+  g = z > 0.f ? 1.f : 0.f;
+}
+// the backward's factor at one element: the stored derivative (ESGPT_ACT_DERIV), or act'(pre)
+__device__ __forceinline__ float act_factor(float aux, int act) {
+  return (act & ESGPT_ACT_DERIV) ? aux : act_grad(aux, act & 7);
+}
+
 // Dropout (attention probabilities, residual / input): a counter-based hash of (seed, element index), so the
 // forward and backward regenerate the same keep-mask without storing it. One hash per PAIR of elements: element idx
 // takes the 16-bit half (idx & 1) of h = mix32(pair_lo ^ key ^ pair_hi * 0x9E3779B9), pair = idx >> 1 ("lowbias32"

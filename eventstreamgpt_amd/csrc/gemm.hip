@@ -431,10 +431,10 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
             const int c = n0 + lcol(j) + 8 * g + 4 * h;
             if (row < M && c < N) {
               const float4 f = *reinterpret_cast<const float4*>(aux + (int64_t)row * p.ld_aux + c);
-              acc[i][j][4 * g + 0] *= act_grad(f.x, p.act);
-              acc[i][j][4 * g + 1] *= act_grad(f.y, p.act);
-              acc[i][j][4 * g + 2] *= act_grad(f.z, p.act);
-              acc[i][j][4 * g + 3] *= act_grad(f.w, p.act);
+              acc[i][j][4 * g + 0] *= act_factor(f.x, p.act);
+              acc[i][j][4 * g + 1] *= act_factor(f.y, p.act);
+              acc[i][j][4 * g + 2] *= act_factor(f.z, p.act);
+              acc[i][j][4 * g + 3] *= act_factor(f.w, p.act);
             }
           }
       }
@@ -469,15 +469,36 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
         *o4 = w;
       }
     };
-    if (F32 && p.epi == EPI_BIAS_ACT) {  // the f32 pre-activation, then its activation
-      store_f32(reinterpret_cast<float*>(p.aux_out), p.ld_aux, false);
-      __syncthreads();  // the LDS tile is rewritten below
+    if (F32 && p.epi == EPI_BIAS_ACT) {  // the f32 pre-activation (or its act' under ESGPT_ACT_DERIV), then act
+      if (p.act & ESGPT_ACT_DERIV) {
+        f32x16 yv[FM][FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] = act_fwd(acc[i][j][e], p.act);
+            for (int e = 0; e < 16; ++e) {
+              float y, g;
+              act_fwd_grad(acc[i][j][e], p.act & 7, y, g);
+              yv[i][j][e] = y;
+              acc[i][j][e] = g;
+            }
+        store_f32(reinterpret_cast<float*>(p.aux_out), p.ld_aux, false);
+        __syncthreads();  // the LDS tile is rewritten below
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = yv[i][j];
+      } else {
+        store_f32(reinterpret_cast<float*>(p.aux_out), p.ld_aux, false);
+        __syncthreads();  // the LDS tile is rewritten below
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = act_fwd(acc[i][j][e], p.act);
+      }
     }
     store_f32(reinterpret_cast<float*>(p.C), p.ldc, p.accumulate != 0);
     return;
@@ -493,10 +514,10 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
           const int c = n0 + lcol(j) + 8 * g + 4 * h;
           if (row < M && c < N) {
             const uint2 f = *reinterpret_cast<const uint2*>(p.aux + (int64_t)row * p.ld_aux + c);
-            acc[i][j][4 * g + 0] *= act_grad(bf16_lo(f.x), p.act);
-            acc[i][j][4 * g + 1] *= act_grad(bf16_hi(f.x), p.act);
-            acc[i][j][4 * g + 2] *= act_grad(bf16_lo(f.y), p.act);
-            acc[i][j][4 * g + 3] *= act_grad(bf16_hi(f.y), p.act);
+            acc[i][j][4 * g + 0] *= act_factor(bf16_lo(f.x), p.act);
+            acc[i][j][4 * g + 1] *= act_factor(bf16_hi(f.x), p.act);
+            acc[i][j][4 * g + 2] *= act_factor(bf16_lo(f.y), p.act);
+            acc[i][j][4 * g + 3] *= act_factor(bf16_hi(f.y), p.act);
           }
         }
     }
@@ -532,10 +553,22 @@ __device__ __forceinline__ void gemm_tile(const Prob& p, int lin, __bf16* smem) 
         for (int g = 0; g < 4; ++g) {
           d[i][j][g][0] = pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]);
           d[i][j][g][1] = pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
-          acc[i][j][4 * g + 0] = act_fwd(bf16_lo(d[i][j][g][0]), p.act);
-          acc[i][j][4 * g + 1] = act_fwd(bf16_hi(d[i][j][g][0]), p.act);
-          acc[i][j][4 * g + 2] = act_fwd(bf16_lo(d[i][j][g][1]), p.act);
-          acc[i][j][4 * g + 3] = act_fwd(bf16_hi(d[i][j][g][1]), p.act);
+          if (p.act & ESGPT_ACT_DERIV) {  // act and act' of the bf16 pre-activation; act' is what gets stored
+            float gd[4], yd[4];
+            act_fwd_grad(bf16_lo(d[i][j][g][0]), p.act & 7, yd[0], gd[0]);
+            act_fwd_grad(bf16_hi(d[i][j][g][0]), p.act & 7, yd[1], gd[1]);
+            act_fwd_grad(bf16_lo(d[i][j][g][1]), p.act & 7, yd[2], gd[2]);
+            act_fwd_grad(bf16_hi(d[i][j][g][1]), p.act & 7, yd[3], gd[3]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = yd[e];
+            d[i][j][g][0] = pack_bf16x2(gd[0], gd[1]);
+            d[i][j][g][1] = pack_bf16x2(gd[2], gd[3]);
+          } else {
+            acc[i][j][4 * g + 0] = act_fwd(bf16_lo(d[i][j][g][0]), p.act);
+            acc[i][j][4 * g + 1] = act_fwd(bf16_hi(d[i][j][g][0]), p.act);
+            acc[i][j][4 * g + 2] = act_fwd(bf16_lo(d[i][j][g][1]), p.act);
+            acc[i][j][4 * g + 3] = act_fwd(bf16_hi(d[i][j][g][1]), p.act);
+          }
         }
     store_tile(d, p.aux_out, p.ld_aux);
     __syncthreads();  // the LDS tile is rewritten below
@@ -777,7 +810,36 @@ TileCfg dw_tile(int64_t T, int64_t in, int64_t out) {
   return wg > 3 * 256 ? TileCfg{2, 2} : TileCfg{1, 1};
 }
 
+// activation codes: 0 erf-GELU, 1 tanh-GELU, 2 ReLU, optionally | ESGPT_ACT_DERIV
+bool act_ok(int act) { return act >= 0 && (act & ~ESGPT_ACT_DERIV) <= 2; }
+
 int64_t n_tiles(int64_t M, int64_t N, TileCfg c) { return cdiv(M, 64 * c.fm) * cdiv(N, 64 * c.fn); }
+
+// Large-tile kernel (gemm_big.hip) for a bf16-output product: 256 or 128 output columns per 256-row tile, 0 = the
+// tile GEMM. Product rule (measured in the C3 training step, same box, profiles/r06_c3_big_ab.log): the plain-store
+// forward projections of wide layers (M >= 4096 tokens, K and N >= 512, no activation epilogue: C3's qkv, out_proj
+// and c_proj) on 256 x 128 tiles — 42 vs 50 us per launch in step; c_fc with its activation epilogue (two outputs of
+// 64 MB each) stays on the tile GEMM, whose 2-3 resident workgroups per CU overlap one tile's epilogue with another's
+// k-loop (80 vs 110 us); the backward (large-tile dX + split-K dW + slab reduction) lost to the grouped tile-GEMM
+// backward (about 440 vs 390 us per layer) and exists in the tools build only (ESGPT_GEMM_BIG = 0 / 128 / 256 forces
+// every eligible product there, fwd / dX / dW).
+int big_fwd_cols(int64_t M, int64_t N, int64_t K, bool act) {
+  static const int forced = [] {
+    const char* e = tuning_env("ESGPT_GEMM_BIG");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced == 0 || forced == 128 || forced == 256) return forced;
+  return (!act && M >= 4096 && K >= 512 && N >= 512) ? 128 : 0;
+}
+#ifdef ESGPT_TUNING_HOOKS
+// tools build: the large-tile backward (dX + split-K dW) when ESGPT_GEMM_BIG forces it
+int big_cols(int64_t M, int64_t N, int64_t K) {
+  const int f = big_fwd_cols(M, N, K, false);
+  return (f == 128 || f == 256) && tuning_env("ESGPT_GEMM_BIG") && M >= 4096 && K >= 512 && N >= 512 ? f : 0;
+}
+#else
+int big_cols(int64_t, int64_t, int64_t) { return 0; }
+#endif
 
 struct Plan {
   int splits, kchunk;
@@ -974,12 +1036,44 @@ int linear_bwd_impl(const void* dy, int64_t lddy, const void* x, int64_t ldx, co
   if (f32) {
     ESGPT_REQUIRE(shapes_ok_f32(false, false, dy, lddy, x, ldx, out, in, T, dw, in));
     if (has_dx) ESGPT_REQUIRE(shapes_ok_f32(true, false, dy, lddy, w, in, T, in, out, dx, lddx));
-    ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 16) == 0));
+    ESGPT_REQUIRE(act < 0 || (pre != nullptr && act_ok(act) && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 16) == 0));
   } else {
     ESGPT_REQUIRE(shapes_ok(false, false, dy, lddy, x, ldx, out, in, T, dw, in, true));
     if (has_dx) ESGPT_REQUIRE(shapes_ok(true, false, dy, lddy, w, in, T, in, out, dx, lddx, false));
-    ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2 && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
+    ESGPT_REQUIRE(act < 0 || (pre != nullptr && act_ok(act) && has_dx && ldpre % 4 == 0 && ((uintptr_t)pre % 8) == 0));
   }
+#ifdef ESGPT_TUNING_HOOKS
+  // tools build (ESGPT_GEMM_BIG): wide products: dX and dW (+ db) on the large-tile kernel, each its own launch (+ dW's slab reduction)
+  if (!f32 && !st_dw && big_cols(T, in, out)) {
+    const BigDw plan_w = big_dw_plan(T, in, out);
+    ESGPT_REQUIRE(workspace && workspace_bytes >= plan_w.slab_bytes && plan_w.slab_bytes < (1ull << 31));
+    Prob pw = make_prob(dy, lddy, x, ldx, out, in, T, dw, in, 1, 0, nullptr, alpha, 0, TileCfg{4, 4});
+    pw.rowsum = db;
+    pw.rs_extra = n_extra ? db_extra : nullptr;
+    pw.rs_extra_n = (int)n_extra;
+    pw.slab = reinterpret_cast<float*>(workspace);
+    if (has_dx) {
+      Prob px = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, 0, 0, nullptr, alpha, 0, TileCfg{4, 4});
+      if (act >= 0) {
+        px.epi = EPI_ACT_GRAD;
+        px.act = act;
+        px.aux = reinterpret_cast<const __bf16*>(pre);
+        px.ld_aux = ldpre;
+      }
+      if (px.fast && pw.fast && g_row_tiles == nullptr) {
+        launch_big(px, true, false, big_cols(T, in, out), st);
+        launch_big_dw(pw, st);
+        ESGPT_LAUNCH_CHECK();
+        return ESGPT_OK;
+      }
+    } else if (pw.fast) {
+      launch_big_dw(pw, st);
+      ESGPT_LAUNCH_CHECK();
+      return ESGPT_OK;
+    }
+    return ESGPT_ERR_UNSUPPORTED;  // operands past 2 GiB or a row-tile mask: not for these shapes
+  }
+#endif
   Prob p0{};
   if (has_dx) {
     p0 = make_prob(dy, lddy, w, in, T, in, out, dx, lddx, f32 ? 1 : 0, 0, nullptr, alpha, 0,
@@ -1080,6 +1174,17 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
   const TileCfg tc = fwd_form ? fwd_tile(M, N, K, false) : TileCfg{1, 1};
   Prob p = make_prob(A, lda, B, ldb, M, N, K, C, ldc, f32 ? 1 : 0, accumulate, bias, alpha, kTarget, tc);
   p.row_tiles = g_row_tiles;
+  // bf16-output products with A K-contiguous (the forward and input-gradient forms) on the large-tile kernel, which
+  // never splits K
+  const int big = akc && !f32 && !accumulate ? (bkc ? big_fwd_cols(M, N, K, false) : big_cols(M, N, K)) : 0;
+  if (big) {
+    Prob q = make_prob(A, lda, B, ldb, M, N, K, C, ldc, 0, 0, bias, alpha, 0, tc);
+    q.row_tiles = g_row_tiles;
+    if (launch_big(q, true, bkc, big, as_stream(stream))) {
+      ESGPT_LAUNCH_CHECK();
+      return ESGPT_OK;
+    }
+  }
   if (fwd_form && p.splits == 1) {
     if (const char* e = tuning_env("ESGPT_GEMM_DBG")) p.dbg = atoi(e);
     hipStream_t st = as_stream(stream);
@@ -1116,7 +1221,7 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
 int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64_t in, int64_t out,
                      const float* bias, int act, void* pre, void* y, int64_t ldy, void* stream) {
   ESGPT_REQUIRE(shapes_ok(true, true, x, ldx, w, in, T, out, in, y, ldy, false));
-  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2));
+  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act_ok(act)));
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
   if (T == 0 || out == 0) return ESGPT_OK;
@@ -1131,6 +1236,11 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
   }
   if (const char* e = tuning_env("ESGPT_GEMM_DBG")) p.dbg = atoi(e);
   hipStream_t st = as_stream(stream);
+  if (const int bn = big_fwd_cols(T, out, in, act >= 0))
+    if (launch_big(p, true, true, bn, st)) {
+      ESGPT_LAUNCH_CHECK();
+      return ESGPT_OK;
+    }
   switch (tc.fm * 10 + tc.fn) {
     case 21: launch_fwd<2, 1>(p, st); break;
     case 12: launch_fwd<1, 2>(p, st); break;
@@ -1143,7 +1253,13 @@ int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64
 
 size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx) {
   const TileCfg wc = dw_tile(T, in, out);
-  return slab_bytes(plan(out, in, T, dw_target(has_dx != 0, T, in, out), wc).splits, out, in, wc);
+  const size_t tile = slab_bytes(plan(out, in, T, dw_target(has_dx != 0, T, in, out), wc).splits, out, in, wc);
+  // (tools build, ESGPT_GEMM_BIG: the large-tile dW's split-K slabs; the split-stream form takes the tile kernel)
+#ifdef ESGPT_TUNING_HOOKS
+  return big_cols(T, in, out) ? std::max(tile, big_dw_plan(T, in, out).slab_bytes) : tile;
+#else
+  return tile;
+#endif
 }
 
 int esgpt_linear_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w, int64_t T, int64_t in,
@@ -1178,7 +1294,7 @@ int esgpt_linear_bwd_f32(const float* dy, int64_t lddy, const float* x, int64_t 
 int esgpt_linear_fwd_f32(const float* x, int64_t ldx, const float* w, int64_t T, int64_t in, int64_t out,
                          const float* bias, int act, float* pre, float* y, int64_t ldy, void* stream) {
   ESGPT_REQUIRE(shapes_ok_f32(true, true, x, ldx, w, in, T, out, in, y, ldy));
-  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act <= 2));
+  ESGPT_REQUIRE(act < 0 || (pre != nullptr && act_ok(act)));
   ESGPT_REQUIRE(bias == nullptr || ((uintptr_t)bias % 16) == 0);
   ESGPT_REQUIRE(pre == nullptr || ((uintptr_t)pre % 16) == 0);
   if (T == 0 || out == 0) return ESGPT_OK;

@@ -394,6 +394,18 @@ __device__ __forceinline__ float rowsum_extra(const Prob& p, int m) {
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
+// gemm_big.hip: launches the large-tile kernel (256 x bn tiles, 8 waves, LDS-DMA ring) for a bf16-output, unsplit
+// product with A K-contiguous (false: not applicable, caller launches)
+bool launch_big(Prob p, bool akc, bool bkc, int bn, hipStream_t st);
+// gemm_big.hip, tools build only: the weight-gradient form on the large-tile kernel (split-K slabs + a reduction
+// launch; measured slower than the grouped tile-GEMM backward in the C3 step)
+struct BigDw {
+  int bn, splits, kchunk;
+  size_t slab_bytes;
+};
+BigDw big_dw_plan(int64_t T, int64_t in, int64_t out);
+bool launch_big_dw(Prob p, hipStream_t st);
+
 // tools/lab/gemm_stream.hip (tools build only): launches the streamed-tile kernel for p when enabled and applicable (false: caller launches)
 bool launch_stream(const Prob& p, bool bkc, hipStream_t st);
 

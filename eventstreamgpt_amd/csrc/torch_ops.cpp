@@ -900,7 +900,9 @@ Tensor linear(const Tensor& x_, const Tensor& w, const optional<Tensor>& bias, a
 }
 
 // InnerMLP (transformer.py:378-391): pre = x·W_fcᵀ + b_fc, g = act(pre), y = g·W_projᵀ (+ b_proj when given).
-// Returns (y, pre, g); pre and g are kept for the backward.
+// Returns (y, act'(pre), g), kept for the backward: c_fc's epilogue stores the activation's derivative at the
+// pre-activation (ESGPT_ACT_DERIV) instead of the pre-activation, so c_proj's input-gradient epilogue multiplies
+// instead of evaluating act' (the forward evaluates the same normal density for act anyway).
 std::tuple<Tensor, Tensor, Tensor> mlp(const Tensor& x_, const Tensor& w_fc, const Tensor& w_pj, const Tensor& b_fc,
                                        const optional<Tensor>& b_pj, int64_t act, const Tensor& p_fc,
                                        const Tensor& p_pj, const Tensor& tickets,
@@ -908,7 +910,8 @@ std::tuple<Tensor, Tensor, Tensor> mlp(const Tensor& x_, const Tensor& w_fc, con
   const c10::DeviceGuard guard(x_.device());
   const RowTilesScope rts(row_tiles_, x_.size(0));
   Tensor x = x_.contiguous();
-  auto pg = linear_act(x, w_fc, b_fc, act);
+  TORCH_CHECK(act >= 0 && act <= 2, "mlp: act must be 0 (GELU), 1 (tanh GELU) or 2 (ReLU)");
+  auto pg = linear_act(x, w_fc, b_fc, act | ESGPT_ACT_DERIV);
   Tensor g = std::get<1>(pg);
   const int64_t T = g.size(0), F = g.size(1), D = w_pj.size(0);
   Tensor y = at::empty({T, D}, x.options());

@@ -46,6 +46,7 @@ from . import _lib as L
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 TORCH_LIB_PATH = os.environ.get("ESGPT_AMD_TORCH_LIB", os.path.join(_HERE, "libesgpt_torch.so"))
+ACT_DERIV = 8  # ESGPT_ACT_DERIV (include/esgpt_amd.h): the pre-activation buffer holds act'(pre)
 _state = {"loaded": False}
 
 OPS = ("embed_joint", "embed_split_bags", "embed_epilogue", "embed_epilogue_bwd", "embed_bag_bwd", "attention",
@@ -576,7 +577,8 @@ def _register():
         need_dbpj = ctx.has_bpj and ctx.needs_input_grad[4]
         ok = ctx.gp is not None
         gp = ctx.gp if ok else (None,) * 4
-        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act, pre, True, need_dbpj, split_ok=ctx.split_ok,
+        # `pre` holds act'(pre-activation) (esgpt::mlp stores it with ESGPT_ACT_DERIV): the dX epilogue multiplies
+        dz, dw_pj, db_pj = _linear_bwd(dy, g, w_pj, None, ctx.act | ACT_DERIV, pre, True, need_dbpj, split_ok=ctx.split_ok,
                                        dw_out=_dest(ok, [gp[1]]), db_out=_dest(ok and need_dbpj, [gp[3]]),
                                        row_tiles=ctx.row_tiles)
         need_dx = ctx.needs_input_grad[0]

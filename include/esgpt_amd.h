@@ -408,11 +408,16 @@ int esgpt_gemm_bf16(int a_layout, const void* A, int64_t lda, int b_layout, cons
  *   esgpt_linear_bwd_ex: the same plus n_extra f32 rows db_extra [n_extra, out] added into db before the alpha
  *     scaling, db = alpha·(Σ_rows dy + Σ_b db_extra[b]) — the generative head's bias gradient, whose position-0
  *     rows the loss kernel accumulates per subject (model_output.py:1253-1721; replaces a sum + scale + add).
+ *   act | ESGPT_ACT_DERIV (forward and backward together): `pre` carries the activation's DERIVATIVE at the
+ *     pre-activation, act'(pre) (computed in the forward's epilogue from the same bf16 / f32 pre-activation, beside
+ *     act(pre)), instead of pre itself; the backward multiplies by it. The transcendental work of act' moves into
+ *     the forward epilogue, which evaluates the same normal density for act anyway (InnerMLP: esgpt::mlp).
  *   esgpt_linear_bwd_split: esgpt_linear_bwd_ex as two launches on two streams: dx on `stream`; dw, db (and the
  *     split-K workspace / counters, which must not be shared with work on `stream`) on `stream_dw` after it waits
  *     for everything queued on `stream` before the call. The caller joins `stream_dw` back (an event wait) before
  *     reading dw / db. Same tiles and split plan as the grouped launch: bitwise equal results. The weight gradient
  *     then leaves backward's critical path (transformer.py:133-163, 378-391 Linear backward). */
+#define ESGPT_ACT_DERIV 8
 int esgpt_linear_fwd(const void* x, int64_t ldx, const void* w, int64_t T, int64_t in, int64_t out,
                      const float* bias, int act, void* pre, void* y, int64_t ldy, void* stream);
 size_t esgpt_linear_bwd_workspace(int64_t T, int64_t in, int64_t out, int has_dx);

@@ -476,12 +476,34 @@ def test_gemm_kernel(M, N, K, a_kc, b_kc):
     assert ((acc.double().cpu() - want).abs().max() / want.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(4100, 520, 520), (4352, 1032, 1000), (16384, 1536, 512), (4104, 2048, 2056)])
+def test_gemm_big_tiles(M, N, K):
+    """The large-tile kernel (gemm_big.hip: 256 x 128 / 256 x 256 tiles, 8 waves, LDS-DMA ring of 32-k stages) that
+    the wide forward products take (M >= 4096, K and N >= 512), with ragged row / column tiles and a partial last
+    k-stage, vs an f64 matmul of the same bf16 values (bf16 output + bias)."""
+    from eventstreamgpt_amd import _lib as L
+    from eventstreamgpt_amd.fused import _gemm
+
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).bfloat16()
+    b = torch.randn(N, K, generator=g).bfloat16()
+    bias = torch.randn(N, generator=g)
+    ref = a.double() @ b.double().t() + bias.double()
+    cb = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    _gemm(a.to(DEV), L.GEMM_K_CONTIG, K, b.to(DEV), L.GEMM_K_CONTIG, K, M, N, K, cb, bias=bias.to(DEV))
+    err = (cb.double().cpu() - ref).abs() / ref.abs().max()
+    assert err.max().item() < 1e-2, err.max().item()
+    # bf16 rounding of the output only: the mean error stays at the rounding level (a wrong k-stage would not)
+    assert err.mean().item() < 2e-3
+
+
 def _act_ref(z, act):
     F = torch.nn.functional
     return {0: F.gelu(z), 1: F.gelu(z, approximate="tanh"), 2: torch.relu(z)}[act]
 
 
-@pytest.mark.parametrize("T,din,dout", [(8192, 256, 1024), (520, 136, 72), (8, 8, 8), (300, 160, 1000)])
+@pytest.mark.parametrize("T,din,dout", [(8192, 256, 1024), (520, 136, 72), (8, 8, 8), (300, 160, 1000),
+                                        (4100, 520, 1032)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_linear_fwd_act(T, din, dout, act):
     """c_fc epilogue: pre = x·wᵀ + b (bf16) and y = act(pre) vs f64 references."""
@@ -498,8 +520,48 @@ def test_linear_fwd_act(T, din, dout, act):
     assert rel_err(y.cpu(), _act_ref(pre.double().cpu(), act)) < 1e-2
 
 
+@pytest.mark.parametrize("T,din,dout", [(520, 136, 72), (8192, 256, 1024), (4100, 520, 1032)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_linear_act_derivative_storage(T, din, dout, act, dtype):
+    """ESGPT_ACT_DERIV (the InnerMLP path, esgpt::mlp): the forward stores act'(pre) instead of pre beside the same
+    y = act(pre) (bitwise), and the backward that multiplies by the stored derivative equals the backward that
+    evaluates act'(pre) — to f32 rounding in f32 (the same formula, contracted into FMAs per call site), within the
+    derivative's bf16 rounding in bf16; plus the derivative vs an f64 reference of act' at the stored
+    pre-activation."""
+    from eventstreamgpt_amd.fused import linear_bwd, linear_fwd_act
+    from eventstreamgpt_amd.ops import ACT_DERIV
+
+    g = torch.Generator().manual_seed(T + din + dout + act)
+    x = torch.randn(T, din, generator=g).to(dtype).to(DEV)
+    w = (0.1 * torch.randn(dout, din, generator=g)).to(dtype).to(DEV)
+    b = torch.randn(dout, generator=g).to(DEV)
+    pre, y = linear_fwd_act(x, w, b, act)
+    der, y2 = linear_fwd_act(x, w, b, act | ACT_DERIV)
+    assert torch.equal(y, y2)
+    z = pre.double().cpu().requires_grad_(True)
+    want = torch.autograd.grad(_act_ref(z, act).sum(), z)[0]
+    assert (der.double().cpu() - want).abs().max().item() <= (1e-2 if dtype == torch.bfloat16 else 1e-5) * max(
+        1.0, want.abs().max().item())
+    dy = torch.randn(T, dout, generator=g).to(dtype).to(DEV)
+    w2 = (0.1 * torch.randn(dout, din, generator=g)).to(dtype).to(DEV)
+    # the backward of a projection whose INPUT is act(pre): dx = (dy·w2) · act'(pre) — here with `pre` of shape
+    # [T, dout] feeding a projection dout -> din2 = dout (square w3)
+    w3 = (0.1 * torch.randn(dout, dout, generator=g)).to(dtype).to(DEV)
+    dy3 = torch.randn(T, dout, generator=g).to(dtype).to(DEV)
+    a = linear_bwd(dy3, y, w3, act=act, pre=pre, need_dx=True, need_db=True)
+    d = linear_bwd(dy3, y, w3, act=act | ACT_DERIV, pre=der, need_dx=True, need_db=True)
+    assert torch.equal(a[1], d[1]) and torch.equal(a[2], d[2])  # dW, db do not involve the derivative
+    if dtype == torch.float32:  # the same f32 derivative up to the compiler's FMA contraction of its formula
+        assert rel_err(d[0].cpu(), a[0].double().cpu()) < 1e-6
+    else:
+        assert rel_err(d[0].cpu(), a[0].double().cpu()) < 1e-2
+    del dy, w2
+
+
 @pytest.mark.parametrize("T,din,dout", [(8192, 256, 256), (8192, 1024, 256), (8192, 256, 1624), (520, 136, 72),
-                                        (8, 8, 8), (0, 64, 32)])
+                                        (8, 8, 8), (0, 64, 32), (4100, 520, 600), (16390, 136, 72),
+                                        (4352, 2048, 512)])
 @pytest.mark.parametrize("act", [-1, 0, 2])
 @pytest.mark.parametrize("need_dx", [True, False])
 def test_linear_bwd(T, din, dout, act, need_dx):

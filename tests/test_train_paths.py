@@ -224,7 +224,7 @@ def test_replayed_losses_held_across_steps():
         ts.check()
         assert ts.use_graph
         assert all(e[4] == ("fused" if fuse is True else None) for e in ts.graphs.values() if e is not None)
-        return [float(x.reshape(())) for x in held], [p.detach().clone() for p in m.parameters()]
+        return [x if isinstance(x, float) else float(x.reshape(())) for x in held], [p.detach().clone() for p in m.parameters()]
 
     a, pa = run(True, False)
     for fuse in (True, "ring"):
