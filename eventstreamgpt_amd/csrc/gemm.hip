@@ -835,7 +835,7 @@ int big_fwd_cols(int64_t M, int64_t N, int64_t K, bool act) {
 // tools build: the large-tile backward (dX + split-K dW) when ESGPT_GEMM_BIG forces it
 int big_cols(int64_t M, int64_t N, int64_t K) {
   const int f = big_fwd_cols(M, N, K, false);
-  return (f == 128 || f == 256) && tuning_env("ESGPT_GEMM_BIG") && M >= 4096 && K >= 512 && N >= 512 ? f : 0;
+  return (f == 128 || f == 256) && tuning_env("ESGPT_GEMM_BIG") ? f : 0;
 }
 #else
 int big_cols(int64_t, int64_t, int64_t) { return 0; }

@@ -26,6 +26,7 @@
 // The swapped-operand MFMA form makes each lane own one output ROW (its registers hold 4 consecutive columns per
 // register group), as in gemm.hip.
 #include <algorithm>
+#include <cstdio>
 
 #include "common.h"
 #include "gemm_parts.h"
@@ -35,9 +36,7 @@ using namespace esgpt::gk;
 
 namespace {
 
-constexpr int BT = 512;   // threads per workgroup: 8 waves
-constexpr int SK = 32;    // k per stage
-constexpr int TBM = 256;  // tile rows
+constexpr int SK = 32;  // k per stage
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -64,15 +63,15 @@ __device__ __forceinline__ void lgkm_wait() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// One operand's stage image: R rows (m or n) x SK k, filled by LDS-DMA (8 waves).
-template <bool KC, int R>
+// One operand's stage image: R rows (m or n) x SK k, filled by LDS-DMA (NWV waves).
+template <bool KC, int R, int NWV>
 struct BTile {
   static constexpr int kElems = R * SK;
-  static constexpr int kInstr = kElems * 2 / 1024 / 8;  // 1-KiB DMA instructions per wave and stage
+  static constexpr int kInstr = kElems * 2 / 1024 / NWV;  // 1-KiB DMA instructions per wave and stage
   static constexpr int CPR = KC ? SK / 8 : R / 8;       // 16-B chunks per image row
   static constexpr int RPI = 64 / CPR;                  // image rows per instruction
   static constexpr int kReads = KC ? 1 : 2;             // LDS read instructions per fragment
-  static_assert(kInstr >= 1 && kInstr * 8 * 512 == kElems, "tile rows");
+  static_assert(kInstr >= 1 && kInstr * NWV * 512 == kElems, "tile rows");
   static constexpr int kOOB = (int)0x80000000u;
 
   __device__ __forceinline__ static int sw(int row) { return KC ? ((row >> 2) & 3) : 4 * (row & 3); }
@@ -81,7 +80,7 @@ struct BTile {
   }
   __device__ __forceinline__ static void coords(int i, int& row, int& lg) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    row = (wave + 8 * i) * RPI + lane / CPR;
+    row = (wave + NWV * i) * RPI + lane / CPR;
     lg = (lane % CPR) ^ sw(row);
   }
   // per-lane source byte offsets (row0 = the tile's first m / n, nrows = the operand's m / n extent); rows / columns
@@ -108,7 +107,7 @@ struct BTile {
         coords(i, row, lg);
         if ((KC ? lg * 8 : row) >= kvalid) v = kOOB;
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave + 8 * i) * 512), 16, v, so, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(img + (wave + NWV * i) * 512), 16, v, so, 0, 0);
     }
   }
   // MFMA operand fragment of rows sub0 .. sub0 + 31, k-step t (k = 16t .. 16t + 15): lane (r, h) gets row sub0 + r,
@@ -142,16 +141,20 @@ __device__ __forceinline__ void group_tile(int t, int tm, int tn, int& by, int& 
   bx = in / gs;
 }
 
-template <bool AKC, bool BKC, int BN, int NSLOT>
+// Tile TM x BN on NWV waves (8: two per SIMD, one workgroup per CU; 4: one per SIMD, 2-3 workgroups per CU). Wave
+// grid WM x WN: 8 waves as 2 x 4 (4 x 2 for the 256 x 128 tile), 4 waves as 2 x 2.
+template <bool AKC, bool BKC, int TM, int BN, int NWV, int NSLOT>
 struct BigCfg {
-  using TA = BTile<AKC, TBM>;
-  using TB = BTile<BKC, BN>;
-  static constexpr int WN = BN == 256 ? 4 : 2, WM = 8 / WN;  // wave grid
-  static constexpr int FM = TBM / 32 / WM, FN = BN / 32 / WN;  // fragments per wave
+  static constexpr int BT = 64 * NWV;
+  using TA = BTile<AKC, TM, NWV>;
+  using TB = BTile<BKC, BN, NWV>;
+  static constexpr int WN = NWV == 8 ? ((TM == 256 && BN == 128) ? 2 : 4) : 2, WM = NWV / WN;  // wave grid
+  static constexpr int FM = TM / 32 / WM, FN = BN / 32 / WN;  // fragments per wave
+  static_assert(FM >= 1 && FN >= 1 && FM * 32 * WM == TM && FN * 32 * WN == BN, "wave grid");
   static constexpr int STAGE = TA::kElems + TB::kElems;         // bf16 elements per ring slot
   static constexpr int P = TA::kInstr + TB::kInstr;             // DMA instructions per wave and stage
   static constexpr int RING = NSLOT * STAGE;
-  static constexpr int EPI = 128 * (BN + 4) * 2;               // bf16 elements of a 128-row f32 C half-tile
+  static constexpr int EPI = (TM > 128 ? 128 : TM) * (BN + 4) * 2;  // bf16 elements of an f32 C tile (half)
   static constexpr int LDS = RING > EPI ? RING : EPI;           // bf16 elements
   static constexpr int NR = FM * TA::kReads + FN * TB::kReads;  // LDS read instructions per k-step
   static_assert(NSLOT >= 3 && NSLOT <= 6 && (NSLOT - 1) * P < 64, "ring");
@@ -162,13 +165,13 @@ struct BigCfg {
 // tokens each): the f32 partial tile goes to a slab in fragment order (every wave-instruction a contiguous 1 KiB)
 // and the bias gradient's row sums (one extra MFMA against a ones operand per k-step, spread over the waves of the
 // tile's first column block) to the row-sum slab; big_slab_reduce_kernel sums the slabs.
-template <bool AKC, bool BKC, int BN, int NSLOT, bool DW = false>
-__global__ __launch_bounds__(BT) void gemm_big_kernel(Prob p) {
-  using C = BigCfg<AKC, BKC, BN, NSLOT>;
+template <bool AKC, bool BKC, int TM, int BN, int NWV, int NSLOT, bool DW = false>
+__global__ __launch_bounds__(64 * NWV) void gemm_big_kernel(Prob p) {
+  using C = BigCfg<AKC, BKC, TM, BN, NWV, NSLOT>;
+  constexpr int BT = C::BT;
   using TA = typename C::TA;
   using TB = typename C::TB;
   constexpr int FM = C::FM, FN = C::FN, WN = C::WN, P = C::P, STAGE = C::STAGE;
-  static_assert(!DW || FM == WN, "row-sum fragments: one per wave of a wave row");
   __shared__ __attribute__((aligned(16))) __bf16 smem[C::LDS];
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
@@ -178,11 +181,12 @@ __global__ __launch_bounds__(BT) void gemm_big_kernel(Prob p) {
   int bx, by;
   group_tile(tile, p.tm, p.tn, by, bx);
   const int M = p.M, N = p.N;
-  const int m0 = by * TBM, n0 = bx * BN;
+  const int m0 = by * TM, n0 = bx * BN;
   const int kb = DW ? bz * p.kchunk : 0, ke = DW ? min(p.K, kb + p.kchunk) : p.K;
   const int ns = ke > kb ? (ke - kb + SK - 1) / SK : 0;
   const bool want_rs = DW && p.rowsum != nullptr && bx == 0;  // workgroup-uniform
 
+  static_assert(!DW || FM <= WN, "row sums: at most one fragment row per wave");
   f32x16 acc[FM][FN], racc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
@@ -239,7 +243,7 @@ __global__ __launch_bounds__(BT) void gemm_big_kernel(Prob p) {
 #pragma unroll
         for (int b = 0; b < FN; ++b) acc[a][b] = mfma(bfr[b], af[a], acc[a][b]);
         if constexpr (RS)
-          if (a == wn) racc = mfma(ones, af[a], racc);  // a == wn: wave-uniform, one fragment per wave
+          if (a == wn) racc = mfma(ones, af[a], racc);  // wave-uniform: fragment row a on wave column a
       }
     };
     const int pro = min(NSLOT, ns);
@@ -276,14 +280,14 @@ __global__ __launch_bounds__(BT) void gemm_big_kernel(Prob p) {
       for (int b = 0; b < FN; ++b)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int64_t idx = 4 * (((((int64_t)bz * ntile + tile) * 8 + wave) * (FM * FN) + a * FN + b) * 4 + g) * 64 +
+          const int64_t idx = 4 * (((((int64_t)bz * ntile + tile) * NWV + wave) * (FM * FN) + a * FN + b) * 4 + g) * 64 +
                               4 * lane;
           *reinterpret_cast<float4*>(p.slab + idx) =
               make_float4(acc[a][b][4 * g], acc[a][b][4 * g + 1], acc[a][b][4 * g + 2], acc[a][b][4 * g + 3]);
         }
-    if (want_rs && h == 0) {
+    if (want_rs && h == 0 && wn < FM) {  // fragment row a = wn
       const int row = m0 + wm * 32 * FM + 32 * wn + r;
-      if (row < M) p.slab[(int64_t)p.splits * ntile * TBM * BN + (int64_t)bz * M + row] = racc[0];
+      if (row < M) p.slab[(int64_t)p.splits * ntile * TM * BN + (int64_t)bz * M + row] = racc[0];
     }
     return;
   }
@@ -299,8 +303,8 @@ __global__ __launch_bounds__(BT) void gemm_big_kernel(Prob p) {
   auto lcol = [&](int b) { return wn * 32 * FN + 32 * b; };
   const float al = p.alpha ? *p.alpha : 1.f;
   constexpr int kLd = BN + 4;                                     // f32 row pitch
-  constexpr int ROWS_PASS = (TBM * kLd * 4 <= C::LDS * 2) ? TBM : TBM / 2;
-  constexpr int NPASS = TBM / ROWS_PASS;
+  constexpr int ROWS_PASS = (TM * kLd * 4 <= C::LDS * 2) ? TM : TM / 2;
+  constexpr int NPASS = TM / ROWS_PASS;
   static_assert(ROWS_PASS * kLd * 4 <= C::LDS * 2, "f32 epilogue tile");
   float* tf = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -392,21 +396,22 @@ __global__ __launch_bounds__(BT) void gemm_big_kernel(Prob p) {
 // Split-K reduction of the weight-gradient form: thread = one 16-B chunk of the fragment-order slab (tile, wave,
 // fragment, register group, lane), summing its splits in split order (deterministic), then alpha, stored as 4
 // columns of dW; threads past the tiles sum the row-sum slabs into the bias gradient (+ the optional extra rows).
-template <int BN>
+template <int TM, int BN, int NWV>
 __global__ __launch_bounds__(256) void big_slab_reduce_kernel(Prob p) {
-  constexpr int WN = BN == 256 ? 4 : 2, FM = TBM / 32 / (8 / WN), FN = BN / 32 / WN, F = FM * FN;
-  const int64_t ntile = (int64_t)p.tm * p.tn, nch = ntile * TBM * BN / 4;
+  using C = BigCfg<false, false, TM, BN, NWV, 4>;
+  constexpr int WN = C::WN, FM = C::FM, FN = C::FN, F = FM * FN;
+  const int64_t ntile = (int64_t)p.tm * p.tn, nch = ntile * TM * BN / 4;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float al = p.alpha ? *p.alpha : 1.f;
   if (t < nch) {
     const int lane = (int)(t & 63), g = (int)((t >> 6) & 3);
     const int64_t wf = t >> 8;  // (tile, wave, fragment)
-    const int f = (int)(wf % F), wave = (int)((wf / F) & 7);
-    const int64_t tile = wf / F / 8;
+    const int f = (int)(wf % F), wave = (int)((wf / F) % NWV);
+    const int64_t tile = wf / F / NWV;
     int bx, by;
     group_tile((int)tile, p.tm, p.tn, by, bx);
     const int wm = wave / WN, wn = wave % WN, a = f / FN, b = f % FN;
-    const int row = by * TBM + wm * 32 * FM + 32 * a + (lane & 31);
+    const int row = by * TM + wm * 32 * FM + 32 * a + (lane & 31);
     const int col = bx * BN + wn * 32 * FN + 32 * b + 8 * g + 4 * (lane >> 5);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr int kU = 8;
@@ -440,9 +445,9 @@ __global__ __launch_bounds__(256) void big_slab_reduce_kernel(Prob p) {
 
 #endif
 
-template <bool AKC, bool BKC, int BN, int NSLOT>
+template <bool AKC, bool BKC, int TM, int BN, int NWV, int NSLOT>
 void launch_t(const Prob& p, hipStream_t st) {
-  gemm_big_kernel<AKC, BKC, BN, NSLOT><<<dim3((unsigned)(p.tm * p.tn)), BT, 0, st>>>(p);
+  gemm_big_kernel<AKC, BKC, TM, BN, NWV, NSLOT><<<dim3((unsigned)(p.tm * p.tn)), 64 * NWV, 0, st>>>(p);
 }
 
 }  // namespace
@@ -452,32 +457,65 @@ namespace gk {
 
 // Large-tile form of a bf16-output, unsplit product (the forward projections: A and B K-contiguous; the input
 // gradients: B M/N-contiguous). bn = 256 or 128 output columns per tile; p's tile grid is set here.
+#ifdef ESGPT_TUNING_HOOKS
+// tools build: a tile configuration "TM,BN,NWV" from the environment (0 = not set), read once per variable
+struct BigTile {
+  int tm, bn, nwv;
+};
+static BigTile env_tile_big(const char* name) {
+  BigTile t{0, 0, 0};
+  if (const char* e = tuning_env(name)) sscanf(e, "%d,%d,%d", &t.tm, &t.bn, &t.nwv);
+  return t;
+}
+// the configurations compiled into the tools build
+template <bool AKC, bool BKC, bool DW = false>
+static bool launch_cfg(const Prob& p, BigTile t, unsigned grid, hipStream_t st) {
+#define ESGPT_BIG_CFG(TM_, BN_, NW_)                                                              \
+  if (t.tm == TM_ && t.bn == BN_ && t.nwv == NW_) {                                              \
+    gemm_big_kernel<AKC, BKC, TM_, BN_, NW_, 4, DW><<<grid, 64 * NW_, 0, st>>>(p);                \
+    return true;                                                                                 \
+  }
+  ESGPT_BIG_CFG(256, 256, 8)
+  ESGPT_BIG_CFG(256, 128, 8)
+  ESGPT_BIG_CFG(128, 128, 8)
+  ESGPT_BIG_CFG(128, 256, 8)
+  ESGPT_BIG_CFG(128, 128, 4)
+  ESGPT_BIG_CFG(64, 128, 4)
+  ESGPT_BIG_CFG(64, 64, 4)
+#undef ESGPT_BIG_CFG
+  return false;
+}
+#endif
+
 bool launch_big(Prob p, bool akc, bool bkc, int bn, hipStream_t st) {
   if (!akc || p.out_f32 || p.splits != 1 || !p.fast || p.row_tiles || p.accumulate) return false;
   if (bn != 256 && bn != 128) return false;
-  p.fm = TBM / 64;
+  int tm = 256;
+#ifdef ESGPT_TUNING_HOOKS
+  static const BigTile forced = env_tile_big("ESGPT_GEMM_BIG_TILE");  // e.g. "64,128,4"
+  if (forced.tm) {
+    tm = forced.tm;
+    bn = forced.bn;
+  }
+#endif
+  p.fm = tm / 64;
   p.fn = bn / 64;
-  p.tm = (int)cdiv(p.M, TBM);
+  p.tm = (int)cdiv(p.M, tm);
   p.tn = (int)cdiv(p.N, bn);
 #ifdef ESGPT_TUNING_HOOKS
-  static const int slots = [] {  // ring slots of the 256 x 128 tile (tools build: ESGPT_GEMM_BIG_SLOTS = 6)
-    const char* e = tuning_env("ESGPT_GEMM_BIG_SLOTS");
-    return e ? atoi(e) : 4;
-  }();
-  if (bn == 128 && slots == 6) {
-    if (bkc) launch_t<true, true, 128, 6>(p, st);
-    else launch_t<true, false, 128, 6>(p, st);
-    return true;
+  if (forced.tm) {
+    const unsigned grid = (unsigned)(p.tm * p.tn);
+    return bkc ? launch_cfg<true, true>(p, forced, grid, st) : launch_cfg<true, false>(p, forced, grid, st);
   }
 #endif
   if (bkc) {
-    if (bn == 256) launch_t<true, true, 256, 4>(p, st);
-    else launch_t<true, true, 128, 4>(p, st);
+    if (bn == 256) launch_t<true, true, 256, 256, 8, 4>(p, st);
+    else launch_t<true, true, 256, 128, 8, 4>(p, st);
     return true;
   }
 #ifdef ESGPT_TUNING_HOOKS  // the input-gradient form (B M/N-contiguous): tools build only (measured slower in step)
-  if (bn == 256) launch_t<true, false, 256, 4>(p, st);
-  else launch_t<true, false, 128, 4>(p, st);
+  if (bn == 256) launch_t<true, false, 256, 256, 8, 4>(p, st);
+  else launch_t<true, false, 256, 128, 8, 4>(p, st);
   return true;
 #else
   return false;
@@ -485,25 +523,30 @@ bool launch_big(Prob p, bool akc, bool bkc, int bn, hipStream_t st) {
 }
 
 #ifdef ESGPT_TUNING_HOOKS
-// The weight-gradient plan: tile width (256 when the 256 x 256 grid has at least 8 tiles), split count (about one
-// workgroup per CU, every split at least kMinChunk tokens: fewer splits, less slab traffic) and the slab bytes.
+// The weight-gradient plan: tile (256 x 256 when that grid has at least 8 tiles, else 256 x 128; ESGPT_GEMM_BIG_DWTILE
+// forces "TM,BN,NWV"), split count (about one workgroup per CU, every split at least kMinChunk tokens: fewer splits,
+// less slab traffic) and the slab bytes.
 constexpr int kMinChunk = 1024;
 BigDw big_dw_plan(int64_t T, int64_t in, int64_t out) {
+  static const BigTile forced = env_tile_big("ESGPT_GEMM_BIG_DWTILE");
   BigDw d{};
-  d.bn = cdiv(out, TBM) * cdiv(in, 256) >= 8 ? 256 : 128;
-  const int64_t tiles = cdiv(out, TBM) * cdiv(in, d.bn);
-  // few tiles (a square-ish [out, in] of 512 x 512): chunks down to half the usual length
+  d.tm = forced.tm ? forced.tm : 256;
+  d.nwv = forced.tm ? forced.nwv : 8;
+  d.bn = forced.tm ? forced.bn : (cdiv(out, 256) * cdiv(in, 256) >= 8 ? 256 : 128);
+  const int64_t tiles = cdiv(out, d.tm) * cdiv(in, d.bn);
   static const int forced_chunk = [] {  // tools build: ESGPT_GEMM_BIG_DWCHUNK = minimum tokens per split
     const char* e = tuning_env("ESGPT_GEMM_BIG_DWCHUNK");
     return e ? atoi(e) : 0;
   }();
+  // few tiles (a square-ish [out, in] of 512 x 512): chunks down to half the usual length
   const int64_t min_chunk =
       forced_chunk > 0 ? forced_chunk : (tiles * (T / kMinChunk) < 256 ? kMinChunk / 2 : kMinChunk);
-  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(256, tiles), T / min_chunk));
-  const int64_t chunk = cdiv(cdiv(T, splits), SK) * SK;
-  d.splits = (int)cdiv(T, chunk);
+  const int64_t target = forced.nwv == 4 ? 768 : 256;  // 4-wave workgroups: about three per CU
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(cdiv(target, tiles), T / min_chunk));
+  const int64_t chunk = std::max<int64_t>(SK, cdiv(cdiv(T, splits), SK) * SK);
+  d.splits = (int)std::max<int64_t>(1, cdiv(T, chunk));
   d.kchunk = (int)chunk;
-  d.slab_bytes = sizeof(float) * ((size_t)d.splits * tiles * TBM * d.bn + (size_t)d.splits * out);
+  d.slab_bytes = sizeof(float) * ((size_t)d.splits * tiles * d.tm * d.bn + (size_t)d.splits * out);
   return d;
 }
 
@@ -513,21 +556,27 @@ BigDw big_dw_plan(int64_t T, int64_t in, int64_t out) {
 bool launch_big_dw(Prob p, hipStream_t st) {
   if (!p.fast || p.accumulate || p.slab == nullptr) return false;
   const BigDw d = big_dw_plan(p.K, p.N, p.M);
-  p.fm = TBM / 64;
+  p.fm = d.tm / 64;
   p.fn = d.bn / 64;
-  p.tm = (int)cdiv(p.M, TBM);
+  p.tm = (int)cdiv(p.M, d.tm);
   p.tn = (int)cdiv(p.N, d.bn);
   p.splits = d.splits;
   p.kchunk = d.kchunk;
   const unsigned grid = (unsigned)((int64_t)p.tm * p.tn * p.splits);
-  const int64_t nred = (int64_t)p.tm * p.tn * TBM * d.bn / 4 + (p.rowsum ? p.M : 0);
-  if (d.bn == 256) {
-    gemm_big_kernel<false, false, 256, 4, true><<<grid, BT, 0, st>>>(p);
-    big_slab_reduce_kernel<256><<<(unsigned)cdiv(nred, 256), 256, 0, st>>>(p);
-  } else {
-    gemm_big_kernel<false, false, 128, 4, true><<<grid, BT, 0, st>>>(p);
-    big_slab_reduce_kernel<128><<<(unsigned)cdiv(nred, 256), 256, 0, st>>>(p);
-  }
+  const int64_t nred = (int64_t)p.tm * p.tn * d.tm * d.bn / 4 + (p.rowsum ? p.M : 0);
+  const BigTile t{d.tm, d.bn, d.nwv};
+  if (!launch_cfg<false, false, true>(p, t, grid, st)) return false;
+  const unsigned rg = (unsigned)cdiv(nred, 256);
+#define ESGPT_BIG_RED(TM_, BN_, NW_) \
+  if (d.tm == TM_ && d.bn == BN_ && d.nwv == NW_) big_slab_reduce_kernel<TM_, BN_, NW_><<<rg, 256, 0, st>>>(p);
+  ESGPT_BIG_RED(256, 256, 8)
+  ESGPT_BIG_RED(256, 128, 8)
+  ESGPT_BIG_RED(128, 128, 8)
+  ESGPT_BIG_RED(128, 256, 8)
+  ESGPT_BIG_RED(128, 128, 4)
+  ESGPT_BIG_RED(64, 128, 4)
+  ESGPT_BIG_RED(64, 64, 4)
+#undef ESGPT_BIG_RED
   return true;
 }
 

@@ -400,7 +400,7 @@ bool launch_big(Prob p, bool akc, bool bkc, int bn, hipStream_t st);
 // gemm_big.hip, tools build only: the weight-gradient form on the large-tile kernel (split-K slabs + a reduction
 // launch; measured slower than the grouped tile-GEMM backward in the C3 step)
 struct BigDw {
-  int bn, splits, kchunk;
+  int tm, bn, nwv, splits, kchunk;
   size_t slab_bytes;
 };
 BigDw big_dw_plan(int64_t T, int64_t in, int64_t out);
