@@ -702,6 +702,9 @@ def main():
                     "end of the step's graph (TrainStep fuse_optimizer; measured neutral on C2, off by default)")
     ap.add_argument("--no-check-errors", action="store_true", help="measurement hook: TrainStep(check_errors=False) "
                     "(no per-step error-word hand-off to the host)")
+    ap.add_argument("--err-copy", action="store_true", help="measurement hook: each step's error words copied to "
+                    "pinned host memory by a D2H copy on the compute stream (round 5) instead of written by the "
+                    "optimizer launch into mapped host memory")
     ap.add_argument("--loss-pack", action="store_true", help="measurement hook: the replayed step's loss copy "
                     "made by its own pack launch instead of riding in the optimizer's prepare launch")
     ap.add_argument("--row-tiles", action="store_true", help="measurement hook: the dependency-graph projections "
@@ -743,6 +746,10 @@ def main():
         from eventstreamgpt_amd import train as _train
 
         _train.LOSS_IN_OPT = False
+    if args.err_copy:
+        from eventstreamgpt_amd import train as _train
+
+        _train.HOST_ERROR_WORDS = False
     if args.row_tiles:
         from eventstreamgpt_amd import fused
 

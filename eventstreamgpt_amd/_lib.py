@@ -85,7 +85,9 @@ SIGNATURES = {
     "esgpt_adamw_prepare_ex": (_int, [_vp, _vp, _int, _int, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp,
                                       _vp, _i64, _vp, _vp, _i64, _vp]),
     "esgpt_adamw_prepare_tab": (_int, [_vp, _vp, _int, _int, _vp, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp,
-                                       _vp, _i64, _vp, _vp, _i64, _vp]),
+                                       _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
+    "esgpt_host_words_alloc": (_int, [_i64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]),
+    "esgpt_host_words_free": (_int, [_vp]),
     "esgpt_adamw_dev": (_int, [_vp, _vp, _i64, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _vp]),
     "esgpt_device_arch_ok": (_int, []),
     "esgpt_pack": (_int, [_vp, _i64, _vp]),

@@ -83,13 +83,15 @@ __global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict_
                                                             const float* __restrict__ copy_src, int n_copy,
                                                             float* __restrict__ ring,
                                                             float* const* __restrict__ ring_tab,
-                                                            int64_t* __restrict__ ring_ctr, int64_t ring_len) {
+                                                            int64_t* __restrict__ ring_ctr, int64_t ring_len,
+                                                            int32_t* __restrict__ host_words) {
   // The step's hand-off entry riding in this launch, whatever the error state: copy_src (the replayed step's loss,
   // which the next replay overwrites) and the error block's four words, into ring entry ring_ctr % ring_len (stride
   // round_up(n_copy, 4) + 4 floats; the error words 16-B aligned at round_up(n_copy, 4)); the counter then advances.
   // With ring_tab the entries are separate allocations reached through a device table of ring_len pointers (the
   // caller may swap an entry's allocation between launches: a returned loss the caller still holds is never
-  // overwritten).
+  // overwritten). host_words (coherent, mapped host memory, ring_len x 4 words): the error words also land there,
+  // so the host reads them after the step's event without a D2H copy launch.
   if (ring != nullptr || ring_tab != nullptr) {
     const int body = (n_copy + 3) & ~3;
     const int64_t slot = ring_ctr ? *ring_ctr % ring_len : 0;
@@ -97,7 +99,9 @@ __global__ __launch_bounds__(256) void adamw_prepare_kernel(int64_t* __restrict_
     for (int i = threadIdx.x; i < n_copy; i += blockDim.x) e[i] = copy_src[i];
     if (threadIdx.x < 4) {
       int32_t* ew = reinterpret_cast<int32_t*>(e + body);
-      ew[threadIdx.x] = err ? err[threadIdx.x] : 0;
+      const int32_t v = err ? err[threadIdx.x] : 0;
+      ew[threadIdx.x] = v;
+      if (host_words) host_words[slot * 4 + threadIdx.x] = v;
     }
     __syncthreads();  // every thread has read the counter before it advances
     if (ring_ctr && threadIdx.x == 0) *ring_ctr += 1;
@@ -254,18 +258,19 @@ int esgpt_adamw_prepare(int64_t* counters, const int32_t* active, int n_active, 
 static int adamw_prepare_impl(int64_t* counters, const int32_t* active, int n_active, int n_params,
                               const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
                               float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy, float* ring,
-                              float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, void* stream) {
+                              float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, int32_t* host_words,
+                              void* stream) {
   ESGPT_REQUIRE(counters && sched && per_tensor && lr_out && n_active >= 0 && n_params >= 0);
   ESGPT_REQUIRE(n_active == 0 || active);
   ESGPT_REQUIRE(!(ring && ring_tab));
   ESGPT_REQUIRE(n_copy >= 0 && n_copy <= 1024 && ring_len >= 1 && (n_copy == 0 || (copy_src && (ring || ring_tab))) &&
                 (ring || ring_tab || !ring_ctr) && (reinterpret_cast<uintptr_t>(ring) & 15) == 0 &&
-                (reinterpret_cast<uintptr_t>(ring_tab) & 7) == 0);
+                (reinterpret_cast<uintptr_t>(ring_tab) & 7) == 0 && (!host_words || ring_ctr));
   ESGPT_REQUIRE(sched->kind == 0 || (sched->kind == 1 && sched->init_lr > sched->end_lr && sched->total >= sched->warmup));
   esgpt::adamw_prepare_kernel<<<1, 256, 0, esgpt::as_stream(stream)>>>(counters, active, n_active, n_params, *sched,
                                                                        beta1, beta2, per_tensor, lr_out, err,
                                                                        copy_src, (int)n_copy, ring, ring_tab,
-                                                                       ring_ctr, ring_len);
+                                                                       ring_ctr, ring_len, host_words);
   ESGPT_LAUNCH_CHECK();
   return ESGPT_OK;
 }
@@ -275,16 +280,40 @@ int esgpt_adamw_prepare_ex(int64_t* counters, const int32_t* active, int n_activ
                            float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy, float* ring,
                            int64_t* ring_ctr, int64_t ring_len, void* stream) {
   return adamw_prepare_impl(counters, active, n_active, n_params, sched, beta1, beta2, per_tensor, lr_out, err,
-                            copy_src, n_copy, ring, nullptr, ring_ctr, ring_len, stream);
+                            copy_src, n_copy, ring, nullptr, ring_ctr, ring_len, nullptr, stream);
 }
 
 int esgpt_adamw_prepare_tab(int64_t* counters, const int32_t* active, int n_active, int n_params,
                             const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
                             float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy,
-                            float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, void* stream) {
+                            float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, int32_t* host_words,
+                            void* stream) {
   ESGPT_REQUIRE(ring_tab != nullptr);
   return adamw_prepare_impl(counters, active, n_active, n_params, sched, beta1, beta2, per_tensor, lr_out, err,
-                            copy_src, n_copy, nullptr, ring_tab, ring_ctr, ring_len, stream);
+                            copy_src, n_copy, nullptr, ring_tab, ring_ctr, ring_len, host_words, stream);
+}
+
+// Coherent, device-mapped host memory for esgpt_adamw_prepare_tab's host_words (GPU stores reach host memory
+// without a cache flush or a copy launch; the host reads them once the step's event has completed).
+int esgpt_host_words_alloc(int64_t bytes, void** host, void** dev) {
+  ESGPT_REQUIRE(bytes > 0 && host && dev);
+  void* p = nullptr;
+  if (hipHostMalloc(&p, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess || !p)
+    return ESGPT_ERR_LAUNCH;
+  memset(p, 0, (size_t)bytes);
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess || !d) {
+    (void)hipHostFree(p);
+    return ESGPT_ERR_LAUNCH;
+  }
+  *host = p;
+  *dev = d;
+  return ESGPT_OK;
+}
+
+int esgpt_host_words_free(void* host) {
+  if (host == nullptr) return ESGPT_OK;
+  return hipHostFree(host) == hipSuccess ? ESGPT_OK : ESGPT_ERR_LAUNCH;
 }
 
 int esgpt_adamw_dev(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, const float* lr_dev,

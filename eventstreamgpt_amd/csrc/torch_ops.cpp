@@ -994,7 +994,8 @@ void adamw_dev(const Tensor& table, const Tensor& blocks, const Tensor& counters
                int64_t n_params, int64_t kind, int64_t warmup, int64_t total, double power, double init_lr,
                double end_lr, double beta1, double beta2, double eps, double wd, const Tensor& per_tensor,
                const Tensor& lr_dev, const Tensor& err, const optional<Tensor>& copy_src,
-               const optional<Tensor>& ring, const optional<Tensor>& ring_ctr, const optional<Tensor>& ring_tab) {
+               const optional<Tensor>& ring, const optional<Tensor>& ring_ctr, const optional<Tensor>& ring_tab,
+               int64_t host_words) {
   const c10::DeviceGuard guard(table.device());
   TORCH_CHECK(counters.scalar_type() == at::kLong && counters.numel() == n_params + 1, "adamw_dev: counters");
   const bool tb = ring_tab.has_value() && ring_tab->defined();
@@ -1004,6 +1005,7 @@ void adamw_dev(const Tensor& table, const Tensor& blocks, const Tensor& counters
   const int64_t n_copy = cp ? copy_src->numel() : 0;
   TORCH_CHECK(!cp || rg || tb, "adamw_dev: copy_src needs a ring");
   TORCH_CHECK(!(rg && tb), "adamw_dev: ring and ring_tab are exclusive");
+  TORCH_CHECK(host_words == 0 || (tb && rc), "adamw_dev: host_words needs ring_tab and ring_ctr");
   if (tb)
     TORCH_CHECK(ring_tab->scalar_type() == at::kLong && ring_tab->dim() == 1 && ring_tab->is_contiguous() &&
                     ring_tab->numel() >= 1 && (!rc || (ring_ctr->scalar_type() == at::kLong && ring_ctr->numel() == 1)),
@@ -1025,7 +1027,8 @@ void adamw_dev(const Tensor& table, const Tensor& blocks, const Tensor& counters
                                   ptr<float>(lr_dev), ptr<const int32_t>(err),
                                   cp ? ptr<const float>(*copy_src) : nullptr, n_copy,
                                   reinterpret_cast<float* const*>(ring_tab->data_ptr()),
-                                  rc ? ptr<int64_t>(*ring_ctr) : nullptr, ring_tab->numel(), st),
+                                  rc ? ptr<int64_t>(*ring_ctr) : nullptr, ring_tab->numel(),
+                                  reinterpret_cast<int32_t*>(static_cast<uintptr_t>(host_words)), st),
           "adamw_prepare_tab");
   else
     check(esgpt_adamw_prepare_ex(ptr<int64_t>(counters), active.numel() ? ptr<const int32_t>(active) : nullptr,
@@ -1109,7 +1112,7 @@ TORCH_LIBRARY(esgpt, m) {
   m.def("adamw_dev(Tensor table, Tensor blocks, Tensor(a!) counters, Tensor active, int n_params, int kind, "
         "int warmup, int total, float power, float init_lr, float end_lr, float beta1, float beta2, float eps, "
         "float weight_decay, Tensor(b!) per_tensor, Tensor(c!) lr_dev, Tensor err, Tensor? copy_src=None, "
-        "Tensor(d!)? ring=None, Tensor(e!)? ring_ctr=None, Tensor? ring_tab=None) -> ()");
+        "Tensor(d!)? ring=None, Tensor(e!)? ring_ctr=None, Tensor? ring_tab=None, int host_words=0) -> ()");
   m.def("adamw(Tensor table, Tensor blocks, float lr, float beta1, float beta2, float eps, float weight_decay, "
         "int step, Tensor? per_tensor, Tensor err) -> ()");
 }

@@ -356,7 +356,7 @@ def _register():
 
     @fake(lib + "adamw_dev")
     def _(table, blocks, counters, active, n_params, kind, warmup, total, power, init_lr, end_lr, beta1, beta2, eps,
-          wd, per_tensor, lr_dev, err, copy_src=None, ring=None, ring_ctr=None, ring_tab=None):
+          wd, per_tensor, lr_dev, err, copy_src=None, ring=None, ring_ctr=None, ring_tab=None, host_words=0):
         return None
 
     # ---------------------------------------------------------------- autograd formulas

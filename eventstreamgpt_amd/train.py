@@ -148,9 +148,10 @@ class FusedAdamW:
         """The device step over ``plan``: esgpt_adamw_prepare (counters, lr, per-tensor bias corrections — torch's
         one ``step`` per parameter) + the update, both no-ops while the device error block holds a flag. No host
         arguments change between steps (``lr=None``: the installed schedule), so the launch replays in a graph.
-        ``hand`` = (src, ring, ring_ctr, ring_tab): the step's hand-off entry written by the prepare launch (src — the
-        step's loss — and the error block into ring entry ring_ctr % len(ring_tab); TrainStep._claim). Returns whether the
-        launch (and so the hand-off) happened."""
+        ``hand`` = (src, ring, ring_ctr, ring_tab, host_words): the step's hand-off entry written by the prepare launch
+        (src — the step's loss — and the error block into ring entry ring_ctr % len(ring_tab), the error words also into
+        the mapped host words when host_words != 0; TrainStep._claim). Returns whether the launch (and so the hand-off)
+        happened."""
         if not plan["active"]:
             return False
         kind, warm, total, power, init_lr, end_lr = self.schedule
@@ -160,7 +161,7 @@ class FusedAdamW:
         self.ops.adamw_dev(plan["table"], plan["blocks"], self._counters, plan["active_dev"], len(self.params),
                            int(kind), int(warm), int(total), float(power), float(init_lr), float(end_lr), float(b1),
                            float(b2), float(self.eps), float(self.weight_decay), plan["per"], self._lr_dev,
-                           err_word(self.params[0].device), *(hand if hand is not None else (None, None, None, None)))
+                           err_word(self.params[0].device), *(hand if hand is not None else (None, None, None, None, 0)))
         return True
 
     def note_step(self, active):
@@ -562,6 +563,7 @@ class TrainStep:
         # fresh allocation before reuse while anything still shares it), the error words go to the host for check()
         self.ring_len = 64
         self._ring_tab = None
+        self._host_words = None
         self._slots: list = []
         self._ring_n = 0  # host mirror of the device ring counter
         self._vocab = getattr(getattr(model, "config", None), "vocab_size", None)
@@ -588,13 +590,19 @@ class TrainStep:
     # again while ANY tensor still shares its storage (the returned object, a detach(), a view, an index — counted by
     # the storage's use count, not by object identity), the entry gets a fresh allocation and its table slot is
     # re-pointed (one stream-ordered fill) — the caller's tensors keep their value and nothing is copied.
+    # The error words of entry k also land in coherent mapped host memory (esgpt_host_words_alloc), which check()
+    # reads once the step's event has completed: no D2H copy launch per step (a 16-byte copy to pinned memory costs
+    # its launch plus a ~15 us idle gap on the compute stream).
     def _ring_state(self):
         if self._ring_tab is None:
             self._slots = [torch.zeros(8, dtype=torch.float32, device=self.device) for _ in range(self.ring_len)]
             self._ring_tab = torch.tensor([t.data_ptr() for t in self._slots], dtype=torch.int64, device=self.device)
             self._ring_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._slot_users = _storage_users(self._slots[0])  # the ring's own reference alone
-        return None, self._ring_ctr, self._ring_tab
+            if HOST_ERROR_WORDS and self.device.type == "cuda":
+                self._host_words = _HostWords(self.ring_len)
+        hw = self._host_words
+        return None, self._ring_ctr, self._ring_tab, (hw.dev if hw is not None else 0)
 
     def _claim(self) -> int:
         """The ring entry the next optimizer launch writes (its device counter advances with every launch); an entry
@@ -852,7 +860,7 @@ class TrainStep:
         while len(self._pending) > keep or (not self.distributed and self._pending and self._pending[0][0].query()):
             ev, host, batch, active, stepped = self._pending.popleft()
             ev.synchronize()
-            code, mx = int(host[0]), int(host[1])
+            code, mx = host[0].read(host[1]) if isinstance(host, tuple) else (int(host[0]), int(host[1]))
             if code & 0xFFFFFFFF:
                 # the failing step's AdamW was a no-op on the device, and so is every step queued behind it (the
                 # sticky word): take back their step counts and LR steps. The block is cleared after them in
@@ -1038,9 +1046,12 @@ class TrainStep:
         # the step's error block: the words its optimizer launch wrote into ring entry `slot`, else the live block.
         # (Copied on the compute stream: on a side stream — waiting on an event recorded after the step — the C2
         # step measured ~50 us slower, tools/host_bound.py.)
-        host = torch.empty(2, dtype=torch.int64, pin_memory=True)
-        host.copy_(err_word(self.device) if slot is None else self._slots[slot][4:8].view(torch.int64),
-                   non_blocking=True)
+        if slot is not None and self._host_words is not None:
+            host = (self._host_words, slot)  # written by the optimizer launch straight into mapped host memory
+        else:
+            host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+            host.copy_(err_word(self.device) if slot is None else self._slots[slot][4:8].view(torch.int64),
+                       non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._pending.append((ev, host, host_batch, active, stepped))
@@ -1057,6 +1068,29 @@ class TrainStep:
         if self.check_errors:
             self._raise_pending(keep=0)
         check_errors(self.device if self.device.type == "cuda" else None, self._vocab)
+
+
+HOST_ERROR_WORDS = True  # measurement hook (bench.py --err-copy): False = round 5's per-step D2H copy
+
+
+class _HostWords:
+    """ring_len x 4 int32 words of coherent, device-mapped host memory (esgpt_host_words_alloc); freed with the
+    owner. ``read(k)`` = entry k's (flags | sticky << 32, max bad index), as the D2H copy of the error block gave."""
+
+    def __init__(self, n: int):
+        import ctypes
+
+        from . import _lib as L
+
+        lib = L.load()
+        h, d = ctypes.c_void_p(), ctypes.c_void_p()
+        L.check(lib.esgpt_host_words_alloc(16 * n, ctypes.byref(h), ctypes.byref(d)), "host_words_alloc")
+        self.dev = int(d.value)
+        self._words = (ctypes.c_int64 * (2 * n)).from_address(h.value)
+        self._fin = weakref.finalize(self, lib.esgpt_host_words_free, ctypes.c_void_p(h.value))
+
+    def read(self, k: int):
+        return int(self._words[2 * k]), int(self._words[2 * k + 1])
 
 
 def init_distributed():

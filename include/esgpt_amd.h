@@ -525,11 +525,19 @@ int esgpt_adamw_prepare_ex(int64_t* counters, const int32_t* active, int n_activ
                            int64_t* ring_ctr, int64_t ring_len, void* stream);
 /* The same with the hand-off entries as separate allocations: ring_tab is a device array of ring_len pointers (8-B
  * aligned), entry k = ring_tab[k] (16-B aligned, round_up(n_copy, 4) + 4 floats), read at launch time — the caller
- * may re-point an entry between launches (TrainStep does so when it still holds a loss returned from that entry). */
+ * may re-point an entry between launches (TrainStep does so when it still holds a loss returned from that entry).
+ * host_words (optional; requires ring_ctr): the device address of ring_len x 4 int32 words of coherent mapped host
+ * memory (esgpt_host_words_alloc); the error words of entry k are also written to host_words[4k .. 4k+3], which the
+ * host reads once an event recorded after the launch has completed — no D2H copy launch per step. */
 int esgpt_adamw_prepare_tab(int64_t* counters, const int32_t* active, int n_active, int n_params,
                             const esgpt_lr_schedule* sched, double beta1, double beta2, float* per_tensor,
                             float* lr_out, const int32_t* err, const float* copy_src, int64_t n_copy,
-                            float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, void* stream);
+                            float* const* ring_tab, int64_t* ring_ctr, int64_t ring_len, int32_t* host_words,
+                            void* stream);
+/* Coherent, device-mapped, zeroed host memory (hipHostMalloc mapped + coherent): *host = the host address, *dev =
+ * the address kernels write through. Freed with esgpt_host_words_free(host). */
+int esgpt_host_words_alloc(int64_t bytes, void** host, void** dev);
+int esgpt_host_words_free(void* host);
 int esgpt_adamw_dev(const esgpt_adam_tensor* table, const int64_t* blocks, int64_t n_blocks, const float* lr_dev,
                     float beta1, float beta2, float eps, float weight_decay, const float* per_tensor,
                     const int32_t* err, void* stream);

@@ -543,7 +543,7 @@ def test_hand_off_ring_claims_cpu():
     ts = TrainStep(m, OptimizationConfig(init_lr=1e-3), compute_dtype=torch.float32)
     ts.ring_len = 3
     like = torch.zeros(())
-    _, _, tab = ts._ring_state()
+    _, _, tab, _ = ts._ring_state()
     kept = []
     for alias in (lambda x: x, lambda x: x.detach(), lambda x: x.view(1)[None]):
         s = ts._claim()
