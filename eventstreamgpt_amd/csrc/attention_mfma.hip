@@ -15,6 +15,8 @@
 // query half splitting its key tiles by parity; K/V tiles of 64 rows are staged in LDS in pairs. Causal /
 // local-window / fully-padded key tiles are skipped.
 // Roofline: MFMA-bound at large L (algorithmic FLOPs: fwd 4*H*hd*T, bwd 8*H*hd*T, T = allowed (q,k) pairs).
+#include <type_traits>
+
 #include "attn_common.h"
 #include "common.h"
 
@@ -91,6 +93,47 @@ __device__ __forceinline__ bf16x8 perm_frag(const __bf16* T, int ld, int row, in
 
 __device__ __forceinline__ bool allowed(int key, int qpos, int window) {
   return key <= qpos && (window == 0 || qpos - key < window);
+}
+
+// Maximum of a lane's 32 scores as four independent max chains joined at the end (depth 6 instead of a 32-deep chain;
+// the compiler forms v_max3_f32). Not inline asm: the compiler does not insert the MFMA-result -> VALU wait states in
+// front of an asm statement that reads an accumulator (measured: intermittently wrong maxima at hd 16, where the
+// max follows a single MFMA).
+__device__ __forceinline__ float max3_f32(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+// Masks a lane's 32 scores of one 64-key tile without branches: the lane's allowed keys as one 64-bit word (the tile's
+// valid-key ballot, the causal limit key <= qpos, the local window qpos - key < window, the query's validity), then
+// one bit test per element at a compile-time position (the half-wave's 4-row offset is shifted out first).
+__device__ __forceinline__ void mask_tile(f32x16 (&s)[2], uint64_t kbits, bool qvalid, int rel, int window, int h) {
+  // rel = qpos - t0: key t0 + j is causally visible iff j <= rel, inside the window iff j > rel - window
+  uint64_t am = qvalid ? kbits : 0ull;
+  am &= rel >= 63 ? ~0ull : (rel < 0 ? 0ull : ((2ull << rel) - 1ull));
+  if (window) {
+    const int lo = rel - window + 1;  // smallest visible j
+    am &= lo <= 0 ? ~0ull : (lo > 63 ? 0ull : ~((1ull << lo) - 1ull));
+  }
+  const uint64_t okm = am >> (4 * h);
+  const uint32_t w0 = (uint32_t)okm, w1 = (uint32_t)(okm >> 32);
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int pos = (i & 3) + 8 * (i >> 2);  // acc_row(i, 0)
+      const uint32_t w = c ? w1 : w0;
+      s[c][i] = ((w >> pos) & 1u) ? s[c][i] : -INFINITY;
+    }
+}
+
+__device__ __forceinline__ float row_max32(const f32x16 (&s)[2]) {
+  float a[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = k >> 1, i0 = 8 * (k & 1);
+    float x = max3_f32(s[c][i0], s[c][i0 + 1], s[c][i0 + 2]);
+    x = max3_f32(x, s[c][i0 + 3], s[c][i0 + 4]);
+    x = max3_f32(x, s[c][i0 + 5], s[c][i0 + 6]);
+    a[k] = max3_f32(x, s[c][i0 + 7], s[c][i0 + 7]);
+  }
+  return max3_f32(max3_f32(a[0], a[1], a[2]), a[3], a[3]);
 }
 
 // Dropout element counter, identical to the generic kernels': (bh * Lq + q) * Lk + key.
@@ -195,15 +238,19 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   const __bf16* vbase = v + (int64_t)b * Lk * ld_in + hh * HD;
   const uint8_t* kmb = kmask ? kmask + (int64_t)b * Lk : nullptr;
 
-  // pair of tiles (keys kt .. kt+127) -> registers; rows past kmax (never visible to this block) are zeros
+  // pair of tiles (keys kt .. kt+127) -> registers by buffer loads whose range ends after row kmax: rows past it (never
+  // visible to this block) read as zeros with no branch (esgpt_attn_mfma_supported: Lk·ld_in·2 < 2^31)
   bf16x8 rk[NLD], rv[NLD];
+  const int rec = (kmax + 1) * (int)ld_in * 2;
+  const __amdgpu_buffer_rsrc_t rsk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(kbase), (short)0, rec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(vbase), (short)0, rec, 0x00020000);
   auto load_pair = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int c = tid + THREADS * i, row = c / CH, c8 = c % CH, gr = kt + row;
-      const bool ok = gr <= kmax;
-      rk[i] = ok ? *reinterpret_cast<const bf16x8*>(kbase + (int64_t)gr * ld_in + c8 * 8) : zero8();
-      rv[i] = ok ? *reinterpret_cast<const bf16x8*>(vbase + (int64_t)gr * ld_in + c8 * 8) : zero8();
+      const int c = tid + THREADS * i, row = c / CH, c8 = c % CH;
+      const int vo = (kt + row) * (int)ld_in * 2 + c8 * 16;
+      rk[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsk, vo, 0, 0));
+      rv[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsv, vo, 0, 0));
     }
   };
   auto key_ok = [&](int kt) {
@@ -231,49 +278,37 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
     }
     if (!kbits) continue;  // fully padded (or absent) key tile
 
-    f32x16 s[2];
+    // one instance per FULL (tiles inside the causal / local band with every key valid skip the masks): a mask
+    // applied under a runtime branch made the compiler copy all 32 scores on the unmasked path
+    const bool full = kbits == ~0ull && t0 + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - t0 < window);
+    auto tile = [&](auto full_c) {
+    constexpr bool FULL = decltype(full_c)::value;
+    f32x16 s[2] = {zero16(), zero16()};
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      s[c] = zero16();
+    for (int t = 0; t < HD / 16; ++t)  // the two score chains interleaved (no back-to-back dependent MFMAs)
 #pragma unroll
-      for (int t = 0; t < HD / 16; ++t) {
+      for (int c = 0; c < 2; ++c) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(myK + (32 * c + r) * NP + 16 * t + 8 * h);
         s[c] = mfma(a, qf[t], s[c]);
       }
-    }
-    const bool full = kbits == ~0ull && t0 + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - t0 < window);
     // row maximum of the raw scores (the log2(e) scaling is monotonic: max(s)·log2e = max(s·log2e) bit for bit),
     // then p = exp2(s·log2e − m) as one FMA per element (in the log2 domain: m = running max · log2e)
-    float mt = -INFINITY;
-    if (full) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) mt = fmaxf(mt, s[c][i]);
-    } else {
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int kr = 32 * c + acc_row(i, h);
-          const bool ok = qvalid && ((kbits >> kr) & 1ull) && allowed(t0 + kr, qpos, window);
-          s[c][i] = ok ? s[c][i] : -INFINITY;
-          mt = fmaxf(mt, s[c][i]);
-        }
-    }
+    if (!FULL) mask_tile(s, kbits, qvalid, qpos - t0, window, h);
+    float mt = row_max32(s);
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * kLog2e;
     const float mnew = fmaxf(m, mt);
     const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
     const float msub = (mnew == -INFINITY) ? 0.f : mnew;
-    float rs = 0.f;
+    float rsp[4] = {0.f, 0.f, 0.f, 0.f};  // four partial sums: no 32-deep add chain
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const float p = __builtin_amdgcn_exp2f(fmaf(s[c][i], kLog2e, -msub));  // exp2(-inf) = 0
-        rs += p;  // normaliser over undropped probabilities
+        rsp[i & 3] += p;  // normaliser over undropped probabilities
         s[c][i] = p;
       }
+    float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
     if (DROP) {
       uint32_t kw[2] = {0u, 0u};  // keep bits of this lane's keys, at their key position within the 32-key group
       // registers (i, i+1), i even, hold consecutive keys: one hash per pair when the pair is aligned
@@ -354,6 +389,9 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
           oacc[dt] = mfma(vf, pf, oacc[dt]);
         }
       }
+    };
+    if (full) tile(std::true_type{});
+    else tile(std::false_type{});
   }
 
   // ---- merge the two key parities of each query half (the odd-parity wave hands its state over in LDS) ----
@@ -407,12 +445,263 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Forward, wide form (long sequences): one workgroup of NW waves per QB = 32·NW-query block of one (batch, head);
+// every wave owns 32 queries and walks ALL of the block's 64-key tiles itself, so each K / V tile staged in LDS
+// feeds NW waves (the parity form above: 2 per tile). At long L the parity form is bound by the per-CU L2 -> LDS
+// stream (≈128 B/clk per CU for the K / V pairs at the MFMA rate, against the ≈30-35 the CU sustains), which the
+// wider reuse divides by NW / 2. K / V tiles are double-buffered in XOR-swizzled LDS images (attnb::Img: conflict-free
+// 16-B row reads for K, ds_read_b64_tr_b16 for Vᵀ); tile j+2's global loads are issued right after the barrier that
+// publishes tile j+1 and are written to LDS after tile j's compute: one barrier per tile. Tiles past a wave's causal
+// range (or before its window) are skipped by that wave. Same softmax, dropout hash / keep words and outputs as the
+// parity form.
+template <int HD, bool DROP, bool IDX64, int NW>
+__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_fwd_wide_kernel(
+    const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
+    int64_t tq, __bf16* __restrict__ o, int64_t ld_o, float* __restrict__ lse, const uint8_t* __restrict__ kmask,
+    const uint8_t* __restrict__ qmask, int H, int Lq, int Lk, int window, float drop_p,
+    const uint64_t* __restrict__ seed, uint32_t* __restrict__ keep, int nw, int order) {
+  static_assert(HD == 32 || HD == 64 || HD == 128, "wide forward head dims");
+  using Im = esgpt::attnb::Img<HD>;
+  constexpr int T = 64 * NW, QB = 32 * NW;
+  constexpr int CH = HD / 8;                          // 16-B chunks per row
+  constexpr int NLD = (ROWS * CH + T - 1) / T;        // chunks per thread and tensor for one tile
+  constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  __shared__ __attribute__((aligned(16))) __bf16 sK[2][ROWS * HD];
+  __shared__ __attribute__((aligned(16))) __bf16 sV[2][ROWS * HD];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int nqb = (Lq + QB - 1) / QB;
+  int bh, qbi;
+  if (order == 1) {
+    int rank;
+    esgpt::attnb::deal(blockIdx.x, gridDim.x, (int)(gridDim.x / nqb), rank, bh);
+    qbi = nqb - 1 - rank;
+  } else {
+    const int lin = xcd_linear(blockIdx.x, gridDim.x);
+    bh = lin / nqb;
+    qbi = lin % nqb;
+  }
+  const int b = bh / H, hh = bh % H;
+  const DropoutSpec dr = make_dropout(drop_p, seed);
+  constexpr bool idx32 = !IDX64;
+  const int off = Lk - Lq;
+  const int qb = qbi * QB;
+  const int qw = qb + 32 * wave;                              // this wave's first query
+  const int qi = qw + r;
+  const bool qin = qi < Lq;
+  const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
+  const int qpos = qi + off;
+  const bool wave_any = qw < Lq;
+  const int qlo_w = qw + off;                                 // smallest query position of this wave
+  const int qhi_w = min(qw + 31, Lq - 1) + off;               // largest
+
+  bf16x8 qf[HD / 16];
+  const __bf16* qrow = q + ((int64_t)b * tq + qi) * ld_in + hh * HD;
+#pragma unroll
+  for (int t = 0; t < HD / 16; ++t)
+    qf[t] = qin ? *reinterpret_cast<const bf16x8*>(qrow + 16 * t + 8 * h) : zero8();
+  f32x16 oacc[HD / 32];
+#pragma unroll
+  for (int dt = 0; dt < HD / 32; ++dt) oacc[dt] = zero16();
+  float m = -INFINITY, l = 0.f;  // running max (log2 domain) and normaliser
+
+  const int qhi = min(Lq, qb + QB) - 1;
+  const int kmax = min(Lk - 1, qhi + off);
+  const int kmin = window ? max(0, qb + off - window + 1) : 0;
+  const __bf16* kbase = k + (int64_t)b * Lk * ld_in + hh * HD;
+  const __bf16* vbase = v + (int64_t)b * Lk * ld_in + hh * HD;
+  const uint8_t* kmb = kmask ? kmask + (int64_t)b * Lk : nullptr;
+
+  bf16x8 rk[NLD], rv[NLD];
+  const int rec = (kmax + 1) * (int)ld_in * 2;  // buffer range ends after row kmax: later rows read as zeros
+  const __amdgpu_buffer_rsrc_t rsk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(kbase), (short)0, rec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(vbase), (short)0, rec, 0x00020000);
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = tid + T * i, row = c / CH, c8 = c % CH;
+      const int vo = (NLD * T == ROWS * CH || c < ROWS * CH) ? (kt + row) * (int)ld_in * 2 + c8 * 16 : rec;
+      rk[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsk, vo, 0, 0));
+      rv[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsv, vo, 0, 0));
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const int c = tid + T * i, row = c / CH, c8 = c % CH;
+      if (NLD * T == ROWS * CH || c < ROWS * CH) {
+        const int e = Im::off(row, 8 * c8);
+        *reinterpret_cast<bf16x8*>(&sK[buf][e]) = rk[i];
+        *reinterpret_cast<bf16x8*>(&sV[buf][e]) = rv[i];
+      }
+    }
+  };
+  auto key_ok = [&](int kt) {
+    const int key = kt + lane;
+    return key <= kmax && (kmb == nullptr || kmb[key] != 0);
+  };
+
+  const int kt0 = (kmin / ROWS) * ROWS;
+  load_tile(kt0);
+  bool kok = key_ok(kt0), kok_n = false;
+  store_tile(0);
+  __syncthreads();
+  if (kt0 + ROWS <= kmax) {
+    load_tile(kt0 + ROWS);
+    kok_n = key_ok(kt0 + ROWS);
+  }
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  int buf = 0;
+  for (int kt = kt0; kt <= kmax; kt += ROWS) {
+    const uint64_t kbits = __ballot(kok);
+    const bool act = wave_any && kbits != 0 && kt <= qhi_w && (window == 0 || qlo_w - (kt + ROWS - 1) < window);
+    const __bf16* tK = sK[buf];
+    const __bf16* tV = sV[buf];
+    const bool full = kbits == ~0ull && kt + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - kt < window);
+    auto tile = [&](auto full_c) {  // one instance per FULL (see the parity form)
+      constexpr bool FULL = decltype(full_c)::value;
+      f32x16 s[2] = {zero16(), zero16()};
+#pragma unroll
+      for (int t = 0; t < HD / 16; ++t)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(tK + Im::off(32 * c + r, 16 * t + 8 * h));
+          s[c] = mfma(a, qf[t], s[c]);
+        }
+      if (!FULL) mask_tile(s, kbits, qvalid, qpos - kt, window, h);
+      float mt = row_max32(s);
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * kLog2e;
+      const float mnew = fmaxf(m, mt);
+      const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
+      const float msub = (mnew == -INFINITY) ? 0.f : mnew;
+      float rsp[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[c][i], kLog2e, -msub));
+          rsp[i & 3] += p;
+          s[c][i] = p;
+        }
+      float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
+      if (DROP) {
+        uint32_t kw[2] = {0u, 0u};
+        if constexpr (idx32) {
+          const uint32_t rowbase = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk;
+          const bool aligned = (rowbase & 1) == 0;
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+              const uint32_t e = rowbase + (uint32_t)(kt + 32 * c + acc_row(i, h));
+              float m0, m1;
+              if (aligned) {
+                dropout_mult2_32(dr, e, m0, m1);
+              } else {
+                m0 = dropout_mult_32(dr, e);
+                m1 = dropout_mult_32(dr, e + 1);
+              }
+              s[c][i] *= m0;
+              s[c][i + 1] *= m1;
+              kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
+              kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
+            }
+        } else {
+          const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+          const bool aligned = (rowbase & 1) == 0;
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+              const uint64_t e = rowbase + (uint64_t)(kt + 32 * c + acc_row(i, h));
+              float m0, m1;
+              if (aligned) {
+                dropout_mult2(dr, e, m0, m1);
+              } else {
+                m0 = dropout_mult(dr, e);
+                m1 = dropout_mult(dr, e + 1);
+              }
+              s[c][i] *= m0;
+              s[c][i + 1] *= m1;
+              kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
+              kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
+            }
+        }
+        if (keep != nullptr) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const uint32_t w = kw[c] | (uint32_t)__shfl_xor((int)kw[c], 32, 64);
+            const int wi = (kt >> 5) + c;
+            if (h == 0 && qin && wi < nw) keep[((int64_t)bh * Lq + qi) * nw + wi] = w;
+          }
+        }
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = mnew;
+      if (__ballot(alpha != 1.f))
+#pragma unroll
+        for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+          const bf16x8 pf = acc_frag(s[c], ss);
+          const int row0 = 32 * c + 16 * ss + 4 * (g >> 1) + q4;
+#pragma unroll
+          for (int dt = 0; dt < HD / 32; ++dt) {
+            const int col = 32 * dt + 16 * (g & 1) + 4 * p4;
+            const bf16x4 lo = tr_read(tV + Im::off(row0, col)), hi = tr_read(tV + Im::off(row0 + 8, col));
+            bf16x8 vf;
+            vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
+            vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
+            oacc[dt] = mfma(vf, pf, oacc[dt]);
+          }
+        }
+    };
+    if (act) {
+      if (full) tile(std::true_type{});
+      else tile(std::false_type{});
+    }
+    if (kt + ROWS <= kmax) store_tile(buf ^ 1);  // tile kt + 64 (its buffer was last read before the previous barrier)
+    __syncthreads();
+    kok = kok_n;
+    if (kt + 2 * ROWS <= kmax) {
+      load_tile(kt + 2 * ROWS);
+      kok_n = key_ok(kt + 2 * ROWS);
+    }
+    buf ^= 1;
+  }
+
+  int tid2;  // an opaque copy of the thread id (see the parity form's epilogue)
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid2) : "v"(tid));
+  const int qi_e = qb + 32 * (tid2 >> 6) + (tid2 & 31);
+  const bool qin_e = qi_e < Lq;
+  const bool qvalid_e = qin_e && (qmask == nullptr || qmask[(int64_t)b * Lq + qi_e] != 0);
+  const bool ok = qvalid_e && l > 0.f;
+  const float inv = ok ? 1.f / l : 0.f;
+  if (qin_e) {
+    __bf16* orow = o + ((int64_t)b * Lq + qi_e) * ld_o + hh * HD;
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] *= inv;
+      store_col32<32>(orow + 32 * dt, oacc[dt], (tid2 >> 5) & 1);
+    }
+    if ((tid2 & 32) == 0) lse[(int64_t)bh * Lq + qi_e] = ok ? m * kLn2 + logf(l) : 0.f;
+  }
+}
+
 }  // namespace
 
 bool esgpt_attn_mfma_supported(int64_t hd, int64_t Lq, int64_t Lk, int64_t tq, int64_t ld_in, int64_t ld_o) {
   if (!(hd == 16 || hd == 32 || hd == 64 || hd == 128)) return false;
   if (Lk < 16 || Lq > (1 << 30)) return false;  // short dependency-graph sequences use the generic kernel
-  return (ld_in % 8 == 0) && (ld_o % 8 == 0) && (tq >= Lq);
+  // the forward's buffer loads address a batch element's K / V rows with 32-bit byte offsets
+  return (ld_in % 8 == 0) && (ld_o % 8 == 0) && (tq >= Lq) && Lk * ld_in < (int64_t(1) << 30);
 }
 
 // Workgroup order (ESGPT_ATTN_ORDER tuning hook, read once; see attn_fwd_mfma_kernel)
@@ -423,6 +712,41 @@ static int attn_order() {
     v = e ? atoi(e) : 1;  // measured (tools/attn_order_ab.sh, profiles/r05_attn_order_ab.log): order 1 wins everywhere
   }
   return v;
+}
+
+// Waves per workgroup of the wide forward (0: the parity form). Rule (tools/attn_wide_ab.sh): query runs of
+// Lq >= kWideMinLq at hd 64 take 4 waves (128 queries a block); ESGPT_ATTN_FWD_NW (tools builds) forces 0 / 4 / 8.
+constexpr int64_t kWideMinLq = 2048;
+static int fwd_wide_nw(int64_t B, int64_t H, int64_t Lq, int64_t hd) {
+  static int forced = -2;
+  if (forced == -2) {
+    const char* e = tuning_env("ESGPT_ATTN_FWD_NW");
+    forced = e ? atoi(e) : -1;
+    if (forced != -1 && forced != 0 && forced != 4 && forced != 8) forced = -1;
+  }
+  if (hd != 64) return 0;  // hd 128: the wide form's registers spill (the parity form stays)
+  if (forced >= 0) return forced;
+  (void)B;
+  (void)H;
+  return Lq >= kWideMinLq ? 4 : 0;
+}
+
+template <int HD, int NW>
+static void launch_wide(int64_t B, int64_t H, hipStream_t st, const void* q, const void* k, const void* v,
+                        int64_t ld_in, int64_t tq, void* o, int64_t ld_o, float* lse, const uint8_t* kmask,
+                        const uint8_t* qmask, int64_t Lq, int64_t Lk, int64_t window, float drop_p,
+                        const uint64_t* seed, uint32_t* keep) {
+  const int nw = (int)cdiv(Lk, 32);
+  const dim3 grid((unsigned)(cdiv(Lq, 32 * NW) * B * H));
+  const bool idx64 = (uint64_t)(B * H) * (uint64_t)Lq * (uint64_t)Lk > 0xffffffffull;
+#define ESGPT_WIDE(DROP, I64)                                                                                        \
+  attn_fwd_wide_kernel<HD, DROP, I64, NW><<<grid, dim3(64 * NW), 0, st>>>(                                             \
+      (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o, lse, kmask, qmask, (int)H,  \
+      (int)Lq, (int)Lk, (int)window, drop_p, seed, DROP ? keep : nullptr, nw, attn_order())
+  if (drop_p > 0.f && idx64) ESGPT_WIDE(true, true);
+  else if (drop_p > 0.f) ESGPT_WIDE(true, false);
+  else ESGPT_WIDE(false, false);
+#undef ESGPT_WIDE
 }
 
 template <int HD>
@@ -457,7 +781,12 @@ int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
                         int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, uint32_t* keep,
                         hipStream_t st) {
   dim3 grid((unsigned)(cdiv(Lq, ROWS) * B * H));  // 1-D: XCD-aware (query block, batch-head) order in the kernel
-  if (hd == 16)
+  const int nwv = fwd_wide_nw(B, H, Lq, hd);
+  if (nwv == 8)
+    launch_wide<64, 8>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
+  else if (nwv == 4)
+    launch_wide<64, 4>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
+  else if (hd == 16)
     launch_fwd<16>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);
   else if (hd == 32)
     launch_fwd<32>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);

@@ -9,7 +9,7 @@ from eventstreamgpt_amd import ops as O  # noqa: E402
 from eventstreamgpt_amd.kernels import tickets  # noqa: E402
 from tools.gemm_time import gtime  # noqa: E402
 
-tag = os.environ.get("ESGPT_ATTN_ORDER", "-")
+tag = os.environ.get("ESGPT_ATTN_ORDER", "-") + "/nw" + os.environ.get("ESGPT_ATTN_FWD_NW", "-")
 esgpt = O.load()
 for (B, L, H, hd, win, p) in [(32, 256, 4, 64, 0, 0.1), (32, 512, 8, 64, 0, 0.1), (32, 512, 8, 64, 32, 0.1),
                               (16, 1024, 4, 64, 0, 0.1), (4, 4096, 8, 64, 0, 0.0)]:
