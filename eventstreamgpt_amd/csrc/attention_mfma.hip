@@ -456,7 +456,7 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
 // range (or before its window) are skipped by that wave. Same softmax, dropout hash / keep words and outputs as the
 // parity form.
 template <int HD, bool DROP, bool IDX64, int NW>
-__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) void attn_fwd_wide_kernel(
+__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (DROP ? 2 : 3)) void attn_fwd_wide_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, __bf16* __restrict__ o, int64_t ld_o, float* __restrict__ lse, const uint8_t* __restrict__ kmask,
     const uint8_t* __restrict__ qmask, int H, int Lq, int Lk, int window, float drop_p,
@@ -714,9 +714,11 @@ static int attn_order() {
   return v;
 }
 
-// Waves per workgroup of the wide forward (0: the parity form). Rule (tools/attn_wide_ab.sh): query runs of
-// Lq >= kWideMinLq at hd 64 take 4 waves (128 queries a block); ESGPT_ATTN_FWD_NW (tools builds) forces 0 / 4 / 8.
-constexpr int64_t kWideMinLq = 2048;
+// Waves per workgroup of the wide forward (0: the parity form). Rule (tools/attn_wide_time.sh,
+// profiles/r06_attn_wide_ab.log): hd 64 with Lq >= kWideMinLq and at least kWideMinBlocks 128-query blocks (four
+// per CU) take 4 waves (C3: 52.4 -> 49.4 us, B=4 L=4096 H=8: 142 -> 114 us); fewer blocks keep the parity form (C5,
+// 1024 blocks of 64 queries: 45.4 vs 49.9 us; C2: 10.9 vs 15.5 us). ESGPT_ATTN_FWD_NW (tools builds) forces 0 / 4 / 8.
+constexpr int64_t kWideMinLq = 512, kWideMinBlocks = 1024;
 static int fwd_wide_nw(int64_t B, int64_t H, int64_t Lq, int64_t hd) {
   static int forced = -2;
   if (forced == -2) {
@@ -726,9 +728,7 @@ static int fwd_wide_nw(int64_t B, int64_t H, int64_t Lq, int64_t hd) {
   }
   if (hd != 64) return 0;  // hd 128: the wide form's registers spill (the parity form stays)
   if (forced >= 0) return forced;
-  (void)B;
-  (void)H;
-  return Lq >= kWideMinLq ? 4 : 0;
+  return Lq >= kWideMinLq && cdiv(Lq, 128) * B * H >= kWideMinBlocks ? 4 : 0;
 }
 
 template <int HD, int NW>

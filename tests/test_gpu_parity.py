@@ -111,9 +111,11 @@ def _torch_attention(qkv, H, key_mask, window, skf):
                                    (3, 17, 4, 64, 0, True), (2, 300, 4, 16, 0, False), (4, 256, 4, 16, 32, False),
                                    # >= 256 key-block workgroups: the backward without the query-tile split
                                    (32, 256, 8, 64, 0, False), (16, 512, 8, 64, 32, False),
-                                   # the wide forward (Lq >= 1024 at hd 64): 8 waves a block, 4 waves with a ragged
-                                   # last block and a window, static_kv_first
-                                   (16, 1024, 4, 64, 0, False), (2, 1100, 4, 64, 48, False), (2, 1025, 4, 64, 0, True)])
+                                   # the wide forward's rule (hd 64, Lq >= 512, >= 1024 blocks of 128 queries): plain,
+                                   # ragged last block + window, static_kv_first; the wide kernels themselves at every
+                                   # hd-64 shape: tools/attn_wide_tests.sh (forced 4 / 8 waves)
+                                   (16, 1024, 4, 64, 0, False), (32, 512, 8, 64, 0, False), (32, 520, 8, 64, 48, False),
+                                   (32, 513, 8, 64, 0, True)])
 def test_attention_kernel(shape, dtype):
     from eventstreamgpt_amd.kernels import AttentionFn
 
@@ -254,7 +256,7 @@ def _np_keep(seed: int, B: int, H: int, Lq: int, Lk: int, p: float):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 96, 4, 64, 0, False), (3, 40, 2, 16, 7, False), (4, 6, 2, 64, 0, True),
                                    (2, 260, 4, 16, 0, False), (32, 256, 8, 64, 0, False),
-                                   (2, 1030, 4, 64, 0, False), (16, 1024, 4, 64, 0, False)])
+                                   (2, 1030, 4, 64, 0, False), (32, 512, 8, 64, 0, False)])
 def test_attention_dropout(shape, dtype):
     """Attention-probability dropout: kernels vs softmax -> mask/(1-p) -> P.V with the same counter-hash mask."""
     from eventstreamgpt_amd import kernels as K
