@@ -446,24 +446,24 @@ __global__ __launch_bounds__(THREADS, HD == 128 ? 1 : 2) void attn_fwd_mfma_kern
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Forward, wide form (long sequences): one workgroup of NW waves per QB = 32·NW-query block of one (batch, head);
-// every wave owns 32 queries and walks ALL of the block's 64-key tiles itself, so each K / V tile staged in LDS
-// feeds NW waves (the parity form above: 2 per tile). At long L the parity form is bound by the per-CU L2 -> LDS
-// stream (≈128 B/clk per CU for the K / V pairs at the MFMA rate, against the ≈30-35 the CU sustains), which the
-// wider reuse divides by NW / 2. K / V tiles are double-buffered in XOR-swizzled LDS images (attnb::Img: conflict-free
-// 16-B row reads for K, ds_read_b64_tr_b16 for Vᵀ); tile j+2's global loads are issued right after the barrier that
-// publishes tile j+1 and are written to LDS after tile j's compute: one barrier per tile. Tiles past a wave's causal
-// range (or before its window) are skipped by that wave. Same softmax, dropout hash / keep words and outputs as the
-// parity form.
-template <int HD, bool DROP, bool IDX64, int NW>
-__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (DROP ? 2 : 3)) void attn_fwd_wide_kernel(
+// Forward, wide form (long sequences): one workgroup of NW waves per QB = 32·NU·NW-query block of one (batch, head);
+// every wave owns NU 32-query slices and walks ALL of the block's 64-key tiles itself, so each K / V tile staged in
+// LDS feeds NW waves (the parity form above: 2 per tile), and with NU = 2 every K / V fragment a wave reads from LDS
+// feeds two MFMAs (two query slices). At long L the parity form is bound by the per-CU L2 -> LDS stream (≈128 B/clk
+// per CU for the K / V pairs at the MFMA rate, against the ≈30-35 the CU sustains), which the wider reuse divides by
+// NW / 2. K / V tiles are double-buffered in XOR-swizzled LDS images (attnb::Img: conflict-free 16-B row reads for K,
+// ds_read_b64_tr_b16 for Vᵀ); tile j+2's global loads are issued right after the barrier that publishes tile j+1 and
+// are written to LDS after tile j's compute: one barrier per tile. Tiles past a wave's causal range (or before its
+// window) are skipped by that wave. Same softmax, dropout hash / keep words and outputs as the parity form.
+template <int HD, bool DROP, bool IDX64, int NW, int NU>
+__global__ __launch_bounds__(64 * NW, NW >= 8 || NU > 1 ? 1 : (DROP ? 2 : 3)) void attn_fwd_wide_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, __bf16* __restrict__ o, int64_t ld_o, float* __restrict__ lse, const uint8_t* __restrict__ kmask,
     const uint8_t* __restrict__ qmask, int H, int Lq, int Lk, int window, float drop_p,
     const uint64_t* __restrict__ seed, uint32_t* __restrict__ keep, int nw, int order) {
   static_assert(HD == 32 || HD == 64 || HD == 128, "wide forward head dims");
   using Im = esgpt::attnb::Img<HD>;
-  constexpr int T = 64 * NW, QB = 32 * NW;
+  constexpr int T = 64 * NW, QW = 32 * NU, QB = QW * NW;
   constexpr int CH = HD / 8;                          // 16-B chunks per row
   constexpr int NLD = (ROWS * CH + T - 1) / T;        // chunks per thread and tensor for one tile
   constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
@@ -487,24 +487,26 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (DROP ? 2 : 3)) void attn_fw
   constexpr bool idx32 = !IDX64;
   const int off = Lk - Lq;
   const int qb = qbi * QB;
-  const int qw = qb + 32 * wave;                              // this wave's first query
-  const int qi = qw + r;
-  const bool qin = qi < Lq;
-  const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
-  const int qpos = qi + off;
+  const int qw = qb + QW * wave;                              // this wave's first query
   const bool wave_any = qw < Lq;
   const int qlo_w = qw + off;                                 // smallest query position of this wave
-  const int qhi_w = min(qw + 31, Lq - 1) + off;               // largest
+  const int qhi_w = min(qw + QW - 1, Lq - 1) + off;           // largest
 
-  bf16x8 qf[HD / 16];
-  const __bf16* qrow = q + ((int64_t)b * tq + qi) * ld_in + hh * HD;
+  bf16x8 qf[NU][HD / 16];
+  f32x16 oacc[NU][HD / 32];
+  float m[NU], l[NU];  // running max (log2 domain) and normaliser per query slice
 #pragma unroll
-  for (int t = 0; t < HD / 16; ++t)
-    qf[t] = qin ? *reinterpret_cast<const bf16x8*>(qrow + 16 * t + 8 * h) : zero8();
-  f32x16 oacc[HD / 32];
+  for (int u = 0; u < NU; ++u) {
+    const int qi = qw + 32 * u + r;
+    const __bf16* qrow = q + ((int64_t)b * tq + qi) * ld_in + hh * HD;
 #pragma unroll
-  for (int dt = 0; dt < HD / 32; ++dt) oacc[dt] = zero16();
-  float m = -INFINITY, l = 0.f;  // running max (log2 domain) and normaliser
+    for (int t = 0; t < HD / 16; ++t)
+      qf[u][t] = qi < Lq ? *reinterpret_cast<const bf16x8*>(qrow + 16 * t + 8 * h) : zero8();
+#pragma unroll
+    for (int dt = 0; dt < HD / 32; ++dt) oacc[u][dt] = zero16();
+    m[u] = -INFINITY;
+    l[u] = 0.f;
+  }
 
   const int qhi = min(Lq, qb + QB) - 1;
   const int kmax = min(Lk - 1, qhi + off);
@@ -561,95 +563,108 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (DROP ? 2 : 3)) void attn_fw
     const bool full = kbits == ~0ull && kt + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - kt < window);
     auto tile = [&](auto full_c) {  // one instance per FULL (see the parity form)
       constexpr bool FULL = decltype(full_c)::value;
-      f32x16 s[2] = {zero16(), zero16()};
+      f32x16 s[NU][2];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) s[u][0] = s[u][1] = zero16();
 #pragma unroll
       for (int t = 0; t < HD / 16; ++t)
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(tK + Im::off(32 * c + r, 16 * t + 8 * h));
-          s[c] = mfma(a, qf[t], s[c]);
+#pragma unroll
+          for (int u = 0; u < NU; ++u) s[u][c] = mfma(a, qf[u][t], s[u][c]);
         }
-      if (!FULL) mask_tile(s, kbits, qvalid, qpos - kt, window, h);
-      float mt = row_max32(s);
-      mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * kLog2e;
-      const float mnew = fmaxf(m, mt);
-      const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m - mnew);
-      const float msub = (mnew == -INFINITY) ? 0.f : mnew;
-      float rsp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[c][i], kLog2e, -msub));
-          rsp[i & 3] += p;
-          s[c][i] = p;
+      for (int u = 0; u < NU; ++u) {
+        const int qi = qw + 32 * u + r;
+        const bool qin = qi < Lq;
+        if (!FULL) {
+          const bool qvalid = qin && (qmask == nullptr || qmask[(int64_t)b * Lq + qi] != 0);
+          mask_tile(s[u], kbits, qvalid, qi + off - kt, window, h);
         }
-      float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
-      if (DROP) {
-        uint32_t kw[2] = {0u, 0u};
-        if constexpr (idx32) {
-          const uint32_t rowbase = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk;
-          const bool aligned = (rowbase & 1) == 0;
+        float mt = row_max32(s[u]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64)) * kLog2e;
+        const float mnew = fmaxf(m[u], mt);
+        const float alpha = (mnew == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m[u] - mnew);
+        const float msub = (mnew == -INFINITY) ? 0.f : mnew;
+        float rsp[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int i = 0; i < 16; i += 2) {
-              const uint32_t e = rowbase + (uint32_t)(kt + 32 * c + acc_row(i, h));
-              float m0, m1;
-              if (aligned) {
-                dropout_mult2_32(dr, e, m0, m1);
-              } else {
-                m0 = dropout_mult_32(dr, e);
-                m1 = dropout_mult_32(dr, e + 1);
+          for (int i = 0; i < 16; ++i) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[u][c][i], kLog2e, -msub));
+            rsp[i & 3] += p;
+            s[u][c][i] = p;
+          }
+        float rs = (rsp[0] + rsp[1]) + (rsp[2] + rsp[3]);
+        if (DROP) {
+          uint32_t kw[2] = {0u, 0u};
+          if constexpr (idx32) {
+            const uint32_t rowbase = ((uint32_t)bh * (uint32_t)Lq + (uint32_t)qi) * (uint32_t)Lk;
+            const bool aligned = (rowbase & 1) == 0;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int i = 0; i < 16; i += 2) {
+                const uint32_t e = rowbase + (uint32_t)(kt + 32 * c + acc_row(i, h));
+                float m0, m1;
+                if (aligned) {
+                  dropout_mult2_32(dr, e, m0, m1);
+                } else {
+                  m0 = dropout_mult_32(dr, e);
+                  m1 = dropout_mult_32(dr, e + 1);
+                }
+                s[u][c][i] *= m0;
+                s[u][c][i + 1] *= m1;
+                kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
+                kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
               }
-              s[c][i] *= m0;
-              s[c][i + 1] *= m1;
-              kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
-              kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
-            }
-        } else {
-          const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
-          const bool aligned = (rowbase & 1) == 0;
+          } else {
+            const uint64_t rowbase = ((uint64_t)bh * (uint64_t)Lq + (uint64_t)qi) * (uint64_t)Lk;
+            const bool aligned = (rowbase & 1) == 0;
 #pragma unroll
-          for (int c = 0; c < 2; ++c)
+            for (int c = 0; c < 2; ++c)
 #pragma unroll
-            for (int i = 0; i < 16; i += 2) {
-              const uint64_t e = rowbase + (uint64_t)(kt + 32 * c + acc_row(i, h));
-              float m0, m1;
-              if (aligned) {
-                dropout_mult2(dr, e, m0, m1);
-              } else {
-                m0 = dropout_mult(dr, e);
-                m1 = dropout_mult(dr, e + 1);
+              for (int i = 0; i < 16; i += 2) {
+                const uint64_t e = rowbase + (uint64_t)(kt + 32 * c + acc_row(i, h));
+                float m0, m1;
+                if (aligned) {
+                  dropout_mult2(dr, e, m0, m1);
+                } else {
+                  m0 = dropout_mult(dr, e);
+                  m1 = dropout_mult(dr, e + 1);
+                }
+                s[u][c][i] *= m0;
+                s[u][c][i + 1] *= m1;
+                kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
+                kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
               }
-              s[c][i] *= m0;
-              s[c][i + 1] *= m1;
-              kw[c] |= (m0 != 0.f ? 1u : 0u) << acc_row(i, h);
-              kw[c] |= (m1 != 0.f ? 1u : 0u) << acc_row(i + 1, h);
-            }
-        }
-        if (keep != nullptr) {
+          }
+          if (keep != nullptr) {
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const uint32_t w = kw[c] | (uint32_t)__shfl_xor((int)kw[c], 32, 64);
-            const int wi = (kt >> 5) + c;
-            if (h == 0 && qin && wi < nw) keep[((int64_t)bh * Lq + qi) * nw + wi] = w;
+            for (int c = 0; c < 2; ++c) {
+              const uint32_t w = kw[c] | (uint32_t)__shfl_xor((int)kw[c], 32, 64);
+              const int wi = (kt >> 5) + c;
+              if (h == 0 && qin && wi < nw) keep[((int64_t)bh * Lq + qi) * nw + wi] = w;
+            }
           }
         }
+        rs += __shfl_xor(rs, 32, 64);
+        l[u] = l[u] * alpha + rs;
+        m[u] = mnew;
+        if (__ballot(alpha != 1.f))
+#pragma unroll
+          for (int dt = 0; dt < HD / 32; ++dt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) oacc[u][dt][i] *= alpha;
       }
-      rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
-      m = mnew;
-      if (__ballot(alpha != 1.f))
-#pragma unroll
-        for (int dt = 0; dt < HD / 32; ++dt)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) oacc[dt][i] *= alpha;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int ss = 0; ss < 2; ++ss) {
-          const bf16x8 pf = acc_frag(s[c], ss);
+          bf16x8 pf[NU];
+#pragma unroll
+          for (int u = 0; u < NU; ++u) pf[u] = acc_frag(s[u][c], ss);
           const int row0 = 32 * c + 16 * ss + 4 * (g >> 1) + q4;
 #pragma unroll
           for (int dt = 0; dt < HD / 32; ++dt) {
@@ -658,7 +673,8 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (DROP ? 2 : 3)) void attn_fw
             bf16x8 vf;
             vf[0] = lo[0]; vf[1] = lo[1]; vf[2] = lo[2]; vf[3] = lo[3];
             vf[4] = hi[0]; vf[5] = hi[1]; vf[6] = hi[2]; vf[7] = hi[3];
-            oacc[dt] = mfma(vf, pf, oacc[dt]);
+#pragma unroll
+            for (int u = 0; u < NU; ++u) oacc[u][dt] = mfma(vf, pf[u], oacc[u][dt]);
           }
         }
     };
@@ -678,20 +694,23 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : (DROP ? 2 : 3)) void attn_fw
 
   int tid2;  // an opaque copy of the thread id (see the parity form's epilogue)
   asm volatile("v_mov_b32 %0, %1" : "=v"(tid2) : "v"(tid));
-  const int qi_e = qb + 32 * (tid2 >> 6) + (tid2 & 31);
-  const bool qin_e = qi_e < Lq;
-  const bool qvalid_e = qin_e && (qmask == nullptr || qmask[(int64_t)b * Lq + qi_e] != 0);
-  const bool ok = qvalid_e && l > 0.f;
-  const float inv = ok ? 1.f / l : 0.f;
-  if (qin_e) {
-    __bf16* orow = o + ((int64_t)b * Lq + qi_e) * ld_o + hh * HD;
 #pragma unroll
-    for (int dt = 0; dt < HD / 32; ++dt) {
+  for (int u = 0; u < NU; ++u) {
+    const int qi_e = qb + QW * (tid2 >> 6) + 32 * u + (tid2 & 31);
+    const bool qin_e = qi_e < Lq;
+    const bool qvalid_e = qin_e && (qmask == nullptr || qmask[(int64_t)b * Lq + qi_e] != 0);
+    const bool ok = qvalid_e && l[u] > 0.f;
+    const float inv = ok ? 1.f / l[u] : 0.f;
+    if (qin_e) {
+      __bf16* orow = o + ((int64_t)b * Lq + qi_e) * ld_o + hh * HD;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] *= inv;
-      store_col32<32>(orow + 32 * dt, oacc[dt], (tid2 >> 5) & 1);
+      for (int dt = 0; dt < HD / 32; ++dt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[u][dt][i] *= inv;
+        store_col32<32>(orow + 32 * dt, oacc[u][dt], (tid2 >> 5) & 1);
+      }
+      if ((tid2 & 32) == 0) lse[(int64_t)bh * Lq + qi_e] = ok ? m[u] * kLn2 + logf(l[u]) : 0.f;
     }
-    if ((tid2 & 32) == 0) lse[(int64_t)bh * Lq + qi_e] = ok ? m * kLn2 + logf(l) : 0.f;
   }
 }
 
@@ -719,6 +738,18 @@ static int attn_order() {
 // per CU) take 4 waves (C3: 52.4 -> 49.4 us, B=4 L=4096 H=8: 142 -> 114 us); fewer blocks keep the parity form (C5,
 // 1024 blocks of 64 queries: 45.4 vs 49.9 us; C2: 10.9 vs 15.5 us). ESGPT_ATTN_FWD_NW (tools builds) forces 0 / 4 / 8.
 constexpr int64_t kWideMinLq = 512, kWideMinBlocks = 1024;
+// Query slices per wave of the 4-wave wide forward (ESGPT_ATTN_FWD_NU tools hook: 1 or 2; 2 halves the LDS reads
+// per MFMA but needs ~350-440 registers, one wave per SIMD: L=4096 144 -> 257 us, C3 63 -> 93 us same box,
+// profiles/r06_attn_nu_ab.log — tools build only).
+static int fwd_wide_nu() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = tuning_env("ESGPT_ATTN_FWD_NU");
+    v = (e && atoi(e) == 2) ? 2 : 1;
+  }
+  return v;
+}
+
 static int fwd_wide_nw(int64_t B, int64_t H, int64_t Lq, int64_t hd) {
   static int forced = -2;
   if (forced == -2) {
@@ -731,16 +762,16 @@ static int fwd_wide_nw(int64_t B, int64_t H, int64_t Lq, int64_t hd) {
   return Lq >= kWideMinLq && cdiv(Lq, 128) * B * H >= kWideMinBlocks ? 4 : 0;
 }
 
-template <int HD, int NW>
+template <int HD, int NW, int NU>
 static void launch_wide(int64_t B, int64_t H, hipStream_t st, const void* q, const void* k, const void* v,
                         int64_t ld_in, int64_t tq, void* o, int64_t ld_o, float* lse, const uint8_t* kmask,
                         const uint8_t* qmask, int64_t Lq, int64_t Lk, int64_t window, float drop_p,
                         const uint64_t* seed, uint32_t* keep) {
   const int nw = (int)cdiv(Lk, 32);
-  const dim3 grid((unsigned)(cdiv(Lq, 32 * NW) * B * H));
+  const dim3 grid((unsigned)(cdiv(Lq, 32 * NU * NW) * B * H));
   const bool idx64 = (uint64_t)(B * H) * (uint64_t)Lq * (uint64_t)Lk > 0xffffffffull;
 #define ESGPT_WIDE(DROP, I64)                                                                                        \
-  attn_fwd_wide_kernel<HD, DROP, I64, NW><<<grid, dim3(64 * NW), 0, st>>>(                                             \
+  attn_fwd_wide_kernel<HD, DROP, I64, NW, NU><<<grid, dim3(64 * NW), 0, st>>>(                                             \
       (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, ld_in, tq, (__bf16*)o, ld_o, lse, kmask, qmask, (int)H,  \
       (int)Lq, (int)Lk, (int)window, drop_p, seed, DROP ? keep : nullptr, nw, attn_order())
   if (drop_p > 0.f && idx64) ESGPT_WIDE(true, true);
@@ -781,11 +812,15 @@ int esgpt_attn_fwd_mfma(const void* q, const void* k, const void* v, int64_t ld_
                         int64_t Lk, int64_t hd, int64_t window, float drop_p, const uint64_t* seed, uint32_t* keep,
                         hipStream_t st) {
   dim3 grid((unsigned)(cdiv(Lq, ROWS) * B * H));  // 1-D: XCD-aware (query block, batch-head) order in the kernel
-  const int nwv = fwd_wide_nw(B, H, Lq, hd);
+  const int nwv = fwd_wide_nw(B, H, Lq, hd), nu = nwv ? fwd_wide_nu() : 1;
   if (nwv == 8)
-    launch_wide<64, 8>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
+    launch_wide<64, 8, 1>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
+#ifdef ESGPT_TUNING_HOOKS
+  else if (nwv == 4 && nu == 2)  // measured slower everywhere (one wave per SIMD at ~350-440 registers)
+    launch_wide<64, 4, 2>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
+#endif
   else if (nwv == 4)
-    launch_wide<64, 4>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
+    launch_wide<64, 4, 1>(B, H, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, Lq, Lk, window, drop_p, seed, keep);
   else if (hd == 16)
     launch_fwd<16>(grid, st, q, k, v, ld_in, tq, o, ld_o, lse, kmask, qmask, H, Lq, Lk, window, drop_p, seed, keep);
   else if (hd == 32)
