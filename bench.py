@@ -339,13 +339,19 @@ def gemm_bwd_in_step(model, opt_cfg, batch, dtype) -> dict:
 
 
 def _attn_symbol(lib, fwd: bool, hd: int, Lq: int, Lk: int, ld_in: int, ld_o: int, drop: bool,
-                 dtype=torch.bfloat16) -> str:
-    """The kernel esgpt_attn_fwd / _bwd actually launches for these arguments (the library's own dispatch rule)."""
+                 dtype=torch.bfloat16, bh: int = 0) -> str:
+    """The kernel esgpt_attn_fwd / _bwd actually launches for these arguments (the library's own dispatch rule;
+    ``bh`` = batch x heads, for the forward's wide-form rule)."""
     from eventstreamgpt_amd import _lib as L
 
     path = lib.esgpt_attn_path(hd, Lq, Lk, Lq, ld_in, ld_o, L.BF16 if dtype == torch.bfloat16 else L.F32)
     d = "true" if drop else "false"
     if path == 1:
+        # attention_mfma.hip fwd_wide_nw, attention_bwd.hip split2_keys
+        if fwd and hd == 64 and Lq >= 512 and -(-Lq // 128) * bh >= 1024:
+            return f"attn_fwd_wide_kernel<{hd}, {d}, 4 waves>"
+        if not fwd and ((Lk > 256 and (hd == 16 or (hd == 64 and not drop))) or hd == 128):
+            return f"attn_bwd_dkv_kernel<{hd}> + attn_bwd_dq_kernel<{hd}>"
         return f"attn_fwd_mfma_kernel<{hd}, {d}>" if fwd else f"attn_bwd_kernel<{hd}, {d}>"
     if path == 3:
         return (f"attn_fwd_f32_kernel<{hd}, {d}>" if fwd
@@ -507,7 +513,7 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype
     layer = f"{cfg_name} layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"
     f32 = dtype == torch.float32
     fa, ba, ka, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev, dtype)
-    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop, dtype), "mfma", 4.0 * H * hd * T_pairs, fa,
+    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop, dtype, B * H), "mfma", 4.0 * H * hd * T_pairs, fa,
         {"shape": layer + " (global)"}, ka)
     add("attn_bwd", _attn_symbol(lib, False, hd, Lq, Lq, 3 * D, D, drop, dtype), "mfma", 8.0 * H * hd * T_pairs, ba,
         {"shape": layer + " (global)"}, None)
@@ -559,7 +565,7 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype
     fl, bl, kll, _ = _attention_launchers(Bl, Ll, Hl * hd, Hl, torch.ones(Bl, Ll, dtype=torch.bool, device=dev), 0.0,
                                           dev, dtype)
     long_pairs = Bl * Ll * (Ll + 1) / 2
-    add("attn_fwd_long", _attn_symbol(lib, True, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False, dtype), "mfma",
+    add("attn_fwd_long", _attn_symbol(lib, True, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False, dtype, Bl * Hl), "mfma",
         4.0 * Hl * hd * long_pairs, fl, {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"}, kll)
     add("attn_bwd_long", _attn_symbol(lib, False, hd, Ll, Ll, 3 * Hl * hd, Hl * hd, False, dtype), "mfma",
         8.0 * Hl * hd * long_pairs, bl, {"shape": f"B={Bl} H={Hl} L={Ll} hd={hd}, causal, no dropout"}, None)

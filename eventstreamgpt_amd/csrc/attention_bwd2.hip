@@ -45,8 +45,9 @@ struct DkvCfg {
   static constexpr int LDS_BYTES = 2 * (2 * QT * HDP) + 4 * QT * NKW + 8 * QT;
 };
 
+// hd 64 with the forward's keep bits: one workgroup per CU (at two it spilled 16 B per lane)
 template <int HD, int DM, int NWK>
-__global__ __launch_bounds__(64 * NWK, HD == 128 ? 1 : 2) void attn_bwd_dkv_kernel(
+__global__ __launch_bounds__(64 * NWK, HD == 128 || (HD == 64 && DM == DROP_BITS && NWK == 4) ? 1 : 2) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
@@ -322,16 +323,20 @@ __global__ __launch_bounds__(256, HD == 128 ? 1 : 2) void attn_bwd_dq_kernel(
   const uint8_t* kmb = kmask ? kmask + (int64_t)b * Lk : nullptr;
   const uint32_t* kwrow = (bits && qin) ? keep + ((int64_t)bh * Lq + qi) * nw : nullptr;
 
-  // pair of tiles (keys kt .. kt+127) -> registers; rows past kmax are zeros
+  // pair of tiles (keys kt .. kt+127) -> registers by buffer loads whose range ends after row kmax (rows past it read
+  // as zeros, no per-load branch; esgpt_attn_mfma_supported bounds Lk·ld_in·2 below 2^31)
   bf16x8 rk[NLD], rv[NLD];
   uint32_t zw[2] = {0u, 0u};  // keep words of this wave's tile (two 32-key groups), prefetched with the pair
+  const int rec = (kmax + 1) * (int)ld_in * 2;
+  const __amdgpu_buffer_rsrc_t rsk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(kbase), (short)0, rec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(vbase), (short)0, rec, 0x00020000);
   auto load_pair = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      const int c = tid + 256 * i, row = c / CH, c8 = c % CH, gr = kt + row;
-      const bool ok = gr <= kmax;
-      rk[i] = ok ? *reinterpret_cast<const bf16x8*>(kbase + (int64_t)gr * ld_in + c8 * 8) : zero8();
-      rv[i] = ok ? *reinterpret_cast<const bf16x8*>(vbase + (int64_t)gr * ld_in + c8 * 8) : zero8();
+      const int c = tid + 256 * i, row = c / CH, c8 = c % CH;
+      const int vo = (kt + row) * (int)ld_in * 2 + c8 * 16;
+      rk[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsk, vo, 0, 0));
+      rv[i] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rsv, vo, 0, 0));
     }
     if (bits) {
       const int w0 = (kt + ROWS * kp) >> 5;
@@ -375,6 +380,18 @@ __global__ __launch_bounds__(256, HD == 128 ? 1 : 2) void attn_bwd_dq_kernel(
     const int rb = ROWS * kp;  // this wave's tile rows in the pair images
 
     const bool full = kbits == ~0ull && t0 + ROWS - 1 <= qlo_w && (window == 0 || qhi_w - t0 < window);
+    // this lane's visible keys of the tile as one word (valid-key ballot ∩ causal limit ∩ window), the half-wave's
+    // 4-row offset shifted out: each score's test is one bit at a compile-time position
+    uint64_t okm = ~0ull;
+    if (!full) {
+      const int rel = qpos - t0;
+      uint64_t am = kbits & (rel >= 63 ? ~0ull : (rel < 0 ? 0ull : ((2ull << rel) - 1ull)));
+      if (window) {
+        const int lo = rel - window + 1;
+        am &= lo <= 0 ? ~0ull : (lo > 63 ? 0ull : ~((1ull << lo) - 1ull));
+      }
+      okm = am >> (4 * h);
+    }
     // the two 32-key halves one after the other (half the live accumulators)
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -395,7 +412,7 @@ __global__ __launch_bounds__(256, HD == 128 ? 1 : 2) void attn_bwd_dq_kernel(
       for (int i = 0; i < 16; ++i) {
         const int kr = 32 * c + acc_row(i, h);
         const float e = __builtin_amdgcn_exp2f(fmaf(s[i], kLog2e, -lq));  // exp2(-inf) = 0: no row
-        const bool ok = full || (((kbits >> kr) & 1ull) && allowed(t0 + kr, qpos, window));
+        const bool ok = ((uint32_t)(okm >> (32 * c)) >> ((i & 3) + 8 * (i >> 2))) & 1u;
         const float p = ok ? e : 0.f;
         if (DROP) {
           float z;
@@ -492,13 +509,14 @@ int esgpt_attn_bwd_mfma_split(const void* q, const void* k, const void* v, int64
   if (hd == 64) ESGPT_BWD2_HD(64);
   ESGPT_BWD2_HD(128);
 #else
-  // the product takes the split form only at hd = 16 / 128 with 128 keys per dK / dV workgroup (split2_keys); the
-  // hd = 32 / 64 and 64-key forms (measured slower, and the hd-64 ones spill) exist in the tools build only
+  // the product takes the split form at hd = 16 / 64 / 128 with 128 keys per dK / dV workgroup (split2_keys); the
+  // hd = 32 and 64-key forms (measured slower) exist in the tools build only
   (void)keys_per_wg;
 #define ESGPT_BWD2_HD(HD_)                                                                                           \
   return launch2<HD_, 4>(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H, Lq, Lk,  \
                          window, drop_p, seed, keep, st)
   if (hd == 16) ESGPT_BWD2_HD(16);
+  if (hd == 64) ESGPT_BWD2_HD(64);
   if (hd == 128) ESGPT_BWD2_HD(128);
   return ESGPT_ERR_UNSUPPORTED;
 #endif
