@@ -350,7 +350,7 @@ def _attn_symbol(lib, fwd: bool, hd: int, Lq: int, Lk: int, ld_in: int, ld_o: in
         # attention_mfma.hip fwd_wide_nw, attention_bwd.hip split2_keys
         if fwd and hd == 64 and Lq >= 512 and -(-Lq // 128) * bh >= 1024:
             return f"attn_fwd_wide_kernel<{hd}, {d}, 4 waves>"
-        if not fwd and ((Lk > 256 and (hd == 16 or (hd == 64 and not drop))) or hd == 128):
+        if not fwd and ((Lk > 256 and hd in (16, 64)) or hd == 128):
             return f"attn_bwd_dkv_kernel<{hd}> + attn_bwd_dq_kernel<{hd}>"
         return f"attn_fwd_mfma_kernel<{hd}, {d}>" if fwd else f"attn_bwd_kernel<{hd}, {d}>"
     if path == 3:
@@ -513,8 +513,8 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype
     layer = f"{cfg_name} layer: B={B} H={H} L={Lq} hd={hd}, dropout {p_attn}"
     f32 = dtype == torch.float32
     fa, ba, ka, _ = _attention_launchers(B, Lq, D, H, batch.event_mask, p_attn, dev, dtype)
-    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop, dtype, B * H), "mfma", 4.0 * H * hd * T_pairs, fa,
-        {"shape": layer + " (global)"}, ka)
+    add("attn_fwd", _attn_symbol(lib, True, hd, Lq, Lq, 3 * D, D, drop, dtype, B * H), "mfma",
+        4.0 * H * hd * T_pairs, fa, {"shape": layer + " (global)"}, ka)
     add("attn_bwd", _attn_symbol(lib, False, hd, Lq, Lq, 3 * D, D, drop, dtype), "mfma", 8.0 * H * hd * T_pairs, ba,
         {"shape": layer + " (global)"}, None)
     gf, gb, kg = _gemm_launchers(B * Lq, D, F, dev, dtype)

@@ -33,10 +33,12 @@ __device__ __forceinline__ bool allowed(int key, int qpos, int window) {
 // fragments in registers, dKᵀ / dVᵀ accumulators in registers). Per query tile (QT queries): Q and dO staged in LDS,
 // lse / δ / keep words per query row; per wave and 32-query slice S = Q·Kᵀ − lse, dP = dO·Vᵀ − δ (key on the lane),
 // then dVᵀ += dOᵀ·(P∘Z), dKᵀ += Qᵀ·dS from the accumulators as B operands (no LDS round trip).
-template <int HD, int NWK>
+template <int HD, int NWK, int DM>
 struct DkvCfg {
   static constexpr int HDP = HD < 32 ? 32 : HD;
-  static constexpr int QT = HD == 128 ? 32 : 64;
+  // 32-query tiles at hd 128, and at hd 64 with the forward's keep bits (at 64 that instance spilled at two
+  // workgroups per CU)
+  static constexpr int QT = (HD == 128 || (HD == 64 && DM == DROP_BITS)) ? 32 : 64;
   static constexpr int KBW = 32 * NWK;
   static constexpr int THREADS = 64 * NWK;
   static constexpr int NKW = NWK;                             // keep words per query row of the key block
@@ -45,15 +47,14 @@ struct DkvCfg {
   static constexpr int LDS_BYTES = 2 * (2 * QT * HDP) + 4 * QT * NKW + 8 * QT;
 };
 
-// hd 64 with the forward's keep bits: one workgroup per CU (at two it spilled 16 B per lane)
 template <int HD, int DM, int NWK>
-__global__ __launch_bounds__(64 * NWK, HD == 128 || (HD == 64 && DM == DROP_BITS && NWK == 4) ? 1 : 2) void attn_bwd_dkv_kernel(
+__global__ __launch_bounds__(64 * NWK, HD == 128 ? 1 : 2) void attn_bwd_dkv_kernel(
     const __bf16* __restrict__ q, const __bf16* __restrict__ k, const __bf16* __restrict__ v, int64_t ld_in,
     int64_t tq, const __bf16* __restrict__ o, int64_t ld_o, const __bf16* __restrict__ dout, int64_t ld_do,
     const float* __restrict__ lse, const uint8_t* __restrict__ kmask, const uint8_t* __restrict__ qmask,
     __bf16* __restrict__ dk, __bf16* __restrict__ dv, int64_t ld_d, int H, int nbh, int Lq, int Lk, int window,
     float drop_p, const uint64_t* __restrict__ seed, const uint32_t* __restrict__ keep, int nw) {
-  using C = DkvCfg<HD, NWK>;
+  using C = DkvCfg<HD, NWK, DM>;
   constexpr int QT = C::QT, HDP = C::HDP, NKW = C::NKW, KBW = C::KBW, NT = C::THREADS, CPT = C::CPT;
   constexpr bool DROP = DM != DROP_NONE, bits = DM == DROP_BITS;
   using IQ = Img<HDP>;
@@ -181,7 +182,16 @@ __global__ __launch_bounds__(64 * NWK, HD == 128 || (HD == 64 && DM == DROP_BITS
       const bool full = __ballot(kvalid) == ~0ull && qpos_lo >= kw0 + 31 && (window == 0 || qpos_hi - kw0 < window);
       float zk[16];
       const uint32_t* zrow_w = sZ + wave * QT + 32 * qs;
+      uint32_t zbits = 0;  // DROP_BITS: this lane's keep bit of each of its 16 rows (bit i <-> register i)
       if (bits) {
+        // rows acc_row(i, h) = 4h + {0..3, 8..11, 16..19, 24..27}: four 16-B groups of keep words, folded into one
+        // 16-bit mask at once (the words do not stay live across the element loop)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          const uint4 w4 = *reinterpret_cast<const uint4*>(zrow_w + 8 * gq + 4 * h);
+          zbits |= ((w4.x >> r) & 1u) << (4 * gq) | ((w4.y >> r) & 1u) << (4 * gq + 1) |
+                   ((w4.z >> r) & 1u) << (4 * gq + 2) | ((w4.w >> r) & 1u) << (4 * gq + 3);
+        }
       } else if (DROP && idx32) {
 #pragma unroll
         for (int i = 0; i < 16; ++i)
@@ -201,7 +211,7 @@ __global__ __launch_bounds__(64 * NWK, HD == 128 || (HD == 64 && DM == DROP_BITS
         const bool ok = full | (kvalid & (key <= qpos) & ((window == 0) | (qpos - key < window)));
         const float p = ok ? e : 0.f;
         if (DROP) {
-          const float z = bits ? (((zrow_w[ql - 32 * qs] >> r) & 1u) ? dr.scale : 0.f) : zk[i];
+          const float z = bits ? (((zbits >> i) & 1u) ? dr.scale : 0.f) : zk[i];
           const float dl = sDl[ql];
           s[i] = p * z;                          // P∘Z (feeds dV)
           dp[i] = p * (z * (dp[i] + dl) - dl);   // dS
