@@ -350,7 +350,7 @@ def _attn_symbol(lib, fwd: bool, hd: int, Lq: int, Lk: int, ld_in: int, ld_o: in
         # attention_mfma.hip fwd_wide_nw, attention_bwd.hip split2_keys
         if fwd and hd == 64 and Lq >= 512 and -(-Lq // 128) * bh >= 1024:
             return f"attn_fwd_wide_kernel<{hd}, {d}, 4 waves>"
-        if not fwd and ((Lk > 256 and hd in (16, 64)) or hd == 128):
+        if not fwd and ((Lk > 256 and hd == 16) or (Lk >= 2048 and hd == 64 and not drop) or hd == 128):
             return f"attn_bwd_dkv_kernel<{hd}> + attn_bwd_dq_kernel<{hd}>"
         return f"attn_fwd_mfma_kernel<{hd}, {d}>" if fwd else f"attn_bwd_kernel<{hd}, {d}>"
     if path == 3:

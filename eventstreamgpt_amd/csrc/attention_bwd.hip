@@ -501,7 +501,8 @@ int set_lds_attr() {
 // The split backward (attention_bwd2.hip: dK / dV kernel + dQ kernel, no partial sums) for more than one key block
 // of the fused kernel, where that kernel's per-key-block f32 dQ partials dominate its traffic. ESGPT_ATTN_BWD_SPLIT2
 // tuning hook (read once): 0 = never, 1 = always, 64 / 128 = always with that many keys per dK / dV workgroup.
-int split2_keys(int64_t Lk, int64_t hd) {
+constexpr int64_t kSplit64MinLk = 2048;
+int split2_keys(int64_t Lk, int64_t hd, bool drop) {
   static const int forced = [] {
     const char* e = tuning_env("ESGPT_ATTN_BWD_SPLIT2");
     return e ? atoi(e) : -1;
@@ -510,15 +511,17 @@ int split2_keys(int64_t Lk, int64_t hd) {
   if (forced == 64 || forced == 128) return forced;
   if (forced == 1) return 128;
   // measured (tools/attn_split_ab.py, profiles/r05_attn_split_ab.log): faster past one key block at hd = 16 and 128
-  // (L = 520 local-40: 20.0 -> 15.6 us; L = 600: 161.6 -> 118.9 us). hd = 64 since round 6 (dQ kernel: buffer-load
-  // staging, one allowed-key word per lane and tile; dK / dV kernel: keep bits folded into one 16-bit mask per lane,
-  // 32-query tiles with keep bits — no spill at two workgroups per CU; tools/attn_split2_ab.sh, one box,
-  // profiles/r06_attn_split2_ab3.log): C3 130.0 -> 118.8 us, C3 local-32 80.1 -> 72.1, C5 133.1 -> 108.6, L = 4096
-  // 478.6 -> 429.7 (round 5: slower everywhere). Within one key block (C2) the fused kernel stays (29.1 vs 32.8 us).
-  // hd = 32: fused.
+  // (L = 520 local-40: 20.0 -> 15.6 us; L = 600: 161.6 -> 118.9 us). hd = 64: round 6's split kernels (dQ: buffer-load
+  // staging, one allowed-key word per lane and tile; dK / dV: keep bits folded into a 16-bit lane mask, 32-query tiles
+  // with keep bits) win in isolation (tools/attn_split2_ab.sh, profiles/r06_attn_split2_ab3.log: C5 133 -> 109 us,
+  // L = 4096 479 -> 430 us), but inside the C3 / C5 training steps (dropout, keep bits) they lose: C5 3.767 vs 3.845
+  // ms/step, C3 10.79 vs 10.86 alternating on one box (profiles/r06_split_step_ab.log; in-step per layer the split
+  // pair takes 76.7 + 41.3 us against the fused kernel's 93.8 + 9.8, profiles/r06_c5_*_bwd_kernel_stats.csv). So at
+  // hd 64 the split form runs only without dropout past kSplit64MinLk keys (the long-sequence case, where the fused
+  // kernel's per-key-block dQ partials reach 925 MB at L = 4096: 300 MB with the split pair).
   // hd = 128: always (the fused kernel's 512-thread workgroups cap it at 256 registers, where its hd-128 instances
   // spilled 464-572 B per lane to scratch; the split kernels run one wave per SIMD at hd 128 and do not spill)
-  return ((Lk > KB && (hd == 16 || hd == 64)) || hd == 128) ? 128 : 0;
+  return ((Lk > KB && hd == 16) || (Lk >= kSplit64MinLk && hd == 64 && !drop) || hd == 128) ? 128 : 0;
 }
 
 template <int HD>
@@ -526,7 +529,7 @@ int launch(const void* q, const void* k, const void* v, int64_t ld_in, int64_t t
            const void* dout, int64_t ld_do, const float* lse, const uint8_t* kmask, const uint8_t* qmask, void* dq,
            void* dk, void* dv, int64_t ld_d, int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t window,
            float drop_p, const uint64_t* seed, const uint32_t* keep, float* dq32, int32_t* counters, hipStream_t st) {
-  if (const int kpw = split2_keys(Lk, HD))
+  if (const int kpw = split2_keys(Lk, HD, drop_p > 0.f))
     return esgpt_attn_bwd_mfma_split(q, k, v, ld_in, tq, o, ld_o, dout, ld_do, lse, kmask, qmask, dq, dk, dv, ld_d, B, H,
                                      Lq, Lk, HD, window, drop_p, seed, keep, kpw, st);
   constexpr int lds = Cfg<HD>::LDS_BYTES;
@@ -595,7 +598,8 @@ extern "C" int esgpt_debug_stamps(uint64_t* out) {
 
 // f32 dQ partials, one per key block (more than one key block) + the dK / dV exchange slabs of the query-split pairs.
 size_t esgpt_attn_bwd_mfma_workspace(int64_t B, int64_t H, int64_t Lq, int64_t Lk, int64_t hd) {
-  if (split2_keys(Lk, hd)) return 0;  // the split backward needs none
+  if (split2_keys(Lk, hd, true)) return 0;  // the split backward needs none (asked as with dropout: the fused
+                                             // kernel's workspace whenever either may run)
   const size_t dq = Lk > KB ? sizeof(float) * (size_t)(cdiv(Lk, KB) * B * H * Lq * hd) : 0;
   const int64_t hdp = hd < 32 ? 32 : hd;  // exchange slabs hold the padded accumulator tiles
   return dq + sizeof(float) * (size_t)(B * H * cdiv(Lk, KB)) * 2 * KB * hdp;

@@ -44,11 +44,11 @@ def test_workspace_queries_without_gpu():
     lib = _lib.load(require_device=False)
     # MFMA backward: f32 dQ accumulator beyond one 256-key block + the dK/dV exchange slabs of the query-split pairs
     assert lib.esgpt_attn_bwd_workspace(2, 4, 256, 256, 64) == 4 * (2 * 4 * 1) * 2 * 256 * 64
-    # two key blocks at hd 32 (the fused kernel): one f32 dQ partial per key block + the dK / dV exchange slabs
-    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 32) == 2 * 4 * 2 * 4 * 512 * 32 + 4 * (2 * 4 * 2) * 2 * 256 * 32
-    # hd 16 / 64 past one key block and hd 128 take the split dK/dV + dQ kernels: no MFMA workspace (the generic
-    # kernels' delta buffer, B*H*Lq floats, remains the floor)
-    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 64) == 4 * 2 * 4 * 512
+    # two key blocks: one f32 dQ partial per key block + the dK / dV exchange slabs
+    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 64) == 2 * 4 * 2 * 4 * 512 * 64 + 4 * (2 * 4 * 2) * 2 * 256 * 64
+    # hd 16 past one key block and hd 128 take the split dK/dV + dQ kernels: no MFMA workspace (the generic kernels'
+    # delta buffer, B*H*Lq floats, remains the floor)
+    assert lib.esgpt_attn_bwd_workspace(2, 4, 512, 512, 16) == 4 * 2 * 4 * 512
     assert lib.esgpt_attn_bwd_counters(2, 4, 512) == 2 * 2 * 4 * 2
     b = _lib.EsgptBatch()
     b.B, b.L, b.M, b.S = 32, 256, 16, 2

@@ -115,7 +115,9 @@ def _torch_attention(qkv, H, key_mask, window, skf):
                                    # ragged last block + window, static_kv_first; the wide kernels themselves at every
                                    # hd-64 shape: tools/attn_wide_tests.sh (forced 4 / 8 waves)
                                    (16, 1024, 4, 64, 0, False), (32, 512, 8, 64, 0, False), (32, 520, 8, 64, 48, False),
-                                   (32, 513, 8, 64, 0, True)])
+                                   (32, 513, 8, 64, 0, True),
+                                   # the split dK/dV + dQ backward at hd 64 (no dropout, Lk >= 2048), ragged
+                                   (2, 2100, 2, 64, 0, False)])
 def test_attention_kernel(shape, dtype):
     from eventstreamgpt_amd.kernels import AttentionFn
 

@@ -15,6 +15,9 @@ for (B, L, H, hd, win, p) in [(32, 256, 4, 64, 0, 0.1), (32, 512, 8, 64, 0, 0.1)
                               (16, 1024, 4, 64, 0, 0.1), (4, 4096, 8, 64, 0, 0.0)]:
     D = H * hd
     em = torch.ones(B, L, dtype=torch.bool, device="cuda")
+    if os.environ.get("PAD") == "1":  # right padding as in the bench batches: each subject keeps 50-100 % of L events
+        lens = torch.randint(L // 2, L + 1, (B,), generator=torch.Generator().manual_seed(1)).cuda()
+        em = torch.arange(L, device="cuda")[None] < lens[:, None]
     T = B * L * (L + 1) / 2 if not win else B * sum(min(i + 1, win) for i in range(L))
     qkv = (0.5 * torch.randn(B, L, 3 * D, device="cuda")).bfloat16()
     seed = torch.tensor([99], dtype=torch.int64, device="cuda") if p > 0 else None
