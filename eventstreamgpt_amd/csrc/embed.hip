@@ -261,7 +261,11 @@ __global__ __launch_bounds__(256) void embed_joint_fwd_kernel(esgpt_batch bt, Bu
       s_sw[wave][pos] = swt;
     }
   }
-  __syncthreads();
+  // each wave reads back only its own LDS lists: a wave-level barrier (LDS accesses of one wave complete in order),
+  // not a workgroup one — the four events of a workgroup no longer wait for the slowest one's entry loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
   const int64_t n_chunks = (D + 64 * VEC - 1) / (64 * VEC);
   float t = 0.f;
