@@ -456,7 +456,10 @@ __global__ __launch_bounds__(256) void embed_split_bags_kernel(esgpt_batch bt, B
       s_sw[wave][lane] = swt;
     }
   }
-  __syncthreads();
+  // wave-local LDS lists: a wave-level barrier suffices (see embed_joint_fwd_kernel)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int64_t Dx = Dc + Dn;
   for (int64_t d = lane; d < Dx; d += 64) {
     const bool is_cat = d < Dc;
