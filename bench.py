@@ -624,6 +624,10 @@ def roofline_report(model, cfg, batch, dev, p_attn: float, peak_tf: float, opt_c
              "avg_ms": round(ms, 5), wk: work, "timing": "HIP graph of 20 launches, events on the replaying stream"}
         if e["bound"] == "hbm" and r["traffic"]:
             r["achieved_counter_GBs"] = round(r["traffic"] / (ms * 1e-3) / 1e9, 1)  # DRAM-side bytes / time
+            r["frac_counter"] = round(r["achieved_counter_GBs"] / PEAK_HBM_GBS, 5)
+        if e["bound"] == "hbm" and r["frac"] > 1.0:
+            r["note"] = ("per-occurrence bytes (SURVEY 8d) count every gathered row; repeated rows are served from "
+                         "L2 / MALL, so this exceeds the HBM peak: frac_counter is the DRAM-side fraction")
         r.update(e["extra"])
         out.append(r)
     # `roofline` = the step's dominant kernel by device time: the grouped projection backward (gemm_bwd_pair_kernel)
