@@ -518,7 +518,10 @@ def roofline_entries(model, cfg, batch, dev, p_attn: float, cfg_name: str, dtype
     add("attn_bwd", _attn_symbol(lib, False, hd, Lq, Lq, 3 * D, D, drop, dtype), "mfma", 8.0 * H * hd * T_pairs, ba,
         {"shape": layer + " (global)"}, None)
     gf, gb, kg = _gemm_launchers(B * Lq, D, F, dev, dtype)
-    add("gemm_fc_fwd", "gemm_kernel<true, true, ..., F32>" if f32 else "gemm_kernel<true, true, 3, 1, 1>", "mfma",
+    # the tile GEMM's rule (gemm.hip): 128x128 tiles when K and N >= 512 and M >= 4096, else 64x64 for c_fc
+    wide = D >= 512 and F >= 512 and B * Lq >= 4096
+    add("gemm_fc_fwd", "gemm_kernel<true, true, ..., F32>" if f32 else
+        ("gemm_kernel<true, true, 3, 2, 2>" if wide else "gemm_kernel<true, true, 3, 1, 1>"), "mfma",
         2.0 * B * Lq * D * F, gf,
         {"shape": f"{cfg_name} c_fc: [{B * Lq}, {D}] x [{F}, {D}]^T + bias, GELU epilogue"
                   + (", f32 operands (v_mfma_f32_32x32x2_f32)" if f32 else "")}, kg)
