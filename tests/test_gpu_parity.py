@@ -210,10 +210,12 @@ def test_width_bf16_matches_oracle(cfg_name, B):
     _grad_check(m, cfg, batch, out.loss, 1e-2, 3e-2, 0.9995)
 
 
-@pytest.mark.parametrize("cfg_name,B", [("C2", 2), ("C2", 32), ("C3", 1)])
+@pytest.mark.parametrize("cfg_name,B", [("C2", 2), ("C2", 32), ("C3", 1), ("C4", 1), ("C5", 1)])
 def test_width_f32_matches_oracle(cfg_name, B):
-    """f32 at the C2 / C3 widths (C3's 12 layers of global / local-32 attention at L=512): loss and every gradient
-    within 1e-5 of the oracle; C2 also at the bench's full batch (B = 32: every kernel at the shapes the step runs)."""
+    """f32 at the C2 / C3 / C4 / C5 widths (C3's 12 layers of global / local-32 attention at L=512; C4's nested
+    attention with G = 4 SPLIT levels; C5's L = 1024 with the LogNormalMixture TTE and V = 10,210): loss and every
+    gradient within 1e-5 of the oracle; C2 also at the bench's full batch (B = 32: every kernel at the shapes the step
+    runs)."""
     from eventstreamgpt_amd.synthetic import CONFIGS
 
     bc = CONFIGS[cfg_name]
